@@ -1,0 +1,103 @@
+#!/usr/bin/env python3
+"""In-tree build of the native libraries (no pip install, no JIT cache).
+
+* ``_native/libmrsum_kernels.so``: every ``csrc/kernels/*.hip`` compiled by
+  ``hipcc --offload-arch=gfx950 -O3`` (gfx950 only -- no other targets, no
+  CUDA paths) and linked into one shared object.
+* ``_native/libmrsum_runtime.so``: ``csrc/runtime/*.cpp`` host runtime (g++).
+
+Objects are rebuilt only when their source (or a header in the same
+directory) is newer.  Usage: ``python build.py [--force] [-j N]``.
+"""
+
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "llm_map_reduce_summarizer_amd")
+CSRC = os.path.join(PKG, "csrc")
+NATIVE = os.path.join(PKG, "_native")
+OBJ = os.path.join(ROOT, "build", "obj")
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+CXX = os.environ.get("CXX", "g++")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+HIP_FLAGS = ["--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast",
+             "-mcode-object-version=5", "-Wno-unused-result", "-munsafe-fp-atomics"]
+CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-sign-compare"]
+
+
+def _newer(src: str, dst: str, deps) -> bool:
+    if not os.path.exists(dst):
+        return True
+    t = os.path.getmtime(dst)
+    return any(os.path.getmtime(p) > t for p in [src] + list(deps))
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("build failed:\n%s\n%s" % (" ".join(cmd), r.stdout))
+    return r.stdout
+
+
+def build_kernels(force: bool = False, jobs: int = 8) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
+    hdrs = glob.glob(os.path.join(CSRC, "kernels", "*.h"))
+    os.makedirs(OBJ, exist_ok=True)
+    os.makedirs(NATIVE, exist_ok=True)
+    objs = []
+    todo = []
+    for s in srcs:
+        o = os.path.join(OBJ, os.path.basename(s) + ".o")
+        objs.append(o)
+        if force or _newer(s, o, hdrs):
+            todo.append([HIPCC] + HIP_FLAGS + ["-I", os.path.join(CSRC, "kernels"), "-c", s, "-o", o])
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        list(ex.map(_run, todo))
+    out = os.path.join(NATIVE, "libmrsum_kernels.so")
+    if force or todo or not os.path.exists(out):
+        tmp = out + ".tmp"
+        _run([HIPCC, "--offload-arch=%s" % ARCH, "-shared", "-fPIC", "-o", tmp] + objs)
+        os.replace(tmp, out)
+    return out
+
+
+def build_runtime(force: bool = False) -> str:
+    srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
+    os.makedirs(NATIVE, exist_ok=True)
+    out = os.path.join(NATIVE, "libmrsum_runtime.so")
+    if force or any(_newer(s, out, []) for s in srcs):
+        tmp = out + ".tmp"
+        _run([CXX] + CXX_FLAGS + ["-shared", "-o", tmp] + srcs + ["-lpthread"])
+        os.replace(tmp, out)
+    return out
+
+
+def build_all(force: bool = False, jobs: int = 8, kernels: bool = True) -> None:
+    build_runtime(force)
+    if kernels:
+        if not shutil.which(HIPCC) and not os.path.exists(HIPCC):
+            raise RuntimeError("hipcc not found at %s" % HIPCC)
+        build_kernels(force, jobs)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("--runtime-only", action="store_true")
+    a = ap.parse_args()
+    build_all(a.force, a.jobs, kernels=not a.runtime_only)
+    print("built:", ", ".join(sorted(os.listdir(NATIVE))))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

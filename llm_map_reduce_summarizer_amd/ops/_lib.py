@@ -1,0 +1,72 @@
+"""Loading of the in-tree native libraries.
+
+Two shared objects are built by ``build.py`` (``python build.py`` or
+``__graft_entry__.build()``) into ``llm_map_reduce_summarizer_amd/_native/``:
+
+* ``libmrsum_kernels.so`` -- every HIP/CDNA4 kernel (hipcc --offload-arch=gfx950),
+  exposed through ``extern "C"`` launchers that take raw device pointers and a
+  ``hipStream_t``.  Launchers enqueue on the caller's stream, never allocate and
+  never synchronise, so they are legal inside hipGraph capture.
+* ``libmrsum_runtime.so`` -- host C++ runtime: BPE merge loop, paged-KV block
+  allocator, batch packing for the scheduler.
+
+``torch`` must be imported before the kernel library is loaded: both torch and
+our library link ``libamdhip64.so.7`` (same SONAME), and loading torch first
+makes the dynamic loader bind ours to torch's already-mapped HIP runtime so
+streams and device pointers are shared.
+
+On a machine with a GPU the kernel library is REQUIRED (``kernels_lib()``
+raises if it is missing) -- there is deliberately no silent PyTorch fallback
+for the hot path.  ``MRSUM_OPS=torch`` selects the pure-PyTorch reference ops
+explicitly (used by CPU tests and as the numerics oracle).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+NATIVE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native")
+KERNELS_SO = os.path.join(NATIVE_DIR, "libmrsum_kernels.so")
+RUNTIME_SO = os.path.join(NATIVE_DIR, "libmrsum_runtime.so")
+
+_lock = threading.Lock()
+_kernels: Optional[ctypes.CDLL] = None
+_runtime: Optional[ctypes.CDLL] = None
+_runtime_tried = False
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def kernels_lib() -> ctypes.CDLL:
+    """The HIP kernel library; raises if it has not been built."""
+    global _kernels
+    if _kernels is not None:
+        return _kernels
+    with _lock:
+        if _kernels is None:
+            import torch  # noqa: F401  (bind libamdhip64 to torch's copy first)
+            if not os.path.isfile(KERNELS_SO):
+                raise NativeLibraryMissing(
+                    "%s not found: run `python build.py` (hipcc --offload-arch=gfx950) first" % KERNELS_SO)
+            _kernels = ctypes.CDLL(KERNELS_SO, mode=ctypes.RTLD_LOCAL)
+    return _kernels
+
+
+def runtime_lib(required: bool = True) -> Optional[ctypes.CDLL]:
+    """The host C++ runtime library (None if missing and not required)."""
+    global _runtime, _runtime_tried
+    if _runtime is not None:
+        return _runtime
+    with _lock:
+        if _runtime is None and not _runtime_tried:
+            _runtime_tried = True
+            if os.path.isfile(RUNTIME_SO):
+                _runtime = ctypes.CDLL(RUNTIME_SO, mode=ctypes.RTLD_LOCAL)
+    if _runtime is None and required:
+        raise NativeLibraryMissing("%s not found: run `python build.py` first" % RUNTIME_SO)
+    return _runtime

@@ -1,0 +1,163 @@
+"""Process-group setup and the small collectives of the summarizer.
+
+One process per GPU (``torchrun --nproc-per-node N``).  On ROCm the
+``"nccl"`` backend of ``torch.distributed`` *is* RCCL, whose rings run over
+the point-to-point xGMI links of the node; ``gloo`` is used on CPU-only hosts
+(tests).  Rendezvous uses the ``MASTER_ADDR``/``MASTER_PORT`` env vars
+(always 127.0.0.1 in this project's launchers).
+
+Layout: ``world = dp * tp`` with tensor-parallel groups of consecutive ranks
+(``[0..tp-1], [tp..2tp-1], ...``) so a TP group shares the fewest xGMI hops
+on a single node, and data-parallel replicas are the TP groups.
+
+The map-reduce pipeline only needs tiny DP collectives:
+variable-length UTF-8 payloads (summaries, token counts) are all-gathered as
+``uint8`` device tensors after an all-gather of their lengths -- one RCCL
+all-gather of ``world x max_len`` bytes per phase.  TP all-reduces live in
+``parallel/tp.py``.
+"""
+
+from __future__ import annotations
+
+import datetime
+import json
+import logging
+import os
+from dataclasses import dataclass
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+log = logging.getLogger("mrsum.dist")
+
+
+@dataclass
+class ParallelState:
+    world: int = 1
+    rank: int = 0
+    local_rank: int = 0
+    tp: int = 1
+    tp_rank: int = 0
+    dp: int = 1
+    dp_rank: int = 0
+    tp_group: Any = None
+    backend: str = "none"
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+
+_STATE = ParallelState()
+
+
+def is_initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def init_distributed_from_env(backend: Optional[str] = None, timeout_s: float = 1800.0) -> bool:
+    """Initialise the default group when launched by torchrun (WORLD_SIZE > 1)."""
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws <= 1 or is_initialized():
+        return is_initialized()
+    if backend is None:
+        backend = os.environ.get("MRSUM_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    kwargs = {}
+    if backend == "nccl":
+        torch.cuda.set_device(local_rank)
+        kwargs["device_id"] = torch.device("cuda", local_rank)
+    dist.init_process_group(backend=backend, timeout=datetime.timedelta(seconds=timeout_s), **kwargs)
+    log.info("process group up: backend=%s rank=%d/%d", backend, dist.get_rank(), dist.get_world_size())
+    return True
+
+
+def setup_parallel(tp: int = 1) -> ParallelState:
+    """Create (or return) the DP x TP layout for ``tp`` ranks per replica."""
+    global _STATE
+    if not is_initialized():
+        _STATE = ParallelState(tp=1, backend="none")
+        if tp != 1:
+            raise ValueError("tp=%d requires a process group (launch with torchrun)" % tp)
+        return _STATE
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if world % tp:
+        raise ValueError("world size %d is not divisible by tp=%d" % (world, tp))
+    if _STATE.world == world and _STATE.tp == tp and _STATE.backend != "none":
+        return _STATE
+    tp_group = None
+    if tp > 1:
+        for start in range(0, world, tp):
+            g = dist.new_group(list(range(start, start + tp)))
+            if start <= rank < start + tp:
+                tp_group = g
+    _STATE = ParallelState(world=world, rank=rank, local_rank=int(os.environ.get("LOCAL_RANK", rank)), tp=tp,
+                           tp_rank=rank % tp, dp=world // tp, dp_rank=rank // tp, tp_group=tp_group,
+                           backend=dist.get_backend())
+    return _STATE
+
+
+def state() -> ParallelState:
+    return _STATE
+
+
+def _comm_device() -> torch.device:
+    if is_initialized() and dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def all_gather_bytes(payload: bytes, group=None) -> List[bytes]:
+    """Gather one variable-length byte string from every rank (rank order)."""
+    if not is_initialized():
+        return [payload]
+    dev = _comm_device()
+    ws = dist.get_world_size(group)
+    n = torch.tensor([len(payload)], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(n) for _ in range(ws)]
+    dist.all_gather(sizes, n, group=group)
+    lens = [int(s.item()) for s in sizes]
+    m = max(1, max(lens))
+    buf = torch.zeros(m, dtype=torch.uint8, device=dev)
+    if payload:
+        buf[: len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(dev)
+    outs = [torch.empty_like(buf) for _ in range(ws)]
+    dist.all_gather(outs, buf, group=group)
+    return [bytes(o[:l].cpu().numpy().tobytes()) for o, l in zip(outs, lens)]
+
+
+def all_gather_json(obj: Any, group=None) -> List[Any]:
+    return [json.loads(b.decode("utf-8")) for b in all_gather_bytes(json.dumps(obj).encode("utf-8"), group)]
+
+
+def broadcast_json(obj: Any, src: int = 0, group=None) -> Any:
+    if not is_initialized():
+        return obj
+    return all_gather_json(obj if dist.get_rank() == src else None, group)[src]
+
+
+def barrier() -> None:
+    if is_initialized():
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def all_reduce_max(x: float) -> float:
+    if not is_initialized():
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=_comm_device())
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def shutdown() -> None:
+    global _STATE
+    if is_initialized():
+        try:
+            barrier()
+        finally:
+            dist.destroy_process_group()
+    _STATE = ParallelState()

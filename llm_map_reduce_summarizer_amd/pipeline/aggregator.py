@@ -1,0 +1,162 @@
+"""Reduce stage (layer L6): combine chunk summaries into one summary.
+
+Reference: ``ResultAggregator`` (``result_aggregator.py:26-498``).  Kept:
+
+* summaries sorted by ``chunk_index`` and prefixed ``"[Time: a - b]\\n"``
+  (``:79-90``); empty summaries skipped;
+* single pass when hierarchical is off or the summaries total
+  ``<= max_tokens_per_batch`` (6000) tokens (``:95``);
+* otherwise two levels: contiguous batches of
+  ``min(10, max(1, int((6000 - 1000) / avg_tokens)))`` summaries (``:357-380``)
+  reduced concurrently with ``Batch: i/n`` / ``Position`` metadata
+  (``:325-342``), then one final pass (``:346-355``);
+* return ``{"summary", "chunks_aggregated", "processing_time"}``, error text
+  ``"Error generating summary: ..."`` on failure (``:256-259``).
+
+Changed: the reduce calls go through the *executor's*
+provider (Q1: the reference always POSTs to OpenAI), the batch/final
+templates and custom prompts are rendered (Q2/Q3), the reduce temperature is
+configurable (``REDUCE_TEMPERATURE``, default 0.2 as the reference
+hard-codes), and ``max_levels=None`` enables a recursive reduce that keeps
+batching until one prompt fits (the reference stops at 2 levels).
+
+With the local engine every level is ONE batched generate call, so level-1
+batches are spread over the data-parallel ranks and prefilled together.
+"""
+
+from __future__ import annotations
+
+import logging
+import time
+from typing import Any, Dict, List, Optional
+
+from .executor import LLMExecutor
+from .preprocess import format_timestamp
+from .prompts import AGG_BATCH_PROMPT, AGG_FINAL_PROMPT, build_aggregation_messages
+from .providers import GenRequest
+
+log = logging.getLogger("mrsum.aggregator")
+
+
+class ResultAggregator:
+    def __init__(self, executor: Optional[LLMExecutor] = None, max_tokens_per_batch: int = 6000,
+                 tokenizer_name: Optional[str] = None, hierarchical: bool = True, tokenizer=None,
+                 max_levels: Optional[int] = 2, reserved_tokens: int = 1000, max_batch_size: int = 10):
+        self.executor = executor or LLMExecutor()
+        self.max_tokens_per_batch = max_tokens_per_batch
+        if tokenizer is None:
+            tokenizer = getattr(self.executor.backend, "tokenizer", None)
+        if tokenizer is None:
+            from ..engine.tokenizer import get_tokenizer
+            tokenizer = get_tokenizer(tokenizer_name)
+        self.tokenizer = tokenizer
+        self.hierarchical = hierarchical
+        self.max_levels = max_levels
+        self.reserved_tokens = reserved_tokens
+        self.max_batch_size = max_batch_size
+        self.last_plan: Dict[str, Any] = {}
+
+    # --------------------------------------------------------------- helpers
+    def _format_time(self, seconds: float) -> str:
+        return format_timestamp(seconds)
+
+    def _total_tokens(self, texts: List[str]) -> int:
+        return sum(self.tokenizer.count(t) for t in texts)
+
+    def _calculate_batch_size(self, summaries: List[str]) -> int:
+        if not summaries:
+            return 1
+        avg = self._total_tokens(summaries) / len(summaries)
+        per = max(1, int((self.max_tokens_per_batch - self.reserved_tokens) / max(avg, 1e-9)))
+        return min(per, self.max_batch_size)
+
+    def _request(self, summaries: List[str], template: Optional[str], metadata: Optional[Dict[str, Any]],
+                 stage: str) -> GenRequest:
+        msgs = build_aggregation_messages(summaries, template, metadata)
+        cfg = self.executor.config
+        return GenRequest(user=msgs["user"], system=msgs["system"], max_tokens=cfg.MAX_TOKENS,
+                          temperature=cfg.REDUCE_TEMPERATURE, stage=stage)
+
+    async def _run(self, reqs: List[GenRequest], stage: str) -> List[str]:
+        results = await self.executor.generate(reqs, stage=stage)
+        out = []
+        for r in results:
+            if r.error:
+                log.error("aggregation call failed: %s", r.error)
+                out.append("Error generating summary: %s" % r.error)
+            else:
+                out.append(r.text)
+        return out
+
+    async def _single_aggregation(self, summaries: List[str], prompt_template: Optional[str] = None,
+                                  metadata: Optional[Dict[str, Any]] = None) -> str:
+        return (await self._run([self._request(summaries, prompt_template, metadata, "reduce_final")],
+                                "reduce_final"))[0]
+
+    # ------------------------------------------------------------------ main
+    async def aggregate(self, processed_chunks: List[Dict[str, Any]], prompt_template: Optional[str] = None,
+                        metadata: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
+        t0 = time.perf_counter()
+        if not processed_chunks:
+            return {"summary": "", "error": "No chunks provided for aggregation"}
+        processed_chunks = sorted(processed_chunks, key=lambda c: c.get("chunk_index", 0))
+        summaries = []
+        for c in processed_chunks:
+            if c.get("summary"):
+                summaries.append("[Time: %s - %s]\n%s" % (format_timestamp(c.get("start_time", 0)),
+                                                          format_timestamp(c.get("end_time", 0) or 0),
+                                                          c["summary"]))
+            else:
+                log.warning("chunk %s has no summary", c.get("chunk_index", "?"))
+        log.info("aggregating %d summaries", len(summaries))
+        if not self.hierarchical or self._total_tokens(summaries) <= self.max_tokens_per_batch:
+            self.last_plan = {"levels": 1, "calls": [1]}
+            final = await self._single_aggregation(summaries, prompt_template, metadata)
+        else:
+            final = await self._hierarchical_aggregation(summaries, prompt_template, metadata)
+        dt = time.perf_counter() - t0
+        log.info("aggregation done in %.2f s (%s)", dt, self.last_plan)
+        return {"summary": final, "chunks_aggregated": len(processed_chunks), "processing_time": dt,
+                "plan": dict(self.last_plan)}
+
+    async def _hierarchical_aggregation(self, summaries: List[str], prompt_template: Optional[str] = None,
+                                        metadata: Optional[Dict[str, Any]] = None) -> str:
+        calls: List[int] = []
+        current = summaries
+        while True:
+            level = len(calls) + 1
+            bs = self._calculate_batch_size(current)
+            batches = [current[i:i + bs] for i in range(0, len(current), bs)]
+            n = len(batches)
+            reqs = []
+            for i, b in enumerate(batches):
+                meta = dict(metadata or {})
+                meta.update({"Batch": "%d/%d" % (i + 1, n),
+                             "Position": "Covering approximately %.0f%% - %.0f%% of the transcript"
+                                         % (100 * i / n, 100 * (i + 1) / n)})
+                reqs.append(self._request(b, AGG_BATCH_PROMPT, meta, "reduce_l%d" % level))
+            log.info("reduce level %d: %d summaries -> %d batches of <=%d", level, len(current), n, bs)
+            before = len(current)
+            current = await self._run(reqs, "reduce_l%d" % level)
+            calls.append(n)
+            if len(current) == 1:
+                self.last_plan = {"levels": len(calls), "calls": calls}
+                return current[0]
+            if self.max_levels is not None:
+                if len(calls) + 1 >= self.max_levels:  # the final pass is the last allowed level
+                    break
+            elif self._total_tokens(current) <= self.max_tokens_per_batch or n >= before:
+                break  # recursive mode: stop once everything fits (or no progress is possible)
+        template = prompt_template or AGG_FINAL_PROMPT
+        calls.append(1)
+        self.last_plan = {"levels": len(calls), "calls": calls}
+        return (await self._run([self._request(current, template, metadata, "reduce_final")], "reduce_final"))[0]
+
+
+def aggregate_results(processed_chunks: List[Dict[str, Any]], prompt_template: Optional[str] = None,
+                      metadata: Optional[Dict[str, Any]] = None, hierarchical: bool = True,
+                      executor: Optional[LLMExecutor] = None) -> str:
+    """Synchronous wrapper (reference ``result_aggregator.py:501-524``)."""
+    import asyncio
+    agg = ResultAggregator(executor=executor, hierarchical=hierarchical)
+    return asyncio.run(agg.aggregate(processed_chunks, prompt_template, metadata))["summary"]
