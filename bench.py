@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Headline benchmark: end-to-end map-reduce summarisation of a 10 h
+transcript with Llama-3-8B (BASELINE.json: "chunks/sec (whole node) +
+end-to-end wall-clock, 10h transcript, Llama-3-8B").
+
+One step = the full pipeline of the reference's ``TranscriptSummarizer.
+summarize`` (reference main.py:82-257) on a synthetic 10 h transcript:
+preprocess -> chunk (4000-token budget) -> map (one 1000-token summary per
+chunk, temperature 0.3) -> hierarchical reduce (level-1 batches + final pass,
+temperature 0.2), all generation on the local engine (random-init
+Llama-3-8B weights, bf16).  Chunks are data-parallel over the N ranks
+(one process per GPU, RCCL all-gather of the summaries); every rank runs
+the same SPMD pipeline.
+
+value = chunks / end-to-end seconds (whole job; the transcript is fixed, so
+scaling is strong).  ms_per_step = end-to-end wall-clock of one summary.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import logging
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_VALUE = None  # the reference publishes no number
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--hours", type=float, default=10.0)
+    ap.add_argument("--max-new-tokens", type=int, default=1000)
+    ap.add_argument("--chunk-tokens", type=int, default=4000)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--log-level", default="WARNING")
+    args = ap.parse_args()
+
+    logging.basicConfig(level=getattr(logging, args.log_level.upper()), stream=sys.stderr,
+                        format="%(asctime)s %(name)s %(levelname)s %(message)s")
+    import torch
+
+    from llm_map_reduce_summarizer_amd.config import LLMConfig
+    from llm_map_reduce_summarizer_amd.engine.provider import LocalEngineProvider
+    from llm_map_reduce_summarizer_amd.parallel import dist as pdist
+    from llm_map_reduce_summarizer_amd.pipeline.executor import LLMExecutor
+    from llm_map_reduce_summarizer_amd.pipeline.orchestrator import TranscriptSummarizer
+    from llm_map_reduce_summarizer_amd.utils.synth import synthetic_transcript
+
+    pdist.init_distributed_from_env()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    if torch.cuda.is_available():
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+
+    cfg = LLMConfig(MAX_TOKENS=args.max_new_tokens, TEMPERATURE=0.3, REDUCE_TEMPERATURE=0.2)
+    provider = LocalEngineProvider(args.model, cfg, use_graphs=not args.no_graphs)
+    executor = LLMExecutor(config=cfg, provider_obj=provider)
+    summarizer = TranscriptSummarizer(executor=executor, max_tokens_per_chunk=args.chunk_tokens)
+    transcript = synthetic_transcript(args.hours, seed=0)
+    _ = provider.engine  # weight init + KV allocation outside the timed region
+
+    def one():
+        return asyncio.run(summarizer.summarize(transcript))
+
+    for i in range(args.warmup):
+        t = time.perf_counter()
+        rep = one()
+        if rank == 0:
+            print("warmup %d: %.2f s, %d chunks" % (i, time.perf_counter() - t, rep["chunks"]), file=sys.stderr)
+
+    pdist.barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    reports = []
+    for _ in range(args.steps):
+        reports.append(one())
+    pdist.barrier()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    elapsed = pdist.all_reduce_max(time.perf_counter() - t0)
+
+    rep = reports[-1]
+    ms = elapsed / max(1, args.steps) * 1000.0
+    n_chunks = rep["chunks"]
+    value = n_chunks / (ms / 1000.0)
+    eng = rep.get("engine", {})
+    out = {
+        "metric": "chunks/sec (whole node) + end-to-end wall-clock, 10h transcript, Llama-3-8B",
+        "value": round(value, 4),
+        "unit": "chunks/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 2),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+        "dtype": "bf16",
+        "data": "synthetic %gh transcript (utils/synth.py, seed 0); random-init weights" % args.hours,
+        "config": {"model": args.model, "global_batch": n_chunks, "seq_len": args.chunk_tokens,
+                   "parallelism": "dp%d" % world, "max_new_tokens": args.max_new_tokens,
+                   "transcript_hours": args.hours},
+        "e2e_wall_s": round(ms / 1000.0, 3),
+        "phases_s": {k: round(v, 3) for k, v in rep.get("timings", {}).items()},
+        "map_chunks_per_s": round(rep["chunks_per_second"] or 0.0, 3),
+        "reduce_plan": rep.get("reduce_plan"),
+        "tokens_used": rep.get("tokens_used"),
+        "engine_rank0": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in eng.items()},
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    pdist.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

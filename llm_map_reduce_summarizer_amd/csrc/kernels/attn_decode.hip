@@ -1,0 +1,203 @@
+// Paged GQA decode attention, split-K over the context.
+//
+// One query token per sequence.  Work item = (split s, kv head, sequence b):
+// a 256-thread workgroup streams keys [ks, ke) of ONE kv head from the paged
+// cache and serves all G = Hq/Hkv query heads that share it, so every K/V
+// byte is read from HBM exactly once per step (the op is HBM bound: at B=44,
+// 4.5k context, Llama-3-8B reads ~26 GB of KV per step).
+//
+// Lane layout: 16 "key slots" x 16 lanes; lane (slot, dp) owns dims
+// [8dp, 8dp+8) of every key  slot, slot+16, ... of the split, i.e. one 16-B
+// K load + one 16-B V load per key, 4 keys unrolled => 128 B in flight per
+// lane.  Consecutive slots read consecutive rows of a page (one page = P rows
+// of one head, contiguous), so a workgroup step reads 16 x 256 B contiguous.
+// q.k partial dots are reduced over the 16 lanes of a slot with xor
+// shuffles; each slot keeps its own online-softmax state (m, l, o) which the
+// workgroup merges through LDS at the end.  Scores are in the log2 domain
+// (q pre-scaled by log2(e)/sqrt(D)) so the exponentials are exp2.
+//
+// Output: unnormalised partials part_o [B, Hq, S, D] f32 and part_ml
+// [B, Hq, S, 2] = (running max, running sum); attn_decode_combine merges the
+// S splits into out [B, Hq*D] bf16.  Context length = positions[b] + 1 is
+// read on the device, so the launch shape is fixed and the kernel can live
+// inside a captured decode graph.
+#include "common.h"
+
+template <int G>
+__global__ __launch_bounds__(256) void attn_decode_split_kernel(
+    const bf16* __restrict__ q, int q_stride, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ positions,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int P, int S, float scale_log2) {
+    constexpr int D = 128;
+    const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+    const int Hq = Hkv * G;
+    const int tid = threadIdx.x, slot = tid >> 4, dp = tid & 15;
+    const int ctx = positions[b] + 1;
+    int chunk = (ctx + S - 1) / S;
+    chunk = (chunk + 15) & ~15;
+    const int ks = split * chunk;
+    const int ke = min(ctx, ks + chunk);
+
+    __shared__ float sm_o[16][G][D];
+    __shared__ float sm_m[16][G];
+    __shared__ float sm_l[16][G];
+
+    const size_t ml_base = ((size_t)b * Hq + (size_t)kvh * G) * S + split;
+    if (ks >= ke) {
+        if (tid < G) {
+            part_ml[(ml_base + (size_t)tid * S) * 2 + 0] = -INFINITY;
+            part_ml[(ml_base + (size_t)tid * S) * 2 + 1] = 0.f;
+        }
+        return;
+    }
+
+    float qf[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        const uint4 v = *reinterpret_cast<const uint4*>(q + (size_t)b * q_stride + (kvh * G + g) * D + dp * 8);
+        unpack8(v, qf[g]);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qf[g][j] *= scale_log2;
+    }
+    float m[G], l[G], o[G][8];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+        m[g] = -INFINITY;
+        l[g] = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
+    }
+    const int* bt = block_tables + (size_t)b * bt_stride;
+    const size_t head_off = (size_t)kvh * P * D + dp * 8;
+
+    for (int k0 = ks + slot; k0 < ke; k0 += 64) {
+        uint4 kr[4], vr[4];
+        bool valid[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = k0 + 16 * u;
+            valid[u] = k < ke;
+            const int kk = valid[u] ? k : k0;
+            const int page = bt[kk / P];
+            const size_t off = ((size_t)page * Hkv * P + (kk % P)) * D + head_off;
+            kr[u] = *reinterpret_cast<const uint4*>(kc + off);
+            vr[u] = *reinterpret_cast<const uint4*>(vc + off);
+        }
+        float s[4][G];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float kf[8];
+            unpack8(kr[u], kf);
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                float acc = 0.f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc += qf[g][j] * kf[j];
+                acc += __shfl_xor(acc, 1, 64);
+                acc += __shfl_xor(acc, 2, 64);
+                acc += __shfl_xor(acc, 4, 64);
+                acc += __shfl_xor(acc, 8, 64);
+                s[u][g] = valid[u] ? acc : -INFINITY;
+            }
+        }
+        float pr[4][G];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const float mx = fmaxf(fmaxf(s[0][g], s[1][g]), fmaxf(s[2][g], s[3][g]));
+            const float mn = fmaxf(m[g], mx);  // finite: key k0 is always valid
+            const float alpha = exp2f(m[g] - mn);
+            m[g] = mn;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) pr[u][g] = exp2f(s[u][g] - mn);
+            l[g] = l[g] * alpha + (pr[0][g] + pr[1][g]) + (pr[2][g] + pr[3][g]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[g][j] *= alpha;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float vf[8];
+            unpack8(vr[u], vf);
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) o[g][j] += pr[u][g] * vf[j];
+            }
+        }
+    }
+
+    // merge the 16 slots
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sm_o[slot][g][dp * 8 + j] = o[g][j];
+        if (dp == 0) {
+            sm_m[slot][g] = m[g];
+            sm_l[slot][g] = l[g];
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < G * D; i += 256) {
+        const int g = i / D, d = i % D;
+        float M = -INFINITY;
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) M = fmaxf(M, sm_m[s2][g]);
+        float acc = 0.f, L = 0.f;
+#pragma unroll
+        for (int s2 = 0; s2 < 16; ++s2) {
+            const float ms = sm_m[s2][g];
+            const float w = ms == -INFINITY ? 0.f : exp2f(ms - M);
+            acc += w * sm_o[s2][g][d];
+            L += w * sm_l[s2][g];
+        }
+        const size_t pi = ml_base + (size_t)g * S;
+        part_o[pi * D + d] = acc;
+        if (d == 0) {
+            part_ml[pi * 2 + 0] = M;
+            part_ml[pi * 2 + 1] = L;
+        }
+    }
+}
+
+__global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* __restrict__ part_o,
+                                                                  const float* __restrict__ part_ml,
+                                                                  bf16* __restrict__ out, int out_stride, int Hq,
+                                                                  int S) {
+    constexpr int D = 128;
+    const int bh = blockIdx.x, b = bh / Hq, h = bh % Hq, d = threadIdx.x;
+    const float* ml = part_ml + (size_t)bh * S * 2;
+    float M = -INFINITY;
+    for (int s = 0; s < S; ++s) M = fmaxf(M, ml[2 * s]);
+    float num = 0.f, den = 0.f;
+    for (int s = 0; s < S; ++s) {
+        const float ms = ml[2 * s];
+        if (ms == -INFINITY) continue;
+        const float w = exp2f(ms - M);
+        num += w * part_o[((size_t)bh * S + s) * D + d];
+        den += w * ml[2 * s + 1];
+    }
+    out[(size_t)b * out_stride + h * D + d] = (bf16)(den > 0.f ? num / den : 0.f);
+}
+
+MRSUM_API int mrsum_attn_decode(const void* q, int q_stride, const void* kcache, const void* vcache,
+                                const int* block_tables, int bt_stride, const int* positions, void* part_o,
+                                void* part_ml, void* out, int out_stride, int B, int Hq, int Hkv, int D, int P,
+                                int S, float scale, hipStream_t s) {
+    if (B <= 0) return 0;
+    if (D != 128 || Hq % Hkv || S < 1 || P % 16) return (int)hipErrorInvalidValue;
+    const int G = Hq / Hkv;
+    const float sl = scale * 1.4426950408889634f;
+    dim3 grid(S, Hkv, B), block(256);
+    auto Qp = (const bf16*)q; auto K = (const bf16*)kcache; auto V = (const bf16*)vcache;
+    auto PO = (float*)part_o; auto PM = (float*)part_ml;
+    switch (G) {
+        case 1: attn_decode_split_kernel<1><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl); break;
+        case 2: attn_decode_split_kernel<2><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl); break;
+        case 4: attn_decode_split_kernel<4><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl); break;
+        case 8: attn_decode_split_kernel<8><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    int e = (int)hipGetLastError();
+    if (e) return e;
+    attn_decode_combine_kernel<<<B * Hq, 128, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, S);
+    return (int)hipGetLastError();
+}

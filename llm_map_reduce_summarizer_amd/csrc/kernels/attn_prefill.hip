@@ -1,0 +1,223 @@
+// Causal varlen flash attention for prefill on MFMA.
+//
+// Packed batch: qkv [T, row_stride] bf16 (Q heads, then K heads, then V
+// heads, D=128 each, already rotated by rope_kv), cu_seqlens [nseq+1].
+// Work item = (sequence, 128-row query block) x query head; items are listed
+// by the host heaviest-first (causal blocks late in a sequence do the most
+// key tiles), blockIdx.y = query head.
+//
+// Workgroup: 4 waves, wave w owns query rows [32w, 32w+32) of the block.
+// Per 64-key tile (K and V staged through LDS, next tile prefetched into
+// registers while the current one is consumed - issue early / write late):
+//
+//   S^T = K . Q^T   v_mfma_f32_32x32x16_bf16, A = K rows from LDS
+//                   (ds_read_b128, 16-B chunks XOR-swizzled by row&15 so a
+//                   16-lane group hits 16 distinct slots), B = Q^T fragments
+//                   held in VGPRs for the whole loop.  The "swapped" product
+//                   puts one query row per lane (col = lane&31), so the row
+//                   max is 31 in-lane fmax + one xor-32 shuffle.
+//   softmax         online, log2 domain, causal + length mask on the tile.
+//   O^T += V^T . P^T  the S^T accumulator registers, converted to bf16, are
+//                   directly the B operand (cdna_hip_programming.md §3
+//                   "accumulator tile as the next MFMA's operand"); the A
+//                   operand V^T comes from ds_read_b64_tr_b16 transposed
+//                   reads of the row-major V tile, whose 16-B chunks are
+//                   XOR-swizzled by (row&3)<<2 so the four rows of one
+//                   transposed read land on four different 64-B bank ranges.
+//
+// Numerics: bf16 inputs, fp32 accumulation and softmax, bf16 output.
+#include "common.h"
+
+namespace {
+constexpr int D = 128;
+constexpr int BM = 128;  // query rows per workgroup
+constexpr int BN = 64;   // keys per tile
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+__device__ __forceinline__ int k_off(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
+__device__ __forceinline__ int v_off(int row, int chunk) { return row * 256 + ((chunk ^ ((row & 3) << 2)) << 4); }
+
+__device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
+}  // namespace
+
+__global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __restrict__ qkv, int row_stride,
+                                                              const int* __restrict__ cu_seqlens,
+                                                              const int2* __restrict__ items,
+                                                              bf16* __restrict__ out, int out_stride, int Hq,
+                                                              int Hkv, float scale_log2) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * BN * 256];
+    char* ldsK = lds;
+    char* ldsV = lds + BN * 256;
+
+    const int2 it = items[blockIdx.x];
+    const int seq = it.x, qblock = it.y;
+    const int h = blockIdx.y, kvh = h / (Hq / Hkv);
+    const int s0 = cu_seqlens[seq], len = cu_seqlens[seq + 1] - s0;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5, r32 = lane & 31;
+    const bf16* base = qkv + (size_t)s0 * row_stride;
+    const int kcol = (Hq + kvh) * D, vcol = (Hq + Hkv + kvh) * D;
+
+    // Q^T fragments: lane holds Q[row r32][dims 16ks + 8half .. +8] for ks = 0..7
+    const int qi = qblock + 32 * w + r32;
+    bf16x8 qf[8];
+    {
+        const bool ok = qi < len;
+        const bf16* qp = base + (size_t)(ok ? qi : 0) * row_stride + h * D + 8 * half;
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) {
+            uint4 v = *reinterpret_cast<const uint4*>(qp + 16 * ks);
+            if (!ok) v = make_uint4(0, 0, 0, 0);
+            qf[ks] = as_bf16x8(v);
+        }
+    }
+
+    const int kend = min(len, qblock + BM);
+    const int ntiles = (kend + BN - 1) / BN;
+
+    // staging: thread loads rows tid/16 + 16i (i<4), chunk tid%16
+    const int st_chunk = tid & 15, st_row0 = tid >> 4;
+    uint4 kreg[4], vreg[4];
+    auto load_tile = [&](int t) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int key = t * BN + st_row0 + 16 * i;
+            if (key < len) {
+                const bf16* p = base + (size_t)key * row_stride + st_chunk * 8;
+                kreg[i] = *reinterpret_cast<const uint4*>(p + kcol);
+                vreg[i] = *reinterpret_cast<const uint4*>(p + vcol);
+            } else {
+                kreg[i] = make_uint4(0, 0, 0, 0);
+                vreg[i] = make_uint4(0, 0, 0, 0);
+            }
+        }
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = st_row0 + 16 * i;
+            *reinterpret_cast<uint4*>(ldsK + k_off(row, st_chunk)) = kreg[i];
+            *reinterpret_cast<uint4*>(ldsV + v_off(row, st_chunk)) = vreg[i];
+        }
+    };
+
+    f32x16 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
+    float m = -INFINITY, l = 0.f;
+
+    load_tile(0);
+    store_tile();
+    __syncthreads();
+
+    const int wave_last_q = qblock + 32 * w + 31;
+    for (int t = 0; t < ntiles; ++t) {
+        if (t + 1 < ntiles) load_tile(t + 1);
+        const int kv0 = t * BN;
+        if (kv0 <= wave_last_q) {  // wave-uniform: tiles wholly above the diagonal are skipped
+            f32x16 sacc[2];
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) {
+                sacc[kt] = f32x16{};
+                const int row = kt * 32 + r32;
+#pragma unroll
+                for (int ks = 0; ks < 8; ++ks) {
+                    const uint4 kv = *reinterpret_cast<const uint4*>(ldsK + k_off(row, 2 * ks + half));
+                    sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kv), qf[ks], sacc[kt], 0, 0, 0);
+                }
+            }
+            // mask + row max (key index of reg i: kt*32 + (i&3) + 8(i>>2) + 4half)
+            float mt = -INFINITY;
+            const bool need_mask = (kv0 + BN - 1 > qblock + 32 * w) || (kv0 + BN > len);
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    float sv = sacc[kt][i] * scale_log2;
+                    if (need_mask) {
+                        const int key = kv0 + kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * half;
+                        if (key > qi || key >= len) sv = -INFINITY;
+                    }
+                    sacc[kt][i] = sv;
+                    mt = fmaxf(mt, sv);
+                }
+            }
+            mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+            const float mn = fmaxf(m, mt);
+            const float alpha = exp2f(m - mn);  // m == -inf only before the first tile (key 0 is valid)
+            m = mn;
+            float ls = 0.f;
+            bf16x8 pf[2][2];
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float p = exp2f(sacc[kt][i] - mn);
+                    ls += p;
+                    pf[kt][i >> 3][i & 7] = (bf16)p;
+                }
+            }
+            l = l * alpha + ls;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+            // O^T[d][q] += V^T[d][key] P^T[key][q]
+            const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const int col = dt * 32 + 16 * (g & 1) + 4 * p4;  // this lane's address column
+                const int chunk = col >> 3, inoff = (col & 7) * 2;
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const int rowa = kt * 32 + 16 * s + 4 * (g >> 1) + q4;
+                        const int rowb = rowa + 8;
+                        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (lds_v4s*)(ldsV + v_off(rowa, chunk) + inoff));
+                        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (lds_v4s*)(ldsV + v_off(rowb, chunk) + inoff));
+                        typedef short v8s __attribute__((ext_vector_type(8)));
+                        const v8s a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), pf[kt][s],
+                                                                        o[dt], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        if (t + 1 < ntiles) {
+            store_tile();
+            __syncthreads();
+        }
+    }
+
+    // normalise and store: reg i of tile dt holds d = dt*32 + (i&3) + 8(i>>2) + 4half for query qi
+    const float lt = l + __shfl_xor(l, 32, 64);
+    if (qi < len) {
+        const float inv = 1.f / lt;
+        bf16* op = out + (size_t)(s0 + qi) * out_stride + h * D;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+            for (int g4 = 0; g4 < 4; ++g4) {
+                const int d = dt * 32 + 8 * g4 + 4 * half;
+                uint2 v;
+                v.x = pack2(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv);
+                v.y = pack2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
+                *reinterpret_cast<uint2*>(op + d) = v;
+            }
+        }
+    }
+}
+
+MRSUM_API int mrsum_attn_prefill(const void* qkv, int row_stride, const int* cu_seqlens, const int* items,
+                                 int n_items, void* out, int out_stride, int Hq, int Hkv, int Dh, float scale,
+                                 hipStream_t s) {
+    if (n_items <= 0) return 0;
+    if (Dh != D || Hq % Hkv) return (int)hipErrorInvalidValue;
+    dim3 grid(n_items, Hq), block(256);
+    attn_prefill_kernel<<<grid, block, 0, s>>>((const bf16*)qkv, row_stride, cu_seqlens, (const int2*)items,
+                                               (bf16*)out, out_stride, Hq, Hkv, scale * 1.4426950408889634f);
+    return (int)hipGetLastError();
+}

@@ -1,0 +1,79 @@
+// RMSNorm and fused residual-add + RMSNorm.
+//
+//   rmsnorm:      out = x * rsqrt(mean(x^2) + eps) * w
+//   add_rmsnorm:  residual = x + residual (stored bf16, the rounded value is
+//                 what gets normalised); out = rmsnorm(residual) * w
+//
+// One 256-thread block per row; each lane holds VPT 16-byte vectors of the
+// row in registers, so the row is read once and written once (memory bound:
+// 2-3 x D x 2 bytes per row).  D % 8 == 0 and D <= 256*8*VPT.
+#include "common.h"
+
+template <int VPT, bool ADD>
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16* __restrict__ x, bf16* __restrict__ residual,
+                                                      const bf16* __restrict__ w, bf16* __restrict__ out,
+                                                      int D, int x_stride, int out_stride, float eps) {
+    __shared__ float red[16];
+    const int row = blockIdx.x;
+    const int nvec = D >> 3;
+    const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * x_stride);
+    uint4* rr = ADD ? reinterpret_cast<uint4*>(residual + (size_t)row * D) : nullptr;
+    float v[VPT][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int c = threadIdx.x + i * 256;
+        if (c < nvec) {
+            unpack8(xr[c], v[i]);
+            if (ADD) {
+                float r[8];
+                unpack8(rr[c], r);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[i][j] = (float)(bf16)(v[i][j] + r[j]);
+                rr[c] = pack8(v[i]);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+        }
+    }
+    ss = block_sum(ss, red);
+    const float inv = rsqrtf(ss / (float)D + eps);
+    const uint4* wr = reinterpret_cast<const uint4*>(w);
+    uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * out_stride);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int c = threadIdx.x + i * 256;
+        if (c < nvec) {
+            float wf[8];
+            unpack8(wr[c], wf);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[i][j] = v[i][j] * inv * wf[j];
+            orow[c] = pack8(v[i]);
+        }
+    }
+}
+
+template <bool ADD>
+static int launch_rmsnorm(const void* x, void* residual, const void* w, void* out, int T, int D, int x_stride,
+                          int out_stride, float eps, hipStream_t s) {
+    if (T <= 0) return 0;
+    if (D % 8 || D > 256 * 8 * 8) return (int)hipErrorInvalidValue;
+    const int vpt = ceil_div(D / 8, 256);
+    dim3 g(T), b(256);
+    auto X = (const bf16*)x; auto R = (bf16*)residual; auto W = (const bf16*)w; auto O = (bf16*)out;
+    if (vpt <= 1) rmsnorm_kernel<1, ADD><<<g, b, 0, s>>>(X, R, W, O, D, x_stride, out_stride, eps);
+    else if (vpt <= 2) rmsnorm_kernel<2, ADD><<<g, b, 0, s>>>(X, R, W, O, D, x_stride, out_stride, eps);
+    else if (vpt <= 4) rmsnorm_kernel<4, ADD><<<g, b, 0, s>>>(X, R, W, O, D, x_stride, out_stride, eps);
+    else rmsnorm_kernel<8, ADD><<<g, b, 0, s>>>(X, R, W, O, D, x_stride, out_stride, eps);
+    return (int)hipGetLastError();
+}
+
+MRSUM_API int mrsum_rmsnorm(const void* x, const void* w, void* out, int T, int D, int x_stride, int out_stride,
+                            float eps, hipStream_t s) {
+    return launch_rmsnorm<false>(x, nullptr, w, out, T, D, x_stride, out_stride, eps, s);
+}
+
+MRSUM_API int mrsum_add_rmsnorm(const void* x, void* residual, const void* w, void* out, int T, int D,
+                                int x_stride, int out_stride, float eps, hipStream_t s) {
+    return launch_rmsnorm<true>(x, residual, w, out, T, D, x_stride, out_stride, eps, s);
+}

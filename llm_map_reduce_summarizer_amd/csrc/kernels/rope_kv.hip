@@ -1,0 +1,88 @@
+// Rotary embedding on Q and K fused with the paged KV-cache write
+// (SURVEY.md §2.6 K6).
+//
+// qkv      [T, row_stride] bf16: per token [Hq*D | Hkv*D | Hkv*D]; Q and K are
+//          rotated IN PLACE (prefill attention reads them back from here),
+//          rotated K and raw V are also scattered into the paged cache.
+// positions[T] int32, seq_idx[T] int32 (row of block_tables for the token),
+// block_tables [*, bt_stride] int32 page ids,
+// cache    K and V: [num_pages, Hkv, P, D] bf16 (one page = P consecutive
+//          positions of one kv head: 16 KiB at P=64, D=128, so a decode
+//          workgroup streams whole contiguous pages).
+// cos_sin  [max_pos, D/2] float2 (cos, sin), HF "rotate_half" pairing
+//          (i, i + D/2), precomputed on the host (no device trig).
+//
+// One 256-thread block per token; a work item is 8 rotary pairs of one head
+// (two 16-B loads, two 16-B stores) or one 16-B V vector.
+#include "common.h"
+
+template <int D>
+__global__ __launch_bounds__(256) void rope_kv_kernel(bf16* __restrict__ qkv, int row_stride,
+                                                      const int* __restrict__ positions,
+                                                      const int* __restrict__ seq_idx,
+                                                      const int* __restrict__ block_tables, int bt_stride,
+                                                      bf16* __restrict__ kcache, bf16* __restrict__ vcache,
+                                                      const float2* __restrict__ cos_sin, int Hq, int Hkv,
+                                                      int P, int write_cache) {
+    constexpr int HALF = D / 2;
+    constexpr int RI = HALF / 8;   // rotation items per head
+    constexpr int VI = D / 8;      // copy items per v head
+    const int t = blockIdx.x;
+    const int pos = positions[t];
+    bf16* row = qkv + (size_t)t * row_stride;
+    size_t page_base = 0;
+    if (write_cache) {
+        const int page = block_tables[(size_t)seq_idx[t] * bt_stride + pos / P];
+        page_base = (size_t)page * Hkv * P + (pos % P);
+    }
+    const float2* cs = cos_sin + (size_t)pos * HALF;
+    const int n_rot = (Hq + Hkv) * RI;
+    const int n_all = n_rot + Hkv * VI;
+    for (int it = threadIdx.x; it < n_all; it += blockDim.x) {
+        if (it < n_rot) {
+            const int h = it / RI, c = (it % RI) * 8;
+            bf16* hp = row + h * D;
+            float a[8], b[8];
+            unpack8(*reinterpret_cast<const uint4*>(hp + c), a);
+            unpack8(*reinterpret_cast<const uint4*>(hp + c + HALF), b);
+            float ra[8], rb[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float2 e = cs[c + j];
+                ra[j] = a[j] * e.x - b[j] * e.y;
+                rb[j] = b[j] * e.x + a[j] * e.y;
+            }
+            const uint4 pa = pack8(ra), pb = pack8(rb);
+            *reinterpret_cast<uint4*>(hp + c) = pa;
+            *reinterpret_cast<uint4*>(hp + c + HALF) = pb;
+            if (write_cache && h >= Hq) {
+                bf16* kp = kcache + (page_base + (size_t)(h - Hq) * P) * D;
+                *reinterpret_cast<uint4*>(kp + c) = pa;
+                *reinterpret_cast<uint4*>(kp + c + HALF) = pb;
+            }
+        } else if (write_cache) {
+            const int i = it - n_rot;
+            const int h = i / VI, c = (i % VI) * 8;
+            const uint4 v = *reinterpret_cast<const uint4*>(row + (Hq + Hkv + h) * D + c);
+            *reinterpret_cast<uint4*>(vcache + (page_base + (size_t)h * P) * D + c) = v;
+        }
+    }
+}
+
+MRSUM_API int mrsum_rope_kv(void* qkv, int T, int row_stride, const int* positions, const int* seq_idx,
+                            const int* block_tables, int bt_stride, void* kcache, void* vcache,
+                            const void* cos_sin, int Hq, int Hkv, int D, int P, int write_cache,
+                            hipStream_t s) {
+    if (T <= 0) return 0;
+    dim3 g(T), b(256);
+    auto Q = (bf16*)qkv; auto K = (bf16*)kcache; auto V = (bf16*)vcache; auto CS = (const float2*)cos_sin;
+    if (D == 128)
+        rope_kv_kernel<128><<<g, b, 0, s>>>(Q, row_stride, positions, seq_idx, block_tables, bt_stride, K, V, CS,
+                                            Hq, Hkv, P, write_cache);
+    else if (D == 64)
+        rope_kv_kernel<64><<<g, b, 0, s>>>(Q, row_stride, positions, seq_idx, block_tables, bt_stride, K, V, CS,
+                                           Hq, Hkv, P, write_cache);
+    else
+        return (int)hipErrorInvalidValue;
+    return (int)hipGetLastError();
+}

@@ -1,0 +1,60 @@
+"""Model presets for the on-node engine.
+
+The reference never runs a model locally (its map/reduce calls go to hosted
+APIs: ``llm_executor.py:250-409``); BASELINE.json names Llama-3-8B for the
+map stage and Llama-3-70B (fp8, TP=8) for the aggregator.  Shapes are the
+public Llama-3 configs; weights are random-init (seeded)
+because no checkpoints are available offline.  ``tiny*`` presets keep the
+real vocabulary and head_dim=128 (what the HIP attention kernels are built
+for) so CPU tests and GPU smoke runs exercise the same code paths.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, replace
+
+
+@dataclass(frozen=True)
+class ModelConfig:
+    name: str
+    vocab_size: int = 128256
+    hidden: int = 4096
+    n_layers: int = 32
+    n_heads: int = 32
+    n_kv_heads: int = 8
+    head_dim: int = 128
+    ffn: int = 14336
+    rope_theta: float = 500000.0
+    rms_eps: float = 1e-5
+    max_position: int = 40960
+    init_std: float = 0.02
+
+    @property
+    def qkv_dim(self) -> int:
+        return (self.n_heads + 2 * self.n_kv_heads) * self.head_dim
+
+    def n_params(self) -> int:
+        per_layer = (self.hidden * self.qkv_dim + self.n_heads * self.head_dim * self.hidden
+                     + 3 * self.hidden * self.ffn + 2 * self.hidden)
+        return self.n_layers * per_layer + 2 * self.vocab_size * self.hidden + self.hidden
+
+    def kv_bytes_per_token(self, dtype_bytes: int = 2) -> int:
+        return 2 * self.n_layers * self.n_kv_heads * self.head_dim * dtype_bytes
+
+
+PRESETS = {
+    "llama3-8b": ModelConfig("llama3-8b"),
+    "llama3-70b": ModelConfig("llama3-70b", hidden=8192, n_layers=80, n_heads=64, n_kv_heads=8, ffn=28672),
+    # test / smoke configs (real vocab, head_dim 128)
+    "tiny": ModelConfig("tiny", hidden=256, n_layers=2, n_heads=2, n_kv_heads=1, ffn=512, max_position=8192),
+    "tiny-gqa4": ModelConfig("tiny-gqa4", hidden=512, n_layers=2, n_heads=8, n_kv_heads=2, ffn=1024,
+                             max_position=8192),
+}
+
+
+def get_model_config(name: str, **overrides) -> ModelConfig:
+    key = name.lower()
+    if key not in PRESETS:
+        raise ValueError("unknown model %r (known: %s)" % (name, ", ".join(sorted(PRESETS))))
+    cfg = PRESETS[key]
+    return replace(cfg, **overrides) if overrides else cfg

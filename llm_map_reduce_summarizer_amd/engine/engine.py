@@ -1,0 +1,354 @@
+"""The on-node batched generation engine (replaces the reference's remote
+LLM call, ``llm_executor.py:232-409``).
+
+Scheduling model (continuous batching, offline batch):
+
+* A request reserves KV pages for ``prompt + max_new`` tokens at admission.
+* Prefill: waiting requests are packed (varlen, no padding) into forward
+  passes of up to ``max_prefill_tokens`` tokens; each sequence's first
+  token is sampled straight into its decode slot.
+* Decode: the active sequences occupy decode slots ``[0, n)``; a step runs
+  the model over the smallest captured batch bucket >= n.  All per-step
+  state (next ids, positions, generated tokens, stop flags) lives on the
+  device and is advanced by the sampler's finish kernel, so the host only
+  replays a captured hipGraph (``torch.cuda.CUDAGraph``) ``sync_every``
+  times, then reads the stop flags, retires finished sequences (freeing
+  their pages and compacting slots) and admits waiting ones.
+
+This is the "semaphore fan-out" of the reference re-thought for one GPU:
+every chunk of a rank is in flight at once, bounded only by HBM.
+"""
+
+from __future__ import annotations
+
+import logging
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from .. import ops
+from .config import ModelConfig
+from .kv_cache import PagedKVCache
+from .model import LlamaModel
+
+log = logging.getLogger("mrsum.engine")
+
+BUCKETS = (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 128, 160, 192, 224, 256)
+
+
+@dataclass
+class SamplingParams:
+    max_new_tokens: int = 1000
+    temperature: float = 0.3
+    seed: int = 0
+
+
+@dataclass
+class GenOutput:
+    token_ids: List[int]
+    prompt_len: int
+    finish_reason: str  # "stop" | "length"
+
+
+@dataclass
+class _Seq:
+    rid: int
+    prompt: List[int]
+    params: SamplingParams
+    pages: List[int] = field(default_factory=list)
+    slot: int = -1
+
+
+class DecodeState:
+    """Device-resident per-slot decode state (one row per decode slot)."""
+
+    def __init__(self, max_seqs: int, max_pages: int, max_new_cap: int, device, eos: Sequence[int]):
+        i32 = dict(dtype=torch.int32, device=device)
+        self.max_seqs = max_seqs
+        self.next_ids = torch.zeros(max_seqs, **i32)
+        self.positions = torch.zeros(max_seqs, **i32)
+        self.seq_idx = torch.arange(max_seqs, **i32)
+        self.block_tables = torch.zeros(max_seqs, max_pages, **i32)
+        self.gen_count = torch.zeros(max_seqs, **i32)
+        self.max_new = torch.ones(max_seqs, **i32)
+        self.out_tokens = torch.zeros(max_seqs, max_new_cap, **i32)
+        self.done = torch.ones(max_seqs, **i32)
+        self.result = torch.zeros(max_seqs, dtype=torch.int64, device=device)
+        self.temps = torch.zeros(max_seqs, dtype=torch.float32, device=device)
+        self.seeds = torch.zeros(max_seqs, dtype=torch.int64, device=device)
+        eos = list(eos)[:4]
+        self.eos = torch.tensor(eos + [-1] * (4 - len(eos)), **i32)
+        self.n_eos = len(eos)
+
+    _ROW_FIELDS = ("next_ids", "positions", "block_tables", "gen_count", "max_new", "out_tokens", "done", "result",
+                   "temps", "seeds")
+
+    def view(self, start: int, n: int) -> "DecodeState":
+        v = object.__new__(DecodeState)
+        v.max_seqs = n
+        for f in self._ROW_FIELDS:
+            setattr(v, f, getattr(self, f)[start:start + n])
+        v.seq_idx = self.seq_idx[:n]
+        v.eos, v.n_eos = self.eos, self.n_eos
+        return v
+
+    def move_row(self, src: int, dst: int) -> None:
+        for f in self._ROW_FIELDS:
+            t = getattr(self, f)
+            t[dst].copy_(t[src])
+
+    def park_row(self, i: int) -> None:
+        """Idle slot: stopped, position 0, all pages -> scratch page 0."""
+        self.done[i] = 1
+        self.positions[i] = 0
+        self.block_tables[i].zero_()
+        self.gen_count[i] = 0
+
+
+class LLMEngine:
+    def __init__(self, cfg: ModelConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0,
+                 max_num_seqs: int = 256, max_model_len: int = 16384, max_new_cap: int = 2048,
+                 kv_pages: Optional[int] = None, kv_fraction: float = 0.6, page_size: int = 64,
+                 max_prefill_tokens: int = 16384, use_graphs: bool = True, sync_every: int = 16,
+                 eos_ids: Sequence[int] = (128001, 128009), tp_rank: int = 0, tp_size: int = 1, tp_group=None):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        t0 = time.perf_counter()
+        self.model = LlamaModel(cfg, self.device, dtype, seed, tp_rank, tp_size, tp_group)
+        self.init_seconds = time.perf_counter() - t0
+        self.page = page_size
+        self.max_model_len = min(max_model_len, cfg.max_position)
+        self.max_num_seqs = min(max_num_seqs, BUCKETS[-1])
+        self.max_new_cap = max_new_cap
+        self.max_prefill_tokens = max_prefill_tokens
+        self.sync_every = max(1, sync_every)
+        if kv_pages is None:
+            if self.device.type == "cuda":
+                free, _total = torch.cuda.mem_get_info(self.device)
+                budget = int(free * kv_fraction)
+            else:
+                budget = 256 << 20
+            kv_pages = PagedKVCache.size_pages(budget, cfg.n_layers, self.model.hkv, page_size, cfg.head_dim)
+            # no point holding more than every slot at full length
+            kv_pages = min(kv_pages, 1 + self.max_num_seqs * -(-self.max_model_len // page_size))
+        self.kv = PagedKVCache(cfg.n_layers, kv_pages, self.model.hkv, page_size, cfg.head_dim, dtype, self.device)
+        self.max_pages = -(-self.max_model_len // page_size)
+        self.state = DecodeState(self.max_num_seqs, self.max_pages, max_new_cap, self.device, eos_ids)
+        self.use_graphs = use_graphs and self.device.type == "cuda"
+        self._graphs: Dict[int, "torch.cuda.CUDAGraph"] = {}
+        self._workspaces: Dict[int, object] = {}
+        self.stats = {"prefill_tokens": 0, "prefill_s": 0.0, "decode_steps": 0, "decode_tokens": 0,
+                      "decode_s": 0.0, "generate_calls": 0, "graph_captures": 0, "peak_active": 0}
+
+    # ------------------------------------------------------------------ helpers
+    def _bucket(self, n: int) -> int:
+        for b in BUCKETS:
+            if b >= n:
+                return min(b, self.max_num_seqs)
+        return self.max_num_seqs
+
+    def _workspace(self, B: int):
+        if self.device.type != "cuda":
+            return None
+        ws = self._workspaces.get(B)
+        if ws is None:
+            from ..ops.hip import DecodeWorkspace, decode_splits
+            s = decode_splits(B, self.model.hkv, self.max_model_len)
+            ws = DecodeWorkspace(B, self.model.hq, self.cfg.head_dim, s, self.device)
+            self._workspaces[B] = ws
+        return ws
+
+    def _sync(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    # ------------------------------------------------------------------ prefill
+    def _prefill(self, seqs: List[_Seq]) -> None:
+        """Pack ``seqs`` (already holding pages + slots, contiguous slots) and run one prefill."""
+        st, dev = self.state, self.device
+        ids, pos, sidx, cu, last, lens = [], [], [], [0], [], []
+        for s in seqs:
+            n = len(s.prompt)
+            ids.extend(s.prompt)
+            pos.extend(range(n))
+            sidx.extend([s.slot] * n)
+            cu.append(cu[-1] + n)
+            last.append(cu[-1] - 1)
+            lens.append(n)
+        T = len(ids)
+        h = lambda x: torch.tensor(x, dtype=torch.int32).to(dev, non_blocking=True)  # noqa: E731
+        ids_t, pos_t, sidx_t, cu_t = h(ids), h(pos), h(sidx), h(cu)
+        last_t = torch.tensor(last, dtype=torch.long).to(dev, non_blocking=True)
+        items = None
+        if dev.type == "cuda":
+            from ..ops.hip import prefill_items
+            items = prefill_items(lens).to(dev, non_blocking=True)
+        logits = self.model.prefill(ids_t, pos_t, sidx_t, cu_t, last_t, st.block_tables, self.kv.k, self.kv.v,
+                                    seqlens=lens, items=items)
+        first = seqs[0].slot
+        # sampling of the first generated token: position of the fed token = prompt_len - 1
+        v = st.view(first, len(seqs))
+        v.positions.copy_(h([n - 1 for n in lens]))
+        ops.sample(logits, v)
+        self.stats["prefill_tokens"] += T
+
+    # ------------------------------------------------------------------ decode
+    def _decode_once(self, B: int) -> None:
+        st = self.state
+        logits = self.model.decode(st.next_ids[:B], st.positions[:B], st.seq_idx[:B], st.block_tables[:B],
+                                   self.kv.k, self.kv.v, workspace=self._workspace(B))
+        ops.sample(logits, st.view(0, B))
+
+    def _decode_steps(self, B: int, steps: int) -> None:
+        if not self.use_graphs:
+            for _ in range(steps):
+                self._decode_once(B)
+            return
+        g = self._graphs.get(B)
+        if g is None:
+            g = self._capture(B)
+        for _ in range(steps):
+            g.replay()
+
+    def _capture(self, B: int):
+        # snapshot state rows the warm-up step will advance, run it eagerly once (hipBLASLt
+        # heuristics, workspace allocation), restore, then capture.
+        st = self.state
+        snap = {f: getattr(st, f)[:B].clone() for f in DecodeState._ROW_FIELDS}
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            self._decode_once(B)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        for f, t in snap.items():
+            getattr(st, f)[:B].copy_(t)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._decode_once(B)
+        # capture does not execute; restore anyway in case the backend ran the work
+        for f, t in snap.items():
+            getattr(st, f)[:B].copy_(t)
+        self._graphs[B] = g
+        self.stats["graph_captures"] += 1
+        return g
+
+    # ------------------------------------------------------------------ API
+    def generate(self, prompts: Sequence[Sequence[int]], params: Sequence[SamplingParams]) -> List[GenOutput]:
+        if len(prompts) != len(params):
+            raise ValueError("prompts and params differ in length")
+        self.stats["generate_calls"] += 1
+        results: List[Optional[GenOutput]] = [None] * len(prompts)
+        waiting: List[_Seq] = []
+        for i, (p, sp) in enumerate(zip(prompts, params)):
+            p = list(p)
+            if not p:
+                raise ValueError("empty prompt")
+            mn = max(1, min(sp.max_new_tokens, self.max_new_cap))
+            if len(p) + mn > self.max_model_len:
+                raise ValueError("prompt of %d tokens + %d new exceeds max_model_len %d"
+                                 % (len(p), mn, self.max_model_len))
+            if max(p) >= self.cfg.vocab_size or min(p) < 0:
+                raise ValueError("token id out of range")
+            waiting.append(_Seq(i, p, SamplingParams(mn, sp.temperature, sp.seed)))
+        # longest first: better packing and no late long straggler
+        waiting.sort(key=lambda s: -(len(s.prompt) + s.params.max_new_tokens))
+        active: List[_Seq] = []
+        st = self.state
+        while waiting or active:
+            admitted = self._admit(waiting, active)
+            if not active:
+                raise MemoryError("cannot admit any request: KV cache too small")
+            n = len(active)
+            self.stats["peak_active"] = max(self.stats["peak_active"], n)
+            B = self._bucket(n)
+            remaining = int((st.max_new[:n] - st.gen_count[:n]).max())
+            done_now = st.done[:n].clone()
+            steps = min(self.sync_every, max(0, remaining)) if not bool(done_now.all()) else 0
+            if steps:
+                t0 = time.perf_counter()
+                self._decode_steps(B, steps)
+                self._sync()
+                self.stats["decode_s"] += time.perf_counter() - t0
+                self.stats["decode_steps"] += steps
+            done = st.done[:n].cpu()
+            gen = st.gen_count[:n].cpu()
+            fin = [i for i in range(n) if int(done[i])]
+            if fin:
+                toks = st.out_tokens[:n].cpu()
+                for i in fin:
+                    s = active[i]
+                    g = int(gen[i])
+                    ids = toks[i, :g].tolist()
+                    reason = "length" if g >= s.params.max_new_tokens else "stop"
+                    results[s.rid] = GenOutput(ids, len(s.prompt), reason)
+                    self.stats["decode_tokens"] += g
+                    self.kv.alloc.free(s.pages)
+                self._compact(active, set(fin))
+            del admitted
+        return [r for r in results]  # type: ignore[return-value]
+
+    def _admit(self, waiting: List[_Seq], active: List[_Seq]) -> List[_Seq]:
+        st = self.state
+        batch: List[_Seq] = []
+        tokens = 0
+        while waiting and len(active) + len(batch) < self.max_num_seqs:
+            s = waiting[0]
+            need = self.kv.pages_for(len(s.prompt) + s.params.max_new_tokens)
+            if need > self.kv.alloc.available():
+                break
+            if batch and tokens + len(s.prompt) > self.max_prefill_tokens:
+                self._run_prefill(batch, active)
+                batch, tokens = [], 0
+                continue
+            waiting.pop(0)
+            s.pages = self.kv.alloc.alloc(need)
+            s.slot = len(active) + len(batch)
+            row = torch.zeros(self.max_pages, dtype=torch.int32)
+            row[:need] = torch.tensor(s.pages, dtype=torch.int32)
+            st.block_tables[s.slot].copy_(row.to(self.device, non_blocking=True))
+            st.max_new[s.slot] = s.params.max_new_tokens
+            st.gen_count[s.slot] = 0
+            st.done[s.slot] = 0
+            st.temps[s.slot] = float(s.params.temperature)
+            st.seeds[s.slot] = int(s.params.seed)
+            st.result[s.slot] = 0
+            batch.append(s)
+            tokens += len(s.prompt)
+        if batch:
+            self._run_prefill(batch, active)
+        return batch
+
+    def _run_prefill(self, batch: List[_Seq], active: List[_Seq]) -> None:
+        t0 = time.perf_counter()
+        self._prefill(batch)
+        self._sync()
+        self.stats["prefill_s"] += time.perf_counter() - t0
+        active.extend(batch)
+
+    def _compact(self, active: List[_Seq], fin: set) -> None:
+        st = self.state
+        keep = [s for i, s in enumerate(active) if i not in fin]
+        n_old = len(active)
+        for new_slot, s in enumerate(keep):
+            if s.slot != new_slot:
+                st.move_row(s.slot, new_slot)
+                s.slot = new_slot
+        for i in range(len(keep), n_old):
+            st.park_row(i)
+        active[:] = keep
+
+    def engine_stats(self) -> Dict[str, float]:
+        s = dict(self.stats)
+        s["prefill_tok_s"] = s["prefill_tokens"] / s["prefill_s"] if s["prefill_s"] else 0.0
+        s["decode_tok_s"] = s["decode_tokens"] / s["decode_s"] if s["decode_s"] else 0.0
+        s["kv_pages"] = self.kv.num_pages
+        s["weights_gib"] = self.model.weight_bytes() / 2 ** 30
+        if self.device.type == "cuda":
+            s["hbm_peak_gib"] = torch.cuda.max_memory_allocated(self.device) / 2 ** 30
+        return s

@@ -1,0 +1,111 @@
+"""Paged KV cache sized for 288 GB of HBM per GPU.
+
+Layout per layer: ``k``/``v`` [num_pages, Hkv, P, head_dim] bf16, i.e. a page
+holds P consecutive positions of ONE kv head contiguously (16 KiB at P=64,
+hd=128) -- the unit the decode-attention workgroups stream.  Page 0 is a
+scratch page: idle decode slots point at it, real sequences never do.
+
+Allocation is whole-sequence: a request reserves ceil((prompt + max_new) / P)
+pages at admission, so a captured decode graph can run many steps without
+the host touching block tables.  The free list is the native C++ allocator
+(``csrc/runtime/page_alloc.cpp``) when built, else a Python list with the
+same LIFO policy.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import logging
+from typing import List
+
+import torch
+
+from ..ops._lib import runtime_lib
+
+log = logging.getLogger("mrsum.kv")
+
+
+class PageAllocator:
+    def __init__(self, num_pages: int):
+        self.num_pages = num_pages
+        self._lib = runtime_lib(required=False)
+        self._h = None
+        if self._lib is not None and hasattr(self._lib, "mrsum_pages_create"):
+            L = self._lib
+            L.mrsum_pages_create.restype = ctypes.c_void_p
+            L.mrsum_pages_create.argtypes = [ctypes.c_int, ctypes.c_int]
+            L.mrsum_pages_alloc.restype = ctypes.c_int
+            L.mrsum_pages_alloc.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+            L.mrsum_pages_free.restype = ctypes.c_int
+            L.mrsum_pages_free.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+            L.mrsum_pages_available.restype = ctypes.c_int
+            L.mrsum_pages_available.argtypes = [ctypes.c_void_p]
+            L.mrsum_pages_destroy.argtypes = [ctypes.c_void_p]
+            self._h = L.mrsum_pages_create(num_pages, 1)
+        else:
+            self._free = list(range(num_pages - 1, 0, -1))
+
+    @property
+    def native(self) -> bool:
+        return self._h is not None
+
+    def available(self) -> int:
+        if self._h is not None:
+            return self._lib.mrsum_pages_available(self._h)
+        return len(self._free)
+
+    def alloc(self, n: int) -> List[int]:
+        if n <= 0:
+            return []
+        if self._h is not None:
+            buf = (ctypes.c_int * n)()
+            if self._lib.mrsum_pages_alloc(self._h, n, buf) != 0:
+                raise MemoryError("KV cache exhausted (%d pages requested, %d free)" % (n, self.available()))
+            return list(buf)
+        if n > len(self._free):
+            raise MemoryError("KV cache exhausted (%d pages requested, %d free)" % (n, len(self._free)))
+        out = self._free[-n:][::-1]
+        del self._free[-n:]
+        return out
+
+    def free(self, pages: List[int]) -> None:
+        if not pages:
+            return
+        if self._h is not None:
+            buf = (ctypes.c_int * len(pages))(*pages)
+            if self._lib.mrsum_pages_free(self._h, len(pages), buf) != 0:
+                raise ValueError("double free / bad page id")
+            return
+        self._free.extend(reversed(pages))
+
+    def __del__(self):
+        if getattr(self, "_h", None) is not None:
+            try:
+                self._lib.mrsum_pages_destroy(self._h)
+            except Exception:
+                pass
+            self._h = None
+
+
+class PagedKVCache:
+    def __init__(self, n_layers: int, num_pages: int, n_kv_heads: int, page: int, head_dim: int,
+                 dtype: torch.dtype, device: torch.device):
+        if num_pages < 2:
+            raise ValueError("need at least 2 KV pages (page 0 is scratch)")
+        self.page = page
+        self.num_pages = num_pages
+        shape = (n_layers, num_pages, n_kv_heads, page, head_dim)
+        self.k = torch.empty(shape, dtype=dtype, device=device)
+        self.v = torch.empty(shape, dtype=dtype, device=device)
+        self.alloc = PageAllocator(num_pages)
+        log.info("KV cache: %d pages x %d tokens (%.1f GiB)", num_pages, page,
+                 2 * self.k.numel() * self.k.element_size() / 2 ** 30)
+
+    def pages_for(self, n_tokens: int) -> int:
+        return -(-n_tokens // self.page)
+
+    @staticmethod
+    def size_pages(bytes_budget: int, n_layers: int, n_kv_heads: int, page: int, head_dim: int,
+                   dtype_bytes: int = 2) -> int:
+        per_page = 2 * n_layers * n_kv_heads * page * head_dim * dtype_bytes
+        return max(2, bytes_budget // per_page)

@@ -1,0 +1,175 @@
+"""Llama-3 forward pass for the on-node engine (prefill and decode).
+
+Weights are random-init and seeded per tensor (the benchmark setting: no
+checkpoints offline), generated full-size and then sliced for tensor
+parallelism so a model is bit-identical for every TP degree.  Fused layouts:
+
+* ``wqkv`` [(Hq + 2 Hkv) * hd / tp, hidden]: this rank's Q heads, K heads, V heads
+* ``wo``   [hidden, Hq * hd / tp]           (row-parallel, all-reduced)
+* ``wgu``  [2 * ffn / tp, hidden]            ([gate shard; up shard], one GEMM)
+* ``wdown``[hidden, ffn / tp]                (row-parallel, all-reduced)
+* ``lm_head`` [vocab / tp, hidden]           (vocab-parallel, logits all-gathered)
+
+One residual block (both phases)::
+
+    qkv = x @ wqkv^T                 hipBLASLt GEMM
+    rope_kv(qkv -> Q,K rotated; K,V -> paged cache)     HIP
+    a   = attention(qkv)             HIP: flash prefill | paged split-K decode
+    o   = a @ wo^T  (+ TP all-reduce over RCCL)
+    x   = add_rmsnorm(o, residual)   HIP (residual += o, fused)
+    gu  = x @ wgu^T ; act = swiglu(gu) (HIP) ; dn = act @ wdown^T (+ all-reduce)
+    x   = add_rmsnorm(dn, residual, next norm weight)   HIP
+"""
+
+from __future__ import annotations
+
+import hashlib
+import math
+from dataclasses import dataclass
+from typing import Callable, List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from .. import ops
+from ..ops.reference import rope_cos_sin
+from .config import ModelConfig
+
+
+def _seed_for(seed: int, name: str) -> int:
+    return int.from_bytes(hashlib.sha1(("%d:%s" % (seed, name)).encode()).digest()[:8], "little") & ((1 << 63) - 1)
+
+
+def _randn(shape, std: float, seed: int, name: str, device, dtype) -> torch.Tensor:
+    g = torch.Generator(device=device)
+    g.manual_seed(_seed_for(seed, name))
+    t = torch.randn(*shape, generator=g, device=device, dtype=torch.float32 if device.type == "cpu" else dtype)
+    t.mul_(std)
+    return t.to(dtype)
+
+
+@dataclass
+class LayerWeights:
+    ln1: torch.Tensor
+    wqkv: torch.Tensor
+    wo: torch.Tensor
+    ln2: torch.Tensor
+    wgu: torch.Tensor
+    wdown: torch.Tensor
+
+
+class LlamaModel:
+    def __init__(self, cfg: ModelConfig, device: torch.device, dtype: torch.dtype = torch.bfloat16, seed: int = 0,
+                 tp_rank: int = 0, tp_size: int = 1, tp_group=None):
+        if cfg.n_heads % tp_size or cfg.n_kv_heads % tp_size or cfg.ffn % tp_size or cfg.vocab_size % tp_size:
+            raise ValueError("%s does not shard over tp=%d" % (cfg.name, tp_size))
+        self.cfg, self.device, self.dtype = cfg, torch.device(device), dtype
+        self.tp_rank, self.tp_size, self.tp_group = tp_rank, tp_size, tp_group
+        self.hq, self.hkv, self.hd = cfg.n_heads // tp_size, cfg.n_kv_heads // tp_size, cfg.head_dim
+        self.ffn_local = cfg.ffn // tp_size
+        self.vocab_local = cfg.vocab_size // tp_size
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        self._init_weights(seed)
+        self.cos_sin = rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, self.device)
+
+    # ------------------------------------------------------------------ weights
+    def _init_weights(self, seed: int) -> None:
+        c, dev, dt = self.cfg, self.device, self.dtype
+        std = c.init_std
+        r, tp, hd = self.tp_rank, self.tp_size, c.head_dim
+        ones = lambda: torch.ones(c.hidden, device=dev, dtype=dt)  # noqa: E731
+        self.embed = _randn((c.vocab_size, c.hidden), std, seed, "embed", dev, dt)
+        self.layers: List[LayerWeights] = []
+        for i in range(c.n_layers):
+            wq = _randn((c.n_heads * hd, c.hidden), std, seed, "l%d.wq" % i, dev, dt)
+            wk = _randn((c.n_kv_heads * hd, c.hidden), std, seed, "l%d.wk" % i, dev, dt)
+            wv = _randn((c.n_kv_heads * hd, c.hidden), std, seed, "l%d.wv" % i, dev, dt)
+            qs, ks = self.hq * hd, self.hkv * hd
+            wqkv = torch.cat([wq[r * qs:(r + 1) * qs], wk[r * ks:(r + 1) * ks], wv[r * ks:(r + 1) * ks]]).contiguous()
+            del wq, wk, wv
+            wo = _randn((c.hidden, c.n_heads * hd), std, seed, "l%d.wo" % i, dev, dt)
+            wo = wo[:, r * qs:(r + 1) * qs].contiguous()
+            f = self.ffn_local
+            wg = _randn((c.ffn, c.hidden), std, seed, "l%d.wg" % i, dev, dt)
+            wu = _randn((c.ffn, c.hidden), std, seed, "l%d.wu" % i, dev, dt)
+            wgu = torch.cat([wg[r * f:(r + 1) * f], wu[r * f:(r + 1) * f]]).contiguous()
+            del wg, wu
+            wd = _randn((c.hidden, c.ffn), std, seed, "l%d.wd" % i, dev, dt)
+            wd = wd[:, r * f:(r + 1) * f].contiguous()
+            self.layers.append(LayerWeights(ones(), wqkv, wo, ones(), wgu, wd))
+        self.final_norm = ones()
+        lm = _randn((c.vocab_size, c.hidden), std, seed, "lm_head", dev, dt)
+        v = self.vocab_local
+        self.lm_head = lm[r * v:(r + 1) * v].contiguous()
+        del lm
+
+    def weight_bytes(self) -> int:
+        n = self.embed.numel() + self.lm_head.numel() + self.final_norm.numel()
+        for lw in self.layers:
+            n += sum(t.numel() for t in (lw.ln1, lw.wqkv, lw.wo, lw.ln2, lw.wgu, lw.wdown))
+        return n * self.embed.element_size()
+
+    # ------------------------------------------------------------------ comm
+    def _all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+        if self.tp_size > 1:
+            torch.distributed.all_reduce(t, group=self.tp_group)
+        return t
+
+    def _gather_vocab(self, logits: torch.Tensor) -> torch.Tensor:
+        if self.tp_size == 1:
+            return logits
+        parts = [torch.empty_like(logits) for _ in range(self.tp_size)]
+        torch.distributed.all_gather(parts, logits.contiguous(), group=self.tp_group)
+        return torch.cat(parts, dim=-1)
+
+    # ------------------------------------------------------------------ forward
+    def run_layers(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor,
+                   block_tables: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
+                   attention: Callable[[int, torch.Tensor], torch.Tensor]) -> torch.Tensor:
+        """Embedding -> all layers -> final norm; returns normed hidden [T, hidden]."""
+        c = self.cfg
+        residual = ops.embed(ids, self.embed)
+        x = ops.rmsnorm(residual, self.layers[0].ln1, c.rms_eps)
+        page = kcache.shape[3]
+        n = len(self.layers)
+        for i, lw in enumerate(self.layers):
+            qkv = F.linear(x, lw.wqkv)
+            ops.rope_kv(qkv, positions, seq_idx, block_tables, kcache[i], vcache[i], self.cos_sin, self.hq,
+                        self.hkv, self.hd, page)
+            a = attention(i, qkv)
+            o = self._all_reduce(F.linear(a, lw.wo))
+            x = ops.add_rmsnorm(o, residual, lw.ln2, c.rms_eps)
+            act = ops.swiglu(F.linear(x, lw.wgu))
+            dn = self._all_reduce(F.linear(act, lw.wdown))
+            nxt = self.layers[i + 1].ln1 if i + 1 < n else self.final_norm
+            x = ops.add_rmsnorm(dn, residual, nxt, c.rms_eps)
+        return x
+
+    def logits(self, x: torch.Tensor) -> torch.Tensor:
+        return self._gather_vocab(F.linear(x, self.lm_head))
+
+    def prefill(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, cu_seqlens: torch.Tensor,
+                last_rows: torch.Tensor, block_tables: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
+                seqlens: Optional[List[int]] = None, items: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Packed varlen prefill; returns logits of each sequence's last token [nseq, vocab]."""
+        kw = {}
+        if ids.is_cuda:
+            kw = {"seqlens": seqlens, "items": items}
+
+        def attention(i, qkv):
+            return ops.attn_prefill(qkv, cu_seqlens, self.hq, self.hkv, self.hd, self.scale, **kw)
+
+        x = self.run_layers(ids, positions, seq_idx, block_tables, kcache, vcache, attention)
+        return self.logits(x.index_select(0, last_rows))
+
+    def decode(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, block_tables: torch.Tensor,
+               kcache: torch.Tensor, vcache: torch.Tensor, workspace=None) -> torch.Tensor:
+        """One token per sequence; context = positions + 1.  Returns logits [B, vocab]."""
+        page = kcache.shape[3]
+
+        def attention(i, qkv):
+            return ops.attn_decode(qkv, kcache[i], vcache[i], block_tables, positions, self.hq, self.hkv, self.hd,
+                                   page, self.scale, workspace=workspace)
+
+        x = self.run_layers(ids, positions, seq_idx, block_tables, kcache, vcache, attention)
+        return self.logits(x)

@@ -1,0 +1,155 @@
+"""``local`` provider: the MI355X engine behind the executor / aggregator.
+
+Replaces the reference's per-chunk HTTPS calls (``llm_executor.py:250-409``;
+aggregator ``result_aggregator.py:222-253``) with ONE batched generate per
+stage, data-parallel over the ranks of the job:
+
+1. every rank holds the same request list (the CPU front-end is
+   deterministic and SPMD);
+2. requests are assigned to DP replicas by a greedy longest-processing-time
+   balance on (prompt + max_new) tokens -- no communication needed;
+3. each replica runs its share through its own engine (continuous batching:
+   every request of the replica is in flight at once);
+4. results (text + token counts) are all-gathered over RCCL
+   (``parallel.dist.all_gather_json``) so every rank ends the stage with
+   every summary, in request order.
+
+Sampling seeds are derived from the request content, so a summary does not
+depend on which rank produced it or how the batch was formed.
+"""
+
+from __future__ import annotations
+
+import hashlib
+import logging
+import time
+from typing import Any, Dict, List, Optional, Sequence
+
+from ..config import LLMConfig
+from ..parallel import dist as pdist
+from ..pipeline.providers import GenRequest, GenResult, Provider
+from .chat import render_chat
+from .tokenizer import get_tokenizer
+
+log = logging.getLogger("mrsum.local")
+
+
+def _req_seed(base: int, req: GenRequest) -> int:
+    h = hashlib.sha1(("%d|%s|%s" % (base, req.system or "", req.user)).encode("utf-8")).digest()
+    return int.from_bytes(h[:8], "little") & ((1 << 62) - 1)
+
+
+def assign_balanced(costs: Sequence[int], n_bins: int) -> List[int]:
+    """Greedy LPT: returns bin index per item; deterministic."""
+    order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
+    load = [0] * n_bins
+    out = [0] * len(costs)
+    for i in order:
+        b = min(range(n_bins), key=lambda j: (load[j], j))
+        out[i] = b
+        load[b] += costs[i]
+    return out
+
+
+class LocalEngineProvider(Provider):
+    name = "local"
+    batched = True
+
+    def __init__(self, model: str = "llama3-8b", config: Optional[LLMConfig] = None, device: Optional[str] = None,
+                 tp: int = 1, seed: Optional[int] = None, max_model_len: int = 16384, engine=None,
+                 engine_options: Optional[Dict[str, Any]] = None, dtype: Optional[str] = None,
+                 kv_fraction: Optional[float] = None, use_graphs: bool = True, max_num_seqs: Optional[int] = None,
+                 tokenizer: Optional[str] = None, **_ignored):
+        super().__init__(model, config)
+        self.tokenizer = get_tokenizer(tokenizer)
+        if dtype not in (None, "bf16"):
+            raise NotImplementedError("dtype %s is not supported by the local engine yet" % dtype)
+        self.tp = tp
+        self.seed = self.config.ENGINE_SEED if seed is None else seed
+        self.max_model_len = max_model_len
+        self._engine = engine
+        self._device = device
+        self._engine_options = dict(engine_options or {})
+        self._engine_options.setdefault("use_graphs", use_graphs)
+        if kv_fraction is not None:
+            self._engine_options.setdefault("kv_fraction", kv_fraction)
+        if max_num_seqs is not None:
+            self._engine_options.setdefault("max_num_seqs", max_num_seqs)
+        self.timings: Dict[str, float] = {"generate_s": 0.0, "allgather_s": 0.0}
+        self.par = pdist.setup_parallel(tp)
+
+    # ------------------------------------------------------------------ engine
+    @property
+    def engine(self):
+        if self._engine is None:
+            import torch
+            from .config import get_model_config
+            from .engine import LLMEngine
+            if self._device is None:
+                self._device = ("cuda:%d" % (self.par.local_rank % max(1, torch.cuda.device_count()))
+                                if torch.cuda.is_available() else "cpu")
+            opts = dict(max_model_len=self.max_model_len, max_num_seqs=self.config.ENGINE_MAX_NUM_SEQS,
+                        kv_fraction=self.config.ENGINE_KV_FRACTION, eos_ids=self.tokenizer.eos_ids)
+            opts.update(self._engine_options)
+            self._engine = LLMEngine(get_model_config(self.model), device=self._device, seed=self.seed,
+                                     tp_rank=self.par.tp_rank, tp_size=self.par.tp, tp_group=self.par.tp_group,
+                                     **opts)
+            log.info("local engine up: %s on %s (tp=%d, dp=%d) in %.1f s", self.model, self._device, self.par.tp,
+                     self.par.dp, self._engine.init_seconds)
+        return self._engine
+
+    def encode_request(self, req: GenRequest) -> List[int]:
+        ids = render_chat(self.tokenizer, req.user, req.system)
+        budget = self.max_model_len - max(1, req.max_tokens)
+        if len(ids) > budget:
+            log.warning("prompt of %d tokens truncated to %d (max_model_len %d)", len(ids), budget,
+                        self.max_model_len)
+            ids = ids[:budget - 5] + ids[-5:]  # keep the assistant header
+        return ids
+
+    # ------------------------------------------------------------------ API
+    async def generate(self, req: GenRequest) -> GenResult:
+        return (await self.generate_batch([req]))[0]
+
+    async def generate_batch(self, reqs: Sequence[GenRequest]) -> List[GenResult]:
+        from .engine import SamplingParams
+        t0 = time.perf_counter()
+        prompts = [self.encode_request(r) for r in reqs]
+        dp, dp_rank = self.par.dp, self.par.dp_rank
+        owner = assign_balanced([len(p) + r.max_tokens for p, r in zip(prompts, reqs)], dp)
+        mine = [i for i in range(len(reqs)) if owner[i] == dp_rank]
+        local: List[Dict[str, Any]] = []
+        if mine:
+            outs = self.engine.generate(
+                [prompts[i] for i in mine],
+                [SamplingParams(reqs[i].max_tokens, reqs[i].temperature, _req_seed(self.seed, reqs[i])) for i in mine])
+            for i, o in zip(mine, outs):
+                local.append({"i": i, "text": self.tokenizer.decode(o.token_ids), "pt": o.prompt_len,
+                              "ct": len(o.token_ids), "fr": o.finish_reason})
+        t1 = time.perf_counter()
+        self.timings["generate_s"] += t1 - t0
+        if self.par.world > 1:
+            gathered = pdist.all_gather_json(local)
+            # with TP, every rank of a replica holds identical results: keep the tp_rank 0 copies
+            merged = {}
+            for rank, part in enumerate(gathered):
+                if rank % self.par.tp == 0:
+                    for r in part:
+                        merged[r["i"]] = r
+        else:
+            merged = {r["i"]: r for r in local}
+        self.timings["allgather_s"] += time.perf_counter() - t1
+        results = []
+        for i in range(len(reqs)):
+            r = merged.get(i)
+            if r is None:
+                results.append(GenResult("", error="request %d produced no result" % i))
+            else:
+                results.append(GenResult(r["text"], r["pt"], r["ct"], 0.0, extra={"finish_reason": r["fr"]}))
+        return results
+
+    def stats(self) -> Dict[str, Any]:
+        s: Dict[str, Any] = {"model": self.model, "dp": self.par.dp, "tp": self.par.tp, **self.timings}
+        if self._engine is not None:
+            s.update(self._engine.engine_stats())
+        return s

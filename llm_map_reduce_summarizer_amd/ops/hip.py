@@ -1,0 +1,255 @@
+"""ctypes bindings of the gfx950 kernel library (``libmrsum_kernels.so``).
+
+Every wrapper validates shapes, dtypes, devices and strides on the host
+BEFORE launching -- a kernel never sees an operand it would index out of
+bounds (a GPU fault here can reset the whole node) -- then enqueues on the
+current torch stream.  Launchers never synchronise or allocate, so every op
+is capturable in a hipGraph (``torch.cuda.CUDAGraph``).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from ._lib import kernels_lib
+
+_c_int, _c_float, _vp = ctypes.c_int, ctypes.c_float, ctypes.c_void_p
+
+_SIGS = {
+    "mrsum_rmsnorm": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
+    "mrsum_add_rmsnorm": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
+    "mrsum_rope_kv": [_vp, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
+                      _c_int, _vp],
+    "mrsum_swiglu": [_vp, _vp, _c_int, _c_int, _vp],
+    "mrsum_embed": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _vp],
+    "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
+    "mrsum_attn_decode": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
+                          _c_int, _c_int, _c_int, _c_float, _vp],
+    "mrsum_sample": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp,
+                     _c_int, _vp],
+}
+
+_fns = {}
+
+
+def _fn(name: str):
+    f = _fns.get(name)
+    if f is None:
+        lib = kernels_lib()
+        f = getattr(lib, name)
+        f.argtypes = _SIGS[name]
+        f.restype = ctypes.c_int
+        _fns[name] = f
+    return f
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _p(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _check(rc: int, name: str) -> None:
+    if rc != 0:
+        raise RuntimeError("%s launch failed: hipError %d" % (name, rc))
+
+
+def _req(cond: bool, msg: str) -> None:
+    if not cond:
+        raise ValueError(msg)
+
+
+def _bf16_cuda(*ts: torch.Tensor) -> None:
+    for t in ts:
+        _req(t.is_cuda and t.dtype == torch.bfloat16, "expected a bf16 CUDA tensor, got %s %s" % (t.dtype, t.device))
+
+
+def _i32(*ts: torch.Tensor) -> None:
+    for t in ts:
+        _req(t.is_cuda and t.dtype == torch.int32 and t.is_contiguous(), "expected a contiguous int32 CUDA tensor")
+
+
+def _rows_ok(x: torch.Tensor) -> None:
+    _req(x.dim() == 2 and x.stride(1) == 1 and x.stride(0) % 8 == 0 and x.data_ptr() % 16 == 0,
+         "expected a 2-D row-major tensor with 16-byte aligned rows")
+
+
+# ------------------------------------------------------------------ norms
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _bf16_cuda(x, w)
+    _rows_ok(x)
+    T, D = x.shape
+    _req(w.numel() == D and w.is_contiguous() and D % 8 == 0 and D <= 16384, "rmsnorm: bad weight / D")
+    if out is None:
+        out = torch.empty(T, D, dtype=x.dtype, device=x.device)
+    _rows_ok(out)
+    _req(out.shape == (T, D), "rmsnorm: bad out shape")
+    _check(_fn("mrsum_rmsnorm")(_p(x), _p(w), _p(out), T, D, x.stride(0), out.stride(0), eps, _stream()),
+           "rmsnorm")
+    return out
+
+
+def add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _bf16_cuda(x, residual, w)
+    _rows_ok(x)
+    T, D = x.shape
+    _req(residual.shape == (T, D) and residual.is_contiguous(), "add_rmsnorm: residual must be [T, D] contiguous")
+    _req(w.numel() == D and D % 8 == 0 and D <= 16384, "add_rmsnorm: bad weight / D")
+    if out is None:
+        out = torch.empty(T, D, dtype=x.dtype, device=x.device)
+    _rows_ok(out)
+    _check(_fn("mrsum_add_rmsnorm")(_p(x), _p(residual), _p(w), _p(out), T, D, x.stride(0), out.stride(0), eps,
+                                    _stream()), "add_rmsnorm")
+    return out
+
+
+# ------------------------------------------------------------------ rope + kv
+def rope_kv(qkv: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, block_tables: torch.Tensor,
+            kcache: Optional[torch.Tensor], vcache: Optional[torch.Tensor], cos_sin: torch.Tensor,
+            hq: int, hkv: int, d: int, page: int, write_cache: bool = True, check_bounds: bool = False) -> None:
+    _bf16_cuda(qkv)
+    _rows_ok(qkv)
+    T = qkv.shape[0]
+    if T == 0:
+        return
+    _req(qkv.shape[1] >= (hq + 2 * hkv) * d and d in (64, 128), "rope_kv: qkv too narrow / bad head dim")
+    _i32(positions, seq_idx, block_tables)
+    _req(positions.numel() >= T and seq_idx.numel() >= T, "rope_kv: positions/seq_idx shorter than T")
+    _req(cos_sin.is_cuda and cos_sin.dtype == torch.float32 and cos_sin.is_contiguous()
+         and cos_sin.shape[1:] == (d // 2, 2), "rope_kv: cos_sin must be [max_pos, D/2, 2] fp32")
+    if write_cache:
+        _bf16_cuda(kcache, vcache)
+        _req(kcache.is_contiguous() and vcache.is_contiguous() and kcache.shape == vcache.shape
+             and tuple(kcache.shape[1:]) == (hkv, page, d), "rope_kv: cache must be [pages, Hkv, P, D]")
+        _req(block_tables.dim() == 2, "rope_kv: block_tables must be 2-D")
+    if check_bounds:  # host sync; used by tests and prefill (positions live on the host there anyway)
+        pmax = int(positions[:T].max())
+        _req(pmax < cos_sin.shape[0], "rope_kv: position %d beyond rope table" % pmax)
+        if write_cache:
+            _req(pmax // page < block_tables.shape[1], "rope_kv: position beyond block table")
+            _req(int(seq_idx[:T].max()) < block_tables.shape[0] and int(seq_idx[:T].min()) >= 0, "rope_kv: seq_idx")
+    _check(_fn("mrsum_rope_kv")(_p(qkv), T, qkv.stride(0), _p(positions), _p(seq_idx), _p(block_tables),
+                                block_tables.stride(0), _p(kcache) if write_cache else None,
+                                _p(vcache) if write_cache else None, _p(cos_sin), hq, hkv, d, page,
+                                1 if write_cache else 0, _stream()), "rope_kv")
+
+
+# ------------------------------------------------------------------ activations
+def swiglu(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _bf16_cuda(gu)
+    _req(gu.dim() == 2 and gu.is_contiguous() and gu.shape[1] % 16 == 0, "swiglu: gu must be [T, 2F], F % 8 == 0")
+    T, F = gu.shape[0], gu.shape[1] // 2
+    if out is None:
+        out = torch.empty(T, F, dtype=gu.dtype, device=gu.device)
+    _req(out.is_contiguous() and out.shape == (T, F), "swiglu: bad out")
+    _check(_fn("mrsum_swiglu")(_p(gu), _p(out), T, F, _stream()), "swiglu")
+    return out
+
+
+def embed(ids: torch.Tensor, table: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _i32(ids)
+    _bf16_cuda(table)
+    _req(table.is_contiguous() and table.shape[1] % 8 == 0, "embed: table must be [V, D] contiguous")
+    T = ids.numel()
+    V, D = table.shape
+    if out is None:
+        out = torch.empty(T, D, dtype=table.dtype, device=table.device)
+    _req(out.is_contiguous() and out.shape == (T, D), "embed: bad out")
+    _check(_fn("mrsum_embed")(_p(ids), _p(table), _p(out), T, D, V, _stream()), "embed")
+    return out
+
+
+# ------------------------------------------------------------------ attention
+def prefill_items(seqlens, block_m: int = 128) -> torch.Tensor:
+    """(sequence, query-block start) work list, heaviest (latest) blocks first."""
+    items = []
+    for s, n in enumerate(seqlens):
+        for qb in range(0, int(n), block_m):
+            items.append((qb, s))
+    items.sort(key=lambda x: -x[0])
+    return torch.tensor([(s, qb) for qb, s in items], dtype=torch.int32).reshape(-1, 2)
+
+
+def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int, d: int, scale: float,
+                 out: Optional[torch.Tensor] = None, items: Optional[torch.Tensor] = None,
+                 seqlens=None) -> torch.Tensor:
+    _bf16_cuda(qkv)
+    _rows_ok(qkv)
+    _req(d == 128 and hq % hkv == 0 and qkv.shape[1] >= (hq + 2 * hkv) * d, "attn_prefill: bad head config")
+    _i32(cu_seqlens)
+    T = qkv.shape[0]
+    if seqlens is None:
+        cu = cu_seqlens.cpu().tolist()
+        seqlens = [b - a for a, b in zip(cu[:-1], cu[1:])]
+        _req(cu[0] == 0 and cu[-1] <= T and all(n >= 0 for n in seqlens), "attn_prefill: bad cu_seqlens")
+    if items is None:
+        items = prefill_items(seqlens).to(qkv.device)
+    _i32(items)
+    if out is None:
+        out = torch.empty(T, hq * d, dtype=qkv.dtype, device=qkv.device)
+    _rows_ok(out)
+    _req(out.shape[0] >= T and out.shape[1] >= hq * d, "attn_prefill: bad out")
+    _check(_fn("mrsum_attn_prefill")(_p(qkv), qkv.stride(0), _p(cu_seqlens), _p(items), items.shape[0], _p(out),
+                                     out.stride(0), hq, hkv, d, scale, _stream()), "attn_prefill")
+    return out
+
+
+def decode_splits(batch: int, hkv: int, max_ctx: int, target_wgs: int = 2048) -> int:
+    s = max(1, -(-target_wgs // max(1, batch * hkv)))
+    s = min(s, 64, max(1, -(-max_ctx // 64)))
+    return s
+
+
+class DecodeWorkspace:
+    """Split-K partial buffers for attn_decode (allocated once per batch bucket)."""
+
+    def __init__(self, batch: int, hq: int, d: int, splits: int, device):
+        self.splits = splits
+        self.part_o = torch.empty(batch * hq * splits * d, dtype=torch.float32, device=device)
+        self.part_ml = torch.empty(batch * hq * splits * 2, dtype=torch.float32, device=device)
+
+
+def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, block_tables: torch.Tensor,
+                positions: torch.Tensor, hq: int, hkv: int, d: int, page: int, scale: float,
+                out: Optional[torch.Tensor] = None, num_splits: Optional[int] = None,
+                workspace: Optional[DecodeWorkspace] = None) -> torch.Tensor:
+    _bf16_cuda(q, kcache, vcache)
+    _rows_ok(q)
+    B = q.shape[0]
+    _req(d == 128 and hq % hkv == 0 and (hq // hkv) in (1, 2, 4, 8) and page % 16 == 0, "attn_decode: bad config")
+    _req(tuple(kcache.shape[1:]) == (hkv, page, d) and kcache.is_contiguous() and vcache.is_contiguous(),
+         "attn_decode: cache must be [pages, Hkv, P, D]")
+    _i32(block_tables, positions)
+    _req(block_tables.dim() == 2 and block_tables.shape[0] >= B and positions.numel() >= B, "attn_decode: tables")
+    if workspace is None:
+        s = num_splits or decode_splits(B, hkv, block_tables.shape[1] * page)
+        workspace = DecodeWorkspace(B, hq, d, s, q.device)
+    _req(workspace.part_o.numel() >= B * hq * workspace.splits * d, "attn_decode: workspace too small")
+    if out is None:
+        out = torch.empty(B, hq * d, dtype=q.dtype, device=q.device)
+    _rows_ok(out)
+    _check(_fn("mrsum_attn_decode")(_p(q), q.stride(0), _p(kcache), _p(vcache), _p(block_tables),
+                                    block_tables.stride(0), _p(positions), _p(workspace.part_o),
+                                    _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
+                                    workspace.splits, scale, _stream()), "attn_decode")
+    return out
+
+
+# ------------------------------------------------------------------ sampler
+def sample(logits: torch.Tensor, st) -> None:
+    """Sample one token per row of ``logits`` into decode state ``st`` (see engine.state)."""
+    _bf16_cuda(logits)
+    _rows_ok(logits)
+    B, V = logits.shape
+    _req(st.temps.numel() >= B and st.next_ids.numel() >= B and st.out_tokens.shape[0] >= B,
+         "sample: state smaller than batch")
+    _check(_fn("mrsum_sample")(_p(logits), logits.stride(0), B, V, _p(st.temps), _p(st.seeds), _p(st.positions),
+                               _p(st.result), _p(st.next_ids), _p(st.positions), _p(st.gen_count), _p(st.max_new),
+                               _p(st.out_tokens), st.out_tokens.stride(0), _p(st.done), _p(st.eos), st.n_eos,
+                               _stream()), "sample")

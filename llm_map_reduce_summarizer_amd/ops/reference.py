@@ -1,0 +1,210 @@
+"""Plain-PyTorch reference implementations of every engine op.
+
+These are (1) the numerics oracle the HIP kernels are tested against
+(fp32 math, same data layouts, same masking rules) and (2) the compute path
+on CPU-only hosts, where the tiny test models run.  On a GPU the engine uses
+``ops.hip`` exclusively (see ``ops/__init__.py``).
+
+Layouts shared with the kernels (``csrc/kernels/*.hip``):
+
+* ``qkv`` [T, (Hq + 2 Hkv) * D]: Q heads, then K heads, then V heads.
+* KV cache per layer: ``kcache``/``vcache`` [num_pages, Hkv, P, D];
+  token at position ``p`` of a sequence lives in page
+  ``block_tables[row, p // P]`` at offset ``p % P``.
+* ``cos_sin`` [max_pos, D/2, 2] fp32 (cos, sin), HF rotate-half pairing.
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+
+LOG2E = 1.4426950408889634
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    xf = x.float()
+    y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+    y = y.to(x.dtype)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    residual.copy_((x.float() + residual.float()).to(residual.dtype))
+    return rmsnorm(residual, w, eps, out)
+
+
+def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None) -> torch.Tensor:
+    inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    t = torch.arange(max_pos, dtype=torch.float64)
+    ang = torch.outer(t, inv)
+    return torch.stack([ang.cos(), ang.sin()], dim=-1).float().contiguous().to(device)
+
+
+def rope_kv(qkv: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, block_tables: torch.Tensor,
+            kcache: Optional[torch.Tensor], vcache: Optional[torch.Tensor], cos_sin: torch.Tensor,
+            hq: int, hkv: int, d: int, page: int, write_cache: bool = True) -> None:
+    T = qkv.shape[0]
+    if T == 0:
+        return
+    half = d // 2
+    pos = positions[:T].long()
+    cs = cos_sin[pos]  # [T, half, 2]
+    cos, sin = cs[..., 0][:, None, :], cs[..., 1][:, None, :]
+    qk = qkv[:, : (hq + hkv) * d].view(T, hq + hkv, d).float()
+    a, b = qk[..., :half], qk[..., half:]
+    ra = a * cos - b * sin
+    rb = b * cos + a * sin
+    rot = torch.cat([ra, rb], dim=-1).to(qkv.dtype)
+    qkv[:, : (hq + hkv) * d] = rot.reshape(T, -1)
+    if write_cache:
+        rows = seq_idx[:T].long()
+        pages = block_tables[rows, pos // page].long()
+        offs = pos % page
+        k = rot[:, hq:]
+        v = qkv[:, (hq + hkv) * d: (hq + 2 * hkv) * d].view(T, hkv, d)
+        kcache[pages, :, offs] = k
+        vcache[pages, :, offs] = v
+
+
+def swiglu(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    f = gu.shape[-1] // 2
+    g, u = gu[..., :f].float(), gu[..., f:].float()
+    y = (g * torch.sigmoid(g) * u).to(gu.dtype)
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def embed(ids: torch.Tensor, table: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    y = table[ids.long().clamp(0, table.shape[0] - 1)]
+    if out is not None:
+        out.copy_(y)
+        return out
+    return y
+
+
+def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int, d: int, scale: float,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    T = qkv.shape[0]
+    if out is None:
+        out = torch.empty(T, hq * d, dtype=qkv.dtype, device=qkv.device)
+    cu = cu_seqlens.tolist()
+    g = hq // hkv
+    for i in range(len(cu) - 1):
+        s, e = cu[i], cu[i + 1]
+        if e <= s:
+            continue
+        n = e - s
+        q = qkv[s:e, : hq * d].view(n, hq, d).float().transpose(0, 1)
+        k = qkv[s:e, hq * d: (hq + hkv) * d].view(n, hkv, d).float().transpose(0, 1)
+        v = qkv[s:e, (hq + hkv) * d: (hq + 2 * hkv) * d].view(n, hkv, d).float().transpose(0, 1)
+        k = k.repeat_interleave(g, dim=0)
+        v = v.repeat_interleave(g, dim=0)
+        sc = torch.matmul(q, k.transpose(1, 2)) * scale
+        mask = torch.ones(n, n, dtype=torch.bool, device=qkv.device).triu(1)
+        sc.masked_fill_(mask, float("-inf"))
+        p = torch.softmax(sc, dim=-1)
+        o = torch.matmul(p, v).transpose(0, 1).reshape(n, hq * d)
+        out[s:e] = o.to(out.dtype)
+    return out
+
+
+def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, block_tables: torch.Tensor,
+                positions: torch.Tensor, hq: int, hkv: int, d: int, page: int, scale: float,
+                out: Optional[torch.Tensor] = None, num_splits: int = 1) -> torch.Tensor:
+    """q: [B, >= hq*d] (rows of the qkv buffer); context = positions + 1."""
+    B = q.shape[0]
+    if out is None:
+        out = torch.empty(B, hq * d, dtype=q.dtype, device=q.device)
+    g = hq // hkv
+    for b in range(B):
+        ctx = int(positions[b]) + 1
+        npg = (ctx + page - 1) // page
+        pages = block_tables[b, :npg].long()
+        k = kcache[pages].permute(1, 0, 2, 3).reshape(hkv, npg * page, d)[:, :ctx].float()
+        v = vcache[pages].permute(1, 0, 2, 3).reshape(hkv, npg * page, d)[:, :ctx].float()
+        qq = q[b, : hq * d].view(hkv, g, d).float()
+        sc = torch.matmul(qq, k.transpose(1, 2)) * scale
+        p = torch.softmax(sc, dim=-1)
+        o = torch.matmul(p, v).reshape(hq * d)
+        out[b] = o.to(out.dtype)
+    return out
+
+
+# ----------------------------------------------------------------- sampler
+_M1 = 0xbf58476d1ce4e5b9
+_M2 = 0x94d049bb133111eb
+_GOLD = 0x9E3779B97F4A7C15
+_TOKMUL = 0xD1B54A32D192ED03
+_U64 = (1 << 64) - 1
+
+
+def _s64(x: int) -> int:
+    x &= _U64
+    return x - (1 << 64) if x >= (1 << 63) else x
+
+
+def _lsr(x: torch.Tensor, n: int) -> torch.Tensor:
+    return (x >> n) & ((1 << (64 - n)) - 1)
+
+
+def _mix64_t(x: torch.Tensor) -> torch.Tensor:
+    x = x ^ _lsr(x, 30)
+    x = x * _s64(_M1)
+    x = x ^ _lsr(x, 27)
+    x = x * _s64(_M2)
+    x = x ^ _lsr(x, 31)
+    return x
+
+
+def gumbel_noise(seed: int, position: int, vocab: int, device=None) -> torch.Tensor:
+    """The sampler kernel's counter-based Gumbel noise for one row (fp32)."""
+    k0 = _mix64_t(torch.tensor([_s64(seed * _GOLD + position + 1)], dtype=torch.int64))
+    tok = torch.arange(vocab, dtype=torch.int64)
+    h = _mix64_t(k0 ^ (tok * _s64(_TOKMUL)))
+    u = (_lsr(h, 40).double() + 0.5) / 16777216.0
+    return (-torch.log(-torch.log(u))).float().to(device)
+
+
+def sample_tokens(logits: torch.Tensor, temps: torch.Tensor, seeds: torch.Tensor,
+                  positions: torch.Tensor) -> torch.Tensor:
+    """Gumbel-max sampling (argmax when temperature <= 0); ties -> lowest id."""
+    B, V = logits.shape
+    out = torch.empty(B, dtype=torch.int32)
+    for b in range(B):
+        row = logits[b].float().cpu()
+        t = float(temps[b])
+        if t > 0:
+            row = row / t + gumbel_noise(int(seeds[b]), int(positions[b]), V)
+        out[b] = int(torch.argmax(row))
+    return out.to(logits.device)
+
+
+def sample_finish(tokens: torch.Tensor, st) -> None:
+    """Bookkeeping identical to the finish kernel (st = engine DecodeState)."""
+    B = tokens.shape[0]
+    eos = set(int(x) for x in st.eos.tolist()[: st.n_eos])
+    for b in range(B):
+        if int(st.done[b]):
+            continue
+        tok = int(tokens[b])
+        g = int(st.gen_count[b])
+        st.out_tokens[b, g] = tok
+        st.gen_count[b] = g + 1
+        st.next_ids[b] = tok
+        if g + 1 >= int(st.max_new[b]) or tok in eos:
+            st.done[b] = 1
+        else:
+            st.positions[b] += 1
+
+
+def attention_scale(d: int) -> float:
+    return 1.0 / math.sqrt(d)
