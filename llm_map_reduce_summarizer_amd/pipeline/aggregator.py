@@ -136,7 +136,7 @@ class ResultAggregator:
                                          % (100 * i / n, 100 * (i + 1) / n)})
                 reqs.append(self._request(b, AGG_BATCH_PROMPT, meta, "reduce_l%d" % level))
             log.info("reduce level %d: %d summaries -> %d batches of <=%d", level, len(current), n, bs)
-            before = len(current)
+            before = self._total_tokens(current) if self.max_levels is None else 0
             current = await self._run(reqs, "reduce_l%d" % level)
             calls.append(n)
             if len(current) == 1:
@@ -145,8 +145,10 @@ class ResultAggregator:
             if self.max_levels is not None:
                 if len(calls) + 1 >= self.max_levels:  # the final pass is the last allowed level
                     break
-            elif self._total_tokens(current) <= self.max_tokens_per_batch or n >= before:
-                break  # recursive mode: stop once everything fits (or no progress is possible)
+            else:
+                after = self._total_tokens(current)
+                if after <= self.max_tokens_per_batch or after >= before:
+                    break  # recursive mode: stop once everything fits (or a level no longer shrinks it)
         template = prompt_template or AGG_FINAL_PROMPT
         calls.append(1)
         self.last_plan = {"levels": len(calls), "calls": calls}

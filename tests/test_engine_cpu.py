@@ -1,0 +1,149 @@
+"""Engine on the CPU (reference ops): scheduling, KV paging, sampling rules."""
+
+import math
+
+import pytest
+import torch
+
+from llm_map_reduce_summarizer_amd.engine.chat import render_chat
+from llm_map_reduce_summarizer_amd.engine.config import get_model_config
+from llm_map_reduce_summarizer_amd.engine.engine import LLMEngine, SamplingParams
+from llm_map_reduce_summarizer_amd.engine.kv_cache import PageAllocator
+from llm_map_reduce_summarizer_amd.engine.tokenizer import get_tokenizer
+from llm_map_reduce_summarizer_amd.ops import reference
+
+
+@pytest.fixture(scope="module")
+def eng():
+    return LLMEngine(get_model_config("tiny", init_std=0.05), device="cpu", max_model_len=512, max_num_seqs=8,
+                     kv_pages=64, sync_every=3, max_prefill_tokens=128)
+
+
+def _prompts(k=5):
+    return [[128000] + [(i * 31 + j * 7) % 100000 + 3 for j in range(8 + 23 * i)] for i in range(k)]
+
+
+def test_lengths_and_pages_returned(eng):
+    ps = [SamplingParams(1 + 3 * i, 0.3, i) for i in range(5)]
+    outs = eng.generate(_prompts(), ps)
+    assert [len(o.token_ids) for o in outs] == [p.max_new_tokens for p in ps]
+    assert all(o.finish_reason == "length" for o in outs)
+    assert eng.kv.alloc.available() == eng.kv.num_pages - 1
+    assert [o.prompt_len for o in outs] == [len(p) for p in _prompts()]
+
+
+def test_deterministic_and_batch_invariant(eng):
+    ps = [SamplingParams(6, 0.3, 10 + i) for i in range(5)]
+    a = eng.generate(_prompts(), ps)
+    b = eng.generate(_prompts()[::-1], ps[::-1])[::-1]
+    assert [o.token_ids for o in a] == [o.token_ids for o in b]
+
+
+def test_greedy_decode_matches_full_prefill(eng):
+    outs = eng.generate(_prompts(3), [SamplingParams(6, 0.0, 0)] * 3)
+    for p, o in zip(_prompts(3), outs):
+        nxt = eng.generate([p + o.token_ids[:-1]], [SamplingParams(1, 0.0, 0)])[0].token_ids[0]
+        assert nxt == o.token_ids[-1]
+
+
+def test_more_requests_than_slots_and_pages():
+    eng = LLMEngine(get_model_config("tiny"), device="cpu", max_model_len=256, max_num_seqs=3, kv_pages=5,
+                    page_size=64, sync_every=2)
+    prompts = [[128000] + [i + j for j in range(30)] for i in range(7)]
+    outs = eng.generate(prompts, [SamplingParams(4, 0.3, i) for i in range(7)])
+    assert all(len(o.token_ids) == 4 for o in outs)
+    assert eng.stats["peak_active"] <= 3
+
+
+def test_eos_stops(eng):
+    # force EOS: find the greedy first token of a prompt and declare it EOS
+    p = _prompts(1)
+    first = eng.generate(p, [SamplingParams(1, 0.0, 0)])[0].token_ids[0]
+    eos_backup = eng.state.eos.clone(), eng.state.n_eos
+    eng.state.eos[0] = first
+    eng.state.n_eos = 1
+    try:
+        o = eng.generate(p, [SamplingParams(10, 0.0, 0)])[0]
+    finally:
+        eng.state.eos.copy_(eos_backup[0])
+        eng.state.n_eos = eos_backup[1]
+    assert o.token_ids == [first] and o.finish_reason == "stop"
+
+
+def test_rejects_bad_requests(eng):
+    with pytest.raises(ValueError):
+        eng.generate([[1] * 600], [SamplingParams(4)])
+    with pytest.raises(ValueError):
+        eng.generate([[200000]], [SamplingParams(4)])
+    with pytest.raises(ValueError):
+        eng.generate([[]], [SamplingParams(4)])
+
+
+@pytest.mark.parametrize("native", [True, False])
+def test_page_allocator(native):
+    a = PageAllocator(10)
+    if not native and a.native:
+        a = PageAllocator.__new__(PageAllocator)
+        a.num_pages, a._lib, a._h, a._free = 10, None, None, list(range(9, 0, -1))
+    assert a.available() == 9
+    x = a.alloc(4)
+    assert 0 not in x and len(set(x)) == 4
+    with pytest.raises(MemoryError):
+        a.alloc(6)
+    a.free(x)
+    assert a.available() == 9
+    assert a.alloc(1) == [x[0]]  # LIFO reuse
+
+
+def test_native_allocator_double_free():
+    a = PageAllocator(6)
+    if not a.native:
+        pytest.skip("runtime library not built")
+    x = a.alloc(2)
+    a.free(x)
+    with pytest.raises(ValueError):
+        a.free(x)
+    with pytest.raises(ValueError):
+        a.free([0])
+
+
+def test_chat_template():
+    tok = get_tokenizer()
+    ids = render_chat(tok, "hello", "be brief")
+    assert ids[0] == 128000 and ids.count(128009) == 2 and ids[-1] != 128009
+    assert tok.decode(ids) .count("hello") == 1
+    assert render_chat(tok, "hi")[1] == 128006
+
+
+def test_decode_reference_matches_prefill_reference():
+    torch.manual_seed(0)
+    hq, hkv, d, page = 4, 2, 128, 16
+    n = 37
+    qkv = torch.randn(n, (hq + 2 * hkv) * d).to(torch.bfloat16)
+    cu = torch.tensor([0, n], dtype=torch.int32)
+    full = reference.attn_prefill(qkv, cu, hq, hkv, d, 1 / math.sqrt(d))
+    kc = torch.zeros(8, hkv, page, d, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    bt = torch.tensor([[5, 2, 7, 1]], dtype=torch.int32)
+    pos = torch.arange(n, dtype=torch.int32)
+    reference.rope_kv(qkv.clone(), pos, torch.zeros(n, dtype=torch.int32), bt, kc, vc,
+                      reference.rope_cos_sin(64, d, 1e4), hq, hkv, d, page)
+    # the same K/V rotated (prefill path uses rotated qkv): rebuild and compare last row
+    q2 = qkv.clone()
+    reference.rope_kv(q2, pos, torch.zeros(n, dtype=torch.int32), bt, kc, vc, reference.rope_cos_sin(64, d, 1e4),
+                      hq, hkv, d, page)
+    full = reference.attn_prefill(q2, cu, hq, hkv, d, 1 / math.sqrt(d))
+    last = reference.attn_decode(q2[n - 1:n], kc, vc, bt, torch.tensor([n - 1], dtype=torch.int32), hq, hkv, d,
+                                 page, 1 / math.sqrt(d))
+    assert torch.allclose(last.float(), full[n - 1:n].float(), atol=2e-2)
+
+
+def test_gumbel_sampling_statistics():
+    # Gumbel-max at temperature t samples softmax(logits / t)
+    logits = torch.tensor([[1.0, 0.0, -1.0, 0.5]]).to(torch.bfloat16)
+    counts = torch.zeros(4)
+    for s in range(2000):
+        tok = reference.sample_tokens(logits, torch.tensor([1.0]), torch.tensor([s]), torch.tensor([3]))
+        counts[int(tok)] += 1
+    p = torch.softmax(logits.float()[0], 0)
+    assert torch.allclose(counts / counts.sum(), p, atol=0.04)

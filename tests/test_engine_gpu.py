@@ -21,7 +21,7 @@ def _prompts():
 
 
 def test_native_kernels_loaded(eng):
-    import os
+    eng.generate([[128000, 5, 6, 7]], [SamplingParams(2, 0.0, 0)])
     maps = open("/proc/self/maps").read()
     assert "libmrsum_kernels.so" in maps
 

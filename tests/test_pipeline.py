@@ -1,0 +1,125 @@
+"""Map executor, reduce aggregator, orchestrator and CLI on the mock provider
+(BASELINE config 1: the reference example end-to-end on CPU, no GPU, no keys)."""
+
+import asyncio
+import json
+import os
+
+import pytest
+
+from llm_map_reduce_summarizer_amd.config import LLMConfig
+from llm_map_reduce_summarizer_amd.pipeline.aggregator import ResultAggregator
+from llm_map_reduce_summarizer_amd.pipeline.executor import LLMExecutor
+from llm_map_reduce_summarizer_amd.pipeline.orchestrator import TranscriptSummarizer
+from llm_map_reduce_summarizer_amd.pipeline.prompts import render_template
+from llm_map_reduce_summarizer_amd.pipeline.providers import GenRequest, GenResult, MockProvider, Provider
+
+
+def _cfg(**kw):
+    kw.setdefault("RETRY_DELAY", 0.0)
+    return LLMConfig(**kw)
+
+
+def _chunks(n):
+    return [{"chunk_index": i, "start_time": 60.0 * i, "end_time": 60.0 * (i + 1),
+             "text_with_context": "chunk %d text" % i, "text": "t"} for i in range(n)]
+
+
+class EchoProvider(Provider):
+    """Records requests; returns a long deterministic text to drive the reduce planner."""
+    name = "echo"
+
+    def __init__(self, words=400):
+        super().__init__("echo")
+        self.reqs = []
+        self.words = words
+
+    async def generate(self, req):
+        self.reqs.append(req)
+        return GenResult(" ".join(["word%d" % (i % 50) for i in range(self.words)]), 10, self.words)
+
+
+def test_executor_schema_and_counters():
+    ex = LLMExecutor(config=_cfg(), provider="mock")
+    out = asyncio.run(ex.process_chunks(_chunks(4)[::-1], "Summarize: {transcript} ({summary_type})",
+                                        system_prompt="sys"))
+    assert [c["chunk_index"] for c in out] == [0, 1, 2, 3]
+    for c in out:
+        assert c["summary"].startswith("[Mock Mock Response") or c["summary"].startswith("[Mock")
+        assert c["tokens_used"] == 100 and c["system_prompt"] == "sys" and "processing_index" in c
+    assert ex.total_requests == 4 and ex.failed_requests == 0 and ex.total_tokens_used == 400
+
+
+def test_executor_retries_then_error_summary():
+    ex = LLMExecutor(config=_cfg(RETRY_ATTEMPTS=3), provider_obj=MockProvider(fault_rate=1.0))
+    out = asyncio.run(ex.process_chunks(_chunks(2), "{transcript}"))
+    assert all(c["summary"].startswith("[Error processing chunk: ") and "error" in c for c in out)
+    assert ex.failed_requests == 2
+    ex2 = LLMExecutor(config=_cfg(RETRY_ATTEMPTS=6), provider_obj=MockProvider(fault_rate=0.5, seed=3))
+    out2 = asyncio.run(ex2.process_chunks(_chunks(8), "{transcript}"))
+    assert sum(1 for c in out2 if "error" in c) <= 1  # transient faults are absorbed by retries
+
+
+def test_prompt_braces_do_not_crash():
+    # reference bug Q7: a stray {"a"} in a prompt file raised KeyError
+    assert render_template('json: {"a": 1} {transcript} {{x}}', transcript="T") == 'json: {"a": 1} T {x}'
+
+
+def test_aggregator_single_vs_hierarchical():
+    prov = EchoProvider(words=30)
+    ex = LLMExecutor(config=_cfg(), provider_obj=prov)
+    agg = ResultAggregator(executor=ex)
+    chunks = [dict(c, summary="short summary %d" % c["chunk_index"]) for c in _chunks(5)]
+    r = asyncio.run(agg.aggregate(chunks, metadata={"File": "x"}))
+    assert r["plan"] == {"levels": 1, "calls": [1]} and r["chunks_aggregated"] == 5
+    assert "[Time: 00:00 - 01:00]" in prov.reqs[-1].user and "File: x" in prov.reqs[-1].user
+    assert prov.reqs[-1].temperature == pytest.approx(0.2)
+
+    long = " ".join(["lorem%d ipsum" % i for i in range(450)])
+    chunks = [dict(c, summary=long) for c in _chunks(23)]
+    prov.reqs.clear()
+    r = asyncio.run(agg.aggregate(chunks))
+    n_tok = agg.tokenizer.count("[Time: 00:00 - 01:00]\n" + long)
+    bs = min(10, max(1, int(5000 / n_tok)))
+    assert r["plan"]["levels"] == 2 and r["plan"]["calls"] == [-(-23 // bs), 1]
+    assert "Batch: 1/%d" % r["plan"]["calls"][0] in prov.reqs[0].user
+
+
+def test_aggregator_recursive_mode_and_custom_prompt():
+    prov = EchoProvider(words=500)
+    ex = LLMExecutor(config=_cfg(), provider_obj=prov)
+    agg = ResultAggregator(executor=ex, max_levels=None)
+    chunks = [dict(c, summary=" ".join(["w%d" % i for i in range(1200)])) for c in _chunks(30)]
+    r = asyncio.run(agg.aggregate(chunks, prompt_template="TIMELINE SUMMARY\n{summaries}\nn={num_summaries}"))
+    assert r["plan"]["levels"] >= 3
+    assert prov.reqs[-1].user.startswith("TIMELINE SUMMARY") and "SUMMARY 1:" in prov.reqs[-1].user
+
+
+def test_orchestrator_on_reference_example(example_transcript, tmp_path):
+    s = TranscriptSummarizer(provider="mock", max_tokens_per_chunk=4000)
+    save = tmp_path / "chunks.json"
+    rep = asyncio.run(s.summarize(example_transcript, save_intermediate_chunks=str(save),
+                                  metadata={"Speaker": "x"}))
+    for k in ("summary", "processing_time", "tokens_used", "cost", "segments", "chunks", "provider", "model"):
+        assert k in rep
+    assert rep["segments"] == 4778 and rep["provider"] == "mock" and rep["chunks"] > 20
+    data = json.loads(save.read_text())
+    assert set(data) == {"timestamp", "chunks"} and len(data["chunks"]) == rep["chunks"]
+    assert set(data["chunks"][0]) == {"chunk_index", "start_time", "end_time", "summary", "tokens_used"}
+    # resume from the saved file skips the map stage
+    rep2 = asyncio.run(TranscriptSummarizer(provider="mock").summarize(example_transcript,
+                                                                        resume_chunks=str(save)))
+    assert rep2["chunks"] == rep["chunks"] and rep2["tokens_used"] == 0
+
+
+def test_cli_mock_end_to_end(example_transcript, tmp_path, capsys):
+    from llm_map_reduce_summarizer_amd.cli import main
+    inp = tmp_path / "t.json"
+    inp.write_text(json.dumps({"segments": example_transcript["segments"][:600]}))
+    out = tmp_path / "o" / "summary.md"
+    rc = main(["-i", str(inp), "-o", str(out), "--provider", "mock", "--report", "-q",
+               "--max-tokens-per-chunk", "2000"])
+    assert rc == 0 and out.read_text().startswith("# Transcript Summary")
+    rep = json.loads(out.with_suffix(".report.json").read_text())
+    assert rep["provider"] == "mock" and rep["segments"] == 600
+    assert main(["-i", str(tmp_path / "missing.json"), "--provider", "mock"]) == 1

@@ -12,7 +12,7 @@ step() {  # step <name> <timeout> <cmd...>
   echo "=== $name rc=$rc"; tail -n 5 "gpurun_out/$name.log"
   return $rc
 }
-step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider; rc=$?
+step pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider; rc=$?
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 [ "${BENCH:-1}" = "1" ] || exit 0
