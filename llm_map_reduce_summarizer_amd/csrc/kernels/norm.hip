@@ -77,3 +77,66 @@ MRSUM_API int mrsum_add_rmsnorm(const void* x, void* residual, const void* w, vo
                                 int x_stride, int out_stride, float eps, hipStream_t s) {
     return launch_rmsnorm<true>(x, residual, w, out, T, D, x_stride, out_stride, eps, s);
 }
+
+// residual += sum_s parts[s] (fp32 split-K slabs of the producing GEMM, [S, T, D]);
+// out = rmsnorm(residual) * w.  The split-K reduction of the decode GEMMs
+// (skinny_gemm EPI_F32_PARTIAL) is folded into this pass instead of costing
+// its own kernel or atomics.
+template <int VPT>
+__global__ __launch_bounds__(256) void add_rmsnorm_parts_kernel(const float* __restrict__ parts, int S,
+                                                                bf16* __restrict__ residual,
+                                                                const bf16* __restrict__ w, bf16* __restrict__ out,
+                                                                int T, int D, int out_stride, float eps) {
+    __shared__ float red[16];
+    const int row = blockIdx.x;
+    const int nvec = D >> 3;
+    uint4* rr = reinterpret_cast<uint4*>(residual + (size_t)row * D);
+    float v[VPT][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int c = threadIdx.x + i * 256;
+        if (c < nvec) {
+            unpack8(rr[c], v[i]);
+            for (int s = 0; s < S; ++s) {
+                const float4* p = reinterpret_cast<const float4*>(parts + ((size_t)s * T + row) * D + c * 8);
+                const float4 a = p[0], b = p[1];
+                v[i][0] += a.x; v[i][1] += a.y; v[i][2] += a.z; v[i][3] += a.w;
+                v[i][4] += b.x; v[i][5] += b.y; v[i][6] += b.z; v[i][7] += b.w;
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[i][j] = (float)(bf16)v[i][j];
+            rr[c] = pack8(v[i]);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ss += v[i][j] * v[i][j];
+        }
+    }
+    ss = block_sum(ss, red);
+    const float inv = rsqrtf(ss / (float)D + eps);
+    const uint4* wr = reinterpret_cast<const uint4*>(w);
+    uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * out_stride);
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int c = threadIdx.x + i * 256;
+        if (c < nvec) {
+            float wf[8];
+            unpack8(wr[c], wf);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[i][j] = v[i][j] * inv * wf[j];
+            orow[c] = pack8(v[i]);
+        }
+    }
+}
+
+MRSUM_API int mrsum_add_rmsnorm_parts(const void* parts, int S, void* residual, const void* w, void* out, int T,
+                                      int D, int out_stride, float eps, hipStream_t s) {
+    if (T <= 0) return 0;
+    if (D % 8 || D > 256 * 8 * 8 || S < 1) return (int)hipErrorInvalidValue;
+    const int vpt = ceil_div(D / 8, 256);
+    auto P = (const float*)parts; auto R = (bf16*)residual; auto W = (const bf16*)w; auto O = (bf16*)out;
+    if (vpt <= 1) add_rmsnorm_parts_kernel<1><<<T, 256, 0, s>>>(P, S, R, W, O, T, D, out_stride, eps);
+    else if (vpt <= 2) add_rmsnorm_parts_kernel<2><<<T, 256, 0, s>>>(P, S, R, W, O, T, D, out_stride, eps);
+    else if (vpt <= 4) add_rmsnorm_parts_kernel<4><<<T, 256, 0, s>>>(P, S, R, W, O, T, D, out_stride, eps);
+    else add_rmsnorm_parts_kernel<8><<<T, 256, 0, s>>>(P, S, R, W, O, T, D, out_stride, eps);
+    return (int)hipGetLastError();
+}

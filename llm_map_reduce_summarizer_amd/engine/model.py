@@ -6,7 +6,8 @@ parallelism so a model is bit-identical for every TP degree.  Fused layouts:
 
 * ``wqkv`` [(Hq + 2 Hkv) * hd / tp, hidden]: this rank's Q heads, K heads, V heads
 * ``wo``   [hidden, Hq * hd / tp]           (row-parallel, all-reduced)
-* ``wgu``  [2 * ffn / tp, hidden]            ([gate shard; up shard], one GEMM)
+* ``wgu``  [2 * ffn / tp, hidden]            (gate/up shards interleaved in blocks of
+                                             16 rows, one GEMM; see ops.reference.swiglu)
 * ``wdown``[hidden, ffn / tp]                (row-parallel, all-reduced)
 * ``lm_head`` [vocab / tp, hidden]           (vocab-parallel, logits all-gathered)
 
@@ -32,8 +33,10 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
-from ..ops.reference import rope_cos_sin
+from ..ops.reference import interleave_gate_up, rope_cos_sin
 from .config import ModelConfig
+
+SKINNY_MAX_M = 64  # decode rows served by the weight-streaming GEMMs (ops.hip.SKINNY_MAX_M)
 
 
 def _seed_for(seed: int, name: str) -> int:
@@ -92,7 +95,7 @@ class LlamaModel:
             f = self.ffn_local
             wg = _randn((c.ffn, c.hidden), std, seed, "l%d.wg" % i, dev, dt)
             wu = _randn((c.ffn, c.hidden), std, seed, "l%d.wu" % i, dev, dt)
-            wgu = torch.cat([wg[r * f:(r + 1) * f], wu[r * f:(r + 1) * f]]).contiguous()
+            wgu = interleave_gate_up(wg[r * f:(r + 1) * f], wu[r * f:(r + 1) * f]).contiguous()
             del wg, wu
             wd = _randn((c.hidden, c.ffn), std, seed, "l%d.wd" % i, dev, dt)
             wd = wd[:, r * f:(r + 1) * f].contiguous()
@@ -125,28 +128,43 @@ class LlamaModel:
     # ------------------------------------------------------------------ forward
     def run_layers(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor,
                    block_tables: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
-                   attention: Callable[[int, torch.Tensor], torch.Tensor]) -> torch.Tensor:
-        """Embedding -> all layers -> final norm; returns normed hidden [T, hidden]."""
+                   attention: Callable[[int, torch.Tensor], torch.Tensor], decode: bool = False) -> torch.Tensor:
+        """Embedding -> all layers -> final norm; returns normed hidden [T, hidden].
+
+        ``decode`` (T <= 64 rows): projections run on the MFMA weight-streaming
+        kernels with fused epilogues -- split-K fp32 slabs reduced inside
+        add_rmsnorm_parts, SwiGLU inside the gate_up GEMM.
+        """
         c = self.cfg
         residual = ops.embed(ids, self.embed)
         x = ops.rmsnorm(residual, self.layers[0].ln1, c.rms_eps)
         page = kcache.shape[3]
         n = len(self.layers)
+        fast = decode and ids.shape[0] <= SKINNY_MAX_M
         for i, lw in enumerate(self.layers):
-            qkv = F.linear(x, lw.wqkv)
+            nxt = self.layers[i + 1].ln1 if i + 1 < n else self.final_norm
+            qkv = ops.linear(x, lw.wqkv) if fast else F.linear(x, lw.wqkv)
             ops.rope_kv(qkv, positions, seq_idx, block_tables, kcache[i], vcache[i], self.cos_sin, self.hq,
                         self.hkv, self.hd, page)
             a = attention(i, qkv)
-            o = self._all_reduce(F.linear(a, lw.wo))
-            x = ops.add_rmsnorm(o, residual, lw.ln2, c.rms_eps)
-            act = ops.swiglu(F.linear(x, lw.wgu))
-            dn = self._all_reduce(F.linear(act, lw.wdown))
-            nxt = self.layers[i + 1].ln1 if i + 1 < n else self.final_norm
-            x = ops.add_rmsnorm(dn, residual, nxt, c.rms_eps)
+            if fast:
+                tp1 = self.tp_size == 1
+                parts = self._all_reduce(ops.linear_parts(a, lw.wo, None if tp1 else 1))
+                x = ops.add_rmsnorm_parts(parts, residual, lw.ln2, c.rms_eps)
+                act = ops.linear_swiglu(x, lw.wgu)
+                parts = self._all_reduce(ops.linear_parts(act, lw.wdown, None if tp1 else 1))
+                x = ops.add_rmsnorm_parts(parts, residual, nxt, c.rms_eps)
+            else:
+                o = self._all_reduce(F.linear(a, lw.wo))
+                x = ops.add_rmsnorm(o, residual, lw.ln2, c.rms_eps)
+                act = ops.swiglu(F.linear(x, lw.wgu))
+                dn = self._all_reduce(F.linear(act, lw.wdown))
+                x = ops.add_rmsnorm(dn, residual, nxt, c.rms_eps)
         return x
 
     def logits(self, x: torch.Tensor) -> torch.Tensor:
-        return self._gather_vocab(F.linear(x, self.lm_head))
+        return self._gather_vocab(ops.linear(x, self.lm_head) if x.shape[0] <= SKINNY_MAX_M else
+                                  F.linear(x, self.lm_head))
 
     def prefill(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, cu_seqlens: torch.Tensor,
                 last_rows: torch.Tensor, block_tables: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
@@ -171,5 +189,5 @@ class LlamaModel:
             return ops.attn_decode(qkv, kcache[i], vcache[i], block_tables, positions, self.hq, self.hkv, self.hd,
                                    page, self.scale, workspace=workspace)
 
-        x = self.run_layers(ids, positions, seq_idx, block_tables, kcache, vcache, attention)
+        x = self.run_layers(ids, positions, seq_idx, block_tables, kcache, vcache, attention, decode=True)
         return self.logits(x)

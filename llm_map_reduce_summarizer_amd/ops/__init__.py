@@ -48,6 +48,27 @@ def swiglu(gu, out=None):
     return _impl(gu).swiglu(gu, out)
 
 
+def linear(x, w):
+    """x @ w^T (bf16).  GPU: MFMA weight-streaming kernel for decode shapes, hipBLASLt otherwise."""
+    return _impl(x).linear(x, w)
+
+
+def linear_parts(x, w, splits=None):
+    """fp32 split-K partial slabs [S, M, N] of x @ w^T, consumed by add_rmsnorm_parts."""
+    if _use_hip(x):
+        from . import hip
+        return hip.linear_parts(x, w, splits)
+    return reference.linear_parts(x, w, splits or 1)
+
+
+def linear_swiglu(x, w_gu):
+    return _impl(x).linear_swiglu(x, w_gu)
+
+
+def add_rmsnorm_parts(parts, residual, w, eps, out=None):
+    return _impl(residual).add_rmsnorm_parts(parts, residual, w, eps, out)
+
+
 def embed(ids, table, out=None):
     return _impl(table).embed(ids, table, out)
 

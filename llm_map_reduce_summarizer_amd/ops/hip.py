@@ -28,6 +28,8 @@ _SIGS = {
     "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_attn_decode": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
                           _c_int, _c_int, _c_int, _c_float, _vp],
+    "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
+    "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_sample": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp,
                      _c_int, _vp],
 }
@@ -143,7 +145,7 @@ def rope_kv(qkv: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, b
 # ------------------------------------------------------------------ activations
 def swiglu(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     _bf16_cuda(gu)
-    _req(gu.dim() == 2 and gu.is_contiguous() and gu.shape[1] % 16 == 0, "swiglu: gu must be [T, 2F], F % 8 == 0")
+    _req(gu.dim() == 2 and gu.is_contiguous() and gu.shape[1] % 32 == 0, "swiglu: gu must be [T, 2F], F % 16 == 0")
     T, F = gu.shape[0], gu.shape[1] // 2
     if out is None:
         out = torch.empty(T, F, dtype=gu.dtype, device=gu.device)
@@ -253,3 +255,89 @@ def sample(logits: torch.Tensor, st) -> None:
                                _p(st.result), _p(st.next_ids), _p(st.positions), _p(st.gen_count), _p(st.max_new),
                                _p(st.out_tokens), st.out_tokens.stride(0), _p(st.done), _p(st.eos), st.n_eos,
                                _stream()), "sample")
+
+
+# ------------------------------------------------------------------ decode GEMMs (M <= 64)
+SKINNY_MAX_M = 64
+EPI_BF16, EPI_F32_PARTIAL, EPI_SWIGLU = 0, 1, 2
+
+
+def choose_splits(N: int, K: int, nt: int, target_wgs: int = 512, max_splits: int = 8) -> int:
+    """Smallest split-K (dividing K/128) that gives >= target_wgs workgroups."""
+    blocks = K // 128
+    base = N // (16 * nt)
+    for s in range(1, max_splits + 1):
+        if blocks % s == 0 and base * s >= target_wgs:
+            return s
+    best = 1
+    for s in range(1, max_splits + 1):
+        if blocks % s == 0:
+            best = s
+    return best
+
+
+def _skinny(x, w, out, epi, nt, splits, ldo):
+    _bf16_cuda(x, w)
+    _rows_ok(x)
+    M, K = x.shape
+    N = w.shape[0]
+    _req(w.is_contiguous() and w.shape[1] == K, "skinny_gemm: weight must be [N, K] contiguous")
+    _req(1 <= M <= SKINNY_MAX_M and K % 128 == 0 and N % (16 * nt) == 0 and (K // 128) % splits == 0,
+         "skinny_gemm: unsupported shape M=%d N=%d K=%d nt=%d S=%d" % (M, N, K, nt, splits))
+    _check(_fn("mrsum_skinny_gemm")(_p(x), x.stride(0), _p(w), N, K, M, _p(out), ldo, epi, nt, splits, _stream()),
+           "skinny_gemm")
+    return out
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """x @ w^T, bf16 out; MFMA weight-streaming kernel for M <= 64, hipBLASLt above."""
+    M = x.shape[0]
+    if M > SKINNY_MAX_M or M == 0:
+        return torch.nn.functional.linear(x, w, out=out) if out is not None else torch.nn.functional.linear(x, w)
+    N = w.shape[0]
+    nt = 2 if N % 32 == 0 and N >= 16384 else 1
+    if out is None:
+        out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+    _req(out.is_contiguous() and out.shape == (M, N), "linear: bad out")
+    return _skinny(x, w, out, EPI_BF16, nt, 1, N)
+
+
+def linear_parts(x: torch.Tensor, w: torch.Tensor, splits: Optional[int] = None,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """fp32 split-K slabs [S, M, N] of x @ w^T (summed by add_rmsnorm_parts)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if splits is None:
+        splits = choose_splits(N, K, 1)
+    if out is None:
+        out = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
+    _req(out.is_contiguous() and out.shape == (splits, M, N) and out.dtype == torch.float32, "linear_parts: bad out")
+    return _skinny(x, w, out, EPI_F32_PARTIAL, 1, splits, N)
+
+
+def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """silu(gate) * up straight out of the gate_up GEMM (blocked [16 gate | 16 up] weight rows)."""
+    M = x.shape[0]
+    F2 = w_gu.shape[0]
+    if M > SKINNY_MAX_M:
+        return swiglu(torch.nn.functional.linear(x, w_gu), out)
+    if out is None:
+        out = torch.empty(M, F2 // 2, dtype=x.dtype, device=x.device)
+    _req(out.is_contiguous() and out.shape == (M, F2 // 2), "linear_swiglu: bad out")
+    return _skinny(x, w_gu, out, EPI_SWIGLU, 2, 1, F2 // 2)
+
+
+def add_rmsnorm_parts(parts: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _req(parts.is_cuda and parts.dtype == torch.float32 and parts.is_contiguous() and parts.dim() == 3,
+         "add_rmsnorm_parts: parts must be fp32 [S, T, D]")
+    _bf16_cuda(residual, w)
+    S, T, D = parts.shape
+    _req(residual.shape == (T, D) and residual.is_contiguous() and w.numel() == D and D % 8 == 0,
+         "add_rmsnorm_parts: shapes")
+    if out is None:
+        out = torch.empty(T, D, dtype=residual.dtype, device=residual.device)
+    _rows_ok(out)
+    _check(_fn("mrsum_add_rmsnorm_parts")(_p(parts), S, _p(residual), _p(w), _p(out), T, D, out.stride(0), eps,
+                                          _stream()), "add_rmsnorm_parts")
+    return out

@@ -73,14 +73,49 @@ def rope_kv(qkv: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, b
         vcache[pages, :, offs] = v
 
 
-def swiglu(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def interleave_gate_up(wg: torch.Tensor, wu: torch.Tensor) -> torch.Tensor:
+    """[F, H] gate + [F, H] up -> [2F, H] rows in blocks of 32 = [16 gate | 16 up]."""
+    f, h = wg.shape
+    return torch.stack([wg.reshape(f // 16, 16, h), wu.reshape(f // 16, 16, h)], dim=1).reshape(2 * f, h)
+
+
+def split_gate_up(gu: torch.Tensor):
+    """Inverse of the blocked column layout of a gate_up GEMM output."""
     f = gu.shape[-1] // 2
-    g, u = gu[..., :f].float(), gu[..., f:].float()
+    v = gu.reshape(*gu.shape[:-1], f // 16, 2, 16)
+    return v[..., 0, :].reshape(*gu.shape[:-1], f), v[..., 1, :].reshape(*gu.shape[:-1], f)
+
+
+def swiglu(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    g, u = split_gate_up(gu)
+    g, u = g.float(), u.float()
     y = (g * torch.sigmoid(g) * u).to(gu.dtype)
     if out is not None:
         out.copy_(y)
         return out
     return y
+
+
+def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    return torch.nn.functional.linear(x, w)
+
+
+def linear_parts(x: torch.Tensor, w: torch.Tensor, splits: int = 1) -> torch.Tensor:
+    """fp32 split-K partial slabs [S, M, N] of x @ w^T (what skinny_gemm EPI_F32_PARTIAL emits)."""
+    K = x.shape[1]
+    ks = K // splits
+    return torch.stack([x[:, i * ks:(i + 1) * ks].float() @ w[:, i * ks:(i + 1) * ks].float().t()
+                        for i in range(splits)])
+
+
+def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor) -> torch.Tensor:
+    return swiglu(torch.nn.functional.linear(x, w_gu))
+
+
+def add_rmsnorm_parts(parts: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                      out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    residual.copy_((parts.float().sum(0) + residual.float()).to(residual.dtype))
+    return rmsnorm(residual, w, eps, out)
 
 
 def embed(ids: torch.Tensor, table: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

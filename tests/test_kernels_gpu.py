@@ -182,3 +182,51 @@ def test_sampler_eos_and_max_new():
     assert st.positions.cpu().tolist() == [10, 10]  # retired rows keep their position
     hip.sample(logits, st)  # retired rows are untouched
     assert st.gen_count.cpu().tolist() == [1, 1]
+
+
+@pytest.mark.parametrize("M", [1, 5, 16, 24, 48, 64])
+@pytest.mark.parametrize("N,K", [(6144, 4096), (256, 1024), (4096, 14336)])
+def test_skinny_linear(M, N, K):
+    x = _rand(M, K, seed=21)
+    w = _rand(N, K, scale=0.05, seed=22)
+    ref = (x.float() @ w.float().t())
+    _close(hip.linear(x, w), ref, 2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 7, 33])
+@pytest.mark.parametrize("splits", [1, 2, 4, 7])
+def test_skinny_linear_parts(M, splits):
+    N, K = 512, 3584
+    x = _rand(M, K, seed=23)
+    w = _rand(N, K, scale=0.05, seed=24)
+    parts = hip.linear_parts(x, w, splits)
+    assert parts.shape == (splits, M, N)
+    ref = reference.linear_parts(x, w, splits)
+    _close(parts, ref, 1e-3, 1e-3)
+
+
+@pytest.mark.parametrize("M", [1, 17, 64])
+def test_skinny_swiglu(M):
+    F, K = 1024, 2048
+    x = _rand(M, K, seed=25)
+    wg = _rand(F, K, scale=0.05, seed=26)
+    wu = _rand(F, K, scale=0.05, seed=27)
+    wgu = reference.interleave_gate_up(wg, wu).contiguous()
+    g, u = x.float() @ wg.float().t(), x.float() @ wu.float().t()
+    ref = g * torch.sigmoid(g) * u
+    _close(hip.linear_swiglu(x, wgu), ref, 2e-2)
+    # prefill path: hipBLASLt GEMM + blocked-layout swiglu kernel
+    _close(hip.swiglu(torch.nn.functional.linear(x, wgu)), ref, 3e-2)
+
+
+@pytest.mark.parametrize("S,T,D", [(1, 3, 4096), (4, 9, 4096), (2, 1, 8192)])
+def test_add_rmsnorm_parts(S, T, D):
+    g = torch.Generator().manual_seed(28)
+    parts = torch.randn(S, T, D, generator=g).to(DEV)
+    r = _rand(T, D, seed=29)
+    w = _rand(D, seed=30) + 1
+    r1, r2 = r.clone(), r.clone()
+    o1 = hip.add_rmsnorm_parts(parts, r1, w, 1e-5)
+    o2 = reference.add_rmsnorm_parts(parts, r2, w, 1e-5)
+    _close(r1, r2, 2e-2)
+    _close(o1, o2, 3e-2)
