@@ -1,7 +1,7 @@
 // SwiGLU activation (K7) and token-embedding gather (K9).
 //
 // swiglu:  gu [T, 2F] bf16, the fused gate+up GEMM output with its columns in
-//          blocks of 32 = [16 gate | 16 up] (the weight layout the decode GEMM's
+//          blocks of 16 = [8 gate | 8 up] (the weight layout the decode GEMM's
 //          fused SwiGLU epilogue needs); out [T, F] = silu(gate) * up,
 //          16-B vectors, grid-stride.
 // embed:   ids [T] int32 -> out [T, D] = table[ids]; one block per token,
@@ -16,10 +16,9 @@ __global__ __launch_bounds__(256) void swiglu_kernel(const bf16* __restrict__ gu
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         const size_t r = i / fv, c = i % fv;  // output features [8c, 8c+8)
         const uint4* row = reinterpret_cast<const uint4*>(gu + r * 2 * (size_t)F);
-        const size_t gv = (c >> 1) * 4 + (c & 1);  // 16-B vector index of the gate half
-        float g[8], u[8];
-        unpack8(row[gv], g);
-        unpack8(row[gv + 2], u);
+        float g[8], u[8];  // 16-B vector 2c = gate features [8c, 8c+8), 2c+1 = the matching up
+        unpack8(row[2 * c], g);
+        unpack8(row[2 * c + 1], u);
 #pragma unroll
         for (int j = 0; j < 8; ++j) g[j] = g[j] / (1.f + __expf(-g[j])) * u[j];
         reinterpret_cast<uint4*>(out + r * (size_t)F)[c] = pack8(g);
@@ -28,7 +27,7 @@ __global__ __launch_bounds__(256) void swiglu_kernel(const bf16* __restrict__ gu
 
 MRSUM_API int mrsum_swiglu(const void* gu, void* out, int T, int F, hipStream_t s) {
     if (T <= 0) return 0;
-    if (F % 16) return (int)hipErrorInvalidValue;
+    if (F % 8) return (int)hipErrorInvalidValue;
     const size_t n = (size_t)T * (F / 8);
     const int blocks = (int)std::min<size_t>((n + 255) / 256, 256 * 16);
     swiglu_kernel<<<blocks, 256, 0, s>>>((const bf16*)gu, (bf16*)out, T, F);

@@ -16,8 +16,34 @@
 // (two 16-B loads, two 16-B stores) or one 16-B V vector.
 #include "common.h"
 
-template <int D>
-__global__ __launch_bounds__(256) void rope_kv_kernel(bf16* __restrict__ qkv, int row_stride,
+// Source of one token row: the bf16 qkv row itself, or (PARTS) the sum of S
+// fp32 split-K slabs of the decode QKV GEMM -- the GEMM's split-K reduction
+// is folded into this pass.
+template <bool PARTS>
+struct RowSrc {
+    const bf16* row;     // !PARTS
+    const float* parts;  // PARTS: slab 0 row start; slab s at + s * slab_stride
+    size_t slab_stride;
+    int S;
+    __device__ __forceinline__ void load8(int col, float* f) const {
+        if constexpr (!PARTS) {
+            unpack8(*reinterpret_cast<const uint4*>(row + col), f);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = 0.f;
+            for (int s = 0; s < S; ++s) {
+                const float4* p = reinterpret_cast<const float4*>(parts + s * slab_stride + col);
+                const float4 a = p[0], b = p[1];
+                f[0] += a.x; f[1] += a.y; f[2] += a.z; f[3] += a.w;
+                f[4] += b.x; f[5] += b.y; f[6] += b.z; f[7] += b.w;
+            }
+        }
+    }
+};
+
+template <int D, bool PARTS>
+__global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ qkv_in, const float* __restrict__ parts,
+                                                      int S, int T, bf16* __restrict__ qkv_out, int row_stride,
                                                       const int* __restrict__ positions,
                                                       const int* __restrict__ seq_idx,
                                                       const int* __restrict__ block_tables, int bt_stride,
@@ -29,7 +55,16 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16* __restrict__ qkv, in
     constexpr int VI = D / 8;      // copy items per v head
     const int t = blockIdx.x;
     const int pos = positions[t];
-    bf16* row = qkv + (size_t)t * row_stride;
+    const int width = (Hq + 2 * Hkv) * D;
+    RowSrc<PARTS> src;
+    if constexpr (PARTS) {
+        src.parts = parts + (size_t)t * width;
+        src.slab_stride = (size_t)T * width;
+        src.S = S;
+    } else {
+        src.row = qkv_in + (size_t)t * row_stride;
+    }
+    bf16* row = qkv_out + (size_t)t * row_stride;
     size_t page_base = 0;
     if (write_cache) {
         const int page = block_tables[(size_t)seq_idx[t] * bt_stride + pos / P];
@@ -41,10 +76,9 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16* __restrict__ qkv, in
     for (int it = threadIdx.x; it < n_all; it += blockDim.x) {
         if (it < n_rot) {
             const int h = it / RI, c = (it % RI) * 8;
-            bf16* hp = row + h * D;
             float a[8], b[8];
-            unpack8(*reinterpret_cast<const uint4*>(hp + c), a);
-            unpack8(*reinterpret_cast<const uint4*>(hp + c + HALF), b);
+            src.load8(h * D + c, a);
+            src.load8(h * D + c + HALF, b);
             float ra[8], rb[8];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -53,6 +87,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16* __restrict__ qkv, in
                 rb[j] = b[j] * e.x + a[j] * e.y;
             }
             const uint4 pa = pack8(ra), pb = pack8(rb);
+            bf16* hp = row + h * D;
             *reinterpret_cast<uint4*>(hp + c) = pa;
             *reinterpret_cast<uint4*>(hp + c + HALF) = pb;
             if (write_cache && h >= Hq) {
@@ -60,29 +95,59 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(bf16* __restrict__ qkv, in
                 *reinterpret_cast<uint4*>(kp + c) = pa;
                 *reinterpret_cast<uint4*>(kp + c + HALF) = pb;
             }
-        } else if (write_cache) {
+        } else {
             const int i = it - n_rot;
             const int h = i / VI, c = (i % VI) * 8;
-            const uint4 v = *reinterpret_cast<const uint4*>(row + (Hq + Hkv + h) * D + c);
-            *reinterpret_cast<uint4*>(vcache + (page_base + (size_t)h * P) * D + c) = v;
+            const int col = (Hq + Hkv + h) * D + c;
+            uint4 v;
+            if constexpr (PARTS) {
+                float f[8];
+                src.load8(col, f);
+                v = pack8(f);
+                *reinterpret_cast<uint4*>(row + col) = v;
+            } else {
+                v = *reinterpret_cast<const uint4*>(src.row + col);
+                if (qkv_out != qkv_in) *reinterpret_cast<uint4*>(row + col) = v;
+            }
+            if (write_cache) *reinterpret_cast<uint4*>(vcache + (page_base + (size_t)h * P) * D + c) = v;
         }
     }
+}
+
+template <bool PARTS>
+static int launch_rope(const void* qkv_in, const void* parts, int S, void* qkv_out, int T, int row_stride,
+                       const int* positions, const int* seq_idx, const int* block_tables, int bt_stride,
+                       void* kcache, void* vcache, const void* cos_sin, int Hq, int Hkv, int D, int P,
+                       int write_cache, hipStream_t s) {
+    if (T <= 0) return 0;
+    dim3 g(T), b(256);
+    auto QI = (const bf16*)qkv_in; auto PA = (const float*)parts; auto QO = (bf16*)qkv_out;
+    auto K = (bf16*)kcache; auto V = (bf16*)vcache; auto CS = (const float2*)cos_sin;
+    if (D == 128)
+        rope_kv_kernel<128, PARTS><<<g, b, 0, s>>>(QI, PA, S, T, QO, row_stride, positions, seq_idx, block_tables,
+                                                   bt_stride, K, V, CS, Hq, Hkv, P, write_cache);
+    else if (D == 64)
+        rope_kv_kernel<64, PARTS><<<g, b, 0, s>>>(QI, PA, S, T, QO, row_stride, positions, seq_idx, block_tables,
+                                                  bt_stride, K, V, CS, Hq, Hkv, P, write_cache);
+    else
+        return (int)hipErrorInvalidValue;
+    return (int)hipGetLastError();
 }
 
 MRSUM_API int mrsum_rope_kv(void* qkv, int T, int row_stride, const int* positions, const int* seq_idx,
                             const int* block_tables, int bt_stride, void* kcache, void* vcache,
                             const void* cos_sin, int Hq, int Hkv, int D, int P, int write_cache,
                             hipStream_t s) {
-    if (T <= 0) return 0;
-    dim3 g(T), b(256);
-    auto Q = (bf16*)qkv; auto K = (bf16*)kcache; auto V = (bf16*)vcache; auto CS = (const float2*)cos_sin;
-    if (D == 128)
-        rope_kv_kernel<128><<<g, b, 0, s>>>(Q, row_stride, positions, seq_idx, block_tables, bt_stride, K, V, CS,
-                                            Hq, Hkv, P, write_cache);
-    else if (D == 64)
-        rope_kv_kernel<64><<<g, b, 0, s>>>(Q, row_stride, positions, seq_idx, block_tables, bt_stride, K, V, CS,
-                                           Hq, Hkv, P, write_cache);
-    else
-        return (int)hipErrorInvalidValue;
-    return (int)hipGetLastError();
+    return launch_rope<false>(qkv, nullptr, 1, qkv, T, row_stride, positions, seq_idx, block_tables, bt_stride,
+                              kcache, vcache, cos_sin, Hq, Hkv, D, P, write_cache, s);
+}
+
+// parts: fp32 [S, T, (Hq+2Hkv)*D] split-K slabs; qkv_out: bf16 [T, row_stride]
+MRSUM_API int mrsum_rope_kv_parts(const void* parts, int S, void* qkv_out, int T, int row_stride,
+                                  const int* positions, const int* seq_idx, const int* block_tables, int bt_stride,
+                                  void* kcache, void* vcache, const void* cos_sin, int Hq, int Hkv, int D, int P,
+                                  hipStream_t s) {
+    if (S < 1) return (int)hipErrorInvalidValue;
+    return launch_rope<true>(nullptr, parts, S, qkv_out, T, row_stride, positions, seq_idx, block_tables, bt_stride,
+                             kcache, vcache, cos_sin, Hq, Hkv, D, P, 1, s);
 }

@@ -18,8 +18,8 @@
 //    workgroups for 256 CUs; partial slabs are fp32 and summed by the
 //    CONSUMER kernel (add_rmsnorm_partials), not by atomics or an extra pass;
 //  * fused epilogues: bf16 store | fp32 partial slab | SwiGLU (W rows laid
-//    out as [16 gate | 16 up] blocks so one lane holds gate and up of the
-//    same feature: act = silu(g) * u is written directly, the gate_up
+//    out as [8 gate | 8 up] blocks so one workgroup tile holds gate and up of
+//    the same 8 features: act = silu(g) * u is written directly, the gate_up
 //    activation never exists in HBM).
 #include "common.h"
 
@@ -46,18 +46,25 @@ __device__ __forceinline__ void load_a(AFrag<NT>& a, const bf16* __restrict__ W,
     }
 }
 
-template <int NT, int MT>
-__device__ __forceinline__ void mma_block(f32x4 (&acc)[NT][MT], const AFrag<NT>& a, const bf16* __restrict__ x,
-                                          int ldx, int M, int kb, int lane) {
+template <int MT>
+struct BFrag {
+    uint4 v[MT][4];
+};
+
+template <int MT>
+__device__ __forceinline__ void load_b(BFrag<MT>& b, const bf16* __restrict__ x, int ldx, int M, int kb, int lane) {
     const int r = lane & 15, g = lane >> 4;
-    uint4 b[MT][4];
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
         const int row = min(16 * m + r, M - 1);
         const bf16* p = x + (size_t)row * ldx + kb + 8 * g;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) b[m][i] = *reinterpret_cast<const uint4*>(p + 32 * i);
+        for (int i = 0; i < 4; ++i) b.v[m][i] = *reinterpret_cast<const uint4*>(p + 32 * i);
     }
+}
+
+template <int NT, int MT>
+__device__ __forceinline__ void mma_block(f32x4 (&acc)[NT][MT], const AFrag<NT>& a, const BFrag<MT>& b) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -65,7 +72,7 @@ __device__ __forceinline__ void mma_block(f32x4 (&acc)[NT][MT], const AFrag<NT>&
 #pragma unroll
             for (int m = 0; m < MT; ++m)
                 acc[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a.v[t][i]),
-                                                                    __builtin_bit_cast(bf16x8, b[m][i]),
+                                                                    __builtin_bit_cast(bf16x8, b.v[m][i]),
                                                                     acc[t][m], 0, 0, 0);
 }
 }  // namespace
@@ -86,18 +93,23 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16* __restrict
 #pragma unroll
         for (int m = 0; m < MT; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // wave w takes k blocks ks + (w + 4j) * KB
+    // wave w takes k blocks ks + (w + 4j) * KB.  Issue order per block: x fragments of THIS block,
+    // then W of the NEXT block, then the MFMAs -- vmcnt retires loads in issue order, so waiting
+    // for x must not also wait for the prefetched W (which would serialise the stream).
     int kb = ks + w * KB;
     AFrag<NT> a0, a1;
+    BFrag<MT> b;
     if (kb < ke) load_a<NT>(a0, W, K, n0, kb, lane);
     while (kb < ke) {
         const int kb1 = kb + 4 * KB;
+        load_b<MT>(b, x, ldx, M, kb, lane);
         if (kb1 < ke) load_a<NT>(a1, W, K, n0, kb1, lane);
-        mma_block<NT, MT>(acc, a0, x, ldx, M, kb, lane);
+        mma_block<NT, MT>(acc, a0, b);
         if (kb1 >= ke) break;
         const int kb2 = kb1 + 4 * KB;
+        load_b<MT>(b, x, ldx, M, kb1, lane);
         if (kb2 < ke) load_a<NT>(a0, W, K, n0, kb2, lane);
-        mma_block<NT, MT>(acc, a1, x, ldx, M, kb1, lane);
+        mma_block<NT, MT>(acc, a1, b);
         kb = kb2;
     }
 
@@ -127,20 +139,21 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16* __restrict
         } else if constexpr (EPI == EPI_F32_PARTIAL) {
             float* o = reinterpret_cast<float*>(out) + ((size_t)blockIdx.y * M + m) * ldo + n0 + n4;
             *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
-        } else {  // SWIGLU: rows [0,16) gate, [16,32) up of feature block blockIdx.x
-            if (n4 < 16) {
+        } else {  // SWIGLU: tile rows [0, BN/2) gate, [BN/2, BN) up of features [blockIdx.x*BN/2, +BN/2)
+            constexpr int H = BN / 2;
+            if (n4 < H) {
                 float r[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    float u = red[0][m][n4 + 16 + j] + red[1][m][n4 + 16 + j] + red[2][m][n4 + 16 + j] +
-                              red[3][m][n4 + 16 + j];
-                    float g = v[j];
+                    const float u = red[0][m][n4 + H + j] + red[1][m][n4 + H + j] + red[2][m][n4 + H + j] +
+                                    red[3][m][n4 + H + j];
+                    const float g = v[j];
                     r[j] = g / (1.f + __expf(-g)) * u;
                 }
                 uint2 o;
                 o.x = pack2(r[0], r[1]);
                 o.y = pack2(r[2], r[3]);
-                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)m * ldo + blockIdx.x * 16 + n4) = o;
+                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)m * ldo + blockIdx.x * H + n4) = o;
             }
         }
     }
@@ -160,14 +173,14 @@ static int launch_mt(int mt, dim3 grid, hipStream_t s, const bf16* x, int ldx, c
 }
 
 // epi: 0 bf16 [M, ldo], 1 fp32 partial [S, M, ldo], 2 swiglu bf16 [M, ldo] (ldo >= N/2)
-// nt: 16-row W tiles per workgroup (1 or 2; swiglu needs 2); splits: S (K/S multiple of 128)
+// nt: 16-row W tiles per workgroup (1 or 2; swiglu needs 1); splits: S (K/S multiple of 128)
 MRSUM_API int mrsum_skinny_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
                                 int epi, int nt, int splits, hipStream_t s) {
     if (M <= 0) return 0;
     if (M > 64 || K % KB || splits < 1 || (K / KB) % splits || (nt != 1 && nt != 2) || N % (16 * nt))
         return (int)hipErrorInvalidValue;
     if (epi != EPI_F32_PARTIAL && splits != 1) return (int)hipErrorInvalidValue;
-    if (epi == EPI_SWIGLU && nt != 2) return (int)hipErrorInvalidValue;
+    if (epi == EPI_SWIGLU && nt != 1) return (int)hipErrorInvalidValue;  // weight blocks of [8 gate | 8 up]
     const int kper = K / splits;
     const int mt = (M + 15) / 16;
     dim3 grid(N / (16 * nt), splits);
@@ -175,10 +188,10 @@ MRSUM_API int mrsum_skinny_gemm(const void* x, int ldx, const void* W, int N, in
     if (nt == 1) {
         if (epi == EPI_BF16) return launch_mt<1, EPI_BF16>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper);
         if (epi == EPI_F32_PARTIAL) return launch_mt<1, EPI_F32_PARTIAL>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper);
+        if (epi == EPI_SWIGLU) return launch_mt<1, EPI_SWIGLU>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper);
     } else {
         if (epi == EPI_BF16) return launch_mt<2, EPI_BF16>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper);
         if (epi == EPI_F32_PARTIAL) return launch_mt<2, EPI_F32_PARTIAL>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper);
-        if (epi == EPI_SWIGLU) return launch_mt<2, EPI_SWIGLU>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper);
     }
     return (int)hipErrorInvalidValue;
 }

@@ -7,7 +7,7 @@ parallelism so a model is bit-identical for every TP degree.  Fused layouts:
 * ``wqkv`` [(Hq + 2 Hkv) * hd / tp, hidden]: this rank's Q heads, K heads, V heads
 * ``wo``   [hidden, Hq * hd / tp]           (row-parallel, all-reduced)
 * ``wgu``  [2 * ffn / tp, hidden]            (gate/up shards interleaved in blocks of
-                                             16 rows, one GEMM; see ops.reference.swiglu)
+                                             8 rows, one GEMM; see ops.reference.swiglu)
 * ``wdown``[hidden, ffn / tp]                (row-parallel, all-reduced)
 * ``lm_head`` [vocab / tp, hidden]           (vocab-parallel, logits all-gathered)
 
@@ -143,9 +143,13 @@ class LlamaModel:
         fast = decode and ids.shape[0] <= SKINNY_MAX_M
         for i, lw in enumerate(self.layers):
             nxt = self.layers[i + 1].ln1 if i + 1 < n else self.final_norm
-            qkv = ops.linear(x, lw.wqkv) if fast else F.linear(x, lw.wqkv)
-            ops.rope_kv(qkv, positions, seq_idx, block_tables, kcache[i], vcache[i], self.cos_sin, self.hq,
-                        self.hkv, self.hd, page)
+            if fast:
+                qkv = ops.rope_kv_parts(ops.linear_parts(x, lw.wqkv), positions, seq_idx, block_tables, kcache[i],
+                                        vcache[i], self.cos_sin, self.hq, self.hkv, self.hd, page)
+            else:
+                qkv = F.linear(x, lw.wqkv)
+                ops.rope_kv(qkv, positions, seq_idx, block_tables, kcache[i], vcache[i], self.cos_sin, self.hq,
+                            self.hkv, self.hd, page)
             a = attention(i, qkv)
             if fast:
                 tp1 = self.tp_size == 1

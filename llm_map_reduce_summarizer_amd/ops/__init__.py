@@ -44,6 +44,12 @@ def rope_kv(qkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, 
                               write_cache)
 
 
+def rope_kv_parts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page):
+    """Sum split-K fp32 QKV slabs + RoPE + paged KV write; returns the bf16 qkv rows."""
+    return _impl(parts).rope_kv_parts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d,
+                                      page)
+
+
 def swiglu(gu, out=None):
     return _impl(gu).swiglu(gu, out)
 

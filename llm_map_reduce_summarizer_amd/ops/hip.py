@@ -23,6 +23,8 @@ _SIGS = {
     "mrsum_add_rmsnorm": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_rope_kv": [_vp, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
                       _c_int, _vp],
+    "mrsum_rope_kv_parts": [_vp, _c_int, _vp, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _c_int,
+                            _c_int, _c_int, _c_int, _vp],
     "mrsum_swiglu": [_vp, _vp, _c_int, _c_int, _vp],
     "mrsum_embed": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _vp],
     "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
@@ -142,10 +144,32 @@ def rope_kv(qkv: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, b
                                 1 if write_cache else 0, _stream()), "rope_kv")
 
 
+def rope_kv_parts(parts: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, block_tables: torch.Tensor,
+                  kcache: torch.Tensor, vcache: torch.Tensor, cos_sin: torch.Tensor, hq: int, hkv: int, d: int,
+                  page: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Sum the QKV GEMM's fp32 split-K slabs [S, T, (hq+2hkv)d], rotate Q/K, write bf16 qkv + paged K/V."""
+    _req(parts.is_cuda and parts.dtype == torch.float32 and parts.is_contiguous() and parts.dim() == 3,
+         "rope_kv_parts: parts must be fp32 [S, T, W]")
+    S, T, W = parts.shape
+    _req(W == (hq + 2 * hkv) * d and d in (64, 128), "rope_kv_parts: width")
+    _i32(positions, seq_idx, block_tables)
+    _req(positions.numel() >= T and seq_idx.numel() >= T and block_tables.dim() == 2, "rope_kv_parts: tables")
+    _req(cos_sin.is_cuda and cos_sin.dtype == torch.float32 and cos_sin.shape[1:] == (d // 2, 2), "cos_sin")
+    _bf16_cuda(kcache, vcache)
+    _req(kcache.is_contiguous() and vcache.is_contiguous() and tuple(kcache.shape[1:]) == (hkv, page, d), "cache")
+    if out is None:
+        out = torch.empty(T, W, dtype=torch.bfloat16, device=parts.device)
+    _rows_ok(out)
+    _check(_fn("mrsum_rope_kv_parts")(_p(parts), S, _p(out), T, out.stride(0), _p(positions), _p(seq_idx),
+                                      _p(block_tables), block_tables.stride(0), _p(kcache), _p(vcache), _p(cos_sin),
+                                      hq, hkv, d, page, _stream()), "rope_kv_parts")
+    return out
+
+
 # ------------------------------------------------------------------ activations
 def swiglu(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     _bf16_cuda(gu)
-    _req(gu.dim() == 2 and gu.is_contiguous() and gu.shape[1] % 32 == 0, "swiglu: gu must be [T, 2F], F % 16 == 0")
+    _req(gu.dim() == 2 and gu.is_contiguous() and gu.shape[1] % 32 == 0, "swiglu: gu must be [T, 2F], F % 16 == 0")  # noqa
     T, F = gu.shape[0], gu.shape[1] // 2
     if out is None:
         out = torch.empty(T, F, dtype=gu.dtype, device=gu.device)
@@ -316,7 +340,7 @@ def linear_parts(x: torch.Tensor, w: torch.Tensor, splits: Optional[int] = None,
 
 
 def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """silu(gate) * up straight out of the gate_up GEMM (blocked [16 gate | 16 up] weight rows)."""
+    """silu(gate) * up straight out of the gate_up GEMM (blocked [8 gate | 8 up] weight rows)."""
     M = x.shape[0]
     F2 = w_gu.shape[0]
     if M > SKINNY_MAX_M:
@@ -324,7 +348,7 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tenso
     if out is None:
         out = torch.empty(M, F2 // 2, dtype=x.dtype, device=x.device)
     _req(out.is_contiguous() and out.shape == (M, F2 // 2), "linear_swiglu: bad out")
-    return _skinny(x, w_gu, out, EPI_SWIGLU, 2, 1, F2 // 2)
+    return _skinny(x, w_gu, out, EPI_SWIGLU, 1, 1, F2 // 2)
 
 
 def add_rmsnorm_parts(parts: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,

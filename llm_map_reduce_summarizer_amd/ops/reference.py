@@ -73,16 +73,26 @@ def rope_kv(qkv: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, b
         vcache[pages, :, offs] = v
 
 
+def rope_kv_parts(parts: torch.Tensor, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page,
+                  out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    qkv = parts.float().sum(0).to(torch.bfloat16)
+    rope_kv(qkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page)
+    if out is not None:
+        out.copy_(qkv)
+        return out
+    return qkv
+
+
 def interleave_gate_up(wg: torch.Tensor, wu: torch.Tensor) -> torch.Tensor:
-    """[F, H] gate + [F, H] up -> [2F, H] rows in blocks of 32 = [16 gate | 16 up]."""
+    """[F, H] gate + [F, H] up -> [2F, H] rows in blocks of 16 = [8 gate | 8 up]."""
     f, h = wg.shape
-    return torch.stack([wg.reshape(f // 16, 16, h), wu.reshape(f // 16, 16, h)], dim=1).reshape(2 * f, h)
+    return torch.stack([wg.reshape(f // 8, 8, h), wu.reshape(f // 8, 8, h)], dim=1).reshape(2 * f, h)
 
 
 def split_gate_up(gu: torch.Tensor):
     """Inverse of the blocked column layout of a gate_up GEMM output."""
     f = gu.shape[-1] // 2
-    v = gu.reshape(*gu.shape[:-1], f // 16, 2, 16)
+    v = gu.reshape(*gu.shape[:-1], f // 8, 2, 8)
     return v[..., 0, :].reshape(*gu.shape[:-1], f), v[..., 1, :].reshape(*gu.shape[:-1], f)
 
 

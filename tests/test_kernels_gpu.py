@@ -230,3 +230,23 @@ def test_add_rmsnorm_parts(S, T, D):
     o2 = reference.add_rmsnorm_parts(parts, r2, w, 1e-5)
     _close(r1, r2, 2e-2)
     _close(o1, o2, 3e-2)
+
+
+@pytest.mark.parametrize("S", [1, 3])
+def test_rope_kv_parts(S):
+    hq, hkv, d, page = 4, 2, 128, 64
+    T = 5
+    W = (hq + 2 * hkv) * d
+    g = torch.Generator().manual_seed(31)
+    parts = torch.randn(S, T, W, generator=g).to(DEV)
+    positions = torch.tensor([0, 63, 64, 7, 300], dtype=torch.int32, device=DEV)
+    seq_idx = torch.tensor([0, 0, 0, 1, 1], dtype=torch.int32, device=DEV)
+    bt = torch.tensor([[3, 5, 1, 7, 2, 6], [4, 0, 0, 0, 6, 2]], dtype=torch.int32, device=DEV)
+    cs = reference.rope_cos_sin(1024, d, 500000.0, DEV)
+    k1, v1 = _cache_setup(hq, hkv, d, page, 8)
+    k2, v2 = _cache_setup(hq, hkv, d, page, 8)
+    o1 = hip.rope_kv_parts(parts, positions, seq_idx, bt, k1, v1, cs, hq, hkv, d, page)
+    o2 = reference.rope_kv_parts(parts, positions, seq_idx, bt, k2, v2, cs, hq, hkv, d, page)
+    _close(o1, o2, 3e-2)
+    _close(k1, k2, 3e-2)
+    _close(v1, v2, 3e-2)
