@@ -17,17 +17,67 @@
 // (q pre-scaled by log2(e)/sqrt(D)) so the exponentials are exp2.
 //
 // Output: unnormalised partials part_o [B, Hq, S, D] f32 and part_ml
-// [B, Hq, S, 2] = (running max, running sum); attn_decode_combine merges the
-// S splits into out [B, Hq*D] bf16.  Context length = positions[b] + 1 is
-// read on the device, so the launch shape is fixed and the kernel can live
-// inside a captured decode graph.
+// [B, Hq, S, 2] = (running max, running sum), merged into out [B, Hq*D] bf16
+// IN THE SAME LAUNCH by the last of the S split workgroups of a (b, kv head)
+// to finish: every split publishes its slab (vmcnt drain, barrier, one
+// agent-scope release) and draws a ticket from a per-(b, kv head) counter;
+// the ticket S-1 holder acquires (agent scope) and combines, then re-arms the
+// counter to 0 for the next launch / graph replay (cdna_hip_programming.md
+// §5 "in-launch split-K reduction", placement-independent across XCDs).
+// With no counter buffer a separate combine kernel is launched instead.
+// Context length = positions[b] + 1 is read on the device, so the launch
+// shape is fixed and the kernel can live inside a captured decode graph.
 #include "common.h"
+
+// Publish this workgroup's partials and, if it is the last split of (b, kvh) to arrive, merge all S.
+template <int G>
+__device__ __forceinline__ void combine_if_last(const float* part_o, const float* part_ml, int* counters,
+                                                bf16* out, int out_stride, int b, int kvh, int Hq, int Hkv, int S,
+                                                int* s_last) {
+    constexpr int D = 128;
+    const int tid = threadIdx.x;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slab stores
+    __syncthreads();
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int prev = __hip_atomic_fetch_add(counters + b * Hkv + kvh, 1, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+        *s_last = prev == S - 1;
+    }
+    __syncthreads();
+    if (!*s_last) return;
+    if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    for (int i = tid; i < G * D; i += 256) {
+        const int g = i / D, d = i % D;
+        const int h = kvh * G + g;
+        const size_t bh = (size_t)b * Hq + h;
+        const float* ml = part_ml + bh * S * 2;
+        float M = -INFINITY;
+        for (int s = 0; s < S; ++s) M = fmaxf(M, ml[2 * s]);
+        float num = 0.f, den = 0.f;
+        for (int s = 0; s < S; ++s) {
+            const float ms = ml[2 * s];
+            if (ms == -INFINITY) continue;
+            const float w = exp2f(ms - M);
+            num += w * part_o[(bh * S + s) * D + d];
+            den += w * ml[2 * s + 1];
+        }
+        out[(size_t)b * out_stride + h * D + d] = (bf16)(den > 0.f ? num / den : 0.f);
+    }
+    if (tid == 0) __hip_atomic_store(counters + b * Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 template <int G>
 __global__ __launch_bounds__(256) void attn_decode_split_kernel(
     const bf16* __restrict__ q, int q_stride, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ positions,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int P, int S, float scale_log2) {
+    float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int P, int S, float scale_log2,
+    int* __restrict__ counters, bf16* __restrict__ out, int out_stride) {
     constexpr int D = 128;
     const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
     const int Hq = Hkv * G;
@@ -41,6 +91,7 @@ __global__ __launch_bounds__(256) void attn_decode_split_kernel(
     __shared__ float sm_o[16][G][D];
     __shared__ float sm_m[16][G];
     __shared__ float sm_l[16][G];
+    __shared__ int s_last;
 
     const size_t ml_base = ((size_t)b * Hq + (size_t)kvh * G) * S + split;
     if (ks >= ke) {
@@ -48,6 +99,7 @@ __global__ __launch_bounds__(256) void attn_decode_split_kernel(
             part_ml[(ml_base + (size_t)tid * S) * 2 + 0] = -INFINITY;
             part_ml[(ml_base + (size_t)tid * S) * 2 + 1] = 0.f;
         }
+        if (counters) combine_if_last<G>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, &s_last);
         return;
     }
 
@@ -156,6 +208,7 @@ __global__ __launch_bounds__(256) void attn_decode_split_kernel(
             part_ml[pi * 2 + 1] = L;
         }
     }
+    if (counters) combine_if_last<G>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, &s_last);
 }
 
 __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* __restrict__ part_o,
@@ -181,7 +234,7 @@ __global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* _
 MRSUM_API int mrsum_attn_decode(const void* q, int q_stride, const void* kcache, const void* vcache,
                                 const int* block_tables, int bt_stride, const int* positions, void* part_o,
                                 void* part_ml, void* out, int out_stride, int B, int Hq, int Hkv, int D, int P,
-                                int S, float scale, hipStream_t s) {
+                                int S, float scale, int* counters, hipStream_t s) {
     if (B <= 0) return 0;
     if (D != 128 || Hq % Hkv || S < 1 || P % 16) return (int)hipErrorInvalidValue;
     const int G = Hq / Hkv;
@@ -190,14 +243,14 @@ MRSUM_API int mrsum_attn_decode(const void* q, int q_stride, const void* kcache,
     auto Qp = (const bf16*)q; auto K = (const bf16*)kcache; auto V = (const bf16*)vcache;
     auto PO = (float*)part_o; auto PM = (float*)part_ml;
     switch (G) {
-        case 1: attn_decode_split_kernel<1><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl); break;
-        case 2: attn_decode_split_kernel<2><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl); break;
-        case 4: attn_decode_split_kernel<4><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl); break;
-        case 8: attn_decode_split_kernel<8><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl); break;
+        case 1: attn_decode_split_kernel<1><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl, counters, (bf16*)out, out_stride); break;
+        case 2: attn_decode_split_kernel<2><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl, counters, (bf16*)out, out_stride); break;
+        case 4: attn_decode_split_kernel<4><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl, counters, (bf16*)out, out_stride); break;
+        case 8: attn_decode_split_kernel<8><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl, counters, (bf16*)out, out_stride); break;
         default: return (int)hipErrorInvalidValue;
     }
     int e = (int)hipGetLastError();
-    if (e) return e;
+    if (e || counters) return e;
     attn_decode_combine_kernel<<<B * Hq, 128, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, S);
     return (int)hipGetLastError();
 }

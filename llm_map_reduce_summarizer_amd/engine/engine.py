@@ -160,7 +160,7 @@ class LLMEngine:
         if ws is None:
             from ..ops.hip import DecodeWorkspace, decode_splits
             s = decode_splits(B, self.model.hkv, self.max_model_len)
-            ws = DecodeWorkspace(B, self.model.hq, self.cfg.head_dim, s, self.device)
+            ws = DecodeWorkspace(B, self.model.hq, self.cfg.head_dim, s, self.device, self.model.hkv)
             self._workspaces[B] = ws
         return ws
 

@@ -36,8 +36,6 @@ from .. import ops
 from ..ops.reference import interleave_gate_up, rope_cos_sin
 from .config import ModelConfig
 
-SKINNY_MAX_M = 64  # decode rows served by the weight-streaming GEMMs (ops.hip.SKINNY_MAX_M)
-
 
 def _seed_for(seed: int, name: str) -> int:
     return int.from_bytes(hashlib.sha1(("%d:%s" % (seed, name)).encode()).digest()[:8], "little") & ((1 << 63) - 1)
@@ -131,44 +129,29 @@ class LlamaModel:
                    attention: Callable[[int, torch.Tensor], torch.Tensor], decode: bool = False) -> torch.Tensor:
         """Embedding -> all layers -> final norm; returns normed hidden [T, hidden].
 
-        ``decode`` (T <= 64 rows): projections run on the MFMA weight-streaming
-        kernels with fused epilogues -- split-K fp32 slabs reduced inside
-        add_rmsnorm_parts, SwiGLU inside the gate_up GEMM.
+        Projections go through the fused blocks of ``ops`` (qkv_rope, proj_add_rmsnorm,
+        gate_up_swiglu): at decode row counts they run on the MFMA weight-streaming kernels
+        with fused epilogues (split-K fp32 slabs reduced inside rope_kv_parts /
+        add_rmsnorm_parts, SwiGLU inside the gate_up GEMM), at prefill sizes on hipBLASLt.
         """
         c = self.cfg
         residual = ops.embed(ids, self.embed)
         x = ops.rmsnorm(residual, self.layers[0].ln1, c.rms_eps)
         page = kcache.shape[3]
         n = len(self.layers)
-        fast = decode and ids.shape[0] <= SKINNY_MAX_M
+        ar = self._all_reduce if self.tp_size > 1 else None
         for i, lw in enumerate(self.layers):
             nxt = self.layers[i + 1].ln1 if i + 1 < n else self.final_norm
-            if fast:
-                qkv = ops.rope_kv_parts(ops.linear_parts(x, lw.wqkv), positions, seq_idx, block_tables, kcache[i],
-                                        vcache[i], self.cos_sin, self.hq, self.hkv, self.hd, page)
-            else:
-                qkv = F.linear(x, lw.wqkv)
-                ops.rope_kv(qkv, positions, seq_idx, block_tables, kcache[i], vcache[i], self.cos_sin, self.hq,
-                            self.hkv, self.hd, page)
+            qkv = ops.qkv_rope(x, lw.wqkv, positions, seq_idx, block_tables, kcache[i], vcache[i], self.cos_sin,
+                               self.hq, self.hkv, self.hd, page)
             a = attention(i, qkv)
-            if fast:
-                tp1 = self.tp_size == 1
-                parts = self._all_reduce(ops.linear_parts(a, lw.wo, None if tp1 else 1))
-                x = ops.add_rmsnorm_parts(parts, residual, lw.ln2, c.rms_eps)
-                act = ops.linear_swiglu(x, lw.wgu)
-                parts = self._all_reduce(ops.linear_parts(act, lw.wdown, None if tp1 else 1))
-                x = ops.add_rmsnorm_parts(parts, residual, nxt, c.rms_eps)
-            else:
-                o = self._all_reduce(F.linear(a, lw.wo))
-                x = ops.add_rmsnorm(o, residual, lw.ln2, c.rms_eps)
-                act = ops.swiglu(F.linear(x, lw.wgu))
-                dn = self._all_reduce(F.linear(act, lw.wdown))
-                x = ops.add_rmsnorm(dn, residual, nxt, c.rms_eps)
+            x = ops.proj_add_rmsnorm(a, lw.wo, residual, lw.ln2, c.rms_eps, "o", ar)
+            act = ops.gate_up_swiglu(x, lw.wgu)
+            x = ops.proj_add_rmsnorm(act, lw.wdown, residual, nxt, c.rms_eps, "down", ar)
         return x
 
     def logits(self, x: torch.Tensor) -> torch.Tensor:
-        return self._gather_vocab(ops.linear(x, self.lm_head) if x.shape[0] <= SKINNY_MAX_M else
-                                  F.linear(x, self.lm_head))
+        return self._gather_vocab(F.linear(x, self.lm_head))  # hipBLASLt streams the 1 GB head at ~5.4 TB/s
 
     def prefill(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, cu_seqlens: torch.Tensor,
                 last_rows: torch.Tensor, block_tables: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,

@@ -15,6 +15,8 @@ from __future__ import annotations
 
 import os
 
+import torch
+
 from . import reference
 
 _FORCE_TORCH = os.environ.get("MRSUM_OPS", "").lower() == "torch"
@@ -101,3 +103,56 @@ def sample(logits, st):
     n = logits.shape[0]
     toks = reference.sample_tokens(logits, st.temps[:n], st.seeds[:n], st.positions[:n])
     reference.sample_finish(toks, st)
+
+
+# ---------------------------------------------------------------- fused projection blocks
+# The model calls these; each picks (on the GPU) between our MFMA weight-streaming kernel
+# with a fused epilogue and hipBLASLt + a separate HIP kernel, per the measured plan table
+# (ops.hip.plan).  On the CPU they are the reference composition.
+
+def qkv_rope(x, wqkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page):
+    """qkv = x @ wqkv^T, RoPE on Q/K, K/V into the paged cache; returns bf16 qkv rows."""
+    if _use_hip(x):
+        from . import hip
+        p = hip.plan("qkv", x.shape[0], wqkv.shape[0], wqkv.shape[1])
+        if p[0] == "skinny":
+            parts = hip.linear_parts(x, wqkv, p[2], nt=p[1])
+            return hip.rope_kv_parts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv,
+                                     d, page)
+        qkv = torch.nn.functional.linear(x, wqkv)
+        hip.rope_kv(qkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page)
+        return qkv
+    qkv = torch.nn.functional.linear(x, wqkv)
+    reference.rope_kv(qkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page)
+    return qkv
+
+
+def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
+    """residual += a @ w^T (TP-all-reduced when ``all_reduce``); returns rmsnorm(residual) * ln."""
+    if _use_hip(a):
+        from . import hip
+        p = hip.plan(role, a.shape[0], w.shape[0], w.shape[1])
+        if p[0] == "skinny":
+            parts = hip.linear_parts(a, w, 1 if all_reduce else p[2], nt=p[1])
+            if all_reduce:
+                all_reduce(parts)
+            return hip.add_rmsnorm_parts(parts, residual, ln, eps)
+        o = torch.nn.functional.linear(a, w)
+        if all_reduce:
+            all_reduce(o)
+        return hip.add_rmsnorm(o, residual, ln, eps)
+    o = torch.nn.functional.linear(a, w)
+    if all_reduce:
+        all_reduce(o)
+    return reference.add_rmsnorm(o, residual, ln, eps)
+
+
+def gate_up_swiglu(x, wgu):
+    """silu(gate) * up of the fused, [8 gate | 8 up]-blocked gate_up projection."""
+    if _use_hip(x):
+        from . import hip
+        p = hip.plan("gate_up", x.shape[0], wgu.shape[0], wgu.shape[1])
+        if p[0] == "skinny":
+            return hip.linear_swiglu(x, wgu)
+        return hip.swiglu(torch.nn.functional.linear(x, wgu))
+    return reference.swiglu(torch.nn.functional.linear(x, wgu))

@@ -29,7 +29,7 @@ _SIGS = {
     "mrsum_embed": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _vp],
     "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_attn_decode": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
-                          _c_int, _c_int, _c_int, _c_float, _vp],
+                          _c_int, _c_int, _c_int, _c_float, _vp, _vp],
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_sample": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp,
@@ -233,12 +233,16 @@ def decode_splits(batch: int, hkv: int, max_ctx: int, target_wgs: int = 2048) ->
 
 
 class DecodeWorkspace:
-    """Split-K partial buffers for attn_decode (allocated once per batch bucket)."""
+    """Split-K partial buffers + per-(seq, kv head) arrival counters for attn_decode
+    (allocated once per batch bucket; counters start at 0 and every launch re-arms them)."""
 
-    def __init__(self, batch: int, hq: int, d: int, splits: int, device):
+    def __init__(self, batch: int, hq: int, d: int, splits: int, device, hkv: Optional[int] = None,
+                 fused_combine: bool = True):
         self.splits = splits
         self.part_o = torch.empty(batch * hq * splits * d, dtype=torch.float32, device=device)
         self.part_ml = torch.empty(batch * hq * splits * 2, dtype=torch.float32, device=device)
+        self.counters = (torch.zeros(batch * (hkv or hq), dtype=torch.int32, device=device)
+                         if fused_combine else None)
 
 
 def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, block_tables: torch.Tensor,
@@ -255,15 +259,16 @@ def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, blo
     _req(block_tables.dim() == 2 and block_tables.shape[0] >= B and positions.numel() >= B, "attn_decode: tables")
     if workspace is None:
         s = num_splits or decode_splits(B, hkv, block_tables.shape[1] * page)
-        workspace = DecodeWorkspace(B, hq, d, s, q.device)
+        workspace = DecodeWorkspace(B, hq, d, s, q.device, hkv)
     _req(workspace.part_o.numel() >= B * hq * workspace.splits * d, "attn_decode: workspace too small")
+    _req(workspace.counters is None or workspace.counters.numel() >= B * hkv, "attn_decode: counters too small")
     if out is None:
         out = torch.empty(B, hq * d, dtype=q.dtype, device=q.device)
     _rows_ok(out)
     _check(_fn("mrsum_attn_decode")(_p(q), q.stride(0), _p(kcache), _p(vcache), _p(block_tables),
                                     block_tables.stride(0), _p(positions), _p(workspace.part_o),
                                     _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
-                                    workspace.splits, scale, _stream()), "attn_decode")
+                                    workspace.splits, scale, _p(workspace.counters), _stream()), "attn_decode")
     return out
 
 
@@ -327,16 +332,16 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
 
 
 def linear_parts(x: torch.Tensor, w: torch.Tensor, splits: Optional[int] = None,
-                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """fp32 split-K slabs [S, M, N] of x @ w^T (summed by add_rmsnorm_parts)."""
+                 out: Optional[torch.Tensor] = None, nt: int = 1) -> torch.Tensor:
+    """fp32 split-K slabs [S, M, N] of x @ w^T (summed by add_rmsnorm_parts / rope_kv_parts)."""
     M, K = x.shape
     N = w.shape[0]
     if splits is None:
-        splits = choose_splits(N, K, 1)
+        splits = choose_splits(N, K, nt)
     if out is None:
         out = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
     _req(out.is_contiguous() and out.shape == (splits, M, N) and out.dtype == torch.float32, "linear_parts: bad out")
-    return _skinny(x, w, out, EPI_F32_PARTIAL, 1, splits, N)
+    return _skinny(x, w, out, EPI_F32_PARTIAL, nt, splits, N)
 
 
 def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -365,3 +370,28 @@ def add_rmsnorm_parts(parts: torch.Tensor, residual: torch.Tensor, w: torch.Tens
     _check(_fn("mrsum_add_rmsnorm_parts")(_p(parts), S, _p(residual), _p(w), _p(out), T, D, out.stride(0), eps,
                                           _stream()), "add_rmsnorm_parts")
     return out
+
+
+# ------------------------------------------------------------------ per-role GEMM plans
+# Measured on MI355X (tools/exp_stream.py, back-to-back launches, weights beyond the
+# 256 MiB Infinity Cache; Llama-3-8B shapes).  "blas" = torch.nn.functional.linear (hipBLASLt).
+# M <= 16:  ours beats hipBLASLt on every projection (qkv 12 vs 20 us, o 10 vs 20, down 26 vs 27,
+#           gate_up+SwiGLU 45 vs 57 at M=1); M = 48: hipBLASLt wins qkv and gate_up.
+def plan(role: str, M: int, N: int, K: int):
+    if M > SKINNY_MAX_M or K % 128:
+        return ("blas",)
+    blocks = K // 128
+    if role == "qkv":
+        if M > 32:
+            return ("blas",)
+        return ("skinny", 1, 2 if blocks % 2 == 0 else 1)
+    if role in ("o", "down"):
+        if M <= 16 and K >= 2 * N:  # tall-K (down-like): two 16-row tiles, split 2
+            return ("skinny", 2, 2 if blocks % 2 == 0 else 1)
+        if M <= 16:
+            s = choose_splits(N, K, 1, target_wgs=1024)
+            return ("skinny", 1, s)
+        return ("skinny", 2, 2 if blocks % 2 == 0 else 1)
+    if role == "gate_up":
+        return ("skinny", 1, 1) if M <= 8 else ("blas",)
+    return ("blas",)

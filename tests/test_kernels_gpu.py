@@ -109,7 +109,8 @@ def test_attn_prefill_spike():
 
 @pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (4, 4)])
 @pytest.mark.parametrize("splits", [1, 3, 16])
-def test_attn_decode(hq, hkv, splits):
+@pytest.mark.parametrize("fused", [True, False])
+def test_attn_decode(hq, hkv, splits, fused):
     d, page = 128, 64
     ctxs = [1, 65, 700, 129]
     B = len(ctxs)
@@ -128,10 +129,13 @@ def test_attn_decode(hq, hkv, splits):
     pos = torch.tensor([c - 1 for c in ctxs], dtype=torch.int32, device=DEV)
     q = _rand(B, (hq + 2 * hkv) * d, seed=14)
     sc = 1.0 / math.sqrt(d)
-    ws = hip.DecodeWorkspace(B, hq, d, splits, DEV)
-    o1 = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws)
+    ws = hip.DecodeWorkspace(B, hq, d, splits, DEV, hkv, fused_combine=fused)
     o2 = reference.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc)
-    _close(o1, o2, 2e-2)
+    for _ in range(3):  # replays re-use (and must re-arm) the arrival counters
+        o1 = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws)
+        _close(o1, o2, 2e-2)
+    if fused:
+        assert int(ws.counters.abs().sum()) == 0
 
 
 class _St:

@@ -73,7 +73,7 @@ def main():
         bt = (torch.arange(B * npg, dtype=torch.int32, device=dev).view(B, npg) + 1)
         pos = torch.full((B,), ctx - 1, dtype=torch.int32, device=dev)
         q = torch.randn(B, (hq + 2 * hkv) * d, device=dev, dtype=torch.bfloat16)
-        ws = hip.DecodeWorkspace(B, hq, d, hip.decode_splits(B, hkv, ctx), dev)
+        ws = hip.DecodeWorkspace(B, hq, d, hip.decode_splits(B, hkv, ctx), dev, hkv)
         t = timeit(lambda: hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, 1 / math.sqrt(d), workspace=ws))
         gb = B * ctx * hkv * d * 2 * 2 / 1e9
         res["attn_decode"].append({"B": B, "ctx": ctx, "us": round(t * 1e6, 1), "TBps": round(gb / t / 1e3, 2)})
