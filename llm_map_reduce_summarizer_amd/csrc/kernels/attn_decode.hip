@@ -29,12 +29,51 @@
 // shape is fixed and the kernel can live inside a captured decode graph.
 #include "common.h"
 
+constexpr int MAX_SPLITS = 64;
+
+// Merge the S split partials of one (b, kv head) group -- G query heads x D -- with all 256
+// threads: the (max, sum) pairs are read in parallel into LDS and turned into per-split weights
+// once, then each output element sums S slabs with independent (unrolled) loads, so the merge
+// costs ~S/8 memory round trips instead of S dependent ones.
+template <int G>
+__device__ __forceinline__ void combine_group(const float* part_o, const float* part_ml, bf16* out, int out_stride,
+                                              int b, int kvh, int Hq, int S, float* sw /* [G][S] LDS */,
+                                              float* sden /* [G] */) {
+    constexpr int D = 128;
+    const int tid = threadIdx.x;
+    const size_t bh0 = (size_t)b * Hq + (size_t)kvh * G;
+    for (int i = tid; i < G * S; i += 256) sw[i] = part_ml[(bh0 * S + i) * 2];  // g-major: (bh0+g)*S + s
+    __syncthreads();
+    if (tid < G) {
+        float M = -INFINITY;
+        for (int s = 0; s < S; ++s) M = fmaxf(M, sw[tid * S + s]);
+        float den = 0.f;
+        for (int s = 0; s < S; ++s) {
+            const float ms = sw[tid * S + s];
+            const float w = ms == -INFINITY ? 0.f : exp2f(ms - M);
+            sw[tid * S + s] = w;
+            den += w * part_ml[((bh0 + tid) * S + s) * 2 + 1];
+        }
+        sden[tid] = den;
+    }
+    __syncthreads();
+    for (int i = tid; i < G * D; i += 256) {
+        const int g = i / D, d = i % D;
+        const float* po = part_o + (bh0 + g) * S * D + d;
+        const float* w = sw + g * S;
+        float acc = 0.f;
+#pragma unroll 8
+        for (int s = 0; s < S; ++s) acc += w[s] * po[(size_t)s * D];
+        const float den = sden[g];
+        out[(size_t)b * out_stride + (kvh * G + g) * D + d] = (bf16)(den > 0.f ? acc / den : 0.f);
+    }
+}
+
 // Publish this workgroup's partials and, if it is the last split of (b, kvh) to arrive, merge all S.
 template <int G>
 __device__ __forceinline__ void combine_if_last(const float* part_o, const float* part_ml, int* counters,
                                                 bf16* out, int out_stride, int b, int kvh, int Hq, int Hkv, int S,
-                                                int* s_last) {
-    constexpr int D = 128;
+                                                int* s_last, float* sw, float* sden) {
     const int tid = threadIdx.x;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slab stores
     __syncthreads();
@@ -52,23 +91,7 @@ __device__ __forceinline__ void combine_if_last(const float* part_o, const float
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    for (int i = tid; i < G * D; i += 256) {
-        const int g = i / D, d = i % D;
-        const int h = kvh * G + g;
-        const size_t bh = (size_t)b * Hq + h;
-        const float* ml = part_ml + bh * S * 2;
-        float M = -INFINITY;
-        for (int s = 0; s < S; ++s) M = fmaxf(M, ml[2 * s]);
-        float num = 0.f, den = 0.f;
-        for (int s = 0; s < S; ++s) {
-            const float ms = ml[2 * s];
-            if (ms == -INFINITY) continue;
-            const float w = exp2f(ms - M);
-            num += w * part_o[(bh * S + s) * D + d];
-            den += w * ml[2 * s + 1];
-        }
-        out[(size_t)b * out_stride + h * D + d] = (bf16)(den > 0.f ? num / den : 0.f);
-    }
+    combine_group<G>(part_o, part_ml, out, out_stride, b, kvh, Hq, S, sw, sden);
     if (tid == 0) __hip_atomic_store(counters + b * Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -92,6 +115,8 @@ __global__ __launch_bounds__(256) void attn_decode_split_kernel(
     __shared__ float sm_m[16][G];
     __shared__ float sm_l[16][G];
     __shared__ int s_last;
+    __shared__ float s_w[G * MAX_SPLITS];
+    __shared__ float s_den[G];
 
     const size_t ml_base = ((size_t)b * Hq + (size_t)kvh * G) * S + split;
     if (ks >= ke) {
@@ -99,7 +124,7 @@ __global__ __launch_bounds__(256) void attn_decode_split_kernel(
             part_ml[(ml_base + (size_t)tid * S) * 2 + 0] = -INFINITY;
             part_ml[(ml_base + (size_t)tid * S) * 2 + 1] = 0.f;
         }
-        if (counters) combine_if_last<G>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, &s_last);
+        if (counters) combine_if_last<G>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, &s_last, s_w, s_den);
         return;
     }
 
@@ -208,27 +233,17 @@ __global__ __launch_bounds__(256) void attn_decode_split_kernel(
             part_ml[pi * 2 + 1] = L;
         }
     }
-    if (counters) combine_if_last<G>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, &s_last);
+    if (counters) combine_if_last<G>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, &s_last, s_w, s_den);
 }
 
-__global__ __launch_bounds__(128) void attn_decode_combine_kernel(const float* __restrict__ part_o,
+template <int G>
+__global__ __launch_bounds__(256) void attn_decode_combine_kernel(const float* __restrict__ part_o,
                                                                   const float* __restrict__ part_ml,
                                                                   bf16* __restrict__ out, int out_stride, int Hq,
-                                                                  int S) {
-    constexpr int D = 128;
-    const int bh = blockIdx.x, b = bh / Hq, h = bh % Hq, d = threadIdx.x;
-    const float* ml = part_ml + (size_t)bh * S * 2;
-    float M = -INFINITY;
-    for (int s = 0; s < S; ++s) M = fmaxf(M, ml[2 * s]);
-    float num = 0.f, den = 0.f;
-    for (int s = 0; s < S; ++s) {
-        const float ms = ml[2 * s];
-        if (ms == -INFINITY) continue;
-        const float w = exp2f(ms - M);
-        num += w * part_o[((size_t)bh * S + s) * D + d];
-        den += w * ml[2 * s + 1];
-    }
-    out[(size_t)b * out_stride + h * D + d] = (bf16)(den > 0.f ? num / den : 0.f);
+                                                                  int Hkv, int S) {
+    __shared__ float s_w[G * MAX_SPLITS];
+    __shared__ float s_den[G];
+    combine_group<G>(part_o, part_ml, out, out_stride, blockIdx.x / Hkv, blockIdx.x % Hkv, Hq, S, s_w, s_den);
 }
 
 MRSUM_API int mrsum_attn_decode(const void* q, int q_stride, const void* kcache, const void* vcache,
@@ -236,7 +251,7 @@ MRSUM_API int mrsum_attn_decode(const void* q, int q_stride, const void* kcache,
                                 void* part_ml, void* out, int out_stride, int B, int Hq, int Hkv, int D, int P,
                                 int S, float scale, int* counters, hipStream_t s) {
     if (B <= 0) return 0;
-    if (D != 128 || Hq % Hkv || S < 1 || P % 16) return (int)hipErrorInvalidValue;
+    if (D != 128 || Hq % Hkv || S < 1 || S > MAX_SPLITS || P % 16) return (int)hipErrorInvalidValue;
     const int G = Hq / Hkv;
     const float sl = scale * 1.4426950408889634f;
     dim3 grid(S, Hkv, B), block(256);
@@ -251,6 +266,11 @@ MRSUM_API int mrsum_attn_decode(const void* q, int q_stride, const void* kcache,
     }
     int e = (int)hipGetLastError();
     if (e || counters) return e;
-    attn_decode_combine_kernel<<<B * Hq, 128, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, S);
+    switch (G) {
+        case 1: attn_decode_combine_kernel<1><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
+        case 2: attn_decode_combine_kernel<2><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
+        case 4: attn_decode_combine_kernel<4><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
+        case 8: attn_decode_combine_kernel<8><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
+    }
     return (int)hipGetLastError();
 }

@@ -226,9 +226,9 @@ def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int,
     return out
 
 
-def decode_splits(batch: int, hkv: int, max_ctx: int, target_wgs: int = 2048) -> int:
+def decode_splits(batch: int, hkv: int, max_ctx: int, target_wgs: int = 2048, max_splits: int = 32) -> int:
     s = max(1, -(-target_wgs // max(1, batch * hkv)))
-    s = min(s, 64, max(1, -(-max_ctx // 64)))
+    s = min(s, max_splits, max(1, -(-max_ctx // 64)))
     return s
 
 

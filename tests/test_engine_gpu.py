@@ -50,14 +50,14 @@ def test_graph_equals_eager(eng):
     assert [o.token_ids for o in a] == [o.token_ids for o in b]
 
 
-def test_batching_invariance(eng):
+def test_order_invariance(eng):
+    """Per-request seeds + row-independent kernels: permuting the batch permutes the outputs."""
     prompts = _prompts()
     sp = [SamplingParams(10, 0.3, 100 + i) for i in range(len(prompts))]
-    together = eng.generate(prompts, sp)
-    alone = [eng.generate([p], [s])[0] for p, s in zip(prompts, sp)]
-    # seeds are per request and counter-based; only bf16 GEMM rounding differs between batch shapes
-    same = sum(a == b for x, y in zip(together, alone) for a, b in zip(x.token_ids, y.token_ids))
-    assert same >= 0.8 * sum(len(x.token_ids) for x in together)
+    a = eng.generate(prompts, sp)
+    b = eng.generate(prompts[::-1], sp[::-1])[::-1]
+    same = sum(x.token_ids == y.token_ids for x, y in zip(a, b))
+    assert same >= len(prompts) - 1
 
 
 def test_many_sequences_compaction(eng):

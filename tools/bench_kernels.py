@@ -17,19 +17,17 @@ from llm_map_reduce_summarizer_amd.ops import hip  # noqa: E402
 
 
 def timeit(fn, iters=50, warm=5):
+    """Back-to-back launches (as in a decode graph): mean per call."""
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ts = []
+    s.record()
     for _ in range(iters):
-        s.record()
         fn()
-        e.record()
-        e.synchronize()
-        ts.append(s.elapsed_time(e) * 1e-3)
-    ts.sort()
-    return ts[len(ts) // 2]
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) * 1e-3 / iters
 
 
 def main():
@@ -39,7 +37,7 @@ def main():
     shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336),
               "lm_head": (128256, 4096)}
     # a few big weights so every call streams from HBM (working set >> 256 MiB L3)
-    for name, (N, K) in shapes.items():
+    for name, (N, K) in (shapes.items() if os.environ.get("GEMM", "1") == "1" else []):
         ws = [torch.randn(N, K, device=dev, dtype=torch.bfloat16) * 0.02 for _ in range(4)]
         for M in (1, 8, 16, 32, 48, 64):
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
@@ -73,11 +71,15 @@ def main():
         bt = (torch.arange(B * npg, dtype=torch.int32, device=dev).view(B, npg) + 1)
         pos = torch.full((B,), ctx - 1, dtype=torch.int32, device=dev)
         q = torch.randn(B, (hq + 2 * hkv) * d, device=dev, dtype=torch.bfloat16)
-        ws = hip.DecodeWorkspace(B, hq, d, hip.decode_splits(B, hkv, ctx), dev, hkv)
-        t = timeit(lambda: hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, 1 / math.sqrt(d), workspace=ws))
-        gb = B * ctx * hkv * d * 2 * 2 / 1e9
-        res["attn_decode"].append({"B": B, "ctx": ctx, "us": round(t * 1e6, 1), "TBps": round(gb / t / 1e3, 2)})
-        print(json.dumps(res["attn_decode"][-1]), flush=True)
+        for splits in sorted({hip.decode_splits(B, hkv, ctx), 4, 8, 16, 32}):
+            for fused in (True, False):
+                ws = hip.DecodeWorkspace(B, hq, d, splits, dev, hkv, fused_combine=fused)
+                t = timeit(lambda: hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, 1 / math.sqrt(d),
+                                                   workspace=ws))
+                gb = B * ctx * hkv * d * 2 * 2 / 1e9
+                res["attn_decode"].append({"B": B, "ctx": ctx, "S": splits, "fused": fused, "us": round(t * 1e6, 1),
+                                           "TBps": round(gb / t / 1e3, 2)})
+                print(json.dumps(res["attn_decode"][-1]), flush=True)
     # prefill attention
     for nseq, L in ((1, 4096), (8, 4096), (4, 8192)):
         T = nseq * L
