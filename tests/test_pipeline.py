@@ -123,3 +123,16 @@ def test_cli_mock_end_to_end(example_transcript, tmp_path, capsys):
     rep = json.loads(out.with_suffix(".report.json").read_text())
     assert rep["provider"] == "mock" and rep["segments"] == 600
     assert main(["-i", str(tmp_path / "missing.json"), "--provider", "mock"]) == 1
+
+
+def test_simple_aggregator_one_shot():
+    from llm_map_reduce_summarizer_amd.pipeline.simple_aggregator import SimpleAggregator, aggregate_summaries
+    prov = EchoProvider(words=5)
+    ex = LLMExecutor(config=_cfg(), provider_obj=prov)
+    out = asyncio.run(SimpleAggregator(executor=ex).aggregate(["a", "b"], {"File": "f"}))
+    assert out.startswith("word0") and len(prov.reqs) == 1
+    r = prov.reqs[0]
+    assert "SUMMARY 2:" in r.user and "- File: f" in r.user and r.temperature == pytest.approx(0.2)
+    assert r.system.strip().startswith("You are a professional transcript summarizer")
+    ex2 = LLMExecutor(config=_cfg(RETRY_ATTEMPTS=1), provider_obj=MockProvider(fault_rate=1.0))
+    assert aggregate_summaries(["x"], executor=ex2).startswith("Error generating summary: ")
