@@ -226,7 +226,9 @@ def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int,
     return out
 
 
-def decode_splits(batch: int, hkv: int, max_ctx: int, target_wgs: int = 2048, max_splits: int = 32) -> int:
+def decode_splits(batch: int, hkv: int, max_ctx: int, target_wgs: int = 1024, max_splits: int = 64) -> int:
+    """Split-K count for decode attention (measured, tools/bench_kernels.py: B=1 ctx 8k: S 32 -> 26 us vs
+    S 4 -> 110 us; B=39 ctx 4.4k: S 4..7 best at ~185 us, 3.8 TB/s; B=64: S 4 best)."""
     s = max(1, -(-target_wgs // max(1, batch * hkv)))
     s = min(s, max_splits, max(1, -(-max_ctx // 64)))
     return s
@@ -237,7 +239,10 @@ class DecodeWorkspace:
     (allocated once per batch bucket; counters start at 0 and every launch re-arms them)."""
 
     def __init__(self, batch: int, hq: int, d: int, splits: int, device, hkv: Optional[int] = None,
-                 fused_combine: bool = True):
+                 fused_combine: bool = False):
+        # fused_combine (last-arriver merge inside the split kernel) measured SLOWER than the separate
+        # merge kernel at every B >= 8 (the per-workgroup drain + agent release costs more than the
+        # launch boundary it saves: B=39 238 vs 189 us), so the separate kernel is the default.
         self.splits = splits
         self.part_o = torch.empty(batch * hq * splits * d, dtype=torch.float32, device=device)
         self.part_ml = torch.empty(batch * hq * splits * 2, dtype=torch.float32, device=device)
