@@ -274,3 +274,204 @@ MRSUM_API int mrsum_attn_decode(const void* q, int q_stride, const void* kcache,
     }
     return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// MFMA variant (page size 64): the (b, kv head, split) workgroup stages each 64-key page of K and
+// V through LDS (256 threads, 16-B coalesced loads of the contiguous 16 KiB page images, next
+// page prefetched into registers while the current one is consumed), and each wave scores 16 of
+// the 64 keys against all G query heads with MFMA:
+//   S^T[16 keys][16 heads] = K . Q^T        v_mfma_f32_16x16x32_bf16, A = K rows (ds_read_b128,
+//                                           chunks XOR-swizzled by key&15), B = Q^T in VGPRs
+//   O^T[d][head]         += V^T . P^T       v_mfma_f32_16x16x16bf16_1k: the S^T accumulator IS the
+//                                           B operand (same lane map), A = V^T from
+//                                           ds_read_b64_tr_b16 (V chunks swizzled by (key&7)<<1)
+// Softmax is per head column: 4 in-lane values + two xor shuffles per 16 keys.  No q.k lane
+// reductions, no per-key VALU dot products -- the VALU only does the online softmax.
+// Heads G <= 16 (columns >= G are computed on zero q and never stored).
+namespace {
+typedef short s4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s4v lds_s4v;
+__device__ __forceinline__ int dk_off(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
+__device__ __forceinline__ int dv_off(int row, int chunk) { return row * 256 + ((chunk ^ ((row & 7) << 1)) << 4); }
+}  // namespace
+
+template <int G>
+__global__ __launch_bounds__(256) void attn_decode_mfma_kernel(
+    const bf16* __restrict__ q, int q_stride, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ positions,
+    float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int S, float scale_log2) {
+    constexpr int D = 128, PG = 64;
+    __shared__ __attribute__((aligned(16))) char lds[2 * PG * 256 + 2 * 4 * 16 * 4];
+    char* ldsK = lds;
+    char* ldsV = lds + PG * 256;
+    float* sm_ml = reinterpret_cast<float*>(lds + 2 * PG * 256);  // [2][4 waves][16 heads]
+
+    const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+    const int Hq = Hkv * G;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 15, grp = lane >> 4;
+    const int ctx = positions[b] + 1;
+    int chunk = (ctx + S - 1) / S;
+    chunk = (chunk + PG - 1) & ~(PG - 1);
+    const int ks = split * chunk;
+    const int ke = min(ctx, ks + chunk);
+    const size_t ml_base = ((size_t)b * Hq + (size_t)kvh * G) * S + split;
+    if (ks >= ke) {
+        if (tid < G) {
+            part_ml[(ml_base + (size_t)tid * S) * 2 + 0] = -INFINITY;
+            part_ml[(ml_base + (size_t)tid * S) * 2 + 1] = 0.f;
+        }
+        return;
+    }
+    const int ntiles = (ke - ks + PG - 1) / PG;
+
+    // Q^T fragments (B operand of 16x16x32): lane holds Q[head col][dims 32k + 8grp .. +8]
+    bf16x8 qf[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (col < G) v = *reinterpret_cast<const uint4*>(q + (size_t)b * q_stride + (kvh * G + col) * D + 32 * k + 8 * grp);
+        qf[k] = __builtin_bit_cast(bf16x8, v);
+    }
+
+    const int* bt = block_tables + (size_t)b * bt_stride + ks / PG;
+    const int st_row = tid >> 4, st_chunk = tid & 15;
+    uint4 kreg[4], vreg[4];
+    auto load_tile = [&](int t) {
+        const int page = bt[t];
+        const size_t base = ((size_t)page * Hkv + kvh) * PG * D;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const size_t off = base + (size_t)(st_row + 16 * i) * D + st_chunk * 8;
+            kreg[i] = *reinterpret_cast<const uint4*>(kc + off);
+            vreg[i] = *reinterpret_cast<const uint4*>(vc + off);
+        }
+    };
+    auto store_tile = [&]() {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = st_row + 16 * i;
+            *reinterpret_cast<uint4*>(ldsK + dk_off(row, st_chunk)) = kreg[i];
+            *reinterpret_cast<uint4*>(ldsV + dv_off(row, st_chunk)) = vreg[i];
+        }
+    };
+
+    f32x4 o[8];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float m = -INFINITY, lsum = 0.f;
+
+    load_tile(0);
+    store_tile();
+    __syncthreads();
+    for (int t = 0; t < ntiles; ++t) {
+        if (t + 1 < ntiles) load_tile(t + 1);
+        const int key0 = ks + t * PG + 16 * w;  // this wave's 16 keys
+        if (key0 < ke) {                         // wave-uniform
+            f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint4 a = *reinterpret_cast<const uint4*>(ldsK + dk_off(16 * w + col, 4 * k + grp));
+                sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), qf[k], sacc, 0, 0, 0);
+            }
+            float sv[4];
+            float mt = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int key = key0 + 4 * grp + j;
+                sv[j] = key < ke ? sacc[j] * scale_log2 : -INFINITY;
+                mt = fmaxf(mt, sv[j]);
+            }
+            mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+            mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+            const float mn = fmaxf(m, mt);  // finite: key0 < ke is a valid key for every head
+            const float alpha = exp2f(m - mn);
+            m = mn;
+            float pj[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pj[j] = exp2f(sv[j] - mn);
+            lsum = lsum * alpha + (pj[0] + pj[1]) + (pj[2] + pj[3]);
+            s4v pb;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pb[j] = __builtin_bit_cast(short, (bf16)pj[j]);
+            const int q4 = col >> 2, p4 = col & 3;
+            const int vrow = 16 * w + 4 * grp + q4;
+#pragma unroll
+            for (int dt = 0; dt < 8; ++dt) {
+                o[dt] *= alpha;
+                const s4v a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                    (lds_s4v*)(ldsV + dv_off(vrow, 2 * dt + (p4 >> 1)) + 8 * (p4 & 1)));
+                o[dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pb, o[dt], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+        if (t + 1 < ntiles) {
+            store_tile();
+            __syncthreads();
+        }
+    }
+
+    // merge the 4 waves: lane (grp, col) holds O^T[d = 16dt + 4grp + j][head col]
+    lsum += __shfl_xor(lsum, 16, 64);
+    lsum += __shfl_xor(lsum, 32, 64);
+    float* sm_o = reinterpret_cast<float*>(lds);  // [4][128][16] f32 = 32 KiB, reuses the tile buffers
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sm_o[(w * D + 16 * dt + 4 * grp + j) * 16 + col] = o[dt][j];
+    if (grp == 0) {
+        sm_ml[w * 16 + col] = m;
+        sm_ml[64 + w * 16 + col] = lsum;
+    }
+    __syncthreads();
+    for (int i = tid; i < G * D; i += 256) {
+        const int h = i / D, d = i % D;
+        float M = -INFINITY;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, sm_ml[ww * 16 + h]);
+        float acc = 0.f, L = 0.f;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) {
+            const float mw = sm_ml[ww * 16 + h];
+            const float wt = mw == -INFINITY ? 0.f : exp2f(mw - M);
+            acc += wt * sm_o[(ww * D + d) * 16 + h];
+            L += wt * sm_ml[64 + ww * 16 + h];
+        }
+        const size_t pi = ml_base + (size_t)h * S;
+        part_o[pi * D + d] = acc;
+        if (d == 0) {
+            part_ml[pi * 2 + 0] = M;
+            part_ml[pi * 2 + 1] = L;
+        }
+    }
+}
+
+MRSUM_API int mrsum_attn_decode_mfma(const void* q, int q_stride, const void* kcache, const void* vcache,
+                                     const int* block_tables, int bt_stride, const int* positions, void* part_o,
+                                     void* part_ml, void* out, int out_stride, int B, int Hq, int Hkv, int D, int P,
+                                     int S, float scale, hipStream_t s) {
+    if (B <= 0) return 0;
+    if (D != 128 || P != 64 || Hq % Hkv || Hq / Hkv > 16 || S < 1 || S > MAX_SPLITS) return (int)hipErrorInvalidValue;
+    const int G = Hq / Hkv;
+    const float sl = scale * 1.4426950408889634f;
+    dim3 grid(S, Hkv, B), block(256);
+    auto Qp = (const bf16*)q; auto K = (const bf16*)kcache; auto V = (const bf16*)vcache;
+    auto PO = (float*)part_o; auto PM = (float*)part_ml;
+    switch (G) {
+        case 1: attn_decode_mfma_kernel<1><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, S, sl); break;
+        case 2: attn_decode_mfma_kernel<2><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, S, sl); break;
+        case 4: attn_decode_mfma_kernel<4><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, S, sl); break;
+        case 8: attn_decode_mfma_kernel<8><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, S, sl); break;
+        case 16: attn_decode_mfma_kernel<16><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, S, sl); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    int e = (int)hipGetLastError();
+    if (e) return e;
+    switch (G) {
+        case 1: attn_decode_combine_kernel<1><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
+        case 2: attn_decode_combine_kernel<2><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
+        case 4: attn_decode_combine_kernel<4><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
+        case 8: attn_decode_combine_kernel<8><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
+        case 16: attn_decode_combine_kernel<16><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
+    }
+    return (int)hipGetLastError();
+}

@@ -10,6 +10,7 @@ is capturable in a hipGraph (``torch.cuda.CUDAGraph``).
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -30,6 +31,8 @@ _SIGS = {
     "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_attn_decode": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
                           _c_int, _c_int, _c_int, _c_float, _vp, _vp],
+    "mrsum_attn_decode_mfma": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int,
+                               _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_sample": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp,
@@ -250,14 +253,19 @@ class DecodeWorkspace:
                          if fused_combine else None)
 
 
+DECODE_ATTN_IMPL = os.environ.get("MRSUM_DECODE_ATTN", "mfma")
+
+
 def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, block_tables: torch.Tensor,
                 positions: torch.Tensor, hq: int, hkv: int, d: int, page: int, scale: float,
                 out: Optional[torch.Tensor] = None, num_splits: Optional[int] = None,
-                workspace: Optional[DecodeWorkspace] = None) -> torch.Tensor:
+                workspace: Optional[DecodeWorkspace] = None, impl: Optional[str] = None) -> torch.Tensor:
+    """Paged decode attention.  impl "mfma" (page 64, G <= 16: K/V pages staged through LDS, QK^T and PV
+    on MFMA) or "valu" (any page % 16, G in 1/2/4/8: lane-sliced dot products)."""
     _bf16_cuda(q, kcache, vcache)
     _rows_ok(q)
     B = q.shape[0]
-    _req(d == 128 and hq % hkv == 0 and (hq // hkv) in (1, 2, 4, 8) and page % 16 == 0, "attn_decode: bad config")
+    _req(d == 128 and hq % hkv == 0 and (hq // hkv) in (1, 2, 4, 8, 16) and page % 16 == 0, "attn_decode: bad config")
     _req(tuple(kcache.shape[1:]) == (hkv, page, d) and kcache.is_contiguous() and vcache.is_contiguous(),
          "attn_decode: cache must be [pages, Hkv, P, D]")
     _i32(block_tables, positions)
@@ -270,6 +278,13 @@ def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, blo
     if out is None:
         out = torch.empty(B, hq * d, dtype=q.dtype, device=q.device)
     _rows_ok(out)
+    impl = impl or DECODE_ATTN_IMPL
+    if impl == "mfma" and page == 64 and hq // hkv <= 16 and workspace.counters is None:
+        _check(_fn("mrsum_attn_decode_mfma")(_p(q), q.stride(0), _p(kcache), _p(vcache), _p(block_tables),
+                                             block_tables.stride(0), _p(positions), _p(workspace.part_o),
+                                             _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
+                                             workspace.splits, scale, _stream()), "attn_decode_mfma")
+        return out
     _check(_fn("mrsum_attn_decode")(_p(q), q.stride(0), _p(kcache), _p(vcache), _p(block_tables),
                                     block_tables.stride(0), _p(positions), _p(workspace.part_o),
                                     _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,

@@ -107,19 +107,22 @@ def test_attn_prefill_spike():
     _close(hip.attn_prefill(qkv, cu, hq, hkv, d, sc), reference.attn_prefill(qkv, cu, hq, hkv, d, sc), 2e-2)
 
 
-@pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (4, 4)])
+@pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (4, 4), (16, 1)])
 @pytest.mark.parametrize("splits", [1, 3, 16])
-@pytest.mark.parametrize("fused", [True, False])
-def test_attn_decode(hq, hkv, splits, fused):
+@pytest.mark.parametrize("impl", ["mfma", "valu", "valu_fused"])
+def test_attn_decode(hq, hkv, splits, impl):
+    if impl != "mfma" and hq // hkv == 16:
+        pytest.skip("valu kernel supports G <= 8")
+    fused = impl == "valu_fused"
     d, page = 128, 64
-    ctxs = [1, 65, 700, 129]
+    ctxs = [1, 65, 700, 129, 64, 1000]
     B = len(ctxs)
     n_pages = 64
     g = torch.Generator().manual_seed(13)
     kc = (torch.randn(n_pages, hkv, page, d, generator=g)).to(torch.bfloat16).to(DEV)
     vc = (torch.randn(n_pages, hkv, page, d, generator=g)).to(torch.bfloat16).to(DEV)
     perm = torch.randperm(n_pages - 1, generator=g) + 1
-    bt = torch.zeros(B, 16, dtype=torch.int32)
+    bt = torch.zeros(B, 20, dtype=torch.int32)
     used = 0
     for b, c in enumerate(ctxs):
         npg = -(-c // page)
@@ -132,7 +135,7 @@ def test_attn_decode(hq, hkv, splits, fused):
     ws = hip.DecodeWorkspace(B, hq, d, splits, DEV, hkv, fused_combine=fused)
     o2 = reference.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc)
     for _ in range(3):  # replays re-use (and must re-arm) the arrival counters
-        o1 = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws)
+        o1 = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws, impl=impl[:4])
         _close(o1, o2, 2e-2)
     if fused:
         assert int(ws.counters.abs().sum()) == 0

@@ -72,12 +72,13 @@ def main():
         pos = torch.full((B,), ctx - 1, dtype=torch.int32, device=dev)
         q = torch.randn(B, (hq + 2 * hkv) * d, device=dev, dtype=torch.bfloat16)
         for splits in sorted({hip.decode_splits(B, hkv, ctx), 4, 8, 16, 32}):
-            for fused in (True, False):
+            for impl in ("mfma", "valu"):
+                fused = False
                 ws = hip.DecodeWorkspace(B, hq, d, splits, dev, hkv, fused_combine=fused)
                 t = timeit(lambda: hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, 1 / math.sqrt(d),
-                                                   workspace=ws))
+                                                   workspace=ws, impl=impl))
                 gb = B * ctx * hkv * d * 2 * 2 / 1e9
-                res["attn_decode"].append({"B": B, "ctx": ctx, "S": splits, "fused": fused, "us": round(t * 1e6, 1),
+                res["attn_decode"].append({"B": B, "ctx": ctx, "S": splits, "impl": impl, "us": round(t * 1e6, 1),
                                            "TBps": round(gb / t / 1e3, 2)})
                 print(json.dumps(res["attn_decode"][-1]), flush=True)
     # prefill attention
