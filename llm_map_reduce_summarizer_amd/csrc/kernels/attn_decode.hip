@@ -296,7 +296,7 @@ __device__ __forceinline__ int dv_off(int row, int chunk) { return row * 256 + (
 }  // namespace
 
 template <int G>
-__global__ __launch_bounds__(256) void attn_decode_mfma_kernel(
+__global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
     const bf16* __restrict__ q, int q_stride, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ positions,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int S, float scale_log2) {
@@ -335,65 +335,65 @@ __global__ __launch_bounds__(256) void attn_decode_mfma_kernel(
 
     const int* bt = block_tables + (size_t)b * bt_stride + ks / PG;
     const int st_row = tid >> 4, st_chunk = tid & 15;
-    uint4 kreg[4], vreg[4];
-    auto load_tile = [&](int t) {
-        const int page = bt[t];
-        const size_t base = ((size_t)page * Hkv + kvh) * PG * D;
+    const size_t head_off = (size_t)kvh * PG * D + (size_t)st_row * D + st_chunk * 8;
+    // staging registers are plain named arrays indexed only by unrolled constants (a lambda
+    // capturing them by reference put them in scratch), and the prefetch is unconditional
+    // (the last tile is re-read instead of branching) so hipcc keeps the loads in flight.
+    u32x4 kreg[4], vreg[4];
+    {
+        const size_t base = (size_t)bt[0] * Hkv * PG * D + head_off;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const size_t off = base + (size_t)(st_row + 16 * i) * D + st_chunk * 8;
-            kreg[i] = *reinterpret_cast<const uint4*>(kc + off);
-            vreg[i] = *reinterpret_cast<const uint4*>(vc + off);
+            kreg[i] = *reinterpret_cast<const u32x4*>(kc + base + (size_t)16 * i * D);
+            vreg[i] = *reinterpret_cast<const u32x4*>(vc + base + (size_t)16 * i * D);
         }
-    };
-    auto store_tile = [&]() {
+    }
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int row = st_row + 16 * i;
-            *reinterpret_cast<uint4*>(ldsK + dk_off(row, st_chunk)) = kreg[i];
-            *reinterpret_cast<uint4*>(ldsV + dv_off(row, st_chunk)) = vreg[i];
-        }
-    };
+    for (int i = 0; i < 4; ++i) {
+        *reinterpret_cast<u32x4*>(ldsK + dk_off(st_row + 16 * i, st_chunk)) = kreg[i];
+        *reinterpret_cast<u32x4*>(ldsV + dv_off(st_row + 16 * i, st_chunk)) = vreg[i];
+    }
 
     f32x4 o[8];
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
     float m = -INFINITY, lsum = 0.f;
-
-    load_tile(0);
-    store_tile();
+    const int q4 = col >> 2, p4 = col & 3;
     __syncthreads();
+
     for (int t = 0; t < ntiles; ++t) {
-        if (t + 1 < ntiles) load_tile(t + 1);
+        {
+            const int tn = min(t + 1, ntiles - 1);
+            const size_t base = (size_t)bt[tn] * Hkv * PG * D + head_off;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                kreg[i] = *reinterpret_cast<const u32x4*>(kc + base + (size_t)16 * i * D);
+                vreg[i] = *reinterpret_cast<const u32x4*>(vc + base + (size_t)16 * i * D);
+            }
+        }
         const int key0 = ks + t * PG + 16 * w;  // this wave's 16 keys
-        if (key0 < ke) {                         // wave-uniform
+        if (key0 < ke) {
             f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const uint4 a = *reinterpret_cast<const uint4*>(ldsK + dk_off(16 * w + col, 4 * k + grp));
                 sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), qf[k], sacc, 0, 0, 0);
             }
-            float sv[4];
-            float mt = -INFINITY;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int key = key0 + 4 * grp + j;
-                sv[j] = key < ke ? sacc[j] * scale_log2 : -INFINITY;
-                mt = fmaxf(mt, sv[j]);
-            }
+            const int kb = key0 + 4 * grp;
+            const float s0 = kb + 0 < ke ? sacc[0] * scale_log2 : -INFINITY;
+            const float s1 = kb + 1 < ke ? sacc[1] * scale_log2 : -INFINITY;
+            const float s2 = kb + 2 < ke ? sacc[2] * scale_log2 : -INFINITY;
+            const float s3 = kb + 3 < ke ? sacc[3] * scale_log2 : -INFINITY;
+            float mt = fmaxf(fmaxf(s0, s1), fmaxf(s2, s3));
             mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
             mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
             const float mn = fmaxf(m, mt);  // finite: key0 < ke is a valid key for every head
             const float alpha = exp2f(m - mn);
             m = mn;
-            float pj[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) pj[j] = exp2f(sv[j] - mn);
-            lsum = lsum * alpha + (pj[0] + pj[1]) + (pj[2] + pj[3]);
-            s4v pb;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) pb[j] = __builtin_bit_cast(short, (bf16)pj[j]);
-            const int q4 = col >> 2, p4 = col & 3;
+            const float p0 = exp2f(s0 - mn), p1 = exp2f(s1 - mn), p2 = exp2f(s2 - mn), p3 = exp2f(s3 - mn);
+            lsum = lsum * alpha + (p0 + p1) + (p2 + p3);
+            const s4v pb = {__builtin_bit_cast(short, (bf16)p0), __builtin_bit_cast(short, (bf16)p1),
+                            __builtin_bit_cast(short, (bf16)p2), __builtin_bit_cast(short, (bf16)p3)};
             const int vrow = 16 * w + 4 * grp + q4;
 #pragma unroll
             for (int dt = 0; dt < 8; ++dt) {
@@ -405,7 +405,11 @@ __global__ __launch_bounds__(256) void attn_decode_mfma_kernel(
         }
         __syncthreads();
         if (t + 1 < ntiles) {
-            store_tile();
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                *reinterpret_cast<u32x4*>(ldsK + dk_off(st_row + 16 * i, st_chunk)) = kreg[i];
+                *reinterpret_cast<u32x4*>(ldsV + dv_off(st_row + 16 * i, st_chunk)) = vreg[i];
+            }
             __syncthreads();
         }
     }
