@@ -229,9 +229,10 @@ def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int,
     return out
 
 
-def decode_splits(batch: int, hkv: int, max_ctx: int, target_wgs: int = 1024, max_splits: int = 64) -> int:
-    """Split-K count for decode attention (measured, tools/bench_kernels.py: B=1 ctx 8k: S 32 -> 26 us vs
-    S 4 -> 110 us; B=39 ctx 4.4k: S 4..7 best at ~185 us, 3.8 TB/s; B=64: S 4 best)."""
+def decode_splits(batch: int, hkv: int, max_ctx: int, target_wgs: int = 1024, max_splits: int = 32) -> int:
+    """Split-K count for decode attention (measured, MFMA kernel, tools/bench_kernels.py: B=1 ctx 8k: S 16-32
+    -> 18 us vs S 4 -> 40 us; B=8 ctx 4k: S 8 -> 27 us (5.0 TB/s); B=39 ctx 4.4k: S 4-8 -> 131-140 us
+    (5.0-5.35 TB/s); B=64 ctx 2k: S 2-4 -> 104 us)."""
     s = max(1, -(-target_wgs // max(1, batch * hkv)))
     s = min(s, max_splits, max(1, -(-max_ctx // 64)))
     return s
