@@ -9,12 +9,13 @@
 //          clamped to [0, V) so a bad id can never read out of bounds.
 #include "common.h"
 
+// grid (F/8/256 column blocks, T rows): no 64-bit div/mod per element (a size_t i / fv here cost
+// ~20 us per call at T=48, more than the memory traffic).
 __global__ __launch_bounds__(256) void swiglu_kernel(const bf16* __restrict__ gu, bf16* __restrict__ out, int T,
                                                      int F) {
     const int fv = F >> 3;
-    const size_t n = (size_t)T * fv;
-    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-        const size_t r = i / fv, c = i % fv;  // output features [8c, 8c+8)
+    const int r = blockIdx.y;
+    for (int c = blockIdx.x * 256 + threadIdx.x; c < fv; c += gridDim.x * 256) {  // output features [8c, 8c+8)
         const uint4* row = reinterpret_cast<const uint4*>(gu + r * 2 * (size_t)F);
         float g[8], u[8];  // 16-B vector 2c = gate features [8c, 8c+8), 2c+1 = the matching up
         unpack8(row[2 * c], g);
@@ -28,9 +29,12 @@ __global__ __launch_bounds__(256) void swiglu_kernel(const bf16* __restrict__ gu
 MRSUM_API int mrsum_swiglu(const void* gu, void* out, int T, int F, hipStream_t s) {
     if (T <= 0) return 0;
     if (F % 8) return (int)hipErrorInvalidValue;
-    const size_t n = (size_t)T * (F / 8);
-    const int blocks = (int)std::min<size_t>((n + 255) / 256, 256 * 16);
-    swiglu_kernel<<<blocks, 256, 0, s>>>((const bf16*)gu, (bf16*)out, T, F);
+    const int cb = std::min(ceil_div(F / 8, 256), 64);
+    for (int t0 = 0; t0 < T; t0 += 65535) {  // grid.y limit
+        const int tn = std::min(T - t0, 65535);
+        swiglu_kernel<<<dim3(cb, tn), 256, 0, s>>>((const bf16*)gu + (size_t)t0 * 2 * F, (bf16*)out + (size_t)t0 * F,
+                                                   tn, F);
+    }
     return (int)hipGetLastError();
 }
 

@@ -195,3 +195,134 @@ MRSUM_API int mrsum_skinny_gemm(const void* x, int ldx, const void* W, int N, in
     }
     return (int)hipErrorInvalidValue;
 }
+
+
+// ---------------------------------------------------------------------------------------------
+// Medium-M variant (16 < M <= 64): x is shared by every W row, so at these M the per-wave x
+// fragment loads of the kernel above dominate its instruction stream.  Here the workgroup stages
+// each 128-wide k block of x ONCE into LDS (double-buffered, 16-B chunks XOR-swizzled by row&15
+// for conflict-free ds_read_b128), and each of the 4 waves streams its own 16 W rows over the
+// FULL k range (or the split's k range) straight from HBM into A fragments, prefetched one block
+// ahead.  No cross-wave reduction: the epilogue goes straight from the accumulators (SwiGLU pairs
+// gate/up across the lane halves with one xor-32 shuffle).
+namespace {
+__device__ __forceinline__ int xs_off(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
+}
+
+template <int MT, int EPI>
+__global__ __launch_bounds__(256) void skinny_lds_kernel(const bf16* __restrict__ x, int ldx,
+                                                         const bf16* __restrict__ W, int K, int M,
+                                                         void* __restrict__ out, int ldo, int kper) {
+    constexpr int BM = 16 * MT;
+    constexpr int XCH = BM * 16 / 256;  // 16-B x chunks per thread per k block (BM rows x 16 chunks)
+    __shared__ __attribute__((aligned(16))) char xl[2][BM * 256];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, g = lane >> 4;
+    const int n0 = blockIdx.x * 64 + 16 * w;  // this wave's 16 W rows
+    const int ks = blockIdx.y * kper, ke = min(K, ks + kper);
+    const int nkb = (ke - ks) / 128;
+
+    // x staging: chunk id = tid + 256 i -> row = id / 16, chunk = id % 16
+    u32x4 xr[XCH];
+#define LOAD_X(kb)                                                                                         \
+    _Pragma("unroll") for (int i = 0; i < XCH; ++i) xr[i] = *reinterpret_cast<const u32x4*>(               \
+        x + (size_t)min((tid + 256 * i) >> 4, M - 1) * ldx + (kb) + ((tid + 256 * i) & 15) * 8);
+#define STORE_X(buf)                                                                                       \
+    _Pragma("unroll") for (int i = 0; i < XCH; ++i)                                                        \
+        *reinterpret_cast<u32x4*>(&xl[buf][xs_off((tid + 256 * i) >> 4, (tid + 256 * i) & 15)]) = xr[i];
+    const bf16* wrow = W + (size_t)(n0 + r) * K + 8 * g;
+    u32x4 a0[4], a1[4];
+#define LOAD_A(dst, kb) \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) dst[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow + (kb) + 32 * i));
+
+    f32x4 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    LOAD_X(ks);
+    LOAD_A(a0, ks);
+    STORE_X(0);
+    __syncthreads();
+    // two k blocks per trip so the A register sets and LDS buffers have static roles (rule 20)
+#define STEP(j, USE, PREF, CUR)                                                                            \
+    {                                                                                                      \
+        const int kn = ks + min((j) + 1, nkb - 1) * 128; /* unconditional prefetch (last block re-read) */ \
+        LOAD_X(kn);                                                                                        \
+        LOAD_A(PREF, kn);                                                                                  \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                    \
+            _Pragma("unroll") for (int m = 0; m < MT; ++m) {                                               \
+                const u32x4 bv = *reinterpret_cast<const u32x4*>(&xl[CUR][xs_off(16 * m + r, 4 * i + g)]); \
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, USE[i]),       \
+                                                                 __builtin_bit_cast(bf16x8, bv), acc[m], 0, 0, 0); \
+            }                                                                                              \
+        }                                                                                                  \
+        STORE_X(CUR ^ 1);                                                                                  \
+        __syncthreads();                                                                                   \
+    }
+    for (int j = 0; j < nkb; j += 2) {
+        STEP(j, a0, a1, 0);
+        if (j + 1 >= nkb) break;
+        STEP(j + 1, a1, a0, 1);
+    }
+#undef STEP
+#undef LOAD_X
+#undef STORE_X
+#undef LOAD_A
+
+    // C: lane holds out^T[n = n0 + 4g + j][m = 16 mt + r]
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const int mm = 16 * m + r;
+        if constexpr (EPI == EPI_SWIGLU) {
+            // rows 0-7 of the wave tile = gate (g 0,1), rows 8-15 = up (g 2,3) of features blockIdx.x*32 + 8w + ...
+            f32x4 up;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) up[jj] = __shfl_xor(acc[m][jj], 32, 64);
+            if (g < 2 && mm < M) {
+                float rr[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const float gv = acc[m][jj];
+                    rr[jj] = gv / (1.f + __expf(-gv)) * up[jj];
+                }
+                uint2 o;
+                o.x = pack2(rr[0], rr[1]);
+                o.y = pack2(rr[2], rr[3]);
+                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + (n0 >> 1) + 4 * g) = o;
+            }
+        } else if (mm < M) {
+            if constexpr (EPI == EPI_BF16) {
+                uint2 o;
+                o.x = pack2(acc[m][0], acc[m][1]);
+                o.y = pack2(acc[m][2], acc[m][3]);
+                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + n0 + 4 * g) = o;
+            } else {
+                float* o = reinterpret_cast<float*>(out) + ((size_t)blockIdx.y * M + mm) * ldo + n0 + 4 * g;
+                *reinterpret_cast<float4*>(o) = make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
+            }
+        }
+    }
+}
+
+// Same contract as mrsum_skinny_gemm; N % 64 == 0, 16 < M <= 64 (also valid for M <= 16).
+MRSUM_API int mrsum_skinny_lds(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
+                               int epi, int splits, hipStream_t s) {
+    if (M <= 0) return 0;
+    if (M > 64 || K % KB || N % 64 || splits < 1 || (K / KB) % splits) return (int)hipErrorInvalidValue;
+    if (epi != EPI_F32_PARTIAL && splits != 1) return (int)hipErrorInvalidValue;
+    const int kper = K / splits;
+    const int mt = (M + 15) / 16;
+    dim3 grid(N / 64, splits);
+    auto X = (const bf16*)x; auto Wp = (const bf16*)W;
+#define L(MT_, EPI_) skinny_lds_kernel<MT_, EPI_><<<grid, 256, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper)
+#define BY_EPI(MT_) \
+    if (epi == EPI_BF16) L(MT_, EPI_BF16); else if (epi == EPI_F32_PARTIAL) L(MT_, EPI_F32_PARTIAL); else L(MT_, EPI_SWIGLU);
+    switch (mt) {
+        case 1: BY_EPI(1); break;
+        case 2: BY_EPI(2); break;
+        case 3: BY_EPI(3); break;
+        default: BY_EPI(4); break;
+    }
+#undef BY_EPI
+#undef L
+    return (int)hipGetLastError();
+}

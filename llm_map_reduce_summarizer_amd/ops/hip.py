@@ -34,6 +34,7 @@ _SIGS = {
     "mrsum_attn_decode_mfma": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int,
                                _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
+    "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _vp],
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_sample": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp,
                      _c_int, _vp],
@@ -339,6 +340,20 @@ def _skinny(x, w, out, epi, nt, splits, ldo):
     return out
 
 
+def _skinny_lds(x, w, out, epi, splits, ldo):
+    """Medium-M (x staged in LDS) variant; same contract as _skinny with nt fixed at 64-row tiles."""
+    _bf16_cuda(x, w)
+    _rows_ok(x)
+    M, K = x.shape
+    N = w.shape[0]
+    _req(w.is_contiguous() and w.shape[1] == K, "skinny_lds: weight must be [N, K] contiguous")
+    _req(1 <= M <= SKINNY_MAX_M and K % 128 == 0 and N % 64 == 0 and (K // 128) % splits == 0,
+         "skinny_lds: unsupported shape M=%d N=%d K=%d S=%d" % (M, N, K, splits))
+    _check(_fn("mrsum_skinny_lds")(_p(x), x.stride(0), _p(w), N, K, M, _p(out), ldo, epi, splits, _stream()),
+           "skinny_lds")
+    return out
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """x @ w^T, bf16 out; MFMA weight-streaming kernel for M <= 64, hipBLASLt above."""
     M = x.shape[0]
@@ -353,19 +368,23 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
 
 
 def linear_parts(x: torch.Tensor, w: torch.Tensor, splits: Optional[int] = None,
-                 out: Optional[torch.Tensor] = None, nt: int = 1) -> torch.Tensor:
-    """fp32 split-K slabs [S, M, N] of x @ w^T (summed by add_rmsnorm_parts / rope_kv_parts)."""
+                 out: Optional[torch.Tensor] = None, nt: int = 1, kernel: str = "skinny") -> torch.Tensor:
+    """fp32 split-K slabs [S, M, N] of x @ w^T (summed by add_rmsnorm_parts / rope_kv_parts).
+    kernel "skinny" (waves split k, nt 16-row tiles) or "lds" (x staged in LDS, 64-row tiles)."""
     M, K = x.shape
     N = w.shape[0]
     if splits is None:
-        splits = choose_splits(N, K, nt)
+        splits = choose_splits(N, K, nt if kernel == "skinny" else 4)
     if out is None:
         out = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
     _req(out.is_contiguous() and out.shape == (splits, M, N) and out.dtype == torch.float32, "linear_parts: bad out")
+    if kernel == "lds":
+        return _skinny_lds(x, w, out, EPI_F32_PARTIAL, splits, N)
     return _skinny(x, w, out, EPI_F32_PARTIAL, nt, splits, N)
 
 
-def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tensor] = None,
+                  kernel: str = "skinny") -> torch.Tensor:
     """silu(gate) * up straight out of the gate_up GEMM (blocked [8 gate | 8 up] weight rows)."""
     M = x.shape[0]
     F2 = w_gu.shape[0]
@@ -374,6 +393,8 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tenso
     if out is None:
         out = torch.empty(M, F2 // 2, dtype=x.dtype, device=x.device)
     _req(out.is_contiguous() and out.shape == (M, F2 // 2), "linear_swiglu: bad out")
+    if kernel == "lds":
+        return _skinny_lds(x, w_gu, out, EPI_SWIGLU, 1, F2 // 2)
     return _skinny(x, w_gu, out, EPI_SWIGLU, 1, 1, F2 // 2)
 
 

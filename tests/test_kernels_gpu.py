@@ -257,3 +257,22 @@ def test_rope_kv_parts(S):
     _close(o1, o2, 3e-2)
     _close(k1, k2, 3e-2)
     _close(v1, v2, 3e-2)
+
+
+
+@pytest.mark.parametrize("M", [1, 17, 33, 48, 64])
+def test_skinny_lds_all_epilogues(M):
+    K = 1024
+    x = _rand(M, K, seed=40)
+    w = _rand(512, K, scale=0.05, seed=41)
+    ref = x.float() @ w.float().t()
+    o = torch.empty(M, 512, dtype=torch.bfloat16, device=DEV)
+    _close(hip._skinny_lds(x, w, o, hip.EPI_BF16, 1, 512), ref, 2e-2)
+    for S in (1, 2, 8):
+        parts = hip.linear_parts(x, w, S, kernel="lds")
+        _close(parts.sum(0), ref, 1e-3, 1e-3)
+    wg = _rand(256, K, scale=0.05, seed=42)
+    wu = _rand(256, K, scale=0.05, seed=43)
+    g, u = x.float() @ wg.float().t(), x.float() @ wu.float().t()
+    _close(hip.linear_swiglu(x, reference.interleave_gate_up(wg, wu).contiguous(), kernel="lds"),
+           g * torch.sigmoid(g) * u, 2e-2)

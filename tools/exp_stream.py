@@ -42,13 +42,13 @@ for name, (N, K) in {"qkv": (6144, 4096), "o": (4096, 4096), "down": (4096, 1433
         it[0] += 1
         return ws[it[0] % ncopy]
 
-    for blocks in (1024, 4096):
-        for unroll in (4, 8):
+    for blocks in (4096,):
+        for unroll in (8,):
             t = b2b(lambda: lib.mrsum_stream_probe(nxt().data_ptr(), nb, sink.data_ptr(), blocks, unroll,
                                                    torch.cuda.current_stream().cuda_stream))
             out.append({"op": name, "kind": "probe", "blocks": blocks, "unroll": unroll, "us": round(t * 1e6, 1),
                         "TBps": round(nb / t / 1e12, 2)})
-    for M in (1, 4, 16, 48):
+    for M in (int(m) for m in os.environ.get("MS", "1,4,16,48").split(",")):
         x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
         for nt in (1, 2):
             for splits in (1, 2, 4, 8):
@@ -58,8 +58,18 @@ for name, (N, K) in {"qkv": (6144, 4096), "o": (4096, 4096), "down": (4096, 1433
                 t = b2b(lambda: hip._skinny(x, nxt(), o, hip.EPI_F32_PARTIAL, nt, splits, N))
                 out.append({"op": name, "kind": "skinny", "M": M, "nt": nt, "S": splits, "us": round(t * 1e6, 1),
                             "TBps": round(nb / t / 1e12, 2)})
+        for splits in (1, 2, 4):
+            if (K // 128) % splits:
+                continue
+            o = torch.empty(splits, M, N, dtype=torch.float32, device=dev)
+            t = b2b(lambda: hip._skinny_lds(x, nxt(), o, hip.EPI_F32_PARTIAL, splits, N))
+            out.append({"op": name, "kind": "lds", "M": M, "nt": 4, "S": splits, "us": round(t * 1e6, 1),
+                        "TBps": round(nb / t / 1e12, 2)})
         if name == "gate_up":
             o = torch.empty(M, N // 2, dtype=torch.bfloat16, device=dev)
+            t = b2b(lambda: hip._skinny_lds(x, nxt(), o, hip.EPI_SWIGLU, 1, N // 2))
+            out.append({"op": name, "kind": "lds_swiglu", "M": M, "us": round(t * 1e6, 1),
+                        "TBps": round(nb / t / 1e12, 2)})
             t = b2b(lambda: hip._skinny(x, nxt(), o, hip.EPI_SWIGLU, 1, 1, N // 2))
             out.append({"op": name, "kind": "skinny_swiglu", "M": M, "us": round(t * 1e6, 1),
                         "TBps": round(nb / t / 1e12, 2)})
