@@ -110,13 +110,19 @@ def sample(logits, st):
 # with a fused epilogue and hipBLASLt + a separate HIP kernel, per the measured plan table
 # (ops.hip.plan).  On the CPU they are the reference composition.
 
+def _plan_parts(hip, p, x, w, splits):
+    if p[0] == "lds":
+        return hip.linear_parts(x, w, splits or p[1], kernel="lds")
+    return hip.linear_parts(x, w, splits or p[2], nt=p[1])
+
+
 def qkv_rope(x, wqkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page):
     """qkv = x @ wqkv^T, RoPE on Q/K, K/V into the paged cache; returns bf16 qkv rows."""
     if _use_hip(x):
         from . import hip
         p = hip.plan("qkv", x.shape[0], wqkv.shape[0], wqkv.shape[1])
-        if p[0] == "skinny":
-            parts = hip.linear_parts(x, wqkv, p[2], nt=p[1])
+        if p[0] != "blas":
+            parts = _plan_parts(hip, p, x, wqkv, None)
             return hip.rope_kv_parts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv,
                                      d, page)
         qkv = torch.nn.functional.linear(x, wqkv)
@@ -132,8 +138,8 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
     if _use_hip(a):
         from . import hip
         p = hip.plan(role, a.shape[0], w.shape[0], w.shape[1])
-        if p[0] == "skinny":
-            parts = hip.linear_parts(a, w, 1 if all_reduce else p[2], nt=p[1])
+        if p[0] != "blas":
+            parts = _plan_parts(hip, p, a, w, 1 if all_reduce else None)
             if all_reduce:
                 all_reduce(parts)
             return hip.add_rmsnorm_parts(parts, residual, ln, eps)
@@ -152,7 +158,7 @@ def gate_up_swiglu(x, wgu):
     if _use_hip(x):
         from . import hip
         p = hip.plan("gate_up", x.shape[0], wgu.shape[0], wgu.shape[1])
-        if p[0] == "skinny":
-            return hip.linear_swiglu(x, wgu)
+        if p[0] != "blas":
+            return hip.linear_swiglu(x, wgu, kernel=p[0])
         return hip.swiglu(torch.nn.functional.linear(x, wgu))
     return reference.swiglu(torch.nn.functional.linear(x, wgu))

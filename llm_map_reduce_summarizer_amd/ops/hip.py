@@ -415,25 +415,37 @@ def add_rmsnorm_parts(parts: torch.Tensor, residual: torch.Tensor, w: torch.Tens
 
 
 # ------------------------------------------------------------------ per-role GEMM plans
-# Measured on MI355X (tools/exp_stream.py, back-to-back launches, weights beyond the
-# 256 MiB Infinity Cache; Llama-3-8B shapes).  "blas" = torch.nn.functional.linear (hipBLASLt).
-# M <= 16:  ours beats hipBLASLt on every projection (qkv 12 vs 20 us, o 10 vs 20, down 26 vs 27,
-#           gate_up+SwiGLU 45 vs 57 at M=1); M = 48: hipBLASLt wins qkv and gate_up.
+# Measured on MI355X (tools/exp_stream.py, back-to-back launches, weights beyond the 256 MiB
+# Infinity Cache, Llama-3-8B shapes; us per call, ours vs hipBLASLt):
+#   M=1 : qkv 12.1 vs 21.3 | o 9.9 vs 20.5 | gate_up+SwiGLU 44.6 vs 55.4(+swiglu) | down 24.2 vs 24.1
+#   M=16: qkv 15.0 vs 21.8 | o 10.5 vs 20.4 | gate_up 57.3(lds) vs 56.8(+swiglu)  | down 26.8 vs 24.8
+#   M=48: qkv 18.8(lds) vs 20.6(+rope) | o 12.2(lds) vs 20.4 | gate_up 63.2(lds) vs 57.8(+swiglu) | down 33.6(lds) vs 35.8
+# Streaming floor (probe): qkv 9.5, o 7.6, down 20.1, gate_up 39.1.
+# Plan = ("skinny", nt, S) | ("lds", S) | ("blas",)
 def plan(role: str, M: int, N: int, K: int):
     if M > SKINNY_MAX_M or K % 128:
         return ("blas",)
     blocks = K // 128
+
+    def div(s):
+        while blocks % s:
+            s -= 1
+        return s
+
     if role == "qkv":
-        if M > 32:
-            return ("blas",)
-        return ("skinny", 1, 2 if blocks % 2 == 0 else 1)
+        if M <= 8:
+            return ("skinny", 1, div(2))
+        if M <= 32:
+            return ("skinny", 2, div(4)) if N % 32 == 0 else ("skinny", 1, div(2))
+        return ("lds", div(4)) if N % 64 == 0 else ("blas",)
     if role in ("o", "down"):
-        if M <= 16 and K >= 2 * N:  # tall-K (down-like): two 16-row tiles, split 2
-            return ("skinny", 2, 2 if blocks % 2 == 0 else 1)
         if M <= 16:
-            s = choose_splits(N, K, 1, target_wgs=1024)
-            return ("skinny", 1, s)
-        return ("skinny", 2, 2 if blocks % 2 == 0 else 1)
+            return ("skinny", 2, div(2)) if N % 32 == 0 else ("skinny", 1, div(4))
+        return ("lds", div(4)) if N % 64 == 0 else ("blas",)
     if role == "gate_up":
-        return ("skinny", 1, 1) if M <= 8 else ("blas",)
+        if M <= 8:
+            return ("skinny", 1, 1)
+        if M <= 16 and N % 64 == 0:
+            return ("lds", 1)
+        return ("blas",)
     return ("blas",)
