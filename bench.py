@@ -45,6 +45,8 @@ def main() -> int:
     ap.add_argument("--max-new-tokens", type=int, default=1000)
     ap.add_argument("--chunk-tokens", type=int, default=4000)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--stop-at-eos", action="store_true",
+                    help="honour EOS (default: pin every generation to --max-new-tokens so the timed work is fixed)")
     ap.add_argument("--log-level", default="WARNING")
     args = ap.parse_args()
 
@@ -68,7 +70,7 @@ def main() -> int:
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
 
     cfg = LLMConfig(MAX_TOKENS=args.max_new_tokens, TEMPERATURE=0.3, REDUCE_TEMPERATURE=0.2)
-    provider = LocalEngineProvider(args.model, cfg, use_graphs=not args.no_graphs)
+    provider = LocalEngineProvider(args.model, cfg, use_graphs=not args.no_graphs, ignore_eos=not args.stop_at_eos)
     executor = LLMExecutor(config=cfg, provider_obj=provider)
     summarizer = TranscriptSummarizer(executor=executor, max_tokens_per_chunk=args.chunk_tokens)
     transcript = synthetic_transcript(args.hours, seed=0)
@@ -112,7 +114,8 @@ def main() -> int:
         "scaling": "strong",
         "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
         "dtype": "bf16",
-        "data": "synthetic %gh transcript (utils/synth.py, seed 0); random-init weights" % args.hours,
+        "data": ("synthetic %gh transcript (utils/synth.py, seed 0); random-init weights; every generation "
+                 "pinned to max_new_tokens%s" % (args.hours, " (EOS honoured)" if args.stop_at_eos else "")),
         "config": {"model": args.model, "global_batch": n_chunks, "seq_len": args.chunk_tokens,
                    "parallelism": "dp%d" % world, "max_new_tokens": args.max_new_tokens,
                    "transcript_hours": args.hours},

@@ -239,9 +239,21 @@ class LLMEngine:
         return g
 
     # ------------------------------------------------------------------ API
-    def generate(self, prompts: Sequence[Sequence[int]], params: Sequence[SamplingParams]) -> List[GenOutput]:
+    def generate(self, prompts: Sequence[Sequence[int]], params: Sequence[SamplingParams],
+                 ignore_eos: bool = False) -> List[GenOutput]:
+        """Generate for every prompt.  ``ignore_eos`` pins the work to max_new_tokens per request
+        (benchmark mode, SURVEY §7.4: random weights emit EOS at random)."""
         if len(prompts) != len(params):
             raise ValueError("prompts and params differ in length")
+        n_eos = self.state.n_eos
+        if ignore_eos:
+            self.state.n_eos = 0
+        try:
+            return self._generate(prompts, params)
+        finally:
+            self.state.n_eos = n_eos
+
+    def _generate(self, prompts: Sequence[Sequence[int]], params: Sequence[SamplingParams]) -> List[GenOutput]:
         self.stats["generate_calls"] += 1
         results: List[Optional[GenOutput]] = [None] * len(prompts)
         waiting: List[_Seq] = []

@@ -59,12 +59,13 @@ class LocalEngineProvider(Provider):
                  tp: int = 1, seed: Optional[int] = None, max_model_len: int = 16384, engine=None,
                  engine_options: Optional[Dict[str, Any]] = None, dtype: Optional[str] = None,
                  kv_fraction: Optional[float] = None, use_graphs: bool = True, max_num_seqs: Optional[int] = None,
-                 tokenizer: Optional[str] = None, **_ignored):
+                 tokenizer: Optional[str] = None, ignore_eos: bool = False, **_ignored):
         super().__init__(model, config)
         self.tokenizer = get_tokenizer(tokenizer)
         if dtype not in (None, "bf16"):
             raise NotImplementedError("dtype %s is not supported by the local engine yet" % dtype)
         self.tp = tp
+        self.ignore_eos = ignore_eos
         self.seed = self.config.ENGINE_SEED if seed is None else seed
         self.max_model_len = max_model_len
         self._engine = engine
@@ -122,7 +123,8 @@ class LocalEngineProvider(Provider):
         if mine:
             outs = self.engine.generate(
                 [prompts[i] for i in mine],
-                [SamplingParams(reqs[i].max_tokens, reqs[i].temperature, _req_seed(self.seed, reqs[i])) for i in mine])
+                [SamplingParams(reqs[i].max_tokens, reqs[i].temperature, _req_seed(self.seed, reqs[i])) for i in mine],
+                ignore_eos=self.ignore_eos)
             for i, o in zip(mine, outs):
                 local.append({"i": i, "text": self.tokenizer.decode(o.token_ids), "pt": o.prompt_len,
                               "ct": len(o.token_ids), "fr": o.finish_reason})
