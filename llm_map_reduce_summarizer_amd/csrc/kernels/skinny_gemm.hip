@@ -326,3 +326,179 @@ MRSUM_API int mrsum_skinny_lds(const void* x, int ldx, const void* W, int N, int
 #undef L
     return (int)hipGetLastError();
 }
+
+
+// ---------------------------------------------------------------------------------------------
+// FP8 weights (OCP e4m3fn, gfx950's format -- not MI300's fnuz) with one fp32 scale per output row:
+//   out[m, n] = scale[n] * sum_k float(W8[n, k]) * x[m, k]          (W8A16: activations stay bf16)
+// Same decomposition as skinny_gemm_kernel; a lane's 16-B load now carries 16 k-elements of its W
+// row, converted exactly to bf16 with v_cvt_scalef32_pk_bf16_fp8 (2 per instruction) into the A
+// fragments of two consecutive MFMA k-steps.  The k order inside a 64-wide chunk is permuted
+// (lane group g holds k = 16g .. 16g+15 of the chunk) and the x (B) fragments are loaded with the
+// same permutation, so the sum is unchanged.  Half the HBM bytes of the bf16 kernel per weight:
+// this is the decode path of the fp8 Llama-3-70B aggregator.
+namespace {
+template <int NT>
+struct A8Frag {
+    u32x4 v[NT][2];
+};
+
+template <int NT>
+__device__ __forceinline__ void load_a8(A8Frag<NT>& a, const uint8_t* __restrict__ W, int K, int n0, int kb,
+                                        int lane) {
+    const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+        const uint8_t* p = W + (size_t)(n0 + 16 * t + r) * K + kb + 16 * g;
+#pragma unroll
+        for (int c = 0; c < 2; ++c) a.v[t][c] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + 64 * c));
+    }
+}
+
+__device__ __forceinline__ bf16x8 fp8x8_to_bf16(unsigned d0, unsigned d1) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    const bf16x2 a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d0, 1.0f, false);
+    const bf16x2 b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d0, 1.0f, true);
+    const bf16x2 c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d1, 1.0f, false);
+    const bf16x2 d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d1, 1.0f, true);
+    return bf16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
+template <int MT>
+__device__ __forceinline__ void load_b8(BFrag<MT>& b, const bf16* __restrict__ x, int ldx, int M, int kb, int lane) {
+    const int r = lane & 15, g = lane >> 4;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const int row = min(16 * m + r, M - 1);
+        const bf16* p = x + (size_t)row * ldx + kb + 16 * g;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) b.v[m][i] = *reinterpret_cast<const uint4*>(p + 64 * (i >> 1) + 8 * (i & 1));
+    }
+}
+
+template <int NT, int MT>
+__device__ __forceinline__ void mma_block8(f32x4 (&acc)[NT][MT], const A8Frag<NT>& a, const BFrag<MT>& b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const u32x4 raw = a.v[t][i >> 1];
+            const bf16x8 av = (i & 1) ? fp8x8_to_bf16(raw[2], raw[3]) : fp8x8_to_bf16(raw[0], raw[1]);
+#pragma unroll
+            for (int m = 0; m < MT; ++m)
+                acc[t][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, b.v[m][i]),
+                                                                    acc[t][m], 0, 0, 0);
+        }
+}
+}  // namespace
+
+template <int NT, int MT, int EPI>
+__global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict__ x, int ldx,
+                                                         const uint8_t* __restrict__ W,
+                                                         const float* __restrict__ wscale, int K, int M,
+                                                         void* __restrict__ out, int ldo, int kper) {
+    constexpr int BN = 16 * NT, BM = 16 * MT;
+    __shared__ __attribute__((aligned(16))) float red[4][BM][BN + 4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int n0 = blockIdx.x * BN;
+    const int ks = blockIdx.y * kper, ke = min(K, ks + kper);
+
+    f32x4 acc[NT][MT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int m = 0; m < MT; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    int kb = ks + w * KB;
+    A8Frag<NT> a0, a1;
+    BFrag<MT> b;
+    if (kb < ke) load_a8<NT>(a0, W, K, n0, kb, lane);
+    while (kb < ke) {
+        const int kb1 = kb + 4 * KB;
+        load_b8<MT>(b, x, ldx, M, kb, lane);
+        if (kb1 < ke) load_a8<NT>(a1, W, K, n0, kb1, lane);
+        mma_block8<NT, MT>(acc, a0, b);
+        if (kb1 >= ke) break;
+        const int kb2 = kb1 + 4 * KB;
+        load_b8<MT>(b, x, ldx, M, kb1, lane);
+        if (kb2 < ke) load_a8<NT>(a0, W, K, n0, kb2, lane);
+        mma_block8<NT, MT>(acc, a1, b);
+        kb = kb2;
+    }
+
+    const int cn = 4 * (lane >> 4), cm = lane & 15;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) red[w][16 * m + cm][16 * t + cn + j] = acc[t][m][j];
+    __syncthreads();
+
+    constexpr int ITEMS = BM * (BN / 4);
+    for (int it = threadIdx.x; it < ITEMS; it += 256) {
+        const int m = it / (BN / 4), n4 = (it % (BN / 4)) * 4;
+        if (m >= M) continue;
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            v[j] = (red[0][m][n4 + j] + red[1][m][n4 + j] + red[2][m][n4 + j] + red[3][m][n4 + j]) *
+                   wscale[n0 + n4 + j];
+        if constexpr (EPI == EPI_BF16) {
+            uint2 o;
+            o.x = pack2(v[0], v[1]);
+            o.y = pack2(v[2], v[3]);
+            *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)m * ldo + n0 + n4) = o;
+        } else if constexpr (EPI == EPI_F32_PARTIAL) {
+            float* o = reinterpret_cast<float*>(out) + ((size_t)blockIdx.y * M + m) * ldo + n0 + n4;
+            *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {  // SWIGLU, nt == 1: rows [0, 8) gate, [8, 16) up
+            constexpr int H = BN / 2;
+            if (n4 < H) {
+                float rr[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float u = (red[0][m][n4 + H + j] + red[1][m][n4 + H + j] + red[2][m][n4 + H + j] +
+                                     red[3][m][n4 + H + j]) * wscale[n0 + n4 + H + j];
+                    rr[j] = v[j] / (1.f + __expf(-v[j])) * u;
+                }
+                uint2 o;
+                o.x = pack2(rr[0], rr[1]);
+                o.y = pack2(rr[2], rr[3]);
+                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)m * ldo + blockIdx.x * H + n4) = o;
+            }
+        }
+    }
+}
+
+MRSUM_API int mrsum_skinny_fp8(const void* x, int ldx, const void* W, const float* wscale, int N, int K, int M,
+                               void* out, int ldo, int epi, int nt, int splits, hipStream_t s) {
+    if (M <= 0) return 0;
+    if (M > 64 || K % KB || splits < 1 || (K / KB) % splits || (nt != 1 && nt != 2) || N % (16 * nt))
+        return (int)hipErrorInvalidValue;
+    if (epi != EPI_F32_PARTIAL && splits != 1) return (int)hipErrorInvalidValue;
+    if (epi == EPI_SWIGLU && nt != 1) return (int)hipErrorInvalidValue;
+    const int kper = K / splits;
+    const int mt = (M + 15) / 16;
+    dim3 grid(N / (16 * nt), splits);
+    auto X = (const bf16*)x; auto Wp = (const uint8_t*)W;
+#define L(NT_, MT_, EPI_) skinny_fp8_kernel<NT_, MT_, EPI_><<<grid, 256, 0, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper)
+#define BY_MT(NT_, EPI_)                        \
+    switch (mt) {                               \
+        case 1: L(NT_, 1, EPI_); break;         \
+        case 2: L(NT_, 2, EPI_); break;         \
+        case 3: L(NT_, 3, EPI_); break;         \
+        default: L(NT_, 4, EPI_); break;        \
+    }
+    if (nt == 1) {
+        if (epi == EPI_BF16) { BY_MT(1, EPI_BF16) }
+        else if (epi == EPI_F32_PARTIAL) { BY_MT(1, EPI_F32_PARTIAL) }
+        else { BY_MT(1, EPI_SWIGLU) }
+    } else {
+        if (epi == EPI_BF16) { BY_MT(2, EPI_BF16) }
+        else { BY_MT(2, EPI_F32_PARTIAL) }
+    }
+#undef BY_MT
+#undef L
+    return (int)hipGetLastError();
+}

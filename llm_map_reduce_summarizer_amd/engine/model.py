@@ -33,7 +33,7 @@ import torch
 import torch.nn.functional as F
 
 from .. import ops
-from ..ops.reference import interleave_gate_up, rope_cos_sin
+from ..ops.reference import Fp8Weight, interleave_gate_up, rope_cos_sin
 from .config import ModelConfig
 
 
@@ -61,7 +61,14 @@ class LayerWeights:
 
 class LlamaModel:
     def __init__(self, cfg: ModelConfig, device: torch.device, dtype: torch.dtype = torch.bfloat16, seed: int = 0,
-                 tp_rank: int = 0, tp_size: int = 1, tp_group=None):
+                 tp_rank: int = 0, tp_size: int = 1, tp_group=None, weight_dtype: str = "bf16"):
+        """``weight_dtype="fp8"``: the four projection matrices of every layer are stored as OCP e4m3fn
+        with per-output-row fp32 scales (ops.Fp8Weight) -- W8A16 MFMA kernels at decode sizes,
+        hipBLASLt fp8 (dynamic per-token activation scales) at prefill sizes.  Embedding, norms and
+        the LM head stay bf16."""
+        if weight_dtype not in ("bf16", "fp8"):
+            raise ValueError("weight_dtype must be bf16 or fp8")
+        self.weight_dtype = weight_dtype
         if cfg.n_heads % tp_size or cfg.n_kv_heads % tp_size or cfg.ffn % tp_size or cfg.vocab_size % tp_size:
             raise ValueError("%s does not shard over tp=%d" % (cfg.name, tp_size))
         self.cfg, self.device, self.dtype = cfg, torch.device(device), dtype
@@ -97,6 +104,8 @@ class LlamaModel:
             del wg, wu
             wd = _randn((c.hidden, c.ffn), std, seed, "l%d.wd" % i, dev, dt)
             wd = wd[:, r * f:(r + 1) * f].contiguous()
+            if self.weight_dtype == "fp8":
+                wqkv, wo, wgu, wd = (Fp8Weight.quantize(t) for t in (wqkv, wo, wgu, wd))
             self.layers.append(LayerWeights(ones(), wqkv, wo, ones(), wgu, wd))
         self.final_norm = ones()
         lm = _randn((c.vocab_size, c.hidden), std, seed, "lm_head", dev, dt)
@@ -105,10 +114,12 @@ class LlamaModel:
         del lm
 
     def weight_bytes(self) -> int:
-        n = self.embed.numel() + self.lm_head.numel() + self.final_norm.numel()
+        def nb(t):
+            return t.nbytes() if isinstance(t, Fp8Weight) else t.numel() * t.element_size()
+        n = nb(self.embed) + nb(self.lm_head) + nb(self.final_norm)
         for lw in self.layers:
-            n += sum(t.numel() for t in (lw.ln1, lw.wqkv, lw.wo, lw.ln2, lw.wgu, lw.wdown))
-        return n * self.embed.element_size()
+            n += sum(nb(t) for t in (lw.ln1, lw.wqkv, lw.wo, lw.ln2, lw.wgu, lw.wdown))
+        return n
 
     # ------------------------------------------------------------------ comm
     def _all_reduce(self, t: torch.Tensor) -> torch.Tensor:

@@ -62,8 +62,8 @@ class LocalEngineProvider(Provider):
                  tokenizer: Optional[str] = None, ignore_eos: bool = False, **_ignored):
         super().__init__(model, config)
         self.tokenizer = get_tokenizer(tokenizer)
-        if dtype not in (None, "bf16"):
-            raise NotImplementedError("dtype %s is not supported by the local engine yet" % dtype)
+        if dtype not in (None, "bf16", "fp8"):
+            raise ValueError("dtype must be bf16 or fp8, got %s" % dtype)
         self.tp = tp
         self.ignore_eos = ignore_eos
         self.seed = self.config.ENGINE_SEED if seed is None else seed
@@ -72,6 +72,8 @@ class LocalEngineProvider(Provider):
         self._device = device
         self._engine_options = dict(engine_options or {})
         self._engine_options.setdefault("use_graphs", use_graphs)
+        if dtype == "fp8":
+            self._engine_options.setdefault("weight_dtype", "fp8")
         if kv_fraction is not None:
             self._engine_options.setdefault("kv_fraction", kv_fraction)
         if max_num_seqs is not None:

@@ -18,6 +18,7 @@ import os
 import torch
 
 from . import reference
+from .reference import Fp8Weight
 
 _FORCE_TORCH = os.environ.get("MRSUM_OPS", "").lower() == "torch"
 
@@ -57,7 +58,13 @@ def swiglu(gu, out=None):
 
 
 def linear(x, w):
-    """x @ w^T (bf16).  GPU: MFMA weight-streaming kernel for decode shapes, hipBLASLt otherwise."""
+    """x @ w^T (bf16).  GPU: MFMA weight-streaming kernel for decode shapes, hipBLASLt otherwise;
+    ``w`` may be an Fp8Weight (W8A16 decode kernel / hipBLASLt fp8 prefill)."""
+    if isinstance(w, Fp8Weight):
+        if _use_hip(x):
+            from . import hip
+            return hip.fp8_linear(x, w)
+        return reference.linear(x, w)
     return _impl(x).linear(x, w)
 
 
@@ -116,8 +123,27 @@ def _plan_parts(hip, p, x, w, splits):
     return hip.linear_parts(x, w, splits or p[2], nt=p[1])
 
 
+def _fp8_parts(hip, x, w, role, splits):
+    """Split-K fp32 slabs from the fp8 weight-streaming kernel (decode) -- same plan shapes as bf16."""
+    p = hip.plan(role, x.shape[0], w.shape[0], w.shape[1])
+    nt = p[1] if p[0] == "skinny" else 1
+    s = splits or (p[2] if p[0] == "skinny" else (p[1] if p[0] == "lds" else 1))
+    if w.shape[0] % (16 * nt):
+        nt = 1
+    return hip.fp8_linear_parts(x, w, s, nt)
+
+
 def qkv_rope(x, wqkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page):
     """qkv = x @ wqkv^T, RoPE on Q/K, K/V into the paged cache; returns bf16 qkv rows."""
+    if _use_hip(x) and isinstance(wqkv, Fp8Weight):
+        from . import hip
+        if x.shape[0] <= hip.SKINNY_MAX_M:
+            parts = _fp8_parts(hip, x, wqkv, "qkv", None)
+            return hip.rope_kv_parts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d,
+                                     page)
+        qkv = hip.fp8_linear(x, wqkv)
+        hip.rope_kv(qkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page)
+        return qkv
     if _use_hip(x):
         from . import hip
         p = hip.plan("qkv", x.shape[0], wqkv.shape[0], wqkv.shape[1])
@@ -128,13 +154,24 @@ def qkv_rope(x, wqkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin,
         qkv = torch.nn.functional.linear(x, wqkv)
         hip.rope_kv(qkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page)
         return qkv
-    qkv = torch.nn.functional.linear(x, wqkv)
+    qkv = reference.linear(x, wqkv)
     reference.rope_kv(qkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page)
     return qkv
 
 
 def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
     """residual += a @ w^T (TP-all-reduced when ``all_reduce``); returns rmsnorm(residual) * ln."""
+    if _use_hip(a) and isinstance(w, Fp8Weight):
+        from . import hip
+        if a.shape[0] <= hip.SKINNY_MAX_M:
+            parts = _fp8_parts(hip, a, w, role, 1 if all_reduce else None)
+            if all_reduce:
+                all_reduce(parts)
+            return hip.add_rmsnorm_parts(parts, residual, ln, eps)
+        o = hip.fp8_linear(a, w)
+        if all_reduce:
+            all_reduce(o)
+        return hip.add_rmsnorm(o, residual, ln, eps)
     if _use_hip(a):
         from . import hip
         p = hip.plan(role, a.shape[0], w.shape[0], w.shape[1])
@@ -147,7 +184,7 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
         if all_reduce:
             all_reduce(o)
         return hip.add_rmsnorm(o, residual, ln, eps)
-    o = torch.nn.functional.linear(a, w)
+    o = reference.linear(a, w)
     if all_reduce:
         all_reduce(o)
     return reference.add_rmsnorm(o, residual, ln, eps)
@@ -155,10 +192,13 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
 
 def gate_up_swiglu(x, wgu):
     """silu(gate) * up of the fused, [8 gate | 8 up]-blocked gate_up projection."""
+    if _use_hip(x) and isinstance(wgu, Fp8Weight):
+        from . import hip
+        return hip.fp8_linear_swiglu(x, wgu)
     if _use_hip(x):
         from . import hip
         p = hip.plan("gate_up", x.shape[0], wgu.shape[0], wgu.shape[1])
         if p[0] != "blas":
             return hip.linear_swiglu(x, wgu, kernel=p[0])
         return hip.swiglu(torch.nn.functional.linear(x, wgu))
-    return reference.swiglu(torch.nn.functional.linear(x, wgu))
+    return reference.swiglu(reference.linear(x, wgu))

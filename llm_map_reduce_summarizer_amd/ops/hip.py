@@ -35,6 +35,8 @@ _SIGS = {
                                _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _vp],
+    "mrsum_skinny_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
+    "mrsum_quant_fp8_rows": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_sample": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp,
                      _c_int, _vp],
@@ -449,3 +451,60 @@ def plan(role: str, M: int, N: int, K: int):
             return ("lds", 1)
         return ("blas",)
     return ("blas",)
+
+
+# ------------------------------------------------------------------ FP8 (e4m3fn) weights
+def quant_fp8_rows(x: torch.Tensor):
+    """Row-wise dynamic e4m3fn quantisation: returns (q [T, K] float8_e4m3fn, scale [T] fp32)."""
+    _bf16_cuda(x)
+    _rows_ok(x)
+    T, K = x.shape
+    _req(K % 8 == 0 and K <= 32768, "quant_fp8_rows: K")
+    q = torch.empty(T, K, dtype=torch.float8_e4m3fn, device=x.device)
+    sc = torch.empty(T, dtype=torch.float32, device=x.device)
+    _check(_fn("mrsum_quant_fp8_rows")(_p(x), x.stride(0), _p(q), _p(sc), T, K, _stream()), "quant_fp8_rows")
+    return q, sc
+
+
+def _skinny_fp8(x, w, out, epi, nt, splits, ldo):
+    _bf16_cuda(x)
+    _rows_ok(x)
+    M, K = x.shape
+    N = w.q.shape[0]
+    _req(w.q.is_cuda and w.q.dtype == torch.float8_e4m3fn and w.q.is_contiguous() and w.q.shape[1] == K,
+         "skinny_fp8: weight must be e4m3fn [N, K] contiguous")
+    _req(w.scale.dtype == torch.float32 and w.scale.numel() == N, "skinny_fp8: scale")
+    _req(1 <= M <= SKINNY_MAX_M and K % 128 == 0 and N % (16 * nt) == 0 and (K // 128) % splits == 0,
+         "skinny_fp8: unsupported shape M=%d N=%d K=%d nt=%d S=%d" % (M, N, K, nt, splits))
+    _check(_fn("mrsum_skinny_fp8")(_p(x), x.stride(0), _p(w.q), _p(w.scale), N, K, M, _p(out), ldo, epi, nt, splits,
+                                   _stream()), "skinny_fp8")
+    return out
+
+
+def fp8_linear(x: torch.Tensor, w, out_dtype=torch.bfloat16) -> torch.Tensor:
+    """x @ (scale * W8)^T for any M: MFMA W8A16 weight-streaming kernel at decode sizes, hipBLASLt fp8
+    (torch._scaled_mm, row-wise activation x column-wise weight scales) at prefill sizes."""
+    M = x.shape[0]
+    N = w.q.shape[0]
+    if M <= SKINNY_MAX_M:
+        nt = 2 if N % 32 == 0 and N >= 16384 else 1
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+        return _skinny_fp8(x, w, out, EPI_BF16, nt, 1, N)
+    xq, xs = quant_fp8_rows(x)
+    return torch._scaled_mm(xq, w.q.t(), scale_a=xs.view(-1, 1), scale_b=w.scale.view(1, -1), out_dtype=out_dtype)
+
+
+def fp8_linear_parts(x: torch.Tensor, w, splits: int, nt: int = 1) -> torch.Tensor:
+    M, K = x.shape
+    N = w.q.shape[0]
+    out = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
+    return _skinny_fp8(x, w, out, EPI_F32_PARTIAL, nt, splits, N)
+
+
+def fp8_linear_swiglu(x: torch.Tensor, w) -> torch.Tensor:
+    M = x.shape[0]
+    F2 = w.q.shape[0]
+    if M > SKINNY_MAX_M:
+        return swiglu(fp8_linear(x, w))
+    out = torch.empty(M, F2 // 2, dtype=torch.bfloat16, device=x.device)
+    return _skinny_fp8(x, w, out, EPI_SWIGLU, 1, 1, F2 // 2)

@@ -106,7 +106,40 @@ def swiglu(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor
     return y
 
 
-def linear(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+class Fp8Weight:
+    """OCP e4m3fn weight [N, K] with one fp32 scale per output row (W = scale[:, None] * float(q))."""
+
+    def __init__(self, q: torch.Tensor, scale: torch.Tensor):
+        self.q, self.scale = q, scale
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+    def numel(self) -> int:
+        return self.q.numel()
+
+    def nbytes(self) -> int:
+        return self.q.numel() + 4 * self.scale.numel()
+
+    def dequant(self, dtype=torch.float32) -> torch.Tensor:
+        return (self.q.float() * self.scale.float()[:, None]).to(dtype)
+
+    @staticmethod
+    def quantize(w: torch.Tensor) -> "Fp8Weight":
+        wf = w.float()
+        scale = wf.abs().amax(dim=1).clamp_min(1e-12) / 448.0
+        q = (wf / scale[:, None]).clamp(-448.0, 448.0).to(torch.float8_e4m3fn)
+        return Fp8Weight(q.contiguous(), scale.contiguous())
+
+
+def _w(w):
+    return w.dequant(torch.bfloat16) if isinstance(w, Fp8Weight) else w
+
+
+def linear(x: torch.Tensor, w) -> torch.Tensor:
+    if isinstance(w, Fp8Weight):
+        return (x.float() @ w.dequant().t()).to(x.dtype)
     return torch.nn.functional.linear(x, w)
 
 
@@ -114,12 +147,13 @@ def linear_parts(x: torch.Tensor, w: torch.Tensor, splits: int = 1) -> torch.Ten
     """fp32 split-K partial slabs [S, M, N] of x @ w^T (what skinny_gemm EPI_F32_PARTIAL emits)."""
     K = x.shape[1]
     ks = K // splits
-    return torch.stack([x[:, i * ks:(i + 1) * ks].float() @ w[:, i * ks:(i + 1) * ks].float().t()
+    wf = w.dequant() if isinstance(w, Fp8Weight) else w.float()
+    return torch.stack([x[:, i * ks:(i + 1) * ks].float() @ wf[:, i * ks:(i + 1) * ks].t()
                         for i in range(splits)])
 
 
-def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor) -> torch.Tensor:
-    return swiglu(torch.nn.functional.linear(x, w_gu))
+def linear_swiglu(x: torch.Tensor, w_gu) -> torch.Tensor:
+    return swiglu(linear(x, w_gu))
 
 
 def add_rmsnorm_parts(parts: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,

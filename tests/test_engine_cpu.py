@@ -147,3 +147,17 @@ def test_gumbel_sampling_statistics():
         counts[int(tok)] += 1
     p = torch.softmax(logits.float()[0], 0)
     assert torch.allclose(counts / counts.sum(), p, atol=0.04)
+
+
+def test_fp8_weights_engine_cpu():
+    cfg = get_model_config("tiny", init_std=0.05)
+    e8 = LLMEngine(cfg, device="cpu", max_model_len=256, max_num_seqs=4, kv_pages=32, weight_dtype="fp8")
+    e16 = LLMEngine(cfg, device="cpu", max_model_len=256, max_num_seqs=4, kv_pages=32)
+    assert e8.model.weight_bytes() < e16.model.weight_bytes()  # embedding + head (bf16) dominate tiny
+    p = [[128000] + list(range(50, 90))]
+    o8 = e8.generate(p, [SamplingParams(4, 0.0, 0)])[0]
+    assert len(o8.token_ids) == 4
+    from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight
+    w = torch.randn(64, 128)
+    q = Fp8Weight.quantize(w)
+    assert q.q.dtype == torch.float8_e4m3fn and torch.allclose(q.dequant(), w, rtol=0.07, atol=1e-3)

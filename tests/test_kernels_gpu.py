@@ -276,3 +276,36 @@ def test_skinny_lds_all_epilogues(M):
     g, u = x.float() @ wg.float().t(), x.float() @ wu.float().t()
     _close(hip.linear_swiglu(x, reference.interleave_gate_up(wg, wu).contiguous(), kernel="lds"),
            g * torch.sigmoid(g) * u, 2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 5, 17, 48, 64, 200])
+@pytest.mark.parametrize("N,K", [(1280, 8192), (512, 3584)])
+def test_fp8_linear(M, N, K):
+    from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight
+    x = _rand(M, K, seed=50)
+    w = Fp8Weight.quantize(_rand(N, K, scale=0.05, seed=51))
+    ref = x.float() @ w.dequant().t()
+    out = hip.fp8_linear(x, w)
+    if M <= hip.SKINNY_MAX_M:
+        _close(out, ref, 2e-2)  # W8A16: exact weights, bf16 activations
+    else:  # hipBLASLt fp8 with dynamic per-token activation scales
+        _close(out, ref, 0.25, 0.08)
+    for S in (1, 2):
+        parts = hip.fp8_linear_parts(x[:min(M, 64)], w, S)
+        _close(parts.sum(0), ref[:min(M, 64)], 2e-3, 2e-3)
+
+
+def test_fp8_swiglu_and_quant():
+    from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight
+    M, F, K = 9, 512, 1024
+    x = _rand(M, K, seed=52)
+    wg, wu = _rand(F, K, scale=0.05, seed=53), _rand(F, K, scale=0.05, seed=54)
+    w = Fp8Weight.quantize(reference.interleave_gate_up(wg, wu).contiguous())
+    full = x.float() @ w.dequant().t()
+    g, u = reference.split_gate_up(full)
+    _close(hip.fp8_linear_swiglu(x, w), g * torch.sigmoid(g) * u, 3e-2)
+    q, s = hip.quant_fp8_rows(x)
+    ref_q = (x.float() / s[:, None]).to(torch.float8_e4m3fn)
+    assert torch.allclose(s.cpu(), x.float().abs().amax(1).cpu() / 448, rtol=1e-5)
+    assert (q.float() - ref_q.float()).abs().max().item() <= 16.0  # at most one e4m3 ulp at the top binade
+    assert (q.float() == ref_q.float()).float().mean().item() > 0.98
