@@ -67,6 +67,11 @@ def build_parser() -> argparse.ArgumentParser:
     e.add_argument("--kv-fraction", type=float, default=None, help="fraction of free HBM for the KV cache")
     e.add_argument("--no-graphs", action="store_true", help="disable hipGraph capture of decode steps")
     e.add_argument("--tokenizer", default=None, help="tiktoken-format vocabulary file (default: bundled)")
+    e.add_argument("--aggregator-model", default=None,
+                   help="separate local model for the reduce stage (e.g. llama3-70b); default: the map model")
+    e.add_argument("--aggregator-dtype", choices=["bf16", "fp8"], default=None,
+                   help="weight dtype of the aggregator model (fp8 = OCP e4m3fn, per-row scales)")
+    e.add_argument("--aggregator-tp", type=int, default=None, help="TP degree of the aggregator model")
     return p
 
 
@@ -107,12 +112,22 @@ async def async_main(args: argparse.Namespace) -> int:
         popts.update({"dtype": args.dtype, "tp": args.tp, "seed": args.seed, "kv_fraction": args.kv_fraction,
                       "use_graphs": not args.no_graphs, "tokenizer": args.tokenizer,
                       "max_num_seqs": args.max_concurrent_requests})
+    agg_executor = None
+    if args.aggregator_model:
+        if provider != "local":
+            log.error("--aggregator-model needs the local provider")
+            return 1
+        if popts.get("kv_fraction") is None:
+            popts["kv_fraction"] = 0.3  # leave HBM for the second engine
+        aopts = dict(popts, dtype=args.aggregator_dtype, tp=args.aggregator_tp or args.tp, kv_fraction=0.6,
+                     max_model_len=40960)
+        agg_executor = LLMExecutor(config=cfg, provider="local", model=args.aggregator_model, **aopts)
     executor = LLMExecutor(config=cfg, provider=provider, model=args.model,
                            max_concurrent_requests=args.max_concurrent_requests, **popts)
     summarizer = TranscriptSummarizer(
         provider=provider, model=args.model, max_tokens_per_chunk=args.max_tokens_per_chunk,
         max_concurrent_requests=args.max_concurrent_requests, hierarchical_aggregation=not args.no_hierarchical,
-        executor=executor,
+        executor=executor, aggregator_executor=agg_executor,
         chunker_options={"position_mode": args.position_mode, "overlap_tokens": args.chunk_overlap,
                          "apply_overlap": args.chunk_overlap > 0},
         aggregator_options={"max_levels": args.reduce_levels or None})

@@ -62,7 +62,11 @@ class TranscriptSummarizer:
                  max_tokens_per_chunk: int = 4000, max_concurrent_requests: Optional[int] = None,
                  hierarchical_aggregation: bool = True, executor: Optional[LLMExecutor] = None,
                  chunker_options: Optional[Dict[str, Any]] = None, aggregator_options: Optional[Dict[str, Any]] = None,
-                 provider_options: Optional[Dict[str, Any]] = None):
+                 provider_options: Optional[Dict[str, Any]] = None,
+                 aggregator_executor: Optional[LLMExecutor] = None):
+        """``aggregator_executor``: optional separate back-end for the reduce stage (e.g. the fp8
+        Llama-3-70B aggregator of BASELINE config 5 while the map runs on Llama-3-8B); by default the
+        reduce uses the map executor (the reference borrows its executor, result_aggregator.py:225)."""
         self.provider = provider
         self.model = model
         self.max_tokens_per_chunk = max_tokens_per_chunk
@@ -74,6 +78,7 @@ class TranscriptSummarizer:
         self.chunker_options = chunker_options or {}
         self.aggregator_options = aggregator_options or {}
         self.provider_options = provider_options or {}
+        self.aggregator_executor = aggregator_executor
 
     def _ensure_components(self) -> None:
         if self.executor is None:
@@ -86,7 +91,8 @@ class TranscriptSummarizer:
             self.chunker = Chunker(max_tokens_per_chunk=self.max_tokens_per_chunk, tokenizer=tok,
                                    **self.chunker_options)
         if self.aggregator is None:
-            self.aggregator = ResultAggregator(executor=self.executor, hierarchical=self.hierarchical_aggregation,
+            self.aggregator = ResultAggregator(executor=self.aggregator_executor or self.executor,
+                                               hierarchical=self.hierarchical_aggregation,
                                                tokenizer=tok, **self.aggregator_options)
 
     def _get_prompt_template(self, prompt_file: Optional[str] = None) -> str:
@@ -111,6 +117,8 @@ class TranscriptSummarizer:
         self._ensure_components()
         ex = self.executor
         ex.reset_counters()
+        if self.aggregator_executor is not None:
+            self.aggregator_executor.reset_counters()
 
         segments = transcript_data.get("segments", [])
         if limit_segments:
@@ -180,8 +188,9 @@ class TranscriptSummarizer:
         report = {
             "summary": result["summary"],
             "processing_time": elapsed,
-            "tokens_used": ex.total_tokens_used,
-            "cost": ex.total_cost,
+            "tokens_used": ex.total_tokens_used + (self.aggregator_executor.total_tokens_used
+                                                   if self.aggregator_executor is not None else 0),
+            "cost": ex.total_cost + (self.aggregator_executor.total_cost if self.aggregator_executor is not None else 0.0),
             "segments": len(segments),
             "chunks": len(chunks),
             "provider": self.provider,
@@ -191,6 +200,8 @@ class TranscriptSummarizer:
             "timings": timings,
             "reduce_plan": result.get("plan", {}),
             "engine": ex.backend.stats(),
+            "aggregator_engine": (self.aggregator_executor.backend.stats()
+                                  if self.aggregator_executor is not None else None),
         }
         log.info("summarization done in %.2f s; tokens=%d", elapsed, ex.total_tokens_used)
         return report

@@ -288,8 +288,10 @@ def test_fp8_linear(M, N, K):
     out = hip.fp8_linear(x, w)
     if M <= hip.SKINNY_MAX_M:
         _close(out, ref, 2e-2)  # W8A16: exact weights, bf16 activations
-    else:  # hipBLASLt fp8 with dynamic per-token activation scales
-        _close(out, ref, 0.25, 0.08)
+    else:  # hipBLASLt fp8 with dynamic per-token activation scales: e4m3 activation rounding (~3.6% per
+        # element, independent over K) -> check the relative RMS error, not every element
+        rel = ((out.float().cpu() - ref.cpu()).norm() / ref.cpu().norm()).item()
+        assert rel < 0.05, rel
     for S in (1, 2):
         parts = hip.fp8_linear_parts(x[:min(M, 64)], w, S)
         _close(parts.sum(0), ref[:min(M, 64)], 2e-3, 2e-3)
