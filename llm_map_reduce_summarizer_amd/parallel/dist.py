@@ -59,7 +59,8 @@ def is_initialized() -> bool:
 def init_distributed_from_env(backend: Optional[str] = None, timeout_s: float = 1800.0) -> bool:
     """Initialise the default group when launched by torchrun (WORLD_SIZE > 1)."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
-    if ws <= 1 or is_initialized():
+    force = os.environ.get("MRSUM_FORCE_DIST", "0") == "1" and "RANK" in os.environ  # world-1 RCCL rehearsal
+    if (ws <= 1 and not force) or is_initialized():
         return is_initialized()
     if backend is None:
         backend = os.environ.get("MRSUM_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
