@@ -132,7 +132,7 @@ class LocalEngineProvider(Provider):
                               "ct": len(o.token_ids), "fr": o.finish_reason})
         t1 = time.perf_counter()
         self.timings["generate_s"] += t1 - t0
-        if self.par.world > 1:
+        if pdist.is_initialized():  # also at world 1 under torchrun: same RCCL code path as N > 1
             gathered = pdist.all_gather_json(local)
             # with TP, every rank of a replica holds identical results: keep the tp_rank 0 copies
             merged = {}
