@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Decode-step latency of the engine (Llama-3-8B bf16 by default) at the batch sizes the
+summarizer runs: B=1 (final reduce), B~5 (map at DP=8), B=10 (reduce level 1), B=39 (map at DP=1).
+Each sequence has a ~CTX-token prompt; reports ms per decode step (hipGraph replay, pinned length)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--batches", default="1,5,10,39")
+    ap.add_argument("--ctx", type=int, default=4000)
+    ap.add_argument("--new", type=int, default=256)
+    a = ap.parse_args()
+    import torch
+    from llm_map_reduce_summarizer_amd.engine.config import get_model_config
+    from llm_map_reduce_summarizer_amd.engine.engine import LLMEngine, SamplingParams
+    eng = LLMEngine(get_model_config(a.model), device="cuda:0", max_model_len=a.ctx + a.new + 64,
+                    max_num_seqs=64, kv_fraction=0.5, weight_dtype=a.dtype, sync_every=32)
+    res = []
+    for B in (int(b) for b in a.batches.split(",")):
+        prompts = [[128000] + [(i * 7919 + j * 31) % 120000 + 10 for j in range(a.ctx)] for i in range(B)]
+        sp = [SamplingParams(a.new, 0.3, i) for i in range(B)]
+        eng.generate(prompts, [SamplingParams(8, 0.3, i) for i in range(B)], ignore_eos=True)  # capture/warm
+        s0 = dict(eng.stats)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.generate(prompts, sp, ignore_eos=True)
+        wall = time.perf_counter() - t0
+        st = eng.stats
+        steps = st["decode_steps"] - s0["decode_steps"]
+        dec = st["decode_s"] - s0["decode_s"]
+        res.append({"B": B, "ctx": a.ctx, "decode_ms_per_step": round(1000 * dec / max(1, steps), 3),
+                    "prefill_s": round(st["prefill_s"] - s0["prefill_s"], 3), "wall_s": round(wall, 3)})
+        print(json.dumps(res[-1]), flush=True)
+
+
+if __name__ == "__main__":
+    main()
