@@ -47,6 +47,8 @@ def main() -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--stop-at-eos", action="store_true",
                     help="honour EOS (default: pin every generation to --max-new-tokens so the timed work is fixed)")
+    ap.add_argument("--reduce-tp", action="store_true", default=os.environ.get("MRSUM_REDUCE_TP", "0") == "1",
+                    help="run the reduce stages tensor-parallel over all ranks (experimental)")
     ap.add_argument("--log-level", default="WARNING")
     args = ap.parse_args()
 
@@ -70,11 +72,14 @@ def main() -> int:
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
 
     cfg = LLMConfig(MAX_TOKENS=args.max_new_tokens, TEMPERATURE=0.3, REDUCE_TEMPERATURE=0.2)
-    provider = LocalEngineProvider(args.model, cfg, use_graphs=not args.no_graphs, ignore_eos=not args.stop_at_eos)
+    provider = LocalEngineProvider(args.model, cfg, use_graphs=not args.no_graphs, ignore_eos=not args.stop_at_eos,
+                                   reduce_tp=args.reduce_tp)
     executor = LLMExecutor(config=cfg, provider_obj=provider)
     summarizer = TranscriptSummarizer(executor=executor, max_tokens_per_chunk=args.chunk_tokens)
     transcript = synthetic_transcript(args.hours, seed=0)
     _ = provider.engine  # weight init + KV allocation outside the timed region
+    if provider.reduce_tp:
+        _ = provider.reduce_engine
 
     def one():
         return asyncio.run(summarizer.summarize(transcript))
@@ -117,7 +122,8 @@ def main() -> int:
         "data": ("synthetic %gh transcript (utils/synth.py, seed 0); random-init weights; every generation "
                  "pinned to max_new_tokens%s" % (args.hours, " (EOS honoured)" if args.stop_at_eos else "")),
         "config": {"model": args.model, "global_batch": n_chunks, "seq_len": args.chunk_tokens,
-                   "parallelism": "dp%d" % world, "max_new_tokens": args.max_new_tokens,
+                   "parallelism": "dp%d" % world + ("+reduce_tp%d" % world if provider.reduce_tp else ""),
+                   "max_new_tokens": args.max_new_tokens,
                    "transcript_hours": args.hours},
         "e2e_wall_s": round(ms / 1000.0, 3),
         "phases_s": {k: round(v, 3) for k, v in rep.get("timings", {}).items()},

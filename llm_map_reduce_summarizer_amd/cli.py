@@ -67,6 +67,8 @@ def build_parser() -> argparse.ArgumentParser:
     e.add_argument("--kv-fraction", type=float, default=None, help="fraction of free HBM for the KV cache")
     e.add_argument("--no-graphs", action="store_true", help="disable hipGraph capture of decode steps")
     e.add_argument("--tokenizer", default=None, help="tiktoken-format vocabulary file (default: bundled)")
+    e.add_argument("--reduce-tp", action="store_true",
+                   help="reduce stages tensor-parallel over all ranks (map stays data-parallel; experimental)")
     e.add_argument("--aggregator-model", default=None,
                    help="separate local model for the reduce stage (e.g. llama3-70b); default: the map model")
     e.add_argument("--aggregator-dtype", choices=["bf16", "fp8"], default=None,
@@ -111,7 +113,7 @@ async def async_main(args: argparse.Namespace) -> int:
     if provider == "local":
         popts.update({"dtype": args.dtype, "tp": args.tp, "seed": args.seed, "kv_fraction": args.kv_fraction,
                       "use_graphs": not args.no_graphs, "tokenizer": args.tokenizer,
-                      "max_num_seqs": args.max_concurrent_requests})
+                      "max_num_seqs": args.max_concurrent_requests, "reduce_tp": args.reduce_tp})
     agg_executor = None
     if args.aggregator_model:
         if provider != "local":

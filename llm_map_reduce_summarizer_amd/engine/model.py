@@ -130,9 +130,10 @@ class LlamaModel:
     def _gather_vocab(self, logits: torch.Tensor) -> torch.Tensor:
         if self.tp_size == 1:
             return logits
-        parts = [torch.empty_like(logits) for _ in range(self.tp_size)]
-        torch.distributed.all_gather(parts, logits.contiguous(), group=self.tp_group)
-        return torch.cat(parts, dim=-1)
+        B, vl = logits.shape
+        out = torch.empty(self.tp_size * B, vl, dtype=logits.dtype, device=logits.device)
+        torch.distributed.all_gather_into_tensor(out, logits.contiguous(), group=self.tp_group)
+        return out.view(self.tp_size, B, vl).permute(1, 0, 2).reshape(B, self.tp_size * vl)
 
     # ------------------------------------------------------------------ forward
     def run_layers(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor,

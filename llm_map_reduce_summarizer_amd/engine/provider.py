@@ -59,7 +59,7 @@ class LocalEngineProvider(Provider):
                  tp: int = 1, seed: Optional[int] = None, max_model_len: int = 16384, engine=None,
                  engine_options: Optional[Dict[str, Any]] = None, dtype: Optional[str] = None,
                  kv_fraction: Optional[float] = None, use_graphs: bool = True, max_num_seqs: Optional[int] = None,
-                 tokenizer: Optional[str] = None, ignore_eos: bool = False, **_ignored):
+                 tokenizer: Optional[str] = None, ignore_eos: bool = False, reduce_tp: bool = False, **_ignored):
         super().__init__(model, config)
         self.tokenizer = get_tokenizer(tokenizer)
         if dtype not in (None, "bf16", "fp8"):
@@ -80,6 +80,12 @@ class LocalEngineProvider(Provider):
             self._engine_options.setdefault("max_num_seqs", max_num_seqs)
         self.timings: Dict[str, float] = {"generate_s": 0.0, "allgather_s": 0.0}
         self.par = pdist.setup_parallel(tp)
+        # reduce_tp: the reduce stages (few, long, latency-bound sequences) run on a second engine
+        # sharded over ALL ranks (TP = world) instead of on one DP replica
+        self.reduce_tp = bool(reduce_tp) and self.par.world > 1 and tp == 1
+        self._reduce_engine = None
+        if self.reduce_tp:
+            self._engine_options.setdefault("kv_fraction", 0.4)
 
     # ------------------------------------------------------------------ engine
     @property
@@ -101,6 +107,24 @@ class LocalEngineProvider(Provider):
                      self.par.dp, self._engine.init_seconds)
         return self._engine
 
+    @property
+    def reduce_engine(self):
+        """TP=world engine of the same model/seed for the reduce stages (reduce_tp mode)."""
+        if self._reduce_engine is None:
+            import torch
+            from .config import get_model_config
+            from .engine import LLMEngine
+            _ = self.engine  # DP engine first: it sizes its KV cache against the free HBM
+            world = self.par.world
+            opts = dict(self._engine_options)
+            opts.update(max_model_len=self.max_model_len, max_num_seqs=64, kv_fraction=0.5,
+                        eos_ids=self.tokenizer.eos_ids)
+            self._reduce_engine = LLMEngine(get_model_config(self.model), device=self._device, seed=self.seed,
+                                            tp_rank=self.par.rank, tp_size=world,
+                                            tp_group=pdist.tp_group_for(world), **opts)
+            log.info("reduce engine up: %s TP=%d", self.model, world)
+        return self._reduce_engine
+
     def encode_request(self, req: GenRequest) -> List[int]:
         ids = render_chat(self.tokenizer, req.user, req.system)
         budget = self.max_model_len - max(1, req.max_tokens)
@@ -118,6 +142,14 @@ class LocalEngineProvider(Provider):
         from .engine import SamplingParams
         t0 = time.perf_counter()
         prompts = [self.encode_request(r) for r in reqs]
+        if self.reduce_tp and reqs and all(r.stage != "map" for r in reqs):
+            # every rank runs every request on the TP engine; the TP ranks sample identically
+            outs = self.reduce_engine.generate(
+                prompts, [SamplingParams(r.max_tokens, r.temperature, _req_seed(self.seed, r)) for r in reqs],
+                ignore_eos=self.ignore_eos)
+            self.timings["generate_s"] += time.perf_counter() - t0
+            return [GenResult(self.tokenizer.decode(o.token_ids), o.prompt_len, len(o.token_ids), 0.0,
+                              extra={"finish_reason": o.finish_reason}) for o in outs]
         dp, dp_rank = self.par.dp, self.par.dp_rank
         owner = assign_balanced([len(p) + r.max_tokens for p, r in zip(prompts, reqs)], dp)
         mine = [i for i in range(len(reqs)) if owner[i] == dp_rank]
@@ -156,4 +188,6 @@ class LocalEngineProvider(Provider):
         s: Dict[str, Any] = {"model": self.model, "dp": self.par.dp, "tp": self.par.tp, **self.timings}
         if self._engine is not None:
             s.update(self._engine.engine_stats())
+        if self._reduce_engine is not None:
+            s["reduce_engine"] = self._reduce_engine.engine_stats()
         return s

@@ -103,6 +103,29 @@ def state() -> ParallelState:
     return _STATE
 
 
+_TP_GROUPS = {}
+
+
+def tp_group_for(tp: int):
+    """Process group of this rank's ``tp`` consecutive ranks (created once per degree; the
+    whole-world degree uses the default group).  Every rank must call this with the same ``tp``."""
+    if not is_initialized():
+        return None
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if world % tp:
+        raise ValueError("world %d not divisible by tp %d" % (world, tp))
+    if tp == world:
+        return dist.group.WORLD
+    if tp not in _TP_GROUPS:
+        mine = None
+        for start in range(0, world, tp):
+            g = dist.new_group(list(range(start, start + tp)))
+            if start <= rank < start + tp:
+                mine = g
+        _TP_GROUPS[tp] = mine
+    return _TP_GROUPS[tp]
+
+
 def _comm_device() -> torch.device:
     if is_initialized() and dist.get_backend() == "nccl":
         return torch.device("cuda", torch.cuda.current_device())

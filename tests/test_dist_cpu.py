@@ -117,3 +117,22 @@ def test_tp2_matches_tp1():
     assert tp[0] == tp[1]  # both TP ranks sample identically
     same = sum(a == b for a, b in zip(tp[0], ref))
     assert same >= 2, (tp[0], ref)  # greedy; a bf16 near-tie may flip one sequence
+
+
+RTP_SCRIPT = SCRIPT.replace('engine_options={"kv_pages": 512, "max_num_seqs": 16})',
+                            'engine_options={"kv_pages": 512, "max_num_seqs": 16}, reduce_tp=True)')
+
+
+@pytest.mark.slow
+def test_dp2_with_tp2_reduce():
+    code = RTP_SCRIPT % {"root": ROOT}
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE="2",
+               OMP_NUM_THREADS="2")
+    procs = [subprocess.Popen([sys.executable, "-c", code], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = []
+    for p in procs:
+        o, err = p.communicate(timeout=600)
+        assert p.returncode == 0, err[-3000:]
+        outs.append(json.loads([l for l in o.splitlines() if l.startswith("RESULT ")][-1][7:]))
+    assert outs[0]["summary"] == outs[1]["summary"] and outs[0]["plan"]["levels"] >= 2
