@@ -76,44 +76,38 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
     const int kend = min(len, qblock + BM);
     const int ntiles = (kend + BN - 1) / BN;
 
-    // staging: thread loads rows tid/16 + 16i (i<4), chunk tid%16
+    // staging: thread loads rows tid/16 + 16i (i<4), chunk tid%16.  Named u32x4 registers and
+    // UNCONDITIONAL loads (key clamped to the last row of the sequence; such rows are masked out of
+    // the scores, and V rows stay finite) -- a conditional or lambda-captured prefetch made hipcc
+    // serialise the loop on vmcnt(0).
     const int st_chunk = tid & 15, st_row0 = tid >> 4;
-    uint4 kreg[4], vreg[4];
-    auto load_tile = [&](int t) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int key = t * BN + st_row0 + 16 * i;
-            if (key < len) {
-                const bf16* p = base + (size_t)key * row_stride + st_chunk * 8;
-                kreg[i] = *reinterpret_cast<const uint4*>(p + kcol);
-                vreg[i] = *reinterpret_cast<const uint4*>(p + vcol);
-            } else {
-                kreg[i] = make_uint4(0, 0, 0, 0);
-                vreg[i] = make_uint4(0, 0, 0, 0);
-            }
-        }
-    };
-    auto store_tile = [&]() {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int row = st_row0 + 16 * i;
-            *reinterpret_cast<uint4*>(ldsK + k_off(row, st_chunk)) = kreg[i];
-            *reinterpret_cast<uint4*>(ldsV + v_off(row, st_chunk)) = vreg[i];
-        }
-    };
+    u32x4 kreg[4], vreg[4];
+#define LOAD_TILE(t)                                                                              \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                               \
+        const int key = min((t) * BN + st_row0 + 16 * i, len - 1);                               \
+        const bf16* p = base + (size_t)key * row_stride + st_chunk * 8;                          \
+        kreg[i] = *reinterpret_cast<const u32x4*>(p + kcol);                                     \
+        vreg[i] = *reinterpret_cast<const u32x4*>(p + vcol);                                     \
+    }
+#define STORE_TILE()                                                                              \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                               \
+        const int row = st_row0 + 16 * i;                                                         \
+        *reinterpret_cast<u32x4*>(ldsK + k_off(row, st_chunk)) = kreg[i];                        \
+        *reinterpret_cast<u32x4*>(ldsV + v_off(row, st_chunk)) = vreg[i];                        \
+    }
 
     f32x16 o[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
     float m = -INFINITY, l = 0.f;
 
-    load_tile(0);
-    store_tile();
+    LOAD_TILE(0);
+    STORE_TILE();
     __syncthreads();
 
     const int wave_last_q = qblock + 32 * w + 31;
     for (int t = 0; t < ntiles; ++t) {
-        if (t + 1 < ntiles) load_tile(t + 1);
+        LOAD_TILE(min(t + 1, ntiles - 1));
         const int kv0 = t * BN;
         if (kv0 <= wave_last_q) {  // wave-uniform: tiles wholly above the diagonal are skipped
             f32x16 sacc[2];
@@ -129,16 +123,14 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
             }
             // mask + row max (key index of reg i: kt*32 + (i&3) + 8(i>>2) + 4half)
             float mt = -INFINITY;
-            const bool need_mask = (kv0 + BN - 1 > qblock + 32 * w) || (kv0 + BN > len);
+            // causal + length mask as selects (no per-element branches); kmax = last valid key for row qi
+            const int kmax = min(qi, len - 1) - kv0 - 4 * half;
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    float sv = sacc[kt][i] * scale_log2;
-                    if (need_mask) {
-                        const int key = kv0 + kt * 32 + (i & 3) + 8 * (i >> 2) + 4 * half;
-                        if (key > qi || key >= len) sv = -INFINITY;
-                    }
+                    const int koff = kt * 32 + (i & 3) + 8 * (i >> 2);  // key - kv0 - 4*half
+                    const float sv = koff <= kmax ? sacc[kt][i] * scale_log2 : -INFINITY;
                     sacc[kt][i] = sv;
                     mt = fmaxf(mt, sv);
                 }
@@ -187,10 +179,12 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
         }
         __syncthreads();
         if (t + 1 < ntiles) {
-            store_tile();
+            STORE_TILE();
             __syncthreads();
         }
     }
+#undef LOAD_TILE
+#undef STORE_TILE
 
     // normalise and store: reg i of tile dt holds d = dt*32 + (i&3) + 8(i>>2) + 4half for query qi
     const float lt = l + __shfl_xor(l, 32, 64);
