@@ -30,7 +30,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIP_FLAGS = ["--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast",
-             "-mcode-object-version=5", "-Wno-unused-result", "-munsafe-fp-atomics"]
+             "-mcode-object-version=5", "-Wno-unused-result", "-munsafe-fp-atomics",
+             "-Rpass-analysis=kernel-resource-usage"]
 CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-sign-compare"]
 
 
@@ -48,6 +49,27 @@ def _run(cmd):
     return r.stdout
 
 
+def _check_resources(src: str, remarks: str) -> None:
+    """Fail the build if any kernel spills to scratch (always a bug here: a runtime-indexed or
+    address-taken register array -- cdna_hip_programming.md §5.4 rule 20)."""
+    fn = None
+    bad = []
+    for line in remarks.splitlines():
+        if "Function Name:" in line:
+            fn = line.split("Function Name:")[1].split("[")[0].strip()
+        elif "ScratchSize [bytes/lane]:" in line:
+            n = int(line.split("ScratchSize [bytes/lane]:")[1].split()[0])
+            if n:
+                bad.append("%s: %d B/lane" % (fn, n))
+    if bad:
+        raise RuntimeError("scratch (private memory) in %s:\n  %s" % (os.path.basename(src), "\n  ".join(bad)))
+
+
+def _compile_hip(cmd_src):
+    cmd, src = cmd_src
+    _check_resources(src, _run(cmd))
+
+
 def build_kernels(force: bool = False, jobs: int = 8) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     hdrs = glob.glob(os.path.join(CSRC, "kernels", "*.h"))
@@ -59,9 +81,9 @@ def build_kernels(force: bool = False, jobs: int = 8) -> str:
         o = os.path.join(OBJ, os.path.basename(s) + ".o")
         objs.append(o)
         if force or _newer(s, o, hdrs):
-            todo.append([HIPCC] + HIP_FLAGS + ["-I", os.path.join(CSRC, "kernels"), "-c", s, "-o", o])
+            todo.append(([HIPCC] + HIP_FLAGS + ["-I", os.path.join(CSRC, "kernels"), "-c", s, "-o", o], s))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        list(ex.map(_run, todo))
+        list(ex.map(_compile_hip, todo))
     out = os.path.join(NATIVE, "libmrsum_kernels.so")
     if force or todo or not os.path.exists(out):
         tmp = out + ".tmp"
