@@ -437,13 +437,15 @@ def plan(role: str, M: int, N: int, K: int):
     if role == "qkv":
         if M <= 8:
             return ("skinny", 1, div(2))
-        if M <= 32:
+        if M <= 16:
             return ("skinny", 2, div(4)) if N % 32 == 0 else ("skinny", 1, div(2))
-        return ("lds", div(4)) if N % 64 == 0 else ("blas",)
+        return ("lds", div(8)) if N % 64 == 0 else ("blas",)  # M=32/48/64: 15.5/17.1/18.7 vs blas ~20.5
     if role in ("o", "down"):
         if M <= 16:
             return ("skinny", 2, div(2)) if N % 32 == 0 else ("skinny", 1, div(4))
-        return ("lds", div(4)) if N % 64 == 0 else ("blas",)
+        if N % 64:
+            return ("blas",)
+        return ("lds", div(16) if K >= 2 * N else div(8))  # down 30-36 vs blas 32-40; o 11.5-13.3 vs ~20
     if role == "gate_up":
         if M <= 8:
             return ("skinny", 1, 1)

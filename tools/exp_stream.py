@@ -58,7 +58,7 @@ for name, (N, K) in {"qkv": (6144, 4096), "o": (4096, 4096), "down": (4096, 1433
                 t = b2b(lambda: hip._skinny(x, nxt(), o, hip.EPI_F32_PARTIAL, nt, splits, N))
                 out.append({"op": name, "kind": "skinny", "M": M, "nt": nt, "S": splits, "us": round(t * 1e6, 1),
                             "TBps": round(nb / t / 1e12, 2)})
-        for splits in (1, 2, 4):
+        for splits in (1, 2, 4, 8, 16):
             if (K // 128) % splits:
                 continue
             o = torch.empty(splits, M, N, dtype=torch.float32, device=dev)
