@@ -445,7 +445,7 @@ def plan(role: str, M: int, N: int, K: int):
             return ("skinny", 2, div(2)) if N % 32 == 0 else ("skinny", 1, div(4))
         if N % 64:
             return ("blas",)
-        return ("lds", div(16) if K >= 2 * N else div(8))  # down 30-36 vs blas 32-40; o 11.5-13.3 vs ~20
+        return ("lds", div(8))  # down 31-36 vs blas 32-40; o 11.5-13.3 vs ~20 (S=16 slabs cost the consumer more)
     if role == "gate_up":
         if M <= 8:
             return ("skinny", 1, 1)
