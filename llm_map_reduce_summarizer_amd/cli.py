@@ -67,6 +67,10 @@ def build_parser() -> argparse.ArgumentParser:
     e.add_argument("--kv-fraction", type=float, default=None, help="fraction of free HBM for the KV cache")
     e.add_argument("--no-graphs", action="store_true", help="disable hipGraph capture of decode steps")
     e.add_argument("--tokenizer", default=None, help="tiktoken-format vocabulary file (default: bundled)")
+    e.add_argument("--weights", default=os.environ.get("MRSUM_WEIGHTS"),
+                   help="Hugging Face Llama safetensors checkpoint (file or dir) for the map model; "
+                        "default: seeded random init.  With a non-preset --model the dir's config.json is used")
+    e.add_argument("--aggregator-weights", default=None, help="safetensors checkpoint of the aggregator model")
     e.add_argument("--reduce-tp", action="store_true",
                    help="reduce stages tensor-parallel over all ranks (map stays data-parallel; experimental)")
     e.add_argument("--aggregator-model", default=None,
@@ -113,7 +117,8 @@ async def async_main(args: argparse.Namespace) -> int:
     if provider == "local":
         popts.update({"dtype": args.dtype, "tp": args.tp, "seed": args.seed, "kv_fraction": args.kv_fraction,
                       "use_graphs": not args.no_graphs, "tokenizer": args.tokenizer,
-                      "max_num_seqs": args.max_concurrent_requests, "reduce_tp": args.reduce_tp})
+                      "max_num_seqs": args.max_concurrent_requests, "reduce_tp": args.reduce_tp,
+                      "weights": args.weights})
     agg_executor = None
     if args.aggregator_model:
         if provider != "local":
@@ -122,7 +127,7 @@ async def async_main(args: argparse.Namespace) -> int:
         if popts.get("kv_fraction") is None:
             popts["kv_fraction"] = 0.3  # leave HBM for the second engine
         aopts = dict(popts, dtype=args.aggregator_dtype, tp=args.aggregator_tp or args.tp, kv_fraction=0.6,
-                     max_model_len=40960)
+                     max_model_len=40960, weights=args.aggregator_weights)
         agg_executor = LLMExecutor(config=cfg, provider="local", model=args.aggregator_model, **aopts)
     executor = LLMExecutor(config=cfg, provider=provider, model=args.model,
                            max_concurrent_requests=args.max_concurrent_requests, **popts)

@@ -114,14 +114,15 @@ class LLMEngine:
                  kv_pages: Optional[int] = None, kv_fraction: float = 0.6, page_size: int = 64,
                  max_prefill_tokens: int = 16384, use_graphs: bool = True, sync_every: int = 16,
                  eos_ids: Sequence[int] = (128001, 128009), tp_rank: int = 0, tp_size: int = 1, tp_group=None,
-                 weight_dtype: str = "bf16"):
+                 weight_dtype: str = "bf16", weights_path: Optional[str] = None):
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
         t0 = time.perf_counter()
-        self.model = LlamaModel(cfg, self.device, dtype, seed, tp_rank, tp_size, tp_group, weight_dtype=weight_dtype)
+        self.model = LlamaModel(cfg, self.device, dtype, seed, tp_rank, tp_size, tp_group, weight_dtype=weight_dtype,
+                                 weights_path=weights_path)
         self.init_seconds = time.perf_counter() - t0
         self.page = page_size
         self.max_model_len = min(max_model_len, cfg.max_position)

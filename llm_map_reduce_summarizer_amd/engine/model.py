@@ -61,8 +61,12 @@ class LayerWeights:
 
 class LlamaModel:
     def __init__(self, cfg: ModelConfig, device: torch.device, dtype: torch.dtype = torch.bfloat16, seed: int = 0,
-                 tp_rank: int = 0, tp_size: int = 1, tp_group=None, weight_dtype: str = "bf16"):
-        """``weight_dtype="fp8"``: the four projection matrices of every layer are stored as OCP e4m3fn
+                 tp_rank: int = 0, tp_size: int = 1, tp_group=None, weight_dtype: str = "bf16",
+                 weights_path: Optional[str] = None):
+        """``weights_path``: a Hugging Face Llama safetensors checkpoint (file or directory) loaded by
+        engine.weights.load_hf instead of the seeded random init.
+
+        ``weight_dtype="fp8"``: the four projection matrices of every layer are stored as OCP e4m3fn
         with per-output-row fp32 scales (ops.Fp8Weight) -- W8A16 MFMA kernels at decode sizes,
         hipBLASLt fp8 (dynamic per-token activation scales) at prefill sizes.  Embedding, norms and
         the LM head stay bf16."""
@@ -77,7 +81,12 @@ class LlamaModel:
         self.ffn_local = cfg.ffn // tp_size
         self.vocab_local = cfg.vocab_size // tp_size
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
-        self._init_weights(seed)
+        if weights_path:
+            from .weights import load_hf
+            self.layers = [LayerWeights(None, None, None, None, None, None) for _ in range(cfg.n_layers)]
+            load_hf(self, weights_path)
+        else:
+            self._init_weights(seed)
         self.cos_sin = rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, self.device)
 
     # ------------------------------------------------------------------ weights

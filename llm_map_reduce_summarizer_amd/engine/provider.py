@@ -59,7 +59,8 @@ class LocalEngineProvider(Provider):
                  tp: int = 1, seed: Optional[int] = None, max_model_len: int = 16384, engine=None,
                  engine_options: Optional[Dict[str, Any]] = None, dtype: Optional[str] = None,
                  kv_fraction: Optional[float] = None, use_graphs: bool = True, max_num_seqs: Optional[int] = None,
-                 tokenizer: Optional[str] = None, ignore_eos: bool = False, reduce_tp: bool = False, **_ignored):
+                 tokenizer: Optional[str] = None, ignore_eos: bool = False, reduce_tp: bool = False,
+                 weights: Optional[str] = None, **_ignored):
         super().__init__(model, config)
         self.tokenizer = get_tokenizer(tokenizer)
         if dtype not in (None, "bf16", "fp8"):
@@ -72,6 +73,8 @@ class LocalEngineProvider(Provider):
         self._device = device
         self._engine_options = dict(engine_options or {})
         self._engine_options.setdefault("use_graphs", use_graphs)
+        if weights:  # HF safetensors checkpoint (engine/weights.py); else seeded random init
+            self._engine_options.setdefault("weights_path", weights)
         if dtype == "fp8":
             self._engine_options.setdefault("weight_dtype", "fp8")
         if kv_fraction is not None:
@@ -88,6 +91,16 @@ class LocalEngineProvider(Provider):
             self._engine_options.setdefault("kv_fraction", 0.4)
 
     # ------------------------------------------------------------------ engine
+    def model_config(self):
+        """Preset by name, or the checkpoint's config.json when weights are given and the name is
+        not a preset (e.g. ``--model hf --weights /ckpt``)."""
+        from .config import PRESETS, get_model_config
+        wp = self._engine_options.get("weights_path")
+        if wp and self.model.lower() not in PRESETS:
+            from .weights import config_from_hf
+            return config_from_hf(wp, self.model)
+        return get_model_config(self.model)
+
     @property
     def engine(self):
         if self._engine is None:
@@ -100,7 +113,7 @@ class LocalEngineProvider(Provider):
             opts = dict(max_model_len=self.max_model_len, max_num_seqs=self.config.ENGINE_MAX_NUM_SEQS,
                         kv_fraction=self.config.ENGINE_KV_FRACTION, eos_ids=self.tokenizer.eos_ids)
             opts.update(self._engine_options)
-            self._engine = LLMEngine(get_model_config(self.model), device=self._device, seed=self.seed,
+            self._engine = LLMEngine(self.model_config(), device=self._device, seed=self.seed,
                                      tp_rank=self.par.tp_rank, tp_size=self.par.tp, tp_group=self.par.tp_group,
                                      **opts)
             log.info("local engine up: %s on %s (tp=%d, dp=%d) in %.1f s", self.model, self._device, self.par.tp,
@@ -119,7 +132,7 @@ class LocalEngineProvider(Provider):
             opts = dict(self._engine_options)
             opts.update(max_model_len=self.max_model_len, max_num_seqs=64, kv_fraction=0.5,
                         eos_ids=self.tokenizer.eos_ids)
-            self._reduce_engine = LLMEngine(get_model_config(self.model), device=self._device, seed=self.seed,
+            self._reduce_engine = LLMEngine(self.model_config(), device=self._device, seed=self.seed,
                                             tp_rank=self.par.rank, tp_size=world,
                                             tp_group=pdist.tp_group_for(world), **opts)
             log.info("reduce engine up: %s TP=%d", self.model, world)
