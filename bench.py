@@ -49,6 +49,7 @@ def main() -> int:
                     help="honour EOS (default: pin every generation to --max-new-tokens so the timed work is fixed)")
     ap.add_argument("--reduce-tp", action="store_true", default=os.environ.get("MRSUM_REDUCE_TP", "0") == "1",
                     help="run the reduce stages tensor-parallel over all ranks (experimental)")
+    ap.add_argument("--profile", default=None, metavar="DIR", help="torch.profiler trace of the timed steps")
     ap.add_argument("--log-level", default="WARNING")
     args = ap.parse_args()
 
@@ -93,10 +94,12 @@ def main() -> int:
     pdist.barrier()
     if torch.cuda.is_available():
         torch.cuda.synchronize()
+    from llm_map_reduce_summarizer_amd.utils.profiling import maybe_profile
     t0 = time.perf_counter()
     reports = []
-    for _ in range(args.steps):
-        reports.append(one())
+    with maybe_profile(args.profile, rank):
+        for _ in range(args.steps):
+            reports.append(one())
     pdist.barrier()
     if torch.cuda.is_available():
         torch.cuda.synchronize()

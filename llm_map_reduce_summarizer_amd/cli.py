@@ -59,6 +59,8 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--max-new-tokens", type=int, default=None, help="override $MAX_TOKENS")
     g.add_argument("--temperature", type=float, default=None, help="override $TEMPERATURE (map)")
     g.add_argument("--fault-inject", type=float, default=0.0, help="mock provider: failure probability")
+    g.add_argument("--profile", default=None, metavar="DIR",
+                   help="torch.profiler trace of the run: DIR/trace_rank{r}.json + top-kernel table")
     g.add_argument("--log-level", default=os.environ.get("MRSUM_LOG_LEVEL", "INFO"))
     e = p.add_argument_group("local engine")
     e.add_argument("--dtype", choices=["bf16", "fp8"], default=None)
@@ -138,12 +140,14 @@ async def async_main(args: argparse.Namespace) -> int:
         chunker_options={"position_mode": args.position_mode, "overlap_tokens": args.chunk_overlap,
                          "apply_overlap": args.chunk_overlap > 0},
         aggregator_options={"max_levels": args.reduce_levels or None})
-    result = await summarizer.summarize(
-        transcript, merge_same_speaker=not args.no_merge, max_segment_duration=args.max_segment_duration,
-        prompt_file=args.prompt_file, system_prompt_file=args.system_prompt_file,
-        limit_segments=args.limit_segments, save_intermediate_chunks=args.save_chunks,
-        aggregator_prompt_file=args.aggregator_prompt_file, resume_chunks=args.resume_chunks,
-        time_interval_seconds=args.time_interval, preserve_timestamps=not args.no_timestamps)
+    from .utils.profiling import maybe_profile
+    with maybe_profile(args.profile, int(os.environ.get("RANK", "0"))):
+        result = await summarizer.summarize(
+            transcript, merge_same_speaker=not args.no_merge, max_segment_duration=args.max_segment_duration,
+            prompt_file=args.prompt_file, system_prompt_file=args.system_prompt_file,
+            limit_segments=args.limit_segments, save_intermediate_chunks=args.save_chunks,
+            aggregator_prompt_file=args.aggregator_prompt_file, resume_chunks=args.resume_chunks,
+            time_interval_seconds=args.time_interval, preserve_timestamps=not args.no_timestamps)
     executor.backend.close()
     if not _is_writer():
         return 0

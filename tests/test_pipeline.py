@@ -125,6 +125,16 @@ def test_cli_mock_end_to_end(example_transcript, tmp_path, capsys):
     assert main(["-i", str(tmp_path / "missing.json"), "--provider", "mock"]) == 1
 
 
+def test_cli_profile_trace(example_transcript, tmp_path):
+    from llm_map_reduce_summarizer_amd.cli import main
+    inp = tmp_path / "t.json"
+    inp.write_text(json.dumps({"segments": example_transcript["segments"][:50]}))
+    prof = tmp_path / "prof"
+    assert main(["-i", str(inp), "--provider", "mock", "-q", "--profile", str(prof)]) == 0
+    trace = json.loads((prof / "trace_rank0.json").read_text())
+    assert "traceEvents" in trace and (prof / "kernels_rank0.txt").exists()
+
+
 def test_simple_aggregator_one_shot():
     from llm_map_reduce_summarizer_amd.pipeline.simple_aggregator import SimpleAggregator, aggregate_summaries
     prov = EchoProvider(words=5)
