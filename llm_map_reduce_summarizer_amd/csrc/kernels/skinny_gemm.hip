@@ -209,30 +209,46 @@ namespace {
 __device__ __forceinline__ int xs_off(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
 }
 
-template <int MT, int EPI>
-__global__ __launch_bounds__(256) void skinny_lds_kernel(const bf16* __restrict__ x, int ldx,
+// blockDim = 64 * wpb (wpb = 4..8 waves, each owning 16 W rows): the host picks wpb and the split
+// count so the grid is a whole number of workgroups per CU -- with 448 four-wave tiles on 256 CUs a
+// quarter of the CUs streams half as much as the rest and the kernel ends at ~4 TB/s.
+template <int MT, int EPI, int PD>
+__global__ __launch_bounds__(512) void skinny_lds_kernel(const bf16* __restrict__ x, int ldx,
                                                          const bf16* __restrict__ W, int K, int M,
                                                          void* __restrict__ out, int ldo, int kper) {
     constexpr int BM = 16 * MT;
-    constexpr int XCH = BM * 16 / 256;  // 16-B x chunks per thread per k block (BM rows x 16 chunks)
+    constexpr int XCH = BM * 16 / 256;  // 16-B x chunks per thread per k block at wpb = 4 (fewer above)
     __shared__ __attribute__((aligned(16))) char xl[2][BM * 256];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, r = lane & 15, g = lane >> 4;
-    const int n0 = blockIdx.x * 64 + 16 * w;  // this wave's 16 W rows
+    const int nthr = blockDim.x;
+    const int n0 = blockIdx.x * (nthr >> 2) + 16 * w;  // this wave's 16 W rows (16 * wpb rows per WG)
     const int ks = blockIdx.y * kper, ke = min(K, ks + kper);
     const int nkb = (ke - ks) / 128;
 
-    // x staging: chunk id = tid + 256 i -> row = id / 16, chunk = id % 16
+    // x staging: chunk id = tid + nthr i -> row = id / 16, chunk = id % 16 (ids past BM*16 idle)
     u32x4 xr[XCH];
 #define LOAD_X(kb)                                                                                         \
-    _Pragma("unroll") for (int i = 0; i < XCH; ++i) xr[i] = *reinterpret_cast<const u32x4*>(               \
-        x + (size_t)min((tid + 256 * i) >> 4, M - 1) * ldx + (kb) + ((tid + 256 * i) & 15) * 8);
+    _Pragma("unroll") for (int i = 0; i < XCH; ++i) {                                                      \
+        const int id = min(tid + nthr * i, BM * 16 - 1);                                                   \
+        xr[i] = *reinterpret_cast<const u32x4*>(x + (size_t)min(id >> 4, M - 1) * ldx + (kb) + (id & 15) * 8); \
+    }
 #define STORE_X(buf)                                                                                       \
-    _Pragma("unroll") for (int i = 0; i < XCH; ++i)                                                        \
-        *reinterpret_cast<u32x4*>(&xl[buf][xs_off((tid + 256 * i) >> 4, (tid + 256 * i) & 15)]) = xr[i];
+    _Pragma("unroll") for (int i = 0; i < XCH; ++i) {                                                      \
+        const int id = tid + nthr * i;                                                                     \
+        if (id < BM * 16) *reinterpret_cast<u32x4*>(&xl[buf][xs_off(id >> 4, id & 15)]) = xr[i];          \
+    }
     const bf16* wrow = W + (size_t)(n0 + r) * K + 8 * g;
-    u32x4 a0[4], a1[4];
+    u32x4 a0[4], a1[4], a2[4];
 #define LOAD_A(dst, kb) \
     _Pragma("unroll") for (int i = 0; i < 4; ++i) dst[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(wrow + (kb) + 32 * i));
+#define MMA(USE, CUR)                                                                                      \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                        \
+        _Pragma("unroll") for (int m = 0; m < MT; ++m) {                                                   \
+            const u32x4 bv = *reinterpret_cast<const u32x4*>(&xl[CUR][xs_off(16 * m + r, 4 * i + g)]);     \
+            acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, USE[i]),           \
+                                                             __builtin_bit_cast(bf16x8, bv), acc[m], 0, 0, 0); \
+        }                                                                                                  \
+    }
 
     f32x4 acc[MT];
 #pragma unroll
@@ -240,30 +256,49 @@ __global__ __launch_bounds__(256) void skinny_lds_kernel(const bf16* __restrict_
 
     LOAD_X(ks);
     LOAD_A(a0, ks);
+    if constexpr (PD == 2) LOAD_A(a1, ks + min(1, nkb - 1) * 128);
     STORE_X(0);
     __syncthreads();
-    // two k blocks per trip so the A register sets and LDS buffers have static roles (rule 20)
+    if constexpr (PD == 1) {
+        // two k blocks per trip so the A register sets and LDS buffers have static roles (rule 20)
 #define STEP(j, USE, PREF, CUR)                                                                            \
     {                                                                                                      \
         const int kn = ks + min((j) + 1, nkb - 1) * 128; /* unconditional prefetch (last block re-read) */ \
         LOAD_X(kn);                                                                                        \
         LOAD_A(PREF, kn);                                                                                  \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                    \
-            _Pragma("unroll") for (int m = 0; m < MT; ++m) {                                               \
-                const u32x4 bv = *reinterpret_cast<const u32x4*>(&xl[CUR][xs_off(16 * m + r, 4 * i + g)]); \
-                acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, USE[i]),       \
-                                                                 __builtin_bit_cast(bf16x8, bv), acc[m], 0, 0, 0); \
-            }                                                                                              \
-        }                                                                                                  \
+        MMA(USE, CUR);                                                                                     \
         STORE_X(CUR ^ 1);                                                                                  \
         __syncthreads();                                                                                   \
     }
-    for (int j = 0; j < nkb; j += 2) {
-        STEP(j, a0, a1, 0);
-        if (j + 1 >= nkb) break;
-        STEP(j + 1, a1, a0, 1);
-    }
+        for (int j = 0; j < nkb; j += 2) {
+            STEP(j, a0, a1, 0);
+            if (j + 1 >= nkb) break;
+            STEP(j + 1, a1, a0, 1);
+        }
 #undef STEP
+    } else {
+        // prefetch distance 2: W block j+2 is in flight while block j is consumed (x for block j+1 is
+        // issued first, so waiting on it never waits on the newer W loads -- vmcnt is in order).
+        // Three W register sets rotate with static roles; the LDS buffer index is a runtime value.
+#define STEP2(j, USE, PREF)                                                                                \
+    {                                                                                                      \
+        LOAD_X(ks + min((j) + 1, nkb - 1) * 128);                                                          \
+        LOAD_A(PREF, ks + min((j) + 2, nkb - 1) * 128);                                                    \
+        const int cur = (j) & 1;                                                                           \
+        MMA(USE, cur);                                                                                     \
+        STORE_X(cur ^ 1);                                                                                  \
+        __syncthreads();                                                                                   \
+    }
+        for (int j = 0; j < nkb; j += 3) {
+            STEP2(j, a0, a2);
+            if (j + 1 >= nkb) break;
+            STEP2(j + 1, a1, a0);
+            if (j + 2 >= nkb) break;
+            STEP2(j + 2, a2, a1);
+        }
+#undef STEP2
+    }
+#undef MMA
 #undef LOAD_X
 #undef STORE_X
 #undef LOAD_A
@@ -303,19 +338,23 @@ __global__ __launch_bounds__(256) void skinny_lds_kernel(const bf16* __restrict_
     }
 }
 
-// Same contract as mrsum_skinny_gemm; N % 64 == 0, 16 < M <= 64 (also valid for M <= 16).
+// Same contract as mrsum_skinny_gemm; N % (16 wpb) == 0, 16 < M <= 64 (also valid for M <= 16).
 MRSUM_API int mrsum_skinny_lds(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
-                               int epi, int splits, hipStream_t s) {
+                               int epi, int splits, int depth, int wpb, hipStream_t s) {
     if (M <= 0) return 0;
-    if (M > 64 || K % KB || N % 64 || splits < 1 || (K / KB) % splits) return (int)hipErrorInvalidValue;
+    if (wpb < 4 || wpb > 8) return (int)hipErrorInvalidValue;
+    if (M > 64 || K % KB || N % (16 * wpb) || splits < 1 || (K / KB) % splits) return (int)hipErrorInvalidValue;
     if (epi != EPI_F32_PARTIAL && splits != 1) return (int)hipErrorInvalidValue;
     const int kper = K / splits;
     const int mt = (M + 15) / 16;
-    dim3 grid(N / 64, splits);
+    dim3 grid(N / (16 * wpb), splits), block(64 * wpb);
     auto X = (const bf16*)x; auto Wp = (const bf16*)W;
-#define L(MT_, EPI_) skinny_lds_kernel<MT_, EPI_><<<grid, 256, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper)
+#define L(MT_, EPI_)                                                                                 \
+    if (depth == 2) skinny_lds_kernel<MT_, EPI_, 2><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper); \
+    else skinny_lds_kernel<MT_, EPI_, 1><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper)
 #define BY_EPI(MT_) \
-    if (epi == EPI_BF16) L(MT_, EPI_BF16); else if (epi == EPI_F32_PARTIAL) L(MT_, EPI_F32_PARTIAL); else L(MT_, EPI_SWIGLU);
+    if (epi == EPI_BF16) { L(MT_, EPI_BF16); } else if (epi == EPI_F32_PARTIAL) { L(MT_, EPI_F32_PARTIAL); } \
+    else { L(MT_, EPI_SWIGLU); }
     switch (mt) {
         case 1: BY_EPI(1); break;
         case 2: BY_EPI(2); break;

@@ -1,0 +1,203 @@
+// Decode GEMM with an LDS-DMA weight ring: out[M, N] = x[M, K] . W[N, K]^T, M <= 64.
+//
+// Why a second decode GEMM: the register-streaming kernels (skinny_gemm.hip) keep 8-16 KiB of W
+// in flight per workgroup and reach 4-5 TB/s; at M = 16-64 the x fragments they re-read and the
+// per-k-block barrier of the LDS-x variant cap them near 3.5-4 TB/s.  A streaming CU needs
+// ~80-130 KiB in flight to cover loaded HBM latency (MI355X_MICROARCH.md "ldsdma-fill": 8 x 16 KiB
+// ring = 6.4-6.8 TB/s chip-wide), which register staging cannot hold next to the accumulators.
+//
+// Structure (one workgroup per CU, grid = N / (16 WPB) x splitK chosen by the host ~= #CUs):
+//   * ring of D slots in ONE __shared__ array; slot = [16 WPB W rows | 16 MT x rows] x one
+//     128-wide k block, each row block as two 1 KiB pieces of 8 rows x 128 B.  Every piece is ONE
+//     global_load_lds_dwordx4 wave instruction (full 128-B lines, cdna_hip_programming.md §5 "x
+//     operand ... through LDS in full 128-B lines"); lane l lands at piece + 16 l, so the bank
+//     swizzle goes on the SOURCE address (rule 21): LDS chunk slot s of row r holds global chunk
+//     s ^ (r & 7).
+//   * every wave issues the same number of DMA instructions per slot (the x pieces are padded
+//     with dummy pieces into a scratch KiB) so one counted `s_waitcnt vmcnt(NI * (D-2))` retires
+//     exactly the slot about to be read; raw s_barrier (never __syncthreads, whose fence would
+//     drain the ring); the slot consumed in iteration j-1 is refilled right after iteration j's
+//     barrier (WAR ordered by that barrier).
+//   * wave w owns W rows [16w, 16w + 16) of the tile: per k block 4 x v_mfma_f32_16x16x32_bf16
+//     per x tile, A = W fragment (ds_read_b128), B = x fragment (ds_read_b128) -- the same
+//     swapped out^T product and epilogues as skinny_gemm.hip (bf16 | fp32 split-K slab | SwiGLU
+//     over [8 gate | 8 up] row blocks).
+#include "common.h"
+
+namespace {
+enum { EPI_BF16 = 0, EPI_F32_PARTIAL = 1, EPI_SWIGLU = 2 };
+constexpr int KBLK = 128;
+constexpr int LDS_BUDGET = 160 * 1024 - 1024;  // one KiB scratch for the dummy x pieces
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    // gfx9 s_waitcnt: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14; others at max = no wait
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// raw barrier with compiler fences: keeps LDS reads/DMA issues on their side without the vmcnt(0)
+// that __syncthreads() would add
+__device__ __forceinline__ void raw_barrier() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ int img_off(int row, int chunk) {
+    return (((row >> 3) << 1) + (chunk >> 3)) * 1024 + ((row & 7) << 7) + ((((chunk & 7) ^ (row & 7))) << 4);
+}
+
+__device__ __forceinline__ void glds16(const void* g, char* lds) {
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                     (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+}  // namespace
+
+template <int MT, int EPI, int WPB>
+__global__ __launch_bounds__(64 * WPB, 1) void stream_gemm_kernel(const bf16* __restrict__ x, int ldx,
+                                                                  const bf16* __restrict__ W, int K, int M,
+                                                                  void* __restrict__ out, int ldo, int kper) {
+    constexpr int R = 16 * WPB, BM = 16 * MT;
+    constexpr int WBYTES = R * 256, SLOT = WBYTES + BM * 256;
+    constexpr int D = (LDS_BUDGET / SLOT) < 6 ? (LDS_BUDGET / SLOT) : 6;
+    static_assert(D >= 2, "ring too shallow");
+    constexpr int XP = 2 * BM / 8;               // x pieces per slot (= 4 MT)
+    constexpr int XI = (XP + WPB - 1) / WPB;     // x pieces per wave (padded)
+    constexpr int NI = 4 + XI;                   // DMA instructions per wave per slot (W: R/4 pieces / WPB = 4)
+    __shared__ __attribute__((aligned(1024))) char lds[D * SLOT + 1024];
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int n0 = blockIdx.x * R;
+    const int ks = blockIdx.y * kper;
+    const int nkb = kper / KBLK;
+
+    // per-lane source rows/chunks of this wave's pieces (fixed over k)
+    const int prow = lane >> 3, pslot = lane & 7;
+    // W pieces q = 4w + p (p < 4): rows 8 (q >> 1) + prow, k half q & 1
+    const bf16* wsrc[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int q = 4 * w + p;
+        const int row = 8 * (q >> 1) + prow;
+        wsrc[p] = W + (size_t)(n0 + row) * K + ks + 8 * (8 * (q & 1) + (pslot ^ prow));
+    }
+    const bf16* xsrc[XI];
+    int xdst[XI];
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+        const int q = w + WPB * i;  // x piece index; >= XP -> dummy
+        const int qq = q < XP ? q : 0;
+        const int row = 8 * (qq >> 1) + prow;
+        xsrc[i] = x + (size_t)min(row, M - 1) * ldx + ks + 8 * (8 * (qq & 1) + (pslot ^ prow));
+        xdst[i] = q < XP ? WBYTES + q * 1024 : -1;
+    }
+#define ISSUE(slot, kb)                                                                              \
+    {                                                                                                \
+        char* base = lds + (slot) * SLOT;                                                            \
+        _Pragma("unroll") for (int p = 0; p < 4; ++p) glds16(wsrc[p] + (kb), base + (4 * w + p) * 1024); \
+        _Pragma("unroll") for (int i = 0; i < XI; ++i)                                               \
+            glds16(xsrc[i] + (kb), xdst[i] >= 0 ? base + xdst[i] : lds + D * SLOT);                  \
+    }
+
+    f32x4 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // prologue: D-1 slots in flight (clamped k blocks past the end are never read)
+#pragma unroll
+    for (int s = 0; s < D - 1; ++s) ISSUE(s, min(s, nkb - 1) * KBLK);
+
+    const int r = lane & 15, g = lane >> 4;
+    for (int j = 0; j < nkb; ++j) {
+        if (j + D - 2 < nkb) wait_vmcnt<NI * (D - 2)>();  // slots j+1 .. j+D-2 stay in flight
+        else wait_vmcnt<0>();
+        raw_barrier();
+        if (j + D - 1 < nkb) ISSUE((j + D - 1) % D, (j + D - 1) * KBLK);
+        const char* wl = lds + (j % D) * SLOT;
+        const char* xl = wl + WBYTES;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const u32x4 av = *reinterpret_cast<const u32x4*>(wl + img_off(16 * w + r, 4 * i + g));
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                const u32x4 bv = *reinterpret_cast<const u32x4*>(xl + img_off(16 * m + r, 4 * i + g));
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, av),
+                                                                 __builtin_bit_cast(bf16x8, bv), acc[m], 0, 0, 0);
+            }
+        }
+    }
+#undef ISSUE
+
+    // C: lane holds out^T[n = n0 + 16w + 4g + jj][m = 16 mt + r]
+    const int nw = n0 + 16 * w;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const int mm = 16 * m + r;
+        if constexpr (EPI == EPI_SWIGLU) {
+            f32x4 up;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) up[jj] = __shfl_xor(acc[m][jj], 32, 64);
+            if (g < 2 && mm < M) {
+                float rr[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const float gv = acc[m][jj];
+                    rr[jj] = gv / (1.f + __expf(-gv)) * up[jj];
+                }
+                uint2 o;
+                o.x = pack2(rr[0], rr[1]);
+                o.y = pack2(rr[2], rr[3]);
+                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + (nw >> 1) + 4 * g) = o;
+            }
+        } else if (mm < M) {
+            if constexpr (EPI == EPI_BF16) {
+                uint2 o;
+                o.x = pack2(acc[m][0], acc[m][1]);
+                o.y = pack2(acc[m][2], acc[m][3]);
+                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + nw + 4 * g) = o;
+            } else {
+                float* o = reinterpret_cast<float*>(out) + ((size_t)blockIdx.y * M + mm) * ldo + nw + 4 * g;
+                *reinterpret_cast<float4*>(o) = make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
+            }
+        }
+    }
+}
+
+// out: bf16 [M, ldo] (EPI_BF16), fp32 slabs [splits, M, ldo] (EPI_F32_PARTIAL) or bf16 [M, ldo] of
+// N/2 SwiGLU features (EPI_SWIGLU, splits = 1).  N % (16 wpb) == 0, wpb in {4, 5, 6, 7, 8}.
+MRSUM_API int mrsum_stream_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
+                                int epi, int splits, int wpb, hipStream_t s) {
+    if (M <= 0) return 0;
+    if (wpb < 4 || wpb > 8 || M > 64 || K % KBLK || N % (16 * wpb) || splits < 1 || (K / KBLK) % splits)
+        return (int)hipErrorInvalidValue;
+    if (epi != EPI_F32_PARTIAL && splits != 1) return (int)hipErrorInvalidValue;
+    const int kper = K / splits;
+    const int mt = (M + 15) / 16;
+    dim3 grid(N / (16 * wpb), splits), block(64 * wpb);
+    auto X = (const bf16*)x;
+    auto Wp = (const bf16*)W;
+#define L(MT_, EPI_, WPB_) stream_gemm_kernel<MT_, EPI_, WPB_><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper)
+#define BY_WPB(MT_, EPI_)                          \
+    switch (wpb) {                                 \
+        case 4: L(MT_, EPI_, 4); break;            \
+        case 5: L(MT_, EPI_, 5); break;            \
+        case 6: L(MT_, EPI_, 6); break;            \
+        case 7: L(MT_, EPI_, 7); break;            \
+        default: L(MT_, EPI_, 8); break;           \
+    }
+#define BY_EPI(MT_)                                                           \
+    if (epi == EPI_BF16) { BY_WPB(MT_, EPI_BF16) }                            \
+    else if (epi == EPI_F32_PARTIAL) { BY_WPB(MT_, EPI_F32_PARTIAL) }         \
+    else { BY_WPB(MT_, EPI_SWIGLU) }
+    switch (mt) {
+        case 1: BY_EPI(1); break;
+        case 2: BY_EPI(2); break;
+        case 3: BY_EPI(3); break;
+        default: BY_EPI(4); break;
+    }
+#undef BY_EPI
+#undef BY_WPB
+#undef L
+    return (int)hipGetLastError();
+}

@@ -118,6 +118,8 @@ def sample(logits, st):
 # (ops.hip.plan).  On the CPU they are the reference composition.
 
 def _plan_parts(hip, p, x, w, splits):
+    if p[0] == "stream":
+        return hip.linear_parts(x, w, p[2], nt=p[1], kernel="stream")
     if p[0] == "lds":
         return hip.linear_parts(x, w, splits or p[1], kernel="lds")
     return hip.linear_parts(x, w, splits or p[2], nt=p[1])
@@ -125,7 +127,7 @@ def _plan_parts(hip, p, x, w, splits):
 
 def _fp8_parts(hip, x, w, role, splits):
     """Split-K fp32 slabs from the fp8 weight-streaming kernel (decode) -- same plan shapes as bf16."""
-    p = hip.plan(role, x.shape[0], w.shape[0], w.shape[1])
+    p = hip.plan(role, x.shape[0], w.shape[0], w.shape[1], stream=False)
     nt = p[1] if p[0] == "skinny" else 1
     s = splits or (p[2] if p[0] == "skinny" else (p[1] if p[0] == "lds" else 1))
     if w.shape[0] % (16 * nt):
@@ -174,7 +176,7 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
         return hip.add_rmsnorm(o, residual, ln, eps)
     if _use_hip(a):
         from . import hip
-        p = hip.plan(role, a.shape[0], w.shape[0], w.shape[1])
+        p = hip.plan(role, a.shape[0], w.shape[0], w.shape[1], splits=1 if all_reduce else None)
         if p[0] != "blas":
             parts = _plan_parts(hip, p, a, w, 1 if all_reduce else None)
             if all_reduce:
@@ -198,6 +200,8 @@ def gate_up_swiglu(x, wgu):
     if _use_hip(x):
         from . import hip
         p = hip.plan("gate_up", x.shape[0], wgu.shape[0], wgu.shape[1])
+        if p[0] == "stream":
+            return hip.linear_swiglu(x, wgu, kernel="stream", wpb=p[1])
         if p[0] != "blas":
             return hip.linear_swiglu(x, wgu, kernel=p[0])
         return hip.swiglu(torch.nn.functional.linear(x, wgu))

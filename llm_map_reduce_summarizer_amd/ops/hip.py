@@ -34,7 +34,9 @@ _SIGS = {
     "mrsum_attn_decode_mfma": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int,
                                _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
-    "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _vp],
+    "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int,
+                         _vp],
+    "mrsum_stream_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_skinny_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_quant_fp8_rows": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
@@ -342,17 +344,38 @@ def _skinny(x, w, out, epi, nt, splits, ldo):
     return out
 
 
-def _skinny_lds(x, w, out, epi, splits, ldo):
-    """Medium-M (x staged in LDS) variant; same contract as _skinny with nt fixed at 64-row tiles."""
+LDS_DEPTH = int(os.environ.get("MRSUM_LDS_DEPTH", "2"))
+
+
+def _skinny_lds(x, w, out, epi, splits, ldo, depth=None, wpb=4):
+    """Medium-M (x staged in LDS) variant; same contract as _skinny, 16*wpb-row tiles (wpb waves).
+    depth = W prefetch distance in 128-wide k blocks (1 or 2)."""
     _bf16_cuda(x, w)
     _rows_ok(x)
     M, K = x.shape
     N = w.shape[0]
     _req(w.is_contiguous() and w.shape[1] == K, "skinny_lds: weight must be [N, K] contiguous")
-    _req(1 <= M <= SKINNY_MAX_M and K % 128 == 0 and N % 64 == 0 and (K // 128) % splits == 0,
-         "skinny_lds: unsupported shape M=%d N=%d K=%d S=%d" % (M, N, K, splits))
-    _check(_fn("mrsum_skinny_lds")(_p(x), x.stride(0), _p(w), N, K, M, _p(out), ldo, epi, splits, _stream()),
+    _req(1 <= M <= SKINNY_MAX_M and K % 128 == 0 and 4 <= wpb <= 8 and N % (16 * wpb) == 0
+         and (K // 128) % splits == 0, "skinny_lds: unsupported shape M=%d N=%d K=%d S=%d wpb=%d" % (M, N, K, splits, wpb))
+    _check(_fn("mrsum_skinny_lds")(_p(x), x.stride(0), _p(w), N, K, M, _p(out), ldo, epi, splits,
+                                   LDS_DEPTH if depth is None else depth, wpb, _stream()),
            "skinny_lds")
+    return out
+
+
+def _stream_gemm(x, w, out, epi, splits, ldo, wpb):
+    """LDS-DMA weight-ring decode GEMM (csrc/kernels/stream_gemm.hip); same contract as _skinny_lds,
+    one 16*wpb-row tile per workgroup, ~one workgroup per CU."""
+    _bf16_cuda(x, w)
+    _rows_ok(x)
+    M, K = x.shape
+    N = w.shape[0]
+    _req(w.is_contiguous() and w.shape[1] == K, "stream_gemm: weight must be [N, K] contiguous")
+    _req(1 <= M <= SKINNY_MAX_M and K % 128 == 0 and 4 <= wpb <= 8 and N % (16 * wpb) == 0
+         and (K // 128) % splits == 0, "stream_gemm: unsupported shape M=%d N=%d K=%d S=%d wpb=%d"
+         % (M, N, K, splits, wpb))
+    _check(_fn("mrsum_stream_gemm")(_p(x), x.stride(0), _p(w), N, K, M, _p(out), ldo, epi, splits, wpb,
+                                    _stream()), "stream_gemm")
     return out
 
 
@@ -372,7 +395,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
 def linear_parts(x: torch.Tensor, w: torch.Tensor, splits: Optional[int] = None,
                  out: Optional[torch.Tensor] = None, nt: int = 1, kernel: str = "skinny") -> torch.Tensor:
     """fp32 split-K slabs [S, M, N] of x @ w^T (summed by add_rmsnorm_parts / rope_kv_parts).
-    kernel "skinny" (waves split k, nt 16-row tiles) or "lds" (x staged in LDS, 64-row tiles)."""
+    kernel "skinny" (waves split k, nt 16-row tiles), "lds" (x staged in LDS, 64-row tiles) or "stream"
+    (LDS-DMA weight ring; nt = waves per workgroup, 16 * nt-row tiles)."""
     M, K = x.shape
     N = w.shape[0]
     if splits is None:
@@ -380,13 +404,15 @@ def linear_parts(x: torch.Tensor, w: torch.Tensor, splits: Optional[int] = None,
     if out is None:
         out = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
     _req(out.is_contiguous() and out.shape == (splits, M, N) and out.dtype == torch.float32, "linear_parts: bad out")
+    if kernel == "stream":
+        return _stream_gemm(x, w, out, EPI_F32_PARTIAL, splits, N, nt)
     if kernel == "lds":
         return _skinny_lds(x, w, out, EPI_F32_PARTIAL, splits, N)
     return _skinny(x, w, out, EPI_F32_PARTIAL, nt, splits, N)
 
 
 def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tensor] = None,
-                  kernel: str = "skinny") -> torch.Tensor:
+                  kernel: str = "skinny", wpb: int = 4) -> torch.Tensor:
     """silu(gate) * up straight out of the gate_up GEMM (blocked [8 gate | 8 up] weight rows)."""
     M = x.shape[0]
     F2 = w_gu.shape[0]
@@ -395,6 +421,8 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tenso
     if out is None:
         out = torch.empty(M, F2 // 2, dtype=x.dtype, device=x.device)
     _req(out.is_contiguous() and out.shape == (M, F2 // 2), "linear_swiglu: bad out")
+    if kernel == "stream":
+        return _stream_gemm(x, w_gu, out, EPI_SWIGLU, 1, F2 // 2, wpb)
     if kernel == "lds":
         return _skinny_lds(x, w_gu, out, EPI_SWIGLU, 1, F2 // 2)
     return _skinny(x, w_gu, out, EPI_SWIGLU, 1, 1, F2 // 2)
@@ -417,16 +445,50 @@ def add_rmsnorm_parts(parts: torch.Tensor, residual: torch.Tensor, w: torch.Tens
 
 
 # ------------------------------------------------------------------ per-role GEMM plans
-# Measured on MI355X (tools/exp_stream.py, back-to-back launches, weights beyond the 256 MiB
-# Infinity Cache, Llama-3-8B shapes; us per call, ours vs hipBLASLt):
-#   M=1 : qkv 12.1 vs 21.3 | o 9.9 vs 20.5 | gate_up+SwiGLU 44.6 vs 55.4(+swiglu) | down 24.2 vs 24.1
-#   M=16: qkv 15.0 vs 21.8 | o 10.5 vs 20.4 | gate_up 57.3(lds) vs 56.8(+swiglu)  | down 26.8 vs 24.8
-#   M=48: qkv 18.8(lds) vs 20.6(+rope) | o 12.2(lds) vs 20.4 | gate_up 63.2(lds) vs 57.8(+swiglu) | down 33.6(lds) vs 35.8
+# Measured on MI355X (tools/exp_lds_wpb.py, back-to-back launches, weights beyond the 256 MiB
+# Infinity Cache, Llama-3-8B shapes, us per call; profiles/r1_decode_gemm_sweep.txt):
+#   stream (LDS-DMA ring, one WG per CU)   M=1  qkv 10.7 | o 10.2 | gate_up+SwiGLU 44.3 | down 22.0
+#                                          M=39 qkv 11.7 | o 10.2 | gate_up+SwiGLU 44.1 | down 23.2
+#   register-streaming skinny / LDS-x      M=1  qkv 12.1 | o  9.9 | gate_up+SwiGLU 44.6 | down 24.2
+#                                          M=39 qkv 15.8 | o 11.7 | gate_up+SwiGLU 60.7 | down 30.7
+#   hipBLASLt                              M=39 qkv 19.9 | o 19.7 | gate_up 49.8 (+SwiGLU) | down 36.3
+# The stream kernel is flat in M up to 64 and best on grids of exactly one workgroup per CU.
 # Streaming floor (probe): qkv 9.5, o 7.6, down 20.1, gate_up 39.1.
-# Plan = ("skinny", nt, S) | ("lds", S) | ("blas",)
-def plan(role: str, M: int, N: int, K: int):
+# Plan = ("stream", wpb, S) | ("skinny", nt, S) | ("lds", S) | ("blas",)
+N_CU = 256
+
+
+def stream_config(N: int, K: int, swiglu: bool = False, splits: Optional[int] = None, max_splits: int = 16):
+    """(wpb, S) for the stream GEMM whose grid N/(16 wpb) * S best fills one workgroup per CU, or None
+    when no configuration fills >= 70 % of the CUs (then the register-streaming kernels win)."""
+    if K % 128:
+        return None
+    nkb = K // 128
+    best, best_key = None, None
+    for wpb in (4, 5, 6, 7, 8):
+        if N % (16 * wpb):
+            continue
+        tiles = N // (16 * wpb)
+        cands = [1] if swiglu else ([splits] if splits else range(1, max_splits + 1))
+        for S in cands:
+            if nkb % S:
+                continue
+            grid = tiles * S
+            eff = grid / (-(-grid // N_CU) * N_CU)
+            key = (round(eff, 3), -S, wpb)
+            if best_key is None or key > best_key:
+                best, best_key = (wpb, S), key
+    if best is None or best_key[0] < 0.7:
+        return None
+    return best
+
+
+def plan(role: str, M: int, N: int, K: int, splits: Optional[int] = None, stream: bool = True):
     if M > SKINNY_MAX_M or K % 128:
         return ("blas",)
+    cfg = stream_config(N, K, swiglu=(role == "gate_up"), splits=splits) if stream and STREAM_GEMM else None
+    if cfg is not None:
+        return ("stream",) + cfg
     blocks = K // 128
 
     def div(s):
@@ -436,16 +498,16 @@ def plan(role: str, M: int, N: int, K: int):
 
     if role == "qkv":
         if M <= 8:
-            return ("skinny", 1, div(2))
+            return ("skinny", 1, splits or div(2))
         if M <= 16:
-            return ("skinny", 2, div(4)) if N % 32 == 0 else ("skinny", 1, div(2))
-        return ("lds", div(8)) if N % 64 == 0 else ("blas",)  # M=32/48/64: 15.5/17.1/18.7 vs blas ~20.5
+            return ("skinny", 2, splits or div(4)) if N % 32 == 0 else ("skinny", 1, splits or div(2))
+        return ("lds", splits or div(8)) if N % 64 == 0 else ("blas",)
     if role in ("o", "down"):
         if M <= 16:
-            return ("skinny", 2, div(2)) if N % 32 == 0 else ("skinny", 1, div(4))
+            return ("skinny", 2, splits or div(2)) if N % 32 == 0 else ("skinny", 1, splits or div(4))
         if N % 64:
             return ("blas",)
-        return ("lds", div(8))  # down 31-36 vs blas 32-40; o 11.5-13.3 vs ~20 (S=16 slabs cost the consumer more)
+        return ("lds", splits or div(8))
     if role == "gate_up":
         if M <= 8:
             return ("skinny", 1, 1)
@@ -453,6 +515,9 @@ def plan(role: str, M: int, N: int, K: int):
             return ("lds", 1)
         return ("blas",)
     return ("blas",)
+
+
+STREAM_GEMM = os.environ.get("MRSUM_STREAM_GEMM", "1") == "1"
 
 
 # ------------------------------------------------------------------ FP8 (e4m3fn) weights

@@ -261,16 +261,47 @@ def test_rope_kv_parts(S):
 
 
 @pytest.mark.parametrize("M", [1, 17, 33, 48, 64])
-def test_skinny_lds_all_epilogues(M):
-    K = 1024
+@pytest.mark.parametrize("depth,K", [(1, 1024), (2, 1024), (2, 640)])
+def test_skinny_lds_all_epilogues(M, depth, K, monkeypatch):
+    monkeypatch.setattr(hip, "LDS_DEPTH", depth)
     x = _rand(M, K, seed=40)
     w = _rand(512, K, scale=0.05, seed=41)
     ref = x.float() @ w.float().t()
     o = torch.empty(M, 512, dtype=torch.bfloat16, device=DEV)
     _close(hip._skinny_lds(x, w, o, hip.EPI_BF16, 1, 512), ref, 2e-2)
-    for S in (1, 2, 8):
+    for S in ((1, 2, 8) if K == 1024 else (1, 5)):  # K=640: 5 k blocks
         parts = hip.linear_parts(x, w, S, kernel="lds")
         _close(parts.sum(0), ref, 1e-3, 1e-3)
+    for wpb in (5, 6, 7, 8):  # 16 * wpb-row tiles
+        n = 16 * wpb * 3
+        ww = _rand(n, K, scale=0.05, seed=44)
+        S = 2 if (K // 128) % 2 == 0 else 1
+        oo = torch.empty(S, M, n, dtype=torch.float32, device=DEV)
+        _close(hip._skinny_lds(x, ww, oo, hip.EPI_F32_PARTIAL, S, n, depth, wpb).sum(0),
+               x.float() @ ww.float().t(), 1e-3, 1e-3)
+
+
+@pytest.mark.parametrize("M", [1, 9, 16, 39, 64])
+@pytest.mark.parametrize("wpb", [4, 5, 6, 7, 8])
+@pytest.mark.parametrize("K", [128, 384, 1024, 2304])  # 1 .. 18 k blocks: ring prologue / tail paths
+def test_stream_gemm(M, wpb, K):
+    x = _rand(M, K, seed=60)
+    n = 16 * wpb * 3
+    w = _rand(n, K, scale=0.05, seed=61)
+    ref = x.float() @ w.float().t()
+    o = torch.empty(M, n, dtype=torch.bfloat16, device=DEV)
+    _close(hip._stream_gemm(x, w, o, hip.EPI_BF16, 1, n, wpb), ref, 2e-2)
+    nkb = K // 128
+    for S in sorted({1, 2 if nkb % 2 == 0 else 1, nkb}):
+        parts = torch.empty(S, M, n, dtype=torch.float32, device=DEV)
+        _close(hip._stream_gemm(x, w, parts, hip.EPI_F32_PARTIAL, S, n, wpb).sum(0), ref, 1e-3, 1e-3)
+    f = 8 * wpb * 3
+    wg = _rand(f, K, scale=0.05, seed=62)
+    wu = _rand(f, K, scale=0.05, seed=63)
+    g, u = x.float() @ wg.float().t(), x.float() @ wu.float().t()
+    act = torch.empty(M, f, dtype=torch.bfloat16, device=DEV)
+    _close(hip._stream_gemm(x, reference.interleave_gate_up(wg, wu).contiguous(), act, hip.EPI_SWIGLU, 1, f, wpb),
+           g * torch.sigmoid(g) * u, 2e-2)
     wg = _rand(256, K, scale=0.05, seed=42)
     wu = _rand(256, K, scale=0.05, seed=43)
     g, u = x.float() @ wg.float().t(), x.float() @ wu.float().t()

@@ -62,14 +62,16 @@ for name, (N, K) in {"qkv": (6144, 4096), "o": (4096, 4096), "down": (4096, 1433
             if (K // 128) % splits:
                 continue
             o = torch.empty(splits, M, N, dtype=torch.float32, device=dev)
-            t = b2b(lambda: hip._skinny_lds(x, nxt(), o, hip.EPI_F32_PARTIAL, splits, N))
-            out.append({"op": name, "kind": "lds", "M": M, "nt": 4, "S": splits, "us": round(t * 1e6, 1),
-                        "TBps": round(nb / t / 1e12, 2)})
+            for depth in (1, 2):
+                t = b2b(lambda: hip._skinny_lds(x, nxt(), o, hip.EPI_F32_PARTIAL, splits, N, depth))
+                out.append({"op": name, "kind": "lds", "M": M, "depth": depth, "S": splits,
+                            "us": round(t * 1e6, 1), "TBps": round(nb / t / 1e12, 2)})
         if name == "gate_up":
             o = torch.empty(M, N // 2, dtype=torch.bfloat16, device=dev)
-            t = b2b(lambda: hip._skinny_lds(x, nxt(), o, hip.EPI_SWIGLU, 1, N // 2))
-            out.append({"op": name, "kind": "lds_swiglu", "M": M, "us": round(t * 1e6, 1),
-                        "TBps": round(nb / t / 1e12, 2)})
+            for depth in (1, 2):
+                t = b2b(lambda: hip._skinny_lds(x, nxt(), o, hip.EPI_SWIGLU, 1, N // 2, depth))
+                out.append({"op": name, "kind": "lds_swiglu", "M": M, "depth": depth, "us": round(t * 1e6, 1),
+                            "TBps": round(nb / t / 1e12, 2)})
             t = b2b(lambda: hip._skinny(x, nxt(), o, hip.EPI_SWIGLU, 1, 1, N // 2))
             out.append({"op": name, "kind": "skinny_swiglu", "M": M, "us": round(t * 1e6, 1),
                         "TBps": round(nb / t / 1e12, 2)})
