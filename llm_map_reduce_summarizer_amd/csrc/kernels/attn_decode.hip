@@ -40,32 +40,70 @@ __device__ __forceinline__ void combine_group(const float* part_o, const float* 
                                               int b, int kvh, int Hq, int S, float* sw /* [G][S] LDS */,
                                               float* sden /* [G] */) {
     constexpr int D = 128;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const size_t bh0 = (size_t)b * Hq + (size_t)kvh * G;
-    for (int i = tid; i < G * S; i += 256) sw[i] = part_ml[(bh0 * S + i) * 2];  // g-major: (bh0+g)*S + s
-    __syncthreads();
-    if (tid < G) {
-        float M = -INFINITY;
-        for (int s = 0; s < S; ++s) M = fmaxf(M, sw[tid * S + s]);
-        float den = 0.f;
-        for (int s = 0; s < S; ++s) {
-            const float ms = sw[tid * S + s];
-            const float w = ms == -INFINITY ? 0.f : exp2f(ms - M);
-            sw[tid * S + s] = w;
-            den += w * part_ml[((bh0 + tid) * S + s) * 2 + 1];
+    // split weights: one wave per head, one lane per split (S <= MAX_SPLITS = 64), all loads issued
+    // at once -- a serial per-head loop over S dependent L2 loads cost ~5 us at S = 32
+    for (int g = wv; g < G; g += 4) {
+        float ms = -INFINITY, ls = 0.f;
+        if (lane < S) {
+            const float2 v = *reinterpret_cast<const float2*>(part_ml + ((bh0 + g) * S + lane) * 2);
+            ms = v.x;
+            ls = v.y;
         }
-        sden[tid] = den;
+        const float M = wave_max(ms);
+        const float w = ms == -INFINITY ? 0.f : exp2f(ms - M);
+        const float den = wave_sum(w * ls);
+        if (lane < S) sw[g * S + lane] = w;
+        if (lane == 0) sden[g] = den;
     }
     __syncthreads();
-    for (int i = tid; i < G * D; i += 256) {
-        const int g = i / D, d = i % D;
-        const float* po = part_o + (bh0 + g) * S * D + d;
-        const float* w = sw + g * S;
-        float acc = 0.f;
+    // weighted slab sum: float4 items (G * 32 of them) x NH interleaved split subsets, so every thread
+    // has <= S / NH independent 16-B loads in flight at once; subsets merged through LDS
+    constexpr int NV = G * D / 4;
+    constexpr int NH = NV >= 256 ? 1 : 256 / NV;
+    __shared__ float4 red[NH > 1 ? 256 : 1];
+#pragma unroll
+    for (int i0 = 0; i0 < (NV > 256 ? NV : 256); i0 += 256) {  // G = 16: two item rounds
+        const int t = i0 + tid;
+        const int item = t % NV, h = t / NV;
+        const int g = item / (D / 4), d4 = item % (D / 4);
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (h < NH) {
+            const float4* po = reinterpret_cast<const float4*>(part_o + (bh0 + g) * S * D) + d4;
+            const float* w = sw + g * S;
 #pragma unroll 8
-        for (int s = 0; s < S; ++s) acc += w[s] * po[(size_t)s * D];
-        const float den = sden[g];
-        out[(size_t)b * out_stride + (kvh * G + g) * D + d] = (bf16)(den > 0.f ? acc / den : 0.f);
+            for (int s = h; s < S; s += NH) {
+                const float4 v = po[(size_t)s * (D / 4)];
+                const float ws = w[s];
+                acc.x += ws * v.x;
+                acc.y += ws * v.y;
+                acc.z += ws * v.z;
+                acc.w += ws * v.w;
+            }
+        }
+        if constexpr (NH > 1) {
+            red[tid] = acc;
+            __syncthreads();
+            if (h == 0) {
+#pragma unroll
+                for (int j = 1; j < NH; ++j) {
+                    const float4 v = red[j * NV + item];
+                    acc.x += v.x;
+                    acc.y += v.y;
+                    acc.z += v.z;
+                    acc.w += v.w;
+                }
+            }
+        }
+        if (h == 0) {
+            const float den = sden[g];
+            const float inv = den > 0.f ? 1.f / den : 0.f;
+            uint2 o;
+            o.x = pack2(acc.x * inv, acc.y * inv);
+            o.y = pack2(acc.z * inv, acc.w * inv);
+            *reinterpret_cast<uint2*>(out + (size_t)b * out_stride + (kvh * G + g) * D + 4 * d4) = o;
+        }
     }
 }
 

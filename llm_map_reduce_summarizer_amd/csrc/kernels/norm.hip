@@ -19,6 +19,10 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16* __restrict__ x
     const uint4* xr = reinterpret_cast<const uint4*>(x + (size_t)row * x_stride);
     uint4* rr = ADD ? reinterpret_cast<uint4*>(residual + (size_t)row * D) : nullptr;
     float v[VPT][8];
+    const uint4* wr = reinterpret_cast<const uint4*>(w);
+    uint4 wv[VPT];  // norm weights fetched up front, off the reduction's critical path
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) wv[i] = wr[min((int)threadIdx.x + i * 256, nvec - 1)];
     float ss = 0.f;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
@@ -38,14 +42,13 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16* __restrict__ x
     }
     ss = block_sum(ss, red);
     const float inv = rsqrtf(ss / (float)D + eps);
-    const uint4* wr = reinterpret_cast<const uint4*>(w);
     uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * out_stride);
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
         const int c = threadIdx.x + i * 256;
         if (c < nvec) {
             float wf[8];
-            unpack8(wr[c], wf);
+            unpack8(wv[i], wf);
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[i][j] = v[i][j] * inv * wf[j];
             orow[c] = pack8(v[i]);
@@ -93,16 +96,32 @@ __global__ __launch_bounds__(256) void add_rmsnorm_parts_kernel(const float* __r
     uint4* rr = reinterpret_cast<uint4*>(residual + (size_t)row * D);
     float v[VPT][8];
     float ss = 0.f;
+    const uint4* wr = reinterpret_cast<const uint4*>(w);
+    uint4 wv[VPT];  // norm weights fetched up front, off the reduction's critical path
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) wv[i] = wr[min((int)threadIdx.x + i * 256, nvec - 1)];
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
         const int c = threadIdx.x + i * 256;
         if (c < nvec) {
             unpack8(rr[c], v[i]);
-            for (int s = 0; s < S; ++s) {
-                const float4* p = reinterpret_cast<const float4*>(parts + ((size_t)s * T + row) * D + c * 8);
-                const float4 a = p[0], b = p[1];
-                v[i][0] += a.x; v[i][1] += a.y; v[i][2] += a.z; v[i][3] += a.w;
-                v[i][4] += b.x; v[i][5] += b.y; v[i][6] += b.z; v[i][7] += b.w;
+            // slabs in batches of 4, all loads of a batch in flight together (see rope_kv.hip)
+            for (int s0 = 0; s0 < S; s0 += 4) {
+                float4 a[4], b[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float4* p = reinterpret_cast<const float4*>(
+                        parts + ((size_t)min(s0 + u, S - 1) * T + row) * D + c * 8);
+                    a[u] = p[0];
+                    b[u] = p[1];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (s0 + u < S) {
+                        v[i][0] += a[u].x; v[i][1] += a[u].y; v[i][2] += a[u].z; v[i][3] += a[u].w;
+                        v[i][4] += b[u].x; v[i][5] += b[u].y; v[i][6] += b[u].z; v[i][7] += b[u].w;
+                    }
+                }
             }
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[i][j] = (float)(bf16)v[i][j];
@@ -113,14 +132,13 @@ __global__ __launch_bounds__(256) void add_rmsnorm_parts_kernel(const float* __r
     }
     ss = block_sum(ss, red);
     const float inv = rsqrtf(ss / (float)D + eps);
-    const uint4* wr = reinterpret_cast<const uint4*>(w);
     uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * out_stride);
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
         const int c = threadIdx.x + i * 256;
         if (c < nvec) {
             float wf[8];
-            unpack8(wr[c], wf);
+            unpack8(wv[i], wf);
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[i][j] = v[i][j] * inv * wf[j];
             orow[c] = pack8(v[i]);

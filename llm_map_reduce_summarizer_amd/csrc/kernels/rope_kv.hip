@@ -31,11 +31,23 @@ struct RowSrc {
         } else {
 #pragma unroll
             for (int j = 0; j < 8; ++j) f[j] = 0.f;
-            for (int s = 0; s < S; ++s) {
-                const float4* p = reinterpret_cast<const float4*>(parts + s * slab_stride + col);
-                const float4 a = p[0], b = p[1];
-                f[0] += a.x; f[1] += a.y; f[2] += a.z; f[3] += a.w;
-                f[4] += b.x; f[5] += b.y; f[6] += b.z; f[7] += b.w;
+            // slabs in batches of 4 with every load of a batch issued before the first add: a plain
+            // runtime-S loop waits one L2 round trip per slab
+            for (int s0 = 0; s0 < S; s0 += 4) {
+                float4 a[4], b[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float4* p = reinterpret_cast<const float4*>(parts + min(s0 + u, S - 1) * slab_stride + col);
+                    a[u] = p[0];
+                    b[u] = p[1];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (s0 + u < S) {
+                        f[0] += a[u].x; f[1] += a[u].y; f[2] += a[u].z; f[3] += a[u].w;
+                        f[4] += b[u].x; f[5] += b[u].y; f[6] += b[u].z; f[7] += b[u].w;
+                    }
+                }
             }
         }
     }
@@ -53,7 +65,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
     constexpr int HALF = D / 2;
     constexpr int RI = HALF / 8;   // rotation items per head
     constexpr int VI = D / 8;      // copy items per v head
-    const int t = blockIdx.x;
+    const int t = blockIdx.x;  // blockIdx.y: 256-item slice of the token's work (one item per thread)
     const int pos = positions[t];
     const int width = (Hq + 2 * Hkv) * D;
     RowSrc<PARTS> src;
@@ -73,7 +85,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
     const float2* cs = cos_sin + (size_t)pos * HALF;
     const int n_rot = (Hq + Hkv) * RI;
     const int n_all = n_rot + Hkv * VI;
-    for (int it = threadIdx.x; it < n_all; it += blockDim.x) {
+    for (int it = blockIdx.y * blockDim.x + threadIdx.x; it < n_all; it += blockDim.x * gridDim.y) {
         if (it < n_rot) {
             const int h = it / RI, c = (it % RI) * 8;
             float a[8], b[8];
@@ -120,7 +132,8 @@ static int launch_rope(const void* qkv_in, const void* parts, int S, void* qkv_o
                        void* kcache, void* vcache, const void* cos_sin, int Hq, int Hkv, int D, int P,
                        int write_cache, hipStream_t s) {
     if (T <= 0) return 0;
-    dim3 g(T), b(256);
+    const int items = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);
+    dim3 g(T, ceil_div(items, 256)), b(256);
     auto QI = (const bf16*)qkv_in; auto PA = (const float*)parts; auto QO = (bf16*)qkv_out;
     auto K = (bf16*)kcache; auto V = (bf16*)vcache; auto CS = (const float2*)cos_sin;
     if (D == 128)
