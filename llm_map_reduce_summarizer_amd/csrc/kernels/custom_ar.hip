@@ -4,7 +4,8 @@
 // Every rank owns one uncached (hipDeviceMallocUncached) device allocation
 //     [ flags: MAX_BLOCKS x MAX_RANKS u32 | pad | slot 0 | slot 1 ]    slot = max_bytes
 // whose IPC handle is exchanged once; each rank maps all peers' allocations (xGMI on a node).
-// A call (fp32 sum, n elements) runs `nblk` workgroups; block b owns elements [b*chunk, (b+1)*chunk):
+// A call (fp32 sum or u64 max over n bytes <= 1 MiB) runs ceil(n / 16 KiB) workgroups; block b owns
+// bytes [16 KiB b, 16 KiB (b+1)):
 //   1. copy my slice of `in` into MY slot (epoch & 1)            -- local uncached stores
 //   2. system-scope release store of `epoch` into flags[b][me] of EVERY rank (remote over xGMI)
 //   3. spin (system-scope acquire, s_sleep, bounded) until my flags[b][r] >= epoch for all r
@@ -25,6 +26,7 @@ namespace {
 constexpr int MAX_RANKS = 8;
 constexpr int MAX_BLOCKS = 64;
 constexpr size_t HDR = 64 * 1024;  // flags region, slot 0 starts here
+constexpr size_t CH = 16 * 1024;   // bytes per block (fixed: see ar_oneshot_kernel)
 
 struct Peers {
     char* base[MAX_RANKS];  // every rank's allocation (mine included)
@@ -45,21 +47,30 @@ __device__ __forceinline__ void st_release_sys(unsigned* p, unsigned v) {
 }
 }  // namespace
 
-__global__ __launch_bounds__(256) void ar_oneshot_f32_kernel(Peers peers, int rank, int world, size_t slot_bytes,
-                                                            const float* __restrict__ in, float* __restrict__ out,
-                                                            size_t n, size_t chunk, unsigned* __restrict__ epochs,
-                                                            unsigned* __restrict__ error) {
+enum { OP_SUM_F32 = 0, OP_MAX_U64 = 1 };
+
+// Block b always owns bytes [b * CH, (b + 1) * CH) of a message, whatever the op and size, so the
+// slot-reuse argument above holds per block across calls of different kinds.
+template <int OP>
+__global__ __launch_bounds__(256) void ar_oneshot_kernel(Peers peers, int rank, int world, size_t slot_bytes,
+                                                         const char* __restrict__ in, char* __restrict__ out,
+                                                         size_t nbytes, unsigned* __restrict__ epochs,
+                                                         unsigned* __restrict__ error) {
+    constexpr int VB = OP == OP_SUM_F32 ? 16 : 8;  // vector bytes
     __shared__ unsigned s_epoch;
     const int b = blockIdx.x, tid = threadIdx.x;
     if (tid == 0) s_epoch = epochs[b] + 1;
     __syncthreads();
     const unsigned epoch = s_epoch;
     const size_t off = HDR + (size_t)(epoch & 1) * slot_bytes;
-    const size_t e0 = (size_t)b * chunk, e1 = e0 + chunk < n ? e0 + chunk : n;
+    const size_t b0 = (size_t)b * CH, b1 = b0 + CH < nbytes ? b0 + CH : nbytes;
 
-    // 1. my slice -> my slot (16-B vectors; n % 4 == 0 checked by the host)
-    float4* mine = reinterpret_cast<float4*>(peers.base[rank] + off);
-    for (size_t i = e0 / 4 + tid; i < e1 / 4; i += 256) mine[i] = reinterpret_cast<const float4*>(in)[i];
+    // 1. my slice -> my slot
+    char* mine = peers.base[rank] + off;
+    for (size_t i = b0 + (size_t)tid * VB; i < b1; i += 256 * VB) {
+        if constexpr (VB == 16) *reinterpret_cast<float4*>(mine + i) = *reinterpret_cast<const float4*>(in + i);
+        else *reinterpret_cast<unsigned long long*>(mine + i) = *reinterpret_cast<const unsigned long long*>(in + i);
+    }
     // every wave retires its own slot stores at system scope before the flag can be published
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -85,19 +96,43 @@ __global__ __launch_bounds__(256) void ar_oneshot_f32_kernel(Peers peers, int ra
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    // 4. sum every rank's copy of the slice
-    for (size_t i = e0 / 4 + tid; i < e1 / 4; i += 256) {
-        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int r = 0; r < world; ++r) {
-            const float4 v = reinterpret_cast<const float4*>(peers.base[r] + off)[i];
-            acc.x += v.x;
-            acc.y += v.y;
-            acc.z += v.z;
-            acc.w += v.w;
+    // 4. combine every rank's copy of the slice
+    for (size_t i = b0 + (size_t)tid * VB; i < b1; i += 256 * VB) {
+        if constexpr (OP == OP_SUM_F32) {
+            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int r = 0; r < world; ++r) {
+                const float4 v = *reinterpret_cast<const float4*>(peers.base[r] + off + i);
+                acc.x += v.x;
+                acc.y += v.y;
+                acc.z += v.z;
+                acc.w += v.w;
+            }
+            *reinterpret_cast<float4*>(out + i) = acc;
+        } else {
+            unsigned long long m = 0;
+            for (int r = 0; r < world; ++r) {
+                const unsigned long long v = *reinterpret_cast<const unsigned long long*>(peers.base[r] + off + i);
+                m = v > m ? v : m;
+            }
+            *reinterpret_cast<unsigned long long*>(out + i) = m;
         }
-        reinterpret_cast<float4*>(out)[i] = acc;
     }
     if (tid == 0) epochs[b] = epoch;
+}
+
+static int launch_ar(ArHandle* h, int op, const void* in, void* out, size_t nbytes, hipStream_t s) {
+    if (nbytes == 0) return 0;
+    if (nbytes > h->max_bytes || nbytes > (size_t)MAX_BLOCKS * CH) return (int)hipErrorInvalidValue;
+    for (int r = 0; r < h->world; ++r)
+        if (!h->peers.base[r]) return (int)hipErrorInvalidValue;
+    const int nblk = (int)((nbytes + CH - 1) / CH);
+    if (op == OP_SUM_F32)
+        ar_oneshot_kernel<OP_SUM_F32><<<nblk, 256, 0, s>>>(h->peers, h->rank, h->world, h->max_bytes,
+                                                           (const char*)in, (char*)out, nbytes, h->epochs, h->error);
+    else
+        ar_oneshot_kernel<OP_MAX_U64><<<nblk, 256, 0, s>>>(h->peers, h->rank, h->world, h->max_bytes,
+                                                           (const char*)in, (char*)out, nbytes, h->epochs, h->error);
+    return (int)hipGetLastError();
 }
 
 MRSUM_API void* mrsum_ar_create(int rank, int world, size_t max_bytes) {
@@ -155,22 +190,15 @@ MRSUM_API int mrsum_ar_open(void* hv, const void* handles) {
     return 0;
 }
 
+// in-place allowed; n fp32 elements, n % 4 == 0, 4 n <= min(max_bytes, 1 MiB)
 MRSUM_API int mrsum_ar_allreduce_f32(void* hv, const void* in, void* out, size_t n, hipStream_t s) {
-    auto h = (ArHandle*)hv;
-    if (n == 0) return 0;
-    if (n % 4 || n * sizeof(float) > h->max_bytes) return (int)hipErrorInvalidValue;
-    for (int r = 0; r < h->world; ++r)
-        if (!h->peers.base[r]) return (int)hipErrorInvalidValue;
-    // ~16 KiB per block keeps every block's remote reads short; at most MAX_BLOCKS blocks
-    size_t chunk = 4096;
-    int nblk = (int)((n + chunk - 1) / chunk);
-    if (nblk > MAX_BLOCKS) {
-        nblk = MAX_BLOCKS;
-        chunk = ((n + MAX_BLOCKS - 1) / MAX_BLOCKS + 3) & ~(size_t)3;
-    }
-    ar_oneshot_f32_kernel<<<nblk, 256, 0, s>>>(h->peers, h->rank, h->world, h->max_bytes, (const float*)in,
-                                               (float*)out, n, chunk, h->epochs, h->error);
-    return (int)hipGetLastError();
+    if (n % 4) return (int)hipErrorInvalidValue;
+    return launch_ar((ArHandle*)hv, OP_SUM_F32, in, out, n * sizeof(float), s);
+}
+
+// element-wise max of n u64 (sampler keys), in-place allowed
+MRSUM_API int mrsum_ar_allreduce_max_u64(void* hv, const void* in, void* out, size_t n, hipStream_t s) {
+    return launch_ar((ArHandle*)hv, OP_MAX_U64, in, out, n * sizeof(unsigned long long), s);
 }
 
 MRSUM_API int mrsum_ar_error(void* hv) {

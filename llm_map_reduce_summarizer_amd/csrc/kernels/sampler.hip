@@ -14,6 +14,10 @@
 //          next input id, advance the position, and retire the row on EOS or
 //          max_new.  A retired row keeps its position, so a captured decode
 //          graph can keep running it harmlessly until the host drops it.
+// Tensor parallel (vocab-parallel LM head): each rank scans its vocab shard with
+// tok_offset = rank * V_local -- the noise is a function of the GLOBAL token id, so the
+// per-rank winners max-reduced across ranks (8 bytes per row, parallel/custom_ar.py) give the
+// same token as one GPU scanning the whole row, without gathering the logits.
 #include "common.h"
 
 __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
@@ -28,7 +32,7 @@ __device__ __forceinline__ unsigned int order_key(float v) {
     return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
 }
 
-__global__ __launch_bounds__(256) void sample_kernel(const bf16* __restrict__ logits, int ld, int V,
+__global__ __launch_bounds__(256) void sample_kernel(const bf16* __restrict__ logits, int ld, int V, int tok_offset,
                                                      const float* __restrict__ temps,
                                                      const long long* __restrict__ seeds,
                                                      const int* __restrict__ positions,
@@ -53,7 +57,7 @@ __global__ __launch_bounds__(256) void sample_kernel(const bf16* __restrict__ lo
         }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-            const int tok = c + j;
+            const int tok = tok_offset + c + j;
             float v = f[j];
             if (tau > 0.f) {
                 const unsigned long long h = mix64(key0 ^ ((unsigned long long)tok * 0xD1B54A32D192ED03ULL));
@@ -62,7 +66,7 @@ __global__ __launch_bounds__(256) void sample_kernel(const bf16* __restrict__ lo
             }
             const unsigned long long k =
                 ((unsigned long long)order_key(v) << 32) | (unsigned long long)(0xFFFFFFFFu - (unsigned int)tok);
-            if (tok < c1 && k > best) best = k;
+            if (c + j < c1 && k > best) best = k;
         }
     }
 #pragma unroll
@@ -99,17 +103,40 @@ __global__ void sample_finish_kernel(unsigned long long* __restrict__ result, in
     else positions[b] += 1;
 }
 
+static int launch_keys(const void* logits, int ld, int B, int V, int tok_offset, const float* temps,
+                       const long long* seeds, const int* positions, void* result, hipStream_t s) {
+    const int nseg = 32;
+    int seg_len = ceil_div(V, nseg);
+    seg_len = (seg_len + 7) & ~7;
+    sample_kernel<<<dim3(nseg, B), 256, 0, s>>>((const bf16*)logits, ld, V, tok_offset, temps, seeds, positions,
+                                                (unsigned long long*)result, seg_len);
+    return (int)hipGetLastError();
+}
+
+// Gumbel-max keys of a (shard of the) vocabulary, max-folded into result[b] (which must be 0 or an
+// earlier partial key).  Tensor-parallel callers max-reduce result across ranks, then finish.
+MRSUM_API int mrsum_sample_keys(const void* logits, int ld, int B, int V, int tok_offset, const float* temps,
+                                const long long* seeds, const int* positions, void* result, hipStream_t s) {
+    if (B <= 0) return 0;
+    return launch_keys(logits, ld, B, V, tok_offset, temps, seeds, positions, result, s);
+}
+
+MRSUM_API int mrsum_sample_finish(void* result, int* next_ids, int* positions_rw, int* gen_count, const int* max_new,
+                                  int* out_tokens, int out_stride, int* done, const int* eos, int n_eos, int B,
+                                  hipStream_t s) {
+    if (B <= 0) return 0;
+    sample_finish_kernel<<<ceil_div(B, 64), 64, 0, s>>>((unsigned long long*)result, next_ids, positions_rw,
+                                                        gen_count, max_new, out_tokens, out_stride, done, eos,
+                                                        n_eos, B);
+    return (int)hipGetLastError();
+}
+
 MRSUM_API int mrsum_sample(const void* logits, int ld, int B, int V, const float* temps, const long long* seeds,
                            const int* positions, void* result, int* next_ids, int* positions_rw, int* gen_count,
                            const int* max_new, int* out_tokens, int out_stride, int* done, const int* eos, int n_eos,
                            hipStream_t s) {
     if (B <= 0) return 0;
-    const int nseg = 32;
-    int seg_len = ceil_div(V, nseg);
-    seg_len = (seg_len + 7) & ~7;
-    sample_kernel<<<dim3(nseg, B), 256, 0, s>>>((const bf16*)logits, ld, V, temps, seeds, positions,
-                                                (unsigned long long*)result, seg_len);
-    int e = (int)hipGetLastError();
+    int e = launch_keys(logits, ld, B, V, 0, temps, seeds, positions, result, s);
     if (e) return e;
     sample_finish_kernel<<<ceil_div(B, 64), 64, 0, s>>>((unsigned long long*)result, next_ids, positions_rw,
                                                         gen_count, max_new, out_tokens, out_stride, done, eos,

@@ -191,21 +191,29 @@ class LLMEngine:
         if dev.type == "cuda":
             from ..ops.hip import prefill_items
             items = prefill_items(lens).to(dev, non_blocking=True)
+        tp_s = self.model.tp_sampling
         logits = self.model.prefill(ids_t, pos_t, sidx_t, cu_t, last_t, st.block_tables, self.kv.k, self.kv.v,
-                                    seqlens=lens, items=items)
+                                    seqlens=lens, items=items, gather=not tp_s)
         first = seqs[0].slot
         # sampling of the first generated token: position of the fed token = prompt_len - 1
         v = st.view(first, len(seqs))
         v.positions.copy_(h([n - 1 for n in lens]))
-        ops.sample(logits, v)
+        self._sample(logits, v)
         self.stats["prefill_tokens"] += T
 
     # ------------------------------------------------------------------ decode
+    def _sample(self, logits: torch.Tensor, st_view) -> None:
+        if self.model.tp_sampling:  # local vocab shard + cross-rank max of the 8-byte Gumbel keys
+            ops.sample_tp(logits, st_view, self.model.vocab_offset, self.model.custom_ar.max_u64_)
+        else:
+            ops.sample(logits, st_view)
+
     def _decode_once(self, B: int) -> None:
         st = self.state
         logits = self.model.decode(st.next_ids[:B], st.positions[:B], st.seq_idx[:B], st.block_tables[:B],
-                                   self.kv.k, self.kv.v, workspace=self._workspace(B))
-        ops.sample(logits, st.view(0, B))
+                                   self.kv.k, self.kv.v, workspace=self._workspace(B),
+                                   gather=not self.model.tp_sampling)
+        self._sample(logits, st.view(0, B))
 
     def _decode_steps(self, B: int, steps: int) -> None:
         if not self.use_graphs:

@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import hashlib
 import math
+import os
 from dataclasses import dataclass
 from typing import Callable, List, Optional
 
@@ -88,6 +89,13 @@ class LlamaModel:
         else:
             self._init_weights(seed)
         self.cos_sin = rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, self.device)
+        self.vocab_offset = tp_rank * self.vocab_local
+        # TP on GPUs: decode all-reduces (fp32 split-K slabs, <= 1 MiB) and the sampler's key max go
+        # through the one-shot P2P kernel (parallel/custom_ar.py); larger messages through RCCL
+        self.custom_ar = None
+        if tp_size > 1 and self.device.type == "cuda" and os.environ.get("MRSUM_CUSTOM_AR", "1") == "1":
+            from ..parallel.custom_ar import maybe_custom_all_reduce
+            self.custom_ar = maybe_custom_all_reduce(tp_group)
 
     # ------------------------------------------------------------------ weights
     def _init_weights(self, seed: int) -> None:
@@ -133,8 +141,16 @@ class LlamaModel:
     # ------------------------------------------------------------------ comm
     def _all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.tp_size > 1:
-            torch.distributed.all_reduce(t, group=self.tp_group)
+            if self.custom_ar is not None and self.custom_ar.fits(t):
+                self.custom_ar.all_reduce(t)
+            else:
+                torch.distributed.all_reduce(t, group=self.tp_group)
         return t
+
+    @property
+    def tp_sampling(self) -> bool:
+        """Sample from the local vocab shard + 8-byte key max instead of gathering the logits."""
+        return self.tp_size > 1 and self.custom_ar is not None
 
     def _gather_vocab(self, logits: torch.Tensor) -> torch.Tensor:
         if self.tp_size == 1:
@@ -171,13 +187,16 @@ class LlamaModel:
             x = ops.proj_add_rmsnorm(act, lw.wdown, residual, nxt, c.rms_eps, "down", ar)
         return x
 
-    def logits(self, x: torch.Tensor) -> torch.Tensor:
-        return self._gather_vocab(F.linear(x, self.lm_head))  # hipBLASLt streams the 1 GB head at ~5.4 TB/s
+    def logits(self, x: torch.Tensor, gather: bool = True) -> torch.Tensor:
+        local = F.linear(x, self.lm_head)  # hipBLASLt streams the 1 GB head at ~5.4 TB/s
+        return self._gather_vocab(local) if gather else local
 
     def prefill(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, cu_seqlens: torch.Tensor,
                 last_rows: torch.Tensor, block_tables: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
-                seqlens: Optional[List[int]] = None, items: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Packed varlen prefill; returns logits of each sequence's last token [nseq, vocab]."""
+                seqlens: Optional[List[int]] = None, items: Optional[torch.Tensor] = None,
+                gather: bool = True) -> torch.Tensor:
+        """Packed varlen prefill; returns logits of each sequence's last token [nseq, vocab]
+        (this rank's vocab shard [nseq, vocab / tp] when ``gather`` is False)."""
         kw = {}
         if ids.is_cuda:
             kw = {"seqlens": seqlens, "items": items}
@@ -186,11 +205,12 @@ class LlamaModel:
             return ops.attn_prefill(qkv, cu_seqlens, self.hq, self.hkv, self.hd, self.scale, **kw)
 
         x = self.run_layers(ids, positions, seq_idx, block_tables, kcache, vcache, attention)
-        return self.logits(x.index_select(0, last_rows))
+        return self.logits(x.index_select(0, last_rows), gather)
 
     def decode(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, block_tables: torch.Tensor,
-               kcache: torch.Tensor, vcache: torch.Tensor, workspace=None) -> torch.Tensor:
-        """One token per sequence; context = positions + 1.  Returns logits [B, vocab]."""
+               kcache: torch.Tensor, vcache: torch.Tensor, workspace=None, gather: bool = True) -> torch.Tensor:
+        """One token per sequence; context = positions + 1.  Returns logits [B, vocab] (or the local
+        vocab shard when ``gather`` is False)."""
         page = kcache.shape[3]
 
         def attention(i, qkv):
@@ -198,4 +218,4 @@ class LlamaModel:
                                    page, self.scale, workspace=workspace)
 
         x = self.run_layers(ids, positions, seq_idx, block_tables, kcache, vcache, attention, decode=True)
-        return self.logits(x)
+        return self.logits(x, gather)

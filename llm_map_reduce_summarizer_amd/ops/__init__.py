@@ -112,6 +112,12 @@ def sample(logits, st):
     reference.sample_finish(toks, st)
 
 
+def sample_tp(logits, st, tok_offset, max_reduce):
+    """Vocab-parallel sampling over this rank's logits shard (GPU only; see hip.sample_tp)."""
+    from . import hip
+    return hip.sample_tp(logits, st, tok_offset, max_reduce)
+
+
 # ---------------------------------------------------------------- fused projection blocks
 # The model calls these; each picks (on the GPU) between our MFMA weight-streaming kernel
 # with a fused epilogue and hipBLASLt + a separate HIP kernel, per the measured plan table

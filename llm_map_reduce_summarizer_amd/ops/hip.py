@@ -40,6 +40,8 @@ _SIGS = {
     "mrsum_skinny_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_quant_fp8_rows": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
+    "mrsum_sample_keys": [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
+    "mrsum_sample_finish": [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "mrsum_sample": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp,
                      _c_int, _vp],
 }
@@ -310,6 +312,23 @@ def sample(logits: torch.Tensor, st) -> None:
                                _p(st.result), _p(st.next_ids), _p(st.positions), _p(st.gen_count), _p(st.max_new),
                                _p(st.out_tokens), st.out_tokens.stride(0), _p(st.done), _p(st.eos), st.n_eos,
                                _stream()), "sample")
+
+
+def sample_tp(logits: torch.Tensor, st, tok_offset: int, max_reduce) -> None:
+    """Vocab-parallel sampling: Gumbel-max keys over this rank's logits shard (global token ids =
+    tok_offset + column), ``max_reduce(keys)`` across the TP group (in place, unsigned), then the
+    usual decode bookkeeping.  Same token as ``sample`` over the gathered row."""
+    _bf16_cuda(logits)
+    _rows_ok(logits)
+    B, V = logits.shape
+    _req(st.temps.numel() >= B and st.next_ids.numel() >= B and st.out_tokens.shape[0] >= B,
+         "sample_tp: state smaller than batch")
+    _check(_fn("mrsum_sample_keys")(_p(logits), logits.stride(0), B, V, tok_offset, _p(st.temps), _p(st.seeds),
+                                    _p(st.positions), _p(st.result), _stream()), "sample_keys")
+    max_reduce(st.result[:B])
+    _check(_fn("mrsum_sample_finish")(_p(st.result), _p(st.next_ids), _p(st.positions), _p(st.gen_count),
+                                      _p(st.max_new), _p(st.out_tokens), st.out_tokens.stride(0), _p(st.done),
+                                      _p(st.eos), st.n_eos, B, _stream()), "sample_finish")
 
 
 # ------------------------------------------------------------------ decode GEMMs (M <= 64)

@@ -28,6 +28,8 @@ _SIGS = {
     "mrsum_ar_open": ([ctypes.c_void_p, ctypes.c_void_p], ctypes.c_int),
     "mrsum_ar_allreduce_f32": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p],
                                ctypes.c_int),
+    "mrsum_ar_allreduce_max_u64": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                    ctypes.c_void_p], ctypes.c_int),
     "mrsum_ar_error": ([ctypes.c_void_p], ctypes.c_int),
     "mrsum_ar_destroy": ([ctypes.c_void_p], None),
 }
@@ -48,7 +50,7 @@ class CustomAllReduce:
 
     MAX_RANKS = 8
 
-    def __init__(self, group=None, max_bytes: int = 4 << 20):
+    def __init__(self, group=None, max_bytes: int = 1 << 20):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -78,7 +80,7 @@ class CustomAllReduce:
 
     def fits(self, t: torch.Tensor) -> bool:
         return (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() % 4 == 0
-                and t.numel() * 4 <= self.max_bytes)
+                and t.numel() * 4 <= min(self.max_bytes, 1 << 20))
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         """Sum ``t`` over the group in place (RCCL for tensors the P2P path does not take)."""
@@ -89,6 +91,17 @@ class CustomAllReduce:
                                               torch.cuda.current_stream(t.device).cuda_stream)
         if rc:
             raise RuntimeError("custom all-reduce launch failed (%d)" % rc)
+        return t
+
+    def max_u64_(self, t: torch.Tensor) -> torch.Tensor:
+        """Element-wise max over the group, in place, of an int64 tensor holding unsigned 64-bit keys
+        (the sampler's Gumbel-max keys; values are compared as unsigned)."""
+        if not (t.is_cuda and t.dtype == torch.int64 and t.is_contiguous() and t.numel() * 8 <= self.max_bytes):
+            raise ValueError("max_u64_: contiguous int64 cuda tensor of <= max_bytes expected")
+        rc = self._lib.mrsum_ar_allreduce_max_u64(self._h, t.data_ptr(), t.data_ptr(), t.numel(),
+                                                  torch.cuda.current_stream(t.device).cuda_stream)
+        if rc:
+            raise RuntimeError("custom all-reduce (max) launch failed (%d)" % rc)
         return t
 
     def error(self) -> int:
@@ -107,7 +120,7 @@ class CustomAllReduce:
             pass
 
 
-def maybe_custom_all_reduce(group=None, max_bytes: int = 4 << 20) -> Optional[CustomAllReduce]:
+def maybe_custom_all_reduce(group=None, max_bytes: int = 1 << 20) -> Optional[CustomAllReduce]:
     """A CustomAllReduce for ``group`` when every rank is on a GPU, else None (RCCL/gloo path)."""
     if not (dist.is_initialized() and torch.cuda.is_available()):
         return None

@@ -42,6 +42,14 @@ def main():
         torch.cuda.synchronize()
         ref = sum(data(r, 16384, 100 + it) for r in range(world))
         assert torch.equal(x.cpu(), ref), "graph replay %d" % it
+    # u64 max (sampler keys): values above 2^63 must compare as unsigned
+    def i64(u):
+        return u - (1 << 64) if u >= 1 << 63 else u
+
+    keys = torch.tensor([i64((rank + 1) << 62), 5 + rank, -1 if rank == 1 else 7], dtype=torch.int64, device="cuda")
+    ar.max_u64_(keys)
+    torch.cuda.synchronize()
+    assert keys.tolist() == [i64(world << 62), 5 + world - 1, -1], keys.tolist()
     assert ar.error() == 0
     dist.barrier()
     ar.close()
