@@ -47,8 +47,10 @@ def main() -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--stop-at-eos", action="store_true",
                     help="honour EOS (default: pin every generation to --max-new-tokens so the timed work is fixed)")
-    ap.add_argument("--reduce-tp", action="store_true", default=os.environ.get("MRSUM_REDUCE_TP", "0") == "1",
-                    help="run the reduce stages tensor-parallel over all ranks (experimental)")
+    ap.add_argument("--parallel", choices=["auto", "dp", "reduce_tp"], default=os.environ.get("MRSUM_PARALLEL", "auto"),
+                    help="dp: every stage data-parallel over the ranks; reduce_tp: map data-parallel, reduce stages "
+                         "tensor-parallel over all ranks (custom P2P all-reduce); auto: reduce_tp when N > 1 and "
+                         "the P2P all-reduce passes its self-test, else dp")
     ap.add_argument("--profile", default=None, metavar="DIR", help="torch.profiler trace of the timed steps")
     ap.add_argument("--log-level", default="WARNING")
     args = ap.parse_args()
@@ -74,7 +76,7 @@ def main() -> int:
 
     cfg = LLMConfig(MAX_TOKENS=args.max_new_tokens, TEMPERATURE=0.3, REDUCE_TEMPERATURE=0.2)
     provider = LocalEngineProvider(args.model, cfg, use_graphs=not args.no_graphs, ignore_eos=not args.stop_at_eos,
-                                   reduce_tp=args.reduce_tp)
+                                   reduce_tp={"auto": None, "dp": False, "reduce_tp": True}[args.parallel])
     executor = LLMExecutor(config=cfg, provider_obj=provider)
     summarizer = TranscriptSummarizer(executor=executor, max_tokens_per_chunk=args.chunk_tokens)
     transcript = synthetic_transcript(args.hours, seed=0)

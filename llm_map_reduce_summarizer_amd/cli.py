@@ -73,8 +73,11 @@ def build_parser() -> argparse.ArgumentParser:
                    help="Hugging Face Llama safetensors checkpoint (file or dir) for the map model; "
                         "default: seeded random init.  With a non-preset --model the dir's config.json is used")
     e.add_argument("--aggregator-weights", default=None, help="safetensors checkpoint of the aggregator model")
-    e.add_argument("--reduce-tp", action="store_true",
-                   help="reduce stages tensor-parallel over all ranks (map stays data-parallel; experimental)")
+    e.add_argument("--reduce-tp", dest="reduce_tp", action="store_const", const=True, default=None,
+                   help="reduce stages tensor-parallel over all ranks (map stays data-parallel); default: on with "
+                        "several GPUs when the P2P all-reduce passes its self-test")
+    e.add_argument("--no-reduce-tp", dest="reduce_tp", action="store_const", const=False,
+                   help="keep every stage data-parallel")
     e.add_argument("--aggregator-model", default=None,
                    help="separate local model for the reduce stage (e.g. llama3-70b); default: the map model")
     e.add_argument("--aggregator-dtype", choices=["bf16", "fp8"], default=None,

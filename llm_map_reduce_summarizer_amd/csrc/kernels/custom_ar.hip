@@ -84,10 +84,12 @@ __global__ __launch_bounds__(256) void ar_oneshot_kernel(Peers peers, int rank, 
     //    implies runs once, and covers the whole block's later reads through the barrier)
     if (tid < world) {
         const unsigned* f = reinterpret_cast<const unsigned*>(peers.base[rank]) + b * MAX_RANKS + tid;
-        long spins = 0;
+        // sticky error: once a wait has timed out, later calls do not wait again (the host sees the
+        // error word at its next check and stops using this path)
+        long spins = __hip_atomic_load(error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? (1L << 22) : 0;
         while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
             __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1L << 24)) {  // ~ seconds: a peer is gone; flag it and fall through
+            if (++spins > (1L << 22)) {  // ~ a second: a peer is gone or late; flag it and fall through
                 atomicOr(error, 1u);
                 break;
             }

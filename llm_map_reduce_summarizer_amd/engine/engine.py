@@ -143,6 +143,11 @@ class LLMEngine:
         self.max_pages = -(-self.max_model_len // page_size)
         self.state = DecodeState(self.max_num_seqs, self.max_pages, max_new_cap, self.device, eos_ids)
         self.use_graphs = use_graphs and self.device.type == "cuda"
+        if self.use_graphs and self.model.tp_size > 1 and self.model.custom_ar is None:
+            # TP without the P2P all-reduce would put RCCL collectives inside the captured graphs;
+            # replay them eagerly instead (RCCL stays outside any capture)
+            log.warning("TP=%d without the custom all-reduce: decode hipGraphs disabled", self.model.tp_size)
+            self.use_graphs = False
         self._graphs: Dict[int, "torch.cuda.CUDAGraph"] = {}
         self._workspaces: Dict[int, object] = {}
         self.stats = {"prefill_tokens": 0, "prefill_s": 0.0, "decode_steps": 0, "decode_tokens": 0,
@@ -259,9 +264,13 @@ class LLMEngine:
         if ignore_eos:
             self.state.n_eos = 0
         try:
-            return self._generate(prompts, params)
+            out = self._generate(prompts, params)
         finally:
             self.state.n_eos = n_eos
+        if self.model.custom_ar is not None and self.model.custom_ar.error():
+            raise RuntimeError("custom all-reduce: a wait for a peer timed out during this generate; "
+                               "results are invalid (set MRSUM_CUSTOM_AR=0 to use RCCL)")
+        return out
 
     def _generate(self, prompts: Sequence[Sequence[int]], params: Sequence[SamplingParams]) -> List[GenOutput]:
         self.stats["generate_calls"] += 1

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import hashlib
 import logging
+import os
 import time
 from typing import Any, Dict, List, Optional, Sequence
 
@@ -59,7 +60,7 @@ class LocalEngineProvider(Provider):
                  tp: int = 1, seed: Optional[int] = None, max_model_len: int = 16384, engine=None,
                  engine_options: Optional[Dict[str, Any]] = None, dtype: Optional[str] = None,
                  kv_fraction: Optional[float] = None, use_graphs: bool = True, max_num_seqs: Optional[int] = None,
-                 tokenizer: Optional[str] = None, ignore_eos: bool = False, reduce_tp: bool = False,
+                 tokenizer: Optional[str] = None, ignore_eos: bool = False, reduce_tp: Optional[bool] = None,
                  weights: Optional[str] = None, **_ignored):
         super().__init__(model, config)
         self.tokenizer = get_tokenizer(tokenizer)
@@ -84,11 +85,27 @@ class LocalEngineProvider(Provider):
         self.timings: Dict[str, float] = {"generate_s": 0.0, "allgather_s": 0.0}
         self.par = pdist.setup_parallel(tp)
         # reduce_tp: the reduce stages (few, long, latency-bound sequences) run on a second engine
-        # sharded over ALL ranks (TP = world) instead of on one DP replica
+        # sharded over ALL ranks (TP = world) instead of on one DP replica.  None = auto: on when
+        # there are several GPUs and the model shards over them; auto mode drops back to DP for the
+        # reduce if the TP engine has no P2P all-reduce (its decode would run without hipGraphs).
+        self._reduce_tp_auto = reduce_tp is None
+        if reduce_tp is None:
+            import torch
+            reduce_tp = torch.cuda.is_available() and self._tp_world_ok()
         self.reduce_tp = bool(reduce_tp) and self.par.world > 1 and tp == 1
         self._reduce_engine = None
         if self.reduce_tp:
-            self._engine_options.setdefault("kv_fraction", 0.4)
+            self._engine_options.setdefault("kv_fraction", float(os.environ.get("MRSUM_DP_KV_FRACTION", "0.4")))
+
+    def _tp_world_ok(self) -> bool:
+        w = self.par.world
+        if w <= 1 or w > 8:
+            return False
+        try:
+            c = self.model_config()
+        except Exception:
+            return False
+        return c.n_kv_heads % w == 0 and c.n_heads % w == 0 and c.ffn % w == 0 and c.vocab_size % w == 0
 
     # ------------------------------------------------------------------ engine
     def model_config(self):
@@ -130,12 +147,17 @@ class LocalEngineProvider(Provider):
             _ = self.engine  # DP engine first: it sizes its KV cache against the free HBM
             world = self.par.world
             opts = dict(self._engine_options)
-            opts.update(max_model_len=self.max_model_len, max_num_seqs=64, kv_fraction=0.5,
+            opts.update(max_model_len=self.max_model_len, max_num_seqs=64,
+                        kv_fraction=float(os.environ.get("MRSUM_REDUCE_KV_FRACTION", "0.5")),
                         eos_ids=self.tokenizer.eos_ids)
             self._reduce_engine = LLMEngine(self.model_config(), device=self._device, seed=self.seed,
                                             tp_rank=self.par.rank, tp_size=world,
                                             tp_group=pdist.tp_group_for(world), **opts)
             log.info("reduce engine up: %s TP=%d", self.model, world)
+            if self._reduce_tp_auto and self._reduce_engine.model.custom_ar is None and torch.cuda.is_available():
+                # every rank built the same engine and got the same collective verdict
+                log.warning("no P2P all-reduce for the TP reduce engine: reduce stages stay data-parallel")
+                self.reduce_tp = False
         return self._reduce_engine
 
     def encode_request(self, req: GenRequest) -> List[int]:
@@ -155,7 +177,8 @@ class LocalEngineProvider(Provider):
         from .engine import SamplingParams
         t0 = time.perf_counter()
         prompts = [self.encode_request(r) for r in reqs]
-        if self.reduce_tp and reqs and all(r.stage != "map" for r in reqs):
+        if self.reduce_tp and reqs and all(r.stage != "map" for r in reqs) and self.reduce_engine is not None \
+                and self.reduce_tp:
             # every rank runs every request on the TP engine; the TP ranks sample identically
             outs = self.reduce_engine.generate(
                 prompts, [SamplingParams(r.max_tokens, r.temperature, _req_seed(self.seed, r)) for r in reqs],

@@ -104,6 +104,48 @@ class CustomAllReduce:
             raise RuntimeError("custom all-reduce (max) launch failed (%d)" % rc)
         return t
 
+    def self_test(self, iters: int = 4, n: int = 65536) -> bool:
+        """Collective check against torch.distributed on every rank: eager and hipGraph-replayed
+        calls with values that change per call (a stale slot or flag shows up as a mismatch).  All
+        ranks return the same verdict."""
+        ok = True
+        dev = torch.device("cuda", torch.cuda.current_device())
+        try:
+            x = torch.empty(n, device=dev)
+            ref = torch.empty(n, device=dev)
+            base = torch.arange(n, device=dev, dtype=torch.float32).remainder_(251)
+
+            def fill(i):
+                x.copy_(base).mul_(self.rank + 1).add_(i)
+                ref.copy_(x)
+
+            for i in range(iters):
+                fill(i)
+                self.all_reduce(x)
+                dist.all_reduce(ref, group=self.group)
+                ok &= bool(torch.equal(x, ref))
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                self.all_reduce(x)
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                self.all_reduce(x)
+            for i in range(iters):
+                fill(10 + i)
+                g.replay()
+                dist.all_reduce(ref, group=self.group)
+                torch.cuda.synchronize(dev)
+                ok &= bool(torch.equal(x, ref))
+            ok &= self.error() == 0
+        except Exception as e:  # keep the collective sequence aligned across ranks
+            log.warning("custom all-reduce self-test raised: %s", e)
+            ok = False
+        votes = [None] * self.world
+        dist.all_gather_object(votes, ok, group=self.group)
+        return all(votes)
+
     def error(self) -> int:
         """Non-zero if a wait for a peer timed out (the result of that call is garbage)."""
         return int(self._lib.mrsum_ar_error(self._h))
@@ -125,7 +167,12 @@ def maybe_custom_all_reduce(group=None, max_bytes: int = 1 << 20) -> Optional[Cu
     if not (dist.is_initialized() and torch.cuda.is_available()):
         return None
     try:
-        return CustomAllReduce(group, max_bytes)
+        ar = CustomAllReduce(group, max_bytes)
     except Exception as e:  # no IPC (e.g. container without dmabuf): fall back to RCCL
         log.warning("custom all-reduce unavailable, using RCCL: %s", e)
         return None
+    if not ar.self_test():
+        log.warning("custom all-reduce failed its self-test on some rank; using RCCL")
+        ar.close()
+        return None
+    return ar
