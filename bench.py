@@ -35,6 +35,15 @@ sys.path.insert(0, ROOT)
 BASELINE_VALUE = None  # the reference publishes no number
 
 
+def _parallelism(provider, world: int) -> str:
+    """e.g. "dp1", or per stage "map:tp8,reduce_l1:tp8,reduce_final:tp8" (tpK = one engine sharded over K
+    GPUs, dpK = K data-parallel replicas)."""
+    plan = getattr(provider, "stage_plan", {}) or {}
+    if world == 1 or not plan:
+        return "dp%d" % world
+    return ",".join("%s:%s" % (s, "tp%d" % world if int(c["tp"]) > 1 else "dp%d" % world) for s, c in plan.items())
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -47,10 +56,12 @@ def main() -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--stop-at-eos", action="store_true",
                     help="honour EOS (default: pin every generation to --max-new-tokens so the timed work is fixed)")
-    ap.add_argument("--parallel", choices=["auto", "dp", "reduce_tp"], default=os.environ.get("MRSUM_PARALLEL", "auto"),
+    ap.add_argument("--parallel", choices=["auto", "dp", "reduce_tp", "tp"],
+                    default=os.environ.get("MRSUM_PARALLEL", "auto"),
                     help="dp: every stage data-parallel over the ranks; reduce_tp: map data-parallel, reduce stages "
-                         "tensor-parallel over all ranks (custom P2P all-reduce); auto: reduce_tp when N > 1 and "
-                         "the P2P all-reduce passes its self-test, else dp")
+                         "tensor-parallel over all ranks; tp: every stage on one engine sharded over all ranks; "
+                         "auto: per stage, the cheaper of dp / tp under parallel/plan.py's cost model fed with the "
+                         "all-reduce latency and bandwidth measured on these GPUs at start-up")
     ap.add_argument("--profile", default=None, metavar="DIR", help="torch.profiler trace of the timed steps")
     ap.add_argument("--log-level", default="WARNING")
     args = ap.parse_args()
@@ -76,13 +87,11 @@ def main() -> int:
 
     cfg = LLMConfig(MAX_TOKENS=args.max_new_tokens, TEMPERATURE=0.3, REDUCE_TEMPERATURE=0.2)
     provider = LocalEngineProvider(args.model, cfg, use_graphs=not args.no_graphs, ignore_eos=not args.stop_at_eos,
-                                   reduce_tp={"auto": None, "dp": False, "reduce_tp": True}[args.parallel])
+                                   parallel=args.parallel)
     executor = LLMExecutor(config=cfg, provider_obj=provider)
     summarizer = TranscriptSummarizer(executor=executor, max_tokens_per_chunk=args.chunk_tokens)
     transcript = synthetic_transcript(args.hours, seed=0)
-    _ = provider.engine  # weight init + KV allocation outside the timed region
-    if provider.reduce_tp:
-        _ = provider.reduce_engine
+    provider.warm()  # weight init, KV allocation, planner measurements: outside the timed region
 
     def one():
         return asyncio.run(summarizer.summarize(transcript))
@@ -127,7 +136,7 @@ def main() -> int:
         "data": ("synthetic %gh transcript (utils/synth.py, seed 0); random-init weights; every generation "
                  "pinned to max_new_tokens%s" % (args.hours, " (EOS honoured)" if args.stop_at_eos else "")),
         "config": {"model": args.model, "global_batch": n_chunks, "seq_len": args.chunk_tokens,
-                   "parallelism": "dp%d" % world + ("+reduce_tp%d" % world if provider.reduce_tp else ""),
+                   "parallelism": _parallelism(provider, world),
                    "max_new_tokens": args.max_new_tokens,
                    "transcript_hours": args.hours},
         "e2e_wall_s": round(ms / 1000.0, 3),

@@ -78,6 +78,10 @@ def build_parser() -> argparse.ArgumentParser:
                         "several GPUs when the P2P all-reduce passes its self-test")
     e.add_argument("--no-reduce-tp", dest="reduce_tp", action="store_const", const=False,
                    help="keep every stage data-parallel")
+    e.add_argument("--parallel", choices=["auto", "dp", "reduce_tp", "tp"], default=None,
+                   help="multi-GPU policy per stage: dp replicas, one TP=world engine (tp), map dp + reduce tp "
+                        "(reduce_tp), or auto: the cheaper per stage under parallel/plan.py's cost model with the "
+                        "all-reduce latency/bandwidth measured at start-up (default; overrides --reduce-tp)")
     e.add_argument("--aggregator-model", default=None,
                    help="separate local model for the reduce stage (e.g. llama3-70b); default: the map model")
     e.add_argument("--aggregator-dtype", choices=["bf16", "fp8"], default=None,
@@ -123,6 +127,7 @@ async def async_main(args: argparse.Namespace) -> int:
         popts.update({"dtype": args.dtype, "tp": args.tp, "seed": args.seed, "kv_fraction": args.kv_fraction,
                       "use_graphs": not args.no_graphs, "tokenizer": args.tokenizer,
                       "max_num_seqs": args.max_concurrent_requests, "reduce_tp": args.reduce_tp,
+                      "parallel": args.parallel,
                       "weights": args.weights})
     agg_executor = None
     if args.aggregator_model:

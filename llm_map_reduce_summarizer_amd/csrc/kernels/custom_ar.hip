@@ -27,6 +27,11 @@ constexpr int MAX_RANKS = 8;
 constexpr int MAX_BLOCKS = 64;
 constexpr size_t HDR = 64 * 1024;  // flags region, slot 0 starts here
 constexpr size_t CH = 16 * 1024;   // bytes per block (fixed: see ar_oneshot_kernel)
+// push-mode (ar_add_rmsnorm_kernel) flags: [MAX_ROWS][MAX_RANKS] u32 at PUSH_FLAGS inside HDR
+constexpr int MAX_ROWS = 256;
+constexpr size_t PUSH_FLAGS = 16 * 1024;
+static_assert(PUSH_FLAGS >= (size_t)MAX_BLOCKS * MAX_RANKS * 4, "flag regions overlap");
+static_assert(PUSH_FLAGS + (size_t)MAX_ROWS * MAX_RANKS * 4 <= HDR, "push flags exceed header");
 
 struct Peers {
     char* base[MAX_RANKS];  // every rank's allocation (mine included)
@@ -40,6 +45,7 @@ struct ArHandle {
     Peers peers;
     unsigned* epochs;    // [MAX_BLOCKS] local device counters (regular memory)
     unsigned* error;     // [1] set on a timed-out wait
+    unsigned* push_epochs;  // [MAX_ROWS] per-row counters of the push-mode kernel
 };
 
 __device__ __forceinline__ void st_release_sys(unsigned* p, unsigned v) {
@@ -122,6 +128,122 @@ __global__ __launch_bounds__(256) void ar_oneshot_kernel(Peers peers, int rank, 
     if (tid == 0) epochs[b] = epoch;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Push-mode fused all-reduce + residual add + RMSNorm (the row-parallel o / down projections of a
+// TP decode step).  One block per row r of the [T, D] output:
+//   1. v = sum_s parts[s][r]                   -- this rank's split-K slabs, fp32, in registers
+//   2. store v into push[(epoch & 1)][me][r] of EVERY rank   -- remote stores over xGMI (posted:
+//      no round trip, unlike reading the peers' copies)
+//   3. release fence (system scope), then flag[r][me] = epoch on every rank
+//   4. wait until my flag[r][p] >= epoch for all p, acquire
+//   5. a = sum_p push[(epoch & 1)][p][r] in rank order from LOCAL memory (every rank adds the same
+//      values in the same order: the TP replicas stay bit-identical)
+//   6. residual[r] = bf16(residual[r] + a); out[r] = rmsnorm(residual[r]) * w
+// Replaces the one-shot all-reduce + add_rmsnorm_parts pair (one launch less per projection, the
+// split-K sum folded in, so the producing GEMM keeps its split count under TP).  Slot reuse is safe
+// for the same reason as above, per row: a peer can only push call e+2 into my slot e & 1 after
+// passing call e+1's wait for row r, which needs my flag of call e+1, i.e. my call e is complete.
+constexpr size_t push_off(size_t slot_bytes) { return HDR + 2 * slot_bytes; }
+
+template <int VPT>  // float4 vectors per thread: D <= 1024 * VPT
+__global__ __launch_bounds__(256) void ar_add_rmsnorm_kernel(Peers peers, int rank, int world, size_t slot_bytes,
+                                                             const float* __restrict__ parts, int S, int T,
+                                                             bf16* __restrict__ residual, const bf16* __restrict__ w,
+                                                             bf16* __restrict__ out, int D, int out_stride, float eps,
+                                                             unsigned* __restrict__ epochs,
+                                                             unsigned* __restrict__ error) {
+    __shared__ float red[16];
+    __shared__ unsigned s_epoch;
+    const int row = blockIdx.x, tid = threadIdx.x;
+    const int nv = D >> 2;
+    if (tid == 0) s_epoch = epochs[row] + 1;
+    float4 v[VPT];
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int c = tid + i * 256;
+        v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c < nv) {
+            for (int s = 0; s < S; ++s) {
+                const float4 a = reinterpret_cast<const float4*>(parts + ((size_t)s * T + row) * D)[c];
+                v[i].x += a.x; v[i].y += a.y; v[i].z += a.z; v[i].w += a.w;
+            }
+        }
+    }
+    __syncthreads();
+    const unsigned epoch = s_epoch;
+    const size_t region = push_off(slot_bytes) + (size_t)(epoch & 1) * world * slot_bytes;
+    const size_t mine_off = region + (size_t)rank * slot_bytes + (size_t)row * D * 4;
+    for (int p = 0; p < world; ++p) {
+        float4* dst = reinterpret_cast<float4*>(peers.base[p] + mine_off);
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            const int c = tid + i * 256;
+            if (c < nv) dst[c] = v[i];
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid < world) {
+        unsigned* f = reinterpret_cast<unsigned*>(peers.base[tid] + PUSH_FLAGS) + row * MAX_RANKS + rank;
+        st_release_sys(f, epoch);
+    }
+    if (tid < world) {
+        const unsigned* f = reinterpret_cast<const unsigned*>(peers.base[rank] + PUSH_FLAGS) + row * MAX_RANKS + tid;
+        long spins = __hip_atomic_load(error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? (1L << 22) : 0;
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1L << 22)) {
+                atomicOr(error, 1u);
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // 5 + 6: rank-ordered sum from local memory, residual add (bf16 rounding), RMSNorm
+    const char* base = peers.base[rank] + region + (size_t)row * D * 4;
+    bf16* rrow = residual + (size_t)row * D;
+    float ss = 0.f;
+    float x[VPT][4];
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int c = tid + i * 256;
+        if (c < nv) {
+            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int p = 0; p < world; ++p) {
+                const float4 a = reinterpret_cast<const float4*>(base + (size_t)p * slot_bytes)[c];
+                acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+            }
+            const uint2 rv = reinterpret_cast<const uint2*>(rrow)[c];
+            x[i][0] = (float)(bf16)(__uint_as_float(rv.x << 16) + acc.x);
+            x[i][1] = (float)(bf16)(__uint_as_float(rv.x & 0xffff0000u) + acc.y);
+            x[i][2] = (float)(bf16)(__uint_as_float(rv.y << 16) + acc.z);
+            x[i][3] = (float)(bf16)(__uint_as_float(rv.y & 0xffff0000u) + acc.w);
+            reinterpret_cast<uint2*>(rrow)[c] = make_uint2(pack2(x[i][0], x[i][1]), pack2(x[i][2], x[i][3]));
+#pragma unroll
+            for (int j = 0; j < 4; ++j) ss += x[i][j] * x[i][j];
+        }
+    }
+    ss = block_sum(ss, red);
+    const float inv = rsqrtf(ss / (float)D + eps);
+    bf16* orow = out + (size_t)row * out_stride;
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int c = tid + i * 256;
+        if (c < nv) {
+            const uint2 wv = reinterpret_cast<const uint2*>(w)[c];
+            const float w0 = __uint_as_float(wv.x << 16), w1 = __uint_as_float(wv.x & 0xffff0000u);
+            const float w2 = __uint_as_float(wv.y << 16), w3 = __uint_as_float(wv.y & 0xffff0000u);
+            reinterpret_cast<uint2*>(orow)[c] = make_uint2(pack2(x[i][0] * inv * w0, x[i][1] * inv * w1),
+                                                           pack2(x[i][2] * inv * w2, x[i][3] * inv * w3));
+        }
+    }
+    if (tid == 0) epochs[row] = epoch;
+}
+
 static int launch_ar(ArHandle* h, int op, const void* in, void* out, size_t nbytes, hipStream_t s) {
     if (nbytes == 0) return 0;
     if (nbytes > h->max_bytes || nbytes > (size_t)MAX_BLOCKS * CH) return (int)hipErrorInvalidValue;
@@ -145,18 +267,21 @@ MRSUM_API void* mrsum_ar_create(int rank, int world, size_t max_bytes) {
     h->world = world;
     h->max_bytes = max_bytes;
     void* p = nullptr;
-    if (hipExtMallocWithFlags(&p, HDR + 2 * max_bytes, hipDeviceMallocUncached) != hipSuccess) {
+    if (hipExtMallocWithFlags(&p, push_off(max_bytes) + 2 * (size_t)world * max_bytes, hipDeviceMallocUncached) !=
+        hipSuccess) {
         delete h;
         return nullptr;
     }
     h->mine = (char*)p;
-    if (hipMemset(p, 0, HDR) != hipSuccess || hipMalloc((void**)&h->epochs, MAX_BLOCKS * sizeof(unsigned) + 64)) {
+    constexpr size_t n_ctr = MAX_BLOCKS + 16 + MAX_ROWS;  // epochs | error (+pad) | push epochs
+    if (hipMemset(p, 0, HDR) != hipSuccess || hipMalloc((void**)&h->epochs, n_ctr * sizeof(unsigned))) {
         (void)hipFree(p);
         delete h;
         return nullptr;
     }
-    (void)hipMemset(h->epochs, 0, MAX_BLOCKS * sizeof(unsigned) + 64);
+    (void)hipMemset(h->epochs, 0, n_ctr * sizeof(unsigned));
     h->error = h->epochs + MAX_BLOCKS;
+    h->push_epochs = h->epochs + MAX_BLOCKS + 16;
     for (int r = 0; r < MAX_RANKS; ++r) {
         h->peers.base[r] = nullptr;
         h->opened[r] = nullptr;
@@ -201,6 +326,28 @@ MRSUM_API int mrsum_ar_allreduce_f32(void* hv, const void* in, void* out, size_t
 // element-wise max of n u64 (sampler keys), in-place allowed
 MRSUM_API int mrsum_ar_allreduce_max_u64(void* hv, const void* in, void* out, size_t n, hipStream_t s) {
     return launch_ar((ArHandle*)hv, OP_MAX_U64, in, out, n * sizeof(unsigned long long), s);
+}
+
+
+// residual[T, D] += all-reduce(sum_s parts[s]) ; out = rmsnorm(residual) * w   (push-mode, see above)
+// parts fp32 [S, T, D]; residual, w, out bf16; T <= 256, T * D * 4 <= max_bytes, D % 4 == 0, D <= 8192
+MRSUM_API int mrsum_ar_add_rmsnorm(void* hv, const void* parts, int S, int T, void* residual, const void* w,
+                                   void* out, int D, int out_stride, float eps, hipStream_t s) {
+    auto h = (ArHandle*)hv;
+    if (T <= 0) return 0;
+    if (S < 1 || T > MAX_ROWS || D % 4 || D > 8192 || (size_t)T * D * 4 > h->max_bytes) return (int)hipErrorInvalidValue;
+    for (int r = 0; r < h->world; ++r)
+        if (!h->peers.base[r]) return (int)hipErrorInvalidValue;
+    const int vpt = (D / 4 + 255) / 256;
+    auto P = (const float*)parts; auto R = (bf16*)residual; auto W = (const bf16*)w; auto O = (bf16*)out;
+#define AR_NORM(V) ar_add_rmsnorm_kernel<V><<<T, 256, 0, s>>>(h->peers, h->rank, h->world, h->max_bytes, P, S, T, R, \
+                                                            W, O, D, out_stride, eps, h->push_epochs, h->error)
+    if (vpt <= 1) AR_NORM(1);
+    else if (vpt <= 2) AR_NORM(2);
+    else if (vpt <= 4) AR_NORM(4);
+    else AR_NORM(8);
+#undef AR_NORM
+    return (int)hipGetLastError();
 }
 
 MRSUM_API int mrsum_ar_error(void* hv) {

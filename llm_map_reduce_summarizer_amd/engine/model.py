@@ -50,6 +50,27 @@ def _randn(shape, std: float, seed: int, name: str, device, dtype) -> torch.Tens
     return t.to(dtype)
 
 
+class _TPReduce:
+    """The all-reduce handed to ops.proj_add_rmsnorm: RCCL / one-shot P2P sum (``__call__``) plus, on
+    GPUs with the P2P buffers, the fused all-reduce + residual add + RMSNorm kernel for decode rows."""
+
+    def __init__(self, model: "LlamaModel"):
+        self.model = model
+        ar = model.custom_ar
+        self.fused = ar is not None and os.environ.get("MRSUM_FUSED_AR", "1") == "1"
+
+    def __call__(self, t: torch.Tensor) -> torch.Tensor:
+        return self.model._all_reduce(t)
+
+    def fused_ok(self, rows: int, hidden: int) -> bool:
+        ar = self.model.custom_ar
+        return self.fused and rows <= ar.MAX_ROWS and hidden % 4 == 0 and hidden <= 8192 and \
+            rows * hidden * 4 <= ar.max_bytes
+
+    def add_rmsnorm(self, parts, residual, ln, eps):
+        return self.model.custom_ar.add_rmsnorm(parts, residual, ln, eps)
+
+
 @dataclass
 class LayerWeights:
     ln1: torch.Tensor
@@ -176,7 +197,7 @@ class LlamaModel:
         x = ops.rmsnorm(residual, self.layers[0].ln1, c.rms_eps)
         page = kcache.shape[3]
         n = len(self.layers)
-        ar = self._all_reduce if self.tp_size > 1 else None
+        ar = _TPReduce(self) if self.tp_size > 1 else None
         for i, lw in enumerate(self.layers):
             nxt = self.layers[i + 1].ln1 if i + 1 < n else self.final_norm
             qkv = ops.qkv_rope(x, lw.wqkv, positions, seq_idx, block_tables, kcache[i], vcache[i], self.cos_sin,

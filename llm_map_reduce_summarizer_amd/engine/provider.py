@@ -16,6 +16,14 @@ stage, data-parallel over the ranks of the job:
 
 Sampling seeds are derived from the request content, so a summary does not
 depend on which rank produced it or how the batch was formed.
+
+With several GPUs a stage may instead run on ONE engine sharded over all of
+them (TP = world): decode is bound by streaming weights + KV from HBM, which
+DP replicas do not shorten and TP divides.  ``parallel`` selects the policy:
+``dp`` (every stage data-parallel), ``reduce_tp`` (map DP, reduce stages TP),
+``tp`` (every stage TP) or ``auto`` (per stage, the cheaper of the two under
+the cost model of ``parallel/plan.py``, fed with the all-reduce latency and
+bandwidth measured on this job's GPUs at start-up).
 """
 
 from __future__ import annotations
@@ -61,7 +69,7 @@ class LocalEngineProvider(Provider):
                  engine_options: Optional[Dict[str, Any]] = None, dtype: Optional[str] = None,
                  kv_fraction: Optional[float] = None, use_graphs: bool = True, max_num_seqs: Optional[int] = None,
                  tokenizer: Optional[str] = None, ignore_eos: bool = False, reduce_tp: Optional[bool] = None,
-                 weights: Optional[str] = None, **_ignored):
+                 weights: Optional[str] = None, parallel: Optional[str] = None, **_ignored):
         super().__init__(model, config)
         self.tokenizer = get_tokenizer(tokenizer)
         if dtype not in (None, "bf16", "fp8"):
@@ -84,18 +92,23 @@ class LocalEngineProvider(Provider):
             self._engine_options.setdefault("max_num_seqs", max_num_seqs)
         self.timings: Dict[str, float] = {"generate_s": 0.0, "allgather_s": 0.0}
         self.par = pdist.setup_parallel(tp)
-        # reduce_tp: the reduce stages (few, long, latency-bound sequences) run on a second engine
-        # sharded over ALL ranks (TP = world) instead of on one DP replica.  None = auto: on when
-        # there are several GPUs and the model shards over them; auto mode drops back to DP for the
-        # reduce if the TP engine has no P2P all-reduce (its decode would run without hipGraphs).
-        self._reduce_tp_auto = reduce_tp is None
-        if reduce_tp is None:
-            import torch
-            reduce_tp = torch.cuda.is_available() and self._tp_world_ok()
-        self.reduce_tp = bool(reduce_tp) and self.par.world > 1 and tp == 1
+        # parallel policy (module docstring); the legacy reduce_tp flag maps onto it
+        if parallel is None:
+            parallel = os.environ.get("MRSUM_PARALLEL") or {None: "auto", True: "reduce_tp", False: "dp"}[reduce_tp]
+        if parallel not in ("auto", "dp", "reduce_tp", "tp"):
+            raise ValueError("parallel must be auto, dp, reduce_tp or tp (got %r)" % parallel)
+        import torch
+        multi = self.par.world > 1 and tp == 1 and self._tp_world_ok()
+        if parallel == "auto" and not torch.cuda.is_available():
+            parallel = "dp"  # the planner's constants are GPU measurements
+        self.parallel = parallel if multi else "dp"
+        self.reduce_tp = self.parallel != "dp"  # a TP=world engine exists for some stage
         self._reduce_engine = None
+        self._dp_needed = self.parallel != "tp"
+        self.hw = None  # plan.HWModel with this job's measured all-reduce constants (auto mode)
+        self.stage_plan: Dict[str, Any] = {}
         if self.reduce_tp:
-            self._engine_options.setdefault("kv_fraction", float(os.environ.get("MRSUM_DP_KV_FRACTION", "0.4")))
+            self._engine_options.setdefault("kv_fraction", float(os.environ.get("MRSUM_DP_KV_FRACTION", "0.5")))
 
     def _tp_world_ok(self) -> bool:
         w = self.par.world
@@ -139,26 +152,77 @@ class LocalEngineProvider(Provider):
 
     @property
     def reduce_engine(self):
-        """TP=world engine of the same model/seed for the reduce stages (reduce_tp mode)."""
+        """TP=world engine of the same model/seed (the ``tp`` engine of the module docstring)."""
         if self._reduce_engine is None:
             import torch
-            from .config import get_model_config
             from .engine import LLMEngine
-            _ = self.engine  # DP engine first: it sizes its KV cache against the free HBM
             world = self.par.world
             opts = dict(self._engine_options)
+            frac = "0.6" if self.parallel == "tp" else "0.35"  # leave HBM for the DP engine
             opts.update(max_model_len=self.max_model_len, max_num_seqs=64,
-                        kv_fraction=float(os.environ.get("MRSUM_REDUCE_KV_FRACTION", "0.5")),
+                        kv_fraction=float(os.environ.get("MRSUM_REDUCE_KV_FRACTION", frac)),
                         eos_ids=self.tokenizer.eos_ids)
+            if self._device is None:
+                self._device = ("cuda:%d" % (self.par.local_rank % max(1, torch.cuda.device_count()))
+                                if torch.cuda.is_available() else "cpu")
             self._reduce_engine = LLMEngine(self.model_config(), device=self._device, seed=self.seed,
                                             tp_rank=self.par.rank, tp_size=world,
                                             tp_group=pdist.tp_group_for(world), **opts)
-            log.info("reduce engine up: %s TP=%d", self.model, world)
-            if self._reduce_tp_auto and self._reduce_engine.model.custom_ar is None and torch.cuda.is_available():
+            log.info("TP engine up: %s TP=%d", self.model, world)
+            if self._reduce_engine.model.custom_ar is None and torch.cuda.is_available() \
+                    and self.parallel in ("auto", "reduce_tp"):
                 # every rank built the same engine and got the same collective verdict
-                log.warning("no P2P all-reduce for the TP reduce engine: reduce stages stay data-parallel")
-                self.reduce_tp = False
+                log.warning("no P2P all-reduce for the TP engine: every stage stays data-parallel")
+                self.parallel, self.reduce_tp, self._dp_needed = "dp", False, True
         return self._reduce_engine
+
+    def warm(self) -> None:
+        """Build the engines (and measure the planner's constants) outside any timed region."""
+        if self.reduce_tp:
+            _ = self.reduce_engine
+            if self.parallel == "auto":
+                self._measure()
+        if self._dp_needed:
+            _ = self.engine
+
+    def _measure(self):
+        """plan.HWModel with the all-reduce latency / bandwidth of THIS job's GPUs (auto mode)."""
+        if self.hw is None:
+            import torch
+            from ..parallel import plan
+            hw = plan.HWModel()
+            eng = self.reduce_engine
+            ar = eng.model.custom_ar if eng is not None else None
+            if ar is None or self.parallel != "auto":
+                self.hw = plan.with_measurements(hw, tp_ok=ar is not None)
+                return self.hw
+            lat = ar.measure_latency(rows=16, hidden=eng.cfg.hidden)
+            bw = _rccl_bandwidth(eng.model.tp_group, eng.cfg.hidden, torch.device(self._device))
+            self.hw = plan.with_measurements(hw, ar_lat_s=lat, ar_bw=bw, tp_ok=True)
+            log.info("planner constants: all-reduce latency %.1f us (fused, over the local add_rmsnorm), RCCL "
+                     "all-reduce %.1f GB/s", lat * 1e6, bw / 1e9)
+        return self.hw
+
+    def _stage_tp(self, stage: str, prompts: Sequence[Sequence[int]], reqs: Sequence[GenRequest]) -> int:
+        """TP degree for this stage's generate: 1 (DP replicas) or world (one sharded engine)."""
+        world = self.par.world
+        if self.parallel != "dp":
+            _ = self.reduce_engine  # may fall back to dp (no P2P all-reduce on this node)
+        if self.parallel == "dp" or not reqs:
+            return 1
+        if self.parallel == "tp":
+            return world
+        if self.parallel == "reduce_tp":
+            return 1 if stage == "map" else world
+        from ..parallel import plan
+        hw = self._measure()
+        if self.parallel != "auto":  # _measure found no P2P all-reduce and fell back to dp
+            return 1
+        d = plan.ModelDims.of(self.model_config(),
+                              1.0 if self._engine_options.get("weight_dtype") == "fp8" else 2.0)
+        choice = plan.choose(d, hw, [len(p) for p in prompts], [r.max_tokens for r in reqs], world)
+        self.stage_plan[stage] = choice
+        return int(choice["tp"])
 
     def encode_request(self, req: GenRequest) -> List[int]:
         ids = render_chat(self.tokenizer, req.user, req.system)
@@ -177,8 +241,10 @@ class LocalEngineProvider(Provider):
         from .engine import SamplingParams
         t0 = time.perf_counter()
         prompts = [self.encode_request(r) for r in reqs]
-        if self.reduce_tp and reqs and all(r.stage != "map" for r in reqs) and self.reduce_engine is not None \
-                and self.reduce_tp:
+        stage = reqs[0].stage if reqs else "map"
+        tp = self._stage_tp(stage, prompts, reqs) if self.par.world > 1 and self.tp == 1 else 1
+        self.stage_plan.setdefault(stage, {"tp": tp})
+        if tp > 1:
             # every rank runs every request on the TP engine; the TP ranks sample identically
             outs = self.reduce_engine.generate(
                 prompts, [SamplingParams(r.max_tokens, r.temperature, _req_seed(self.seed, r)) for r in reqs],
@@ -221,9 +287,36 @@ class LocalEngineProvider(Provider):
         return results
 
     def stats(self) -> Dict[str, Any]:
-        s: Dict[str, Any] = {"model": self.model, "dp": self.par.dp, "tp": self.par.tp, **self.timings}
+        s: Dict[str, Any] = {"model": self.model, "dp": self.par.dp, "tp": self.par.tp, "parallel": self.parallel,
+                             **self.timings}
+        if self.stage_plan:
+            s["stage_plan"] = dict(self.stage_plan)
+        if self.hw is not None:
+            s["planner_hw"] = {"ar_lat_us": round(self.hw.ar_lat_s * 1e6, 2), "ar_gbps": round(self.hw.ar_bw / 1e9, 1)}
         if self._engine is not None:
             s.update(self._engine.engine_stats())
         if self._reduce_engine is not None:
             s["reduce_engine"] = self._reduce_engine.engine_stats()
         return s
+
+
+def _rccl_bandwidth(group, hidden: int, device, rows: int = 4096) -> float:
+    """Algorithm bandwidth (bytes/s) of one all-reduce of a prefill-sized bf16 activation on ``group``
+    (second of two calls), MAX-reduced over the ranks."""
+    import torch
+    import torch.distributed as dist
+    nccl = dist.get_backend(group) == "nccl"
+    x = torch.ones(rows, hidden, dtype=torch.bfloat16, device=device if nccl else "cpu")
+    best = float("inf")
+    for _ in range(2):
+        pdist.barrier()
+        if nccl:
+            torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        dist.all_reduce(x, group=group)
+        if nccl:
+            torch.cuda.synchronize(device)
+        best = min(best, time.perf_counter() - t0)
+    t = torch.tensor([best], dtype=torch.float64, device=device if nccl else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return x.numel() * 2 / max(float(t.item()), 1e-9)

@@ -167,12 +167,28 @@ def qkv_rope(x, wqkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin,
     return qkv
 
 
+def _fused_ar(all_reduce, rows, hidden):
+    """The fused all-reduce + add + RMSNorm of ``all_reduce`` (``all_reduce.add_rmsnorm(parts, residual,
+    ln, eps)``, parallel/custom_ar.py) when it exists and takes ``rows`` x ``hidden``, else None."""
+    f = getattr(all_reduce, "add_rmsnorm", None)
+    if f is None or not all_reduce.fused_ok(rows, hidden):
+        return None
+    return f
+
+
 def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
-    """residual += a @ w^T (TP-all-reduced when ``all_reduce``); returns rmsnorm(residual) * ln."""
+    """residual += a @ w^T (TP-all-reduced when ``all_reduce``); returns rmsnorm(residual) * ln.
+
+    ``all_reduce`` is a callable summing a tensor over the TP group in place; when it also offers
+    ``add_rmsnorm``/``fused_ok`` (the model's P2P all-reduce) the decode path runs the projection's
+    split-K slabs straight into one fused all-reduce + residual add + RMSNorm kernel."""
     if _use_hip(a) and isinstance(w, Fp8Weight):
         from . import hip
         if a.shape[0] <= hip.SKINNY_MAX_M:
-            parts = _fp8_parts(hip, a, w, role, 1 if all_reduce else None)
+            fused = _fused_ar(all_reduce, a.shape[0], residual.shape[1])
+            parts = _fp8_parts(hip, a, w, role, 1 if (all_reduce and not fused) else None)
+            if fused:
+                return fused(parts, residual, ln, eps)
             if all_reduce:
                 all_reduce(parts)
             return hip.add_rmsnorm_parts(parts, residual, ln, eps)
@@ -182,9 +198,13 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
         return hip.add_rmsnorm(o, residual, ln, eps)
     if _use_hip(a):
         from . import hip
-        p = hip.plan(role, a.shape[0], w.shape[0], w.shape[1], splits=1 if all_reduce else None)
+        fused = _fused_ar(all_reduce, a.shape[0], residual.shape[1])
+        one = 1 if (all_reduce and not fused) else None  # a plain all-reduce takes one slab
+        p = hip.plan(role, a.shape[0], w.shape[0], w.shape[1], splits=one)
         if p[0] != "blas":
-            parts = _plan_parts(hip, p, a, w, 1 if all_reduce else None)
+            parts = _plan_parts(hip, p, a, w, one)
+            if fused:
+                return fused(parts, residual, ln, eps)
             if all_reduce:
                 all_reduce(parts)
             return hip.add_rmsnorm_parts(parts, residual, ln, eps)

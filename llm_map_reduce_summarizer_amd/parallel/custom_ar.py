@@ -30,6 +30,9 @@ _SIGS = {
                                ctypes.c_int),
     "mrsum_ar_allreduce_max_u64": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
                                     ctypes.c_void_p], ctypes.c_int),
+    "mrsum_ar_add_rmsnorm": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                              ctypes.c_void_p], ctypes.c_int),
     "mrsum_ar_error": ([ctypes.c_void_p], ctypes.c_int),
     "mrsum_ar_destroy": ([ctypes.c_void_p], None),
 }
@@ -93,6 +96,35 @@ class CustomAllReduce:
             raise RuntimeError("custom all-reduce launch failed (%d)" % rc)
         return t
 
+    MAX_ROWS = 256
+
+    def fits_rows(self, parts: torch.Tensor) -> bool:
+        """Can ``add_rmsnorm`` take these fp32 split-K slabs [S, T, D]?"""
+        if not (parts.is_cuda and parts.dtype == torch.float32 and parts.is_contiguous() and parts.dim() == 3):
+            return False
+        _, T, D = parts.shape
+        return T <= self.MAX_ROWS and D % 4 == 0 and D <= 8192 and T * D * 4 <= self.max_bytes
+
+    def add_rmsnorm(self, parts: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Fused push-mode all-reduce of this rank's split-K slabs ``parts`` [S, T, D] (fp32) +
+        ``residual += sum`` (bf16, in place) + RMSNorm: returns ``rmsnorm(residual) * w`` [T, D] bf16.
+        One kernel (csrc/kernels/custom_ar.hip: ar_add_rmsnorm_kernel); graph-safe."""
+        if not self.fits_rows(parts):
+            raise ValueError("add_rmsnorm: parts must be contiguous fp32 [S, T<=256, D] within max_bytes")
+        S, T, D = parts.shape
+        if not (residual.dtype == torch.bfloat16 and residual.is_contiguous() and residual.shape == (T, D)
+                and w.dtype == torch.bfloat16 and w.numel() == D):
+            raise ValueError("add_rmsnorm: residual [T, D] / w [D] bf16 expected")
+        if out is None:
+            out = torch.empty(T, D, dtype=torch.bfloat16, device=parts.device)
+        rc = self._lib.mrsum_ar_add_rmsnorm(self._h, parts.data_ptr(), S, T, residual.data_ptr(), w.data_ptr(),
+                                            out.data_ptr(), D, out.stride(0), float(eps),
+                                            torch.cuda.current_stream(parts.device).cuda_stream)
+        if rc:
+            raise RuntimeError("custom all-reduce (add_rmsnorm) launch failed (%d)" % rc)
+        return out
+
     def max_u64_(self, t: torch.Tensor) -> torch.Tensor:
         """Element-wise max over the group, in place, of an int64 tensor holding unsigned 64-bit keys
         (the sampler's Gumbel-max keys; values are compared as unsigned)."""
@@ -138,6 +170,7 @@ class CustomAllReduce:
                 dist.all_reduce(ref, group=self.group)
                 torch.cuda.synchronize(dev)
                 ok &= bool(torch.equal(x, ref))
+            ok &= self._test_fused(dev, iters)
             ok &= self.error() == 0
         except Exception as e:  # keep the collective sequence aligned across ranks
             log.warning("custom all-reduce self-test raised: %s", e)
@@ -145,6 +178,95 @@ class CustomAllReduce:
         votes = [None] * self.world
         dist.all_gather_object(votes, ok, group=self.group)
         return all(votes)
+
+    def _test_fused(self, dev, iters: int, T: int = 5, D: int = 512, S: int = 2) -> bool:
+        """add_rmsnorm against (collective sum of the slabs) + the fp32 reference add_rmsnorm, eager
+        and graph-replayed; every rank must also produce the bit-identical residual."""
+        from ..ops import reference
+        ok = True
+        g = torch.Generator(device="cpu").manual_seed(1234)
+        w = (torch.rand(D, generator=g) + 0.5).to(torch.bfloat16).to(dev)
+        parts = torch.empty(S, T, D, device=dev)
+        res0 = torch.randn(T, D, generator=g).to(torch.bfloat16).to(dev)
+        res = res0.clone()
+        out = torch.empty(T, D, dtype=torch.bfloat16, device=dev)
+
+        def fill(i):
+            gi = torch.Generator(device="cpu").manual_seed(100 * i + self.rank)
+            parts.copy_(torch.randn(S, T, D, generator=gi))
+            res.copy_(res0)
+
+        def check():
+            tot = parts.sum(0)
+            dist.all_reduce(tot, group=self.group)
+            ref_res = res0.clone()
+            ref_out = reference.add_rmsnorm(tot, ref_res, w, 1e-5)
+            good = torch.allclose(res.float(), ref_res.float(), atol=3e-2, rtol=2e-2)
+            good &= torch.allclose(out.float(), ref_out.float(), atol=6e-2, rtol=3e-2)
+            mine = res.float().sum().reshape(1)
+            hi, lo = mine.clone(), mine.clone()
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
+            return bool(good) and bool(torch.equal(hi, lo))
+
+        for i in range(iters):
+            fill(i)
+            self.add_rmsnorm(parts, res, w, 1e-5, out)
+            torch.cuda.synchronize(dev)
+            ok &= check()
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=s):
+            self.add_rmsnorm(parts, res, w, 1e-5, out)
+        for i in range(iters):
+            fill(50 + i)
+            gr.replay()
+            torch.cuda.synchronize(dev)
+            ok &= check()
+        return ok
+
+    def measure_latency(self, rows: int = 16, hidden: int = 4096, calls: int = 64, reps: int = 3) -> float:
+        """Seconds per fused all-reduce + add_rmsnorm call MINUS a local add_rmsnorm_parts call (what a
+        TP decode step pays per all-reduce over the TP=1 graph), both timed inside replayed hipGraphs.
+        MAX over the ranks, so every rank plans with the same number."""
+        from ..ops import hip
+        dev = torch.device("cuda", torch.cuda.current_device())
+        rows = max(1, min(rows, self.max_bytes // (hidden * 4), self.MAX_ROWS))
+        parts = torch.zeros(1, rows, hidden, device=dev)
+        res = torch.zeros(rows, hidden, dtype=torch.bfloat16, device=dev)
+        w = torch.ones(hidden, dtype=torch.bfloat16, device=dev)
+        out = torch.empty_like(res)
+
+        def timed(fn) -> float:
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                fn()
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                for _ in range(calls):
+                    fn()
+            g.replay()
+            torch.cuda.synchronize(dev)
+            best = float("inf")
+            for _ in range(reps):
+                dist.barrier(group=self.group)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                g.replay()
+                e1.record()
+                torch.cuda.synchronize(dev)
+                best = min(best, e0.elapsed_time(e1) / 1000.0 / calls)
+            return best
+
+        t_ar = timed(lambda: self.add_rmsnorm(parts, res, w, 1e-5, out))
+        t_local = timed(lambda: hip.add_rmsnorm_parts(parts, res, w, 1e-5, out))
+        v = torch.tensor([max(0.0, t_ar - t_local)], dtype=torch.float64,
+                         device=dev if dist.get_backend(self.group) == "nccl" else "cpu")
+        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=self.group)
+        return float(v.item())
 
     def error(self) -> int:
         """Non-zero if a wait for a peer timed out (the result of that call is garbage)."""

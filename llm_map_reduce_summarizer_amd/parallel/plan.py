@@ -1,0 +1,136 @@
+"""Per-stage parallelism planner: data-parallel replicas vs. one tensor-parallel engine.
+
+Every stage of the summarizer is a batch of independent generations pinned to ``max_new`` tokens
+(map: one per chunk; reduce level 1: one per batch of summaries; final: one).  On N GPUs a stage can
+run either
+
+* **DP**: the requests are split over N replicas of the model (one per GPU), or
+* **TP**: every request runs on ONE engine whose weights and KV heads are sharded over the N GPUs
+  (two all-reduces per layer on the custom P2P kernel, parallel/custom_ar.py).
+
+Decode is a 1000-step serial loop whose step time is bounded by streaming the weights plus the
+batch's KV cache from HBM, so DP does not shorten it (each replica still streams the full 15 GB of
+weights per step) while TP divides both streams by N at the price of the per-layer all-reduce
+latency.  Prefill is compute-bound: DP divides it by N for free, TP adds RCCL all-reduces of the
+activations.  Which is faster depends on the batch, the context and the all-reduce latency of the
+node, so the choice is a cost model whose hardware constants are *measured*:
+
+* ``hbm_bw``, ``step_floor_s``, ``prefill_flops``: single-GPU decode/prefill measurements of the
+  engine (profiles/r1_decode_step_latency.log: B=1/5/10/39 at 4k context fit
+  t = (W + B ctx kv) / 5.4 TB/s + 0.96 ms to within 3 %; prefill 72k tok/s of Llama-3-8B);
+* ``ar_lat_s`` and ``ar_bw``: timed at start-up on the job's own GPUs (the custom all-reduce
+  inside a replayed hipGraph; one RCCL all-reduce of a prefill-sized activation), MAX-reduced over
+  the ranks so every rank takes the same decision.
+
+The reference has a single form of parallelism, a semaphore-bounded fan-out of HTTPS calls
+(reference llm_executor.py:133-147); this module is the MI355X replacement for choosing how the
+fan-out maps onto GPUs.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, replace
+from typing import Dict, List, Sequence
+
+
+@dataclass(frozen=True)
+class HWModel:
+    hbm_bw: float = 5.4e12          # bytes/s streamed by the decode GEMM + attention kernels
+    step_floor_s: float = 0.96e-3   # fixed per-step cost of the decode graph (kernel latencies), 32 layers
+    prefill_flops: float = 1.1e15   # effective prefill FLOP/s (hipBLASLt GEMMs + flash attention)
+    ar_lat_s: float = 20e-6         # one decode all-reduce (custom P2P kernel), measured at start-up
+    ar_bw: float = 100e9            # RCCL all-reduce algorithm bandwidth (bytes/s), measured at start-up
+    tp_ok: bool = True              # False when the TP engine has no graph-safe all-reduce
+
+
+@dataclass(frozen=True)
+class ModelDims:
+    weight_bytes: float
+    kv_bytes_per_token: float
+    flops_per_token: float
+    n_layers: int
+    hidden: int
+
+    @classmethod
+    def of(cls, cfg, weight_bytes_per_param: float = 2.0) -> "ModelDims":
+        n = cfg.n_params()
+        emb = cfg.vocab_size * cfg.hidden  # the embedding table is gathered, not streamed
+        return cls(weight_bytes=(n - emb) * weight_bytes_per_param, kv_bytes_per_token=cfg.kv_bytes_per_token(),
+                   flops_per_token=2.0 * (n - 2 * emb), n_layers=cfg.n_layers, hidden=cfg.hidden)
+
+
+def decode_step_s(d: ModelDims, hw: HWModel, batch: int, ctx: float, tp: int) -> float:
+    """One decode step of ``batch`` sequences at mean context ``ctx`` on a TP=``tp`` engine."""
+    if batch <= 0:
+        return 0.0
+    stream = (d.weight_bytes + batch * ctx * d.kv_bytes_per_token) / tp / hw.hbm_bw
+    floor = hw.step_floor_s * d.n_layers / 32.0
+    comm = (2 * d.n_layers + 1) * hw.ar_lat_s if tp > 1 else 0.0
+    return stream + floor + comm
+
+
+def prefill_s(d: ModelDims, hw: HWModel, tokens: int, tp: int) -> float:
+    compute = tokens * d.flops_per_token / tp / hw.prefill_flops
+    comm = 2 * d.n_layers * tokens * d.hidden * 2 / hw.ar_bw if tp > 1 else 0.0
+    return compute + comm
+
+
+def _lpt(costs: Sequence[int], bins: int) -> List[List[int]]:
+    order = sorted(range(len(costs)), key=lambda i: (-costs[i], i))
+    load, out = [0] * bins, [[] for _ in range(bins)]
+    for i in order:
+        b = min(range(bins), key=lambda j: (load[j], j))
+        out[b].append(i)
+        load[b] += costs[i]
+    return out
+
+
+def stage_seconds(d: ModelDims, hw: HWModel, prompt_lens: Sequence[int], max_new: Sequence[int], tp: int,
+                  world: int) -> float:
+    """Estimated wall-clock of one stage on ``world`` GPUs as ``world // tp`` replicas of TP=``tp``
+    (requests LPT-balanced over replicas, every generation pinned to its ``max_new``)."""
+    if not prompt_lens:
+        return 0.0
+    dp = max(1, world // tp)
+    bins = _lpt([p + m for p, m in zip(prompt_lens, max_new)], dp)
+    worst = 0.0
+    for idx in bins:
+        if not idx:
+            continue
+        pl = [prompt_lens[i] for i in idx]
+        mn = [max_new[i] for i in idx]
+        t = prefill_s(d, hw, sum(pl), tp)
+        # sequences retire as they reach their max_new: walk the decode in segments of equal batch
+        order = sorted(range(len(idx)), key=lambda k: mn[k])
+        done = 0
+        for k in order:
+            steps = mn[k] - done
+            if steps > 0:
+                live = [j for j in range(len(idx)) if mn[j] > done]
+                ctx = sum(pl[j] for j in live) / len(live) + done + steps / 2.0
+                t += steps * decode_step_s(d, hw, len(live), ctx, tp)
+                done = mn[k]
+        worst = max(worst, t)
+    return worst
+
+
+def choose(d: ModelDims, hw: HWModel, prompt_lens: Sequence[int], max_new: Sequence[int], world: int,
+           candidates: Sequence[int] = ()) -> Dict[str, object]:
+    """Best TP degree for a stage among ``candidates`` (default: 1 and ``world``)."""
+    cands = list(candidates) or ([1, world] if world > 1 else [1])
+    if not hw.tp_ok:
+        cands = [1]
+    est = {tp: stage_seconds(d, hw, prompt_lens, max_new, tp, world) for tp in cands}
+    best = min(cands, key=lambda tp: (est[tp], tp))
+    return {"tp": best, "estimates_s": {str(k): round(v, 3) for k, v in est.items()}}
+
+
+def with_measurements(hw: HWModel, ar_lat_s=None, ar_bw=None, tp_ok=None) -> HWModel:
+    kw = {}
+    if ar_lat_s is not None:
+        kw["ar_lat_s"] = float(ar_lat_s)
+    if ar_bw is not None:
+        kw["ar_bw"] = float(ar_bw)
+    if tp_ok is not None:
+        kw["tp_ok"] = bool(tp_ok)
+    return replace(hw, **kw)

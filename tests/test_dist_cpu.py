@@ -136,3 +136,23 @@ def test_dp2_with_tp2_reduce():
         assert p.returncode == 0, err[-3000:]
         outs.append(json.loads([l for l in o.splitlines() if l.startswith("RESULT ")][-1][7:]))
     assert outs[0]["summary"] == outs[1]["summary"] and outs[0]["plan"]["levels"] >= 2
+
+
+TPALL_SCRIPT = SCRIPT.replace('engine_options={"kv_pages": 512, "max_num_seqs": 16})',
+                              'engine_options={"kv_pages": 512, "max_num_seqs": 16}, parallel="tp")')
+
+
+@pytest.mark.slow
+def test_all_stages_tp2():
+    """parallel="tp": map AND reduce on one TP=2 engine (no DP engine is built)."""
+    code = TPALL_SCRIPT % {"root": ROOT}
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE="2",
+               OMP_NUM_THREADS="2")
+    procs = [subprocess.Popen([sys.executable, "-c", code], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = []
+    for p in procs:
+        o, err = p.communicate(timeout=600)
+        assert p.returncode == 0, err[-3000:]
+        outs.append(json.loads([l for l in o.splitlines() if l.startswith("RESULT ")][-1][7:]))
+    assert outs[0]["summary"] == outs[1]["summary"] and outs[0]["plan"]["levels"] >= 2

@@ -1,0 +1,66 @@
+"""Per-stage parallelism planner (parallel/plan.py): calibration and decisions."""
+
+import json
+import os
+
+import pytest
+
+from llm_map_reduce_summarizer_amd.engine.config import get_model_config
+from llm_map_reduce_summarizer_amd.parallel import plan
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+D8B = plan.ModelDims.of(get_model_config("llama3-8b"))
+
+
+def test_decode_model_matches_measured_single_gpu_steps():
+    """The default constants reproduce the measured MI355X decode steps (profiles/) within 5 %."""
+    path = os.path.join(ROOT, "profiles", "r1_decode_step_latency.log")
+    rows = [json.loads(l) for l in open(path) if l.startswith("{")]
+    assert rows
+    for r in rows:
+        est = plan.decode_step_s(D8B, plan.HWModel(), r["B"], r["ctx"] + 128, 1) * 1e3
+        assert abs(est - r["decode_ms_per_step"]) / r["decode_ms_per_step"] < 0.05, (r, est)
+
+
+def test_tp_divides_streams_and_adds_all_reduces():
+    hw = plan.HWModel(ar_lat_s=0.0)
+    t1 = plan.decode_step_s(D8B, hw, 8, 4000, 1)
+    t8 = plan.decode_step_s(D8B, hw, 8, 4000, 8)
+    floor = hw.step_floor_s
+    assert abs((t8 - floor) * 8 - (t1 - floor)) < 1e-9
+    hw2 = plan.with_measurements(hw, ar_lat_s=10e-6)
+    assert abs(plan.decode_step_s(D8B, hw2, 8, 4000, 8) - t8 - 65 * 10e-6) < 1e-12
+
+
+def test_choice_follows_all_reduce_latency():
+    pl, mn = [3950] * 39, [1000] * 39
+    fast = plan.choose(D8B, plan.with_measurements(plan.HWModel(), ar_lat_s=5e-6), pl, mn, 8)
+    slow = plan.choose(D8B, plan.with_measurements(plan.HWModel(), ar_lat_s=200e-6), pl, mn, 8)
+    assert fast["tp"] == 8 and slow["tp"] == 1
+    assert set(fast["estimates_s"]) == {"1", "8"}
+    # a single long sequence (final reduce) always prefers sharding when all-reduces are cheap
+    assert plan.choose(D8B, plan.with_measurements(plan.HWModel(), ar_lat_s=5e-6), [6000], [1000], 2)["tp"] == 2
+    # no graph-safe all-reduce -> DP only
+    assert plan.choose(D8B, plan.with_measurements(plan.HWModel(), tp_ok=False), pl, mn, 8)["tp"] == 1
+    assert plan.choose(D8B, plan.HWModel(), pl, mn, 1)["tp"] == 1
+
+
+def test_stage_seconds_balances_replicas_and_retires_sequences():
+    hw = plan.HWModel()
+    one = plan.stage_seconds(D8B, hw, [4000], [1000], 1, 1)
+    # two equal requests on two replicas cost the same as one on one
+    assert abs(plan.stage_seconds(D8B, hw, [4000, 4000], [1000, 1000], 1, 2) - one) < 1e-9
+    # a short request retires early: cheaper than two full-length ones in one batch
+    mixed = plan.stage_seconds(D8B, hw, [4000, 4000], [1000, 100], 1, 1)
+    full = plan.stage_seconds(D8B, hw, [4000, 4000], [1000, 1000], 1, 1)
+    assert one < mixed < full
+    assert plan.stage_seconds(D8B, hw, [], [], 1, 1) == 0.0
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_choice_is_deterministic(world):
+    hw = plan.with_measurements(plan.HWModel(), ar_lat_s=15e-6, ar_bw=150e9)
+    pl = [3000 + 37 * i for i in range(23)]
+    a = plan.choose(D8B, hw, pl, [1000] * 23, world)
+    b = plan.choose(D8B, hw, list(pl), [1000] * 23, world)
+    assert a == b

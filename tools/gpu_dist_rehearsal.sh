@@ -5,7 +5,9 @@
 #  (2) two ranks sharing cuda:0 over gloo, every stage data-parallel: DP scatter / all-gather with two
 #      GPU engines;
 #  (3) the same two ranks with the reduce stages tensor-parallel (TP=2 engine: custom P2P all-reduce
-#      inside the decode hipGraphs, vocab-parallel sampling, gloo for the eager prefill all-reduces).
+#      inside the decode hipGraphs, vocab-parallel sampling, gloo for the eager prefill all-reduces);
+#  (4) every stage on the TP=2 engine (--parallel tp) and (5) the planner's choice (--parallel auto;
+#      its measured all-reduce constants are those of two ranks sharing one GPU, not of xGMI).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 MRSUM_FORCE_DIST=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
@@ -21,3 +23,9 @@ MRSUM_DIST_BACKEND=gloo MRSUM_PARALLEL=reduce_tp timeout -k 10 600 python -m tor
   --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 2 --hours 1 --steps 1 \
   --warmup 1 --max-new-tokens 64 --log-level INFO > gpurun_out/dist_gloo2_reduce_tp.log 2>&1 || exit $?
 tail -n 1 gpurun_out/dist_gloo2_reduce_tp.log
+for mode in tp auto; do
+MRSUM_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
+  --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29520 bench.py --gpus 2 --hours 1 --steps 1 \
+  --warmup 1 --max-new-tokens 64 --parallel $mode --log-level INFO > gpurun_out/dist_gloo2_$mode.log 2>&1 || exit $?
+tail -n 1 gpurun_out/dist_gloo2_$mode.log
+done
