@@ -8,7 +8,7 @@
 // bytes [16 KiB b, 16 KiB (b+1)):
 //   1. copy my slice of `in` into MY slot (epoch & 1)            -- local uncached stores
 //   2. system-scope release store of `epoch` into flags[b][me] of EVERY rank (remote over xGMI)
-//   3. spin (system-scope acquire, s_sleep, bounded) until my flags[b][r] >= epoch for all r
+//   3. spin (system-scope acquire, s_sleep, bounded: wait_flag) until my flags[b][r] >= epoch for all r
 //   4. out[slice] = sum_r slot_r[slice]                            -- remote uncached loads
 // The epoch is a per-block counter in device memory advanced by the block itself, so the kernel
 // is replay-safe inside a hipGraph (no host-side arguments change between calls).  Reuse of a slot
@@ -51,6 +51,26 @@ struct ArHandle {
 __device__ __forceinline__ void st_release_sys(unsigned* p, unsigned v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+
+// Spin (relaxed system-scope loads, s_sleep between polls) until *f >= epoch, bounded in WALL time by
+// the 100 MHz s_memrealtime counter: ranks are launched by independent host threads and may lag each
+// other by host-side jitter (GC, logging, a first hipBLASLt call), so the bound is generous (4 s) but
+// finite -- a peer that is gone sets the sticky error word (checked by the host after every generate)
+// instead of hanging the GPU.  Once the error is set, later waits do not spin at all.
+constexpr unsigned long long WAIT_TICKS = 400000000ull;  // 4 s at 100 MHz
+
+__device__ __forceinline__ void wait_flag(const unsigned* f, unsigned epoch, unsigned* error) {
+    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) return;
+    if (__hip_atomic_load(error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS) {
+            atomicOr(error, 1u);
+            break;
+        }
+    }
+}
 }  // namespace
 
 enum { OP_SUM_F32 = 0, OP_MAX_U64 = 1 };
@@ -92,14 +112,7 @@ __global__ __launch_bounds__(256) void ar_oneshot_kernel(Peers peers, int rank, 
         const unsigned* f = reinterpret_cast<const unsigned*>(peers.base[rank]) + b * MAX_RANKS + tid;
         // sticky error: once a wait has timed out, later calls do not wait again (the host sees the
         // error word at its next check and stops using this path)
-        long spins = __hip_atomic_load(error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? (1L << 22) : 0;
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-            __builtin_amdgcn_s_sleep(2);
-            if (++spins > (1L << 22)) {  // ~ a second: a peer is gone or late; flag it and fall through
-                atomicOr(error, 1u);
-                break;
-            }
-        }
+        wait_flag(f, epoch, error);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -191,14 +204,7 @@ __global__ __launch_bounds__(256) void ar_add_rmsnorm_kernel(Peers peers, int ra
     }
     if (tid < world) {
         const unsigned* f = reinterpret_cast<const unsigned*>(peers.base[rank] + PUSH_FLAGS) + row * MAX_RANKS + tid;
-        long spins = __hip_atomic_load(error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? (1L << 22) : 0;
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1L << 22)) {
-                atomicOr(error, 1u);
-                break;
-            }
-        }
+        wait_flag(f, epoch, error);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }

@@ -60,6 +60,16 @@ class _Seq:
     params: SamplingParams
     pages: List[int] = field(default_factory=list)
     slot: int = -1
+    imported: Optional["ImportedPrefill"] = None
+
+
+@dataclass
+class ImportedPrefill:
+    """A prompt prefilled ELSEWHERE (another engine / rank): its first sampled token and this engine's
+    share of its KV, ``kv`` [2, n_layers, ceil(prompt / page), hkv_local, page, head_dim] (K then V,
+    whole pages; rows past the prompt are ignored).  See LLMEngine.prefill_export."""
+    first_token: int
+    kv: Optional[torch.Tensor]
 
 
 class DecodeState:
@@ -149,6 +159,7 @@ class LLMEngine:
             log.warning("TP=%d without the custom all-reduce: decode hipGraphs disabled", self.model.tp_size)
             self.use_graphs = False
         self._graphs: Dict[int, "torch.cuda.CUDAGraph"] = {}
+        self._on_prefill = None
         self._workspaces: Dict[int, object] = {}
         self.stats = {"prefill_tokens": 0, "prefill_s": 0.0, "decode_steps": 0, "decode_tokens": 0,
                       "decode_s": 0.0, "generate_calls": 0, "graph_captures": 0, "peak_active": 0}
@@ -255,16 +266,21 @@ class LLMEngine:
 
     # ------------------------------------------------------------------ API
     def generate(self, prompts: Sequence[Sequence[int]], params: Sequence[SamplingParams],
-                 ignore_eos: bool = False) -> List[GenOutput]:
+                 ignore_eos: bool = False, imported: Optional[Dict[int, ImportedPrefill]] = None,
+                 on_prefill=None) -> List[GenOutput]:
         """Generate for every prompt.  ``ignore_eos`` pins the work to max_new_tokens per request
-        (benchmark mode, SURVEY §7.4: random weights emit EOS at random)."""
+        (benchmark mode, SURVEY §7.4: random weights emit EOS at random).
+
+        ``imported``: request index -> ImportedPrefill; those requests skip the prefill (their KV pages
+        are copied in and decoding starts from the imported first token).  ``on_prefill(seqs)`` is
+        called after every prefill forward with the just-prefilled sequences (pages still held)."""
         if len(prompts) != len(params):
             raise ValueError("prompts and params differ in length")
         n_eos = self.state.n_eos
         if ignore_eos:
             self.state.n_eos = 0
         try:
-            out = self._generate(prompts, params)
+            out = self._generate(prompts, params, imported or {}, on_prefill)
         finally:
             self.state.n_eos = n_eos
         if self.model.custom_ar is not None and self.model.custom_ar.error():
@@ -272,8 +288,10 @@ class LLMEngine:
                                "results are invalid (set MRSUM_CUSTOM_AR=0 to use RCCL)")
         return out
 
-    def _generate(self, prompts: Sequence[Sequence[int]], params: Sequence[SamplingParams]) -> List[GenOutput]:
+    def _generate(self, prompts: Sequence[Sequence[int]], params: Sequence[SamplingParams],
+                  imported: Dict[int, ImportedPrefill], on_prefill) -> List[GenOutput]:
         self.stats["generate_calls"] += 1
+        self._on_prefill = on_prefill
         results: List[Optional[GenOutput]] = [None] * len(prompts)
         waiting: List[_Seq] = []
         for i, (p, sp) in enumerate(zip(prompts, params)):
@@ -286,7 +304,13 @@ class LLMEngine:
                                  % (len(p), mn, self.max_model_len))
             if max(p) >= self.cfg.vocab_size or min(p) < 0:
                 raise ValueError("token id out of range")
-            waiting.append(_Seq(i, p, SamplingParams(mn, sp.temperature, sp.seed)))
+            s = _Seq(i, p, SamplingParams(mn, sp.temperature, sp.seed), imported=imported.get(i))
+            if s.imported is not None:
+                tok = int(s.imported.first_token)
+                if mn == 1 or tok in set(self.state.eos.tolist()[: self.state.n_eos]):
+                    results[i] = GenOutput([tok], len(p), "length" if mn == 1 else "stop")  # done at prefill
+                    continue
+            waiting.append(s)
         # longest first: better packing and no late long straggler
         waiting.sort(key=lambda s: -(len(s.prompt) + s.params.max_new_tokens))
         active: List[_Seq] = []
@@ -333,7 +357,8 @@ class LLMEngine:
             need = self.kv.pages_for(len(s.prompt) + s.params.max_new_tokens)
             if need > self.kv.alloc.available():
                 break
-            if batch and tokens + len(s.prompt) > self.max_prefill_tokens:
+            if batch and (s.imported is not None or tokens + len(s.prompt) > self.max_prefill_tokens):
+                # full prefill batch, or an imported prefill (slots stay in admission order): flush
                 self._run_prefill(batch, active)
                 batch, tokens = [], 0
                 continue
@@ -349,11 +374,36 @@ class LLMEngine:
             st.temps[s.slot] = float(s.params.temperature)
             st.seeds[s.slot] = int(s.params.seed)
             st.result[s.slot] = 0
+            if s.imported is not None:  # no forward pass: KV + first token come from elsewhere
+                self._install(s)
+                active.append(s)
+                continue
             batch.append(s)
             tokens += len(s.prompt)
         if batch:
             self._run_prefill(batch, active)
         return batch
+
+    def _install(self, s: _Seq) -> None:
+        """Copy an imported prefill's KV into ``s``'s pages and set its slot as the sampler would have."""
+        st, imp = self.state, s.imported
+        n = len(s.prompt)
+        npg = self.kv.pages_for(n)
+        if imp.kv is not None:
+            if tuple(imp.kv.shape) != (2, self.cfg.n_layers, npg, self.model.hkv, self.page, self.cfg.head_dim):
+                raise ValueError("imported KV has shape %s" % (tuple(imp.kv.shape),))
+            idx = torch.tensor(s.pages[:npg], dtype=torch.long, device=self.device)
+            kv = imp.kv.to(self.device, non_blocking=True)
+            self.kv.k.index_copy_(1, idx, kv[0])
+            self.kv.v.index_copy_(1, idx, kv[1])
+        i = s.slot
+        st.out_tokens[i, 0] = int(imp.first_token)
+        st.next_ids[i] = int(imp.first_token)
+        st.gen_count[i] = 1
+        st.positions[i] = n
+        st.done[i] = 0
+        s.imported = None  # release the staging buffer
+        self.stats["imported_prefills"] = self.stats.get("imported_prefills", 0) + 1
 
     def _run_prefill(self, batch: List[_Seq], active: List[_Seq]) -> None:
         t0 = time.perf_counter()
@@ -361,6 +411,43 @@ class LLMEngine:
         self._sync()
         self.stats["prefill_s"] += time.perf_counter() - t0
         active.extend(batch)
+        if self._on_prefill is not None:
+            self._on_prefill(batch)
+
+    # ------------------------------------------------------------------ disaggregated prefill
+    def prefill_export(self, prompts: Sequence[Sequence[int]], params: Sequence[SamplingParams], groups: int,
+                       ignore_eos: bool = False):
+        """Prefill ``prompts`` here (full model, all KV heads) and hand them to a TP=``groups`` engine.
+
+        Returns ``(first_tokens, packs)``: the first sampled token of every prompt and, per TP rank
+        g, one flat bf16 tensor holding -- prompt after prompt -- the K pages then the V pages of
+        KV heads [g * Hkv / groups, (g + 1) * Hkv / groups): [2, n_layers, ceil(len / page),
+        Hkv / groups, page, head_dim] each, the layout ImportedPrefill expects.  The pages here are
+        released when this returns.  (Used by the provider: DP prefill, all-to-all, TP decode.)"""
+        if self.model.tp_size != 1 or self.model.hkv % groups:
+            raise ValueError("prefill_export needs a TP=1 engine and Hkv divisible by %d" % groups)
+        hl = self.model.hkv // groups
+        chunks: Dict[int, List[List[torch.Tensor]]] = {}
+
+        def grab(seqs):
+            for s in seqs:
+                npg = self.kv.pages_for(len(s.prompt))
+                idx = torch.tensor(s.pages[:npg], dtype=torch.long, device=self.device)
+                k = self.kv.k.index_select(1, idx)  # [L, npg, Hkv, P, D]
+                v = self.kv.v.index_select(1, idx)
+                chunks[s.rid] = [torch.stack([k[:, :, g * hl:(g + 1) * hl], v[:, :, g * hl:(g + 1) * hl]])
+                                 .reshape(-1) for g in range(groups)]
+
+        one = [SamplingParams(1, p.temperature, p.seed) for p in params]
+        outs = self.generate(prompts, one, ignore_eos=ignore_eos, on_prefill=grab)
+        firsts = [o.token_ids[0] for o in outs]
+        packs = [torch.cat([chunks[i][g] for i in range(len(prompts))]) if prompts else
+                 torch.empty(0, dtype=self.dtype, device=self.device) for g in range(groups)]
+        return firsts, packs
+
+    def import_shape(self, prompt_len: int):
+        """Shape of this engine's ImportedPrefill.kv for a prompt of ``prompt_len`` tokens."""
+        return (2, self.cfg.n_layers, self.kv.pages_for(prompt_len), self.model.hkv, self.page, self.cfg.head_dim)
 
     def _compact(self, active: List[_Seq], fin: set) -> None:
         st = self.state

@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import hashlib
 import logging
+import math
 import os
 import time
 from typing import Any, Dict, List, Optional, Sequence
@@ -106,6 +107,10 @@ class LocalEngineProvider(Provider):
         self._reduce_engine = None
         self._dp_needed = self.parallel != "tp"
         self.hw = None  # plan.HWModel with this job's measured all-reduce constants (auto mode)
+        # TP stages prefill data-parallel on the TP=1 engines and move the KV with one all-to-all
+        self.handoff = self.reduce_tp and os.environ.get("MRSUM_HANDOFF", "1") == "1"
+        if self.handoff:
+            self._dp_needed = True
         self.stage_plan: Dict[str, Any] = {}
         if self.reduce_tp:
             self._engine_options.setdefault("kv_fraction", float(os.environ.get("MRSUM_DP_KV_FRACTION", "0.5")))
@@ -220,9 +225,48 @@ class LocalEngineProvider(Provider):
             return 1
         d = plan.ModelDims.of(self.model_config(),
                               1.0 if self._engine_options.get("weight_dtype") == "fp8" else 2.0)
-        choice = plan.choose(d, hw, [len(p) for p in prompts], [r.max_tokens for r in reqs], world)
+        choice = plan.choose(d, hw, [len(p) for p in prompts], [r.max_tokens for r in reqs], world,
+                             handoff=self.handoff)
         self.stage_plan[stage] = choice
         return int(choice["tp"])
+
+    def _handoff(self, prompts: Sequence[Sequence[int]], sp) -> Dict[int, Any]:
+        """Disaggregated prefill for a TP stage: every rank prefills its LPT share of the prompts on
+        its full (TP=1) engine -- no activation all-reduces -- and ships each prompt's KV heads to the
+        TP rank that owns them in ONE all-to-all (RCCL over xGMI: ~prompt tokens x 128 KiB x
+        (world-1)/world per Llama-3-8B prompt); first tokens are all-gathered.  Returns the
+        ImportedPrefill map for the TP engine's generate."""
+        import torch
+        import torch.distributed as dist
+
+        from .engine import ImportedPrefill
+        t0 = time.perf_counter()
+        world, rank = self.par.world, self.par.rank
+        owner = assign_balanced([len(p) for p in prompts], world)
+        mine = [i for i in range(len(prompts)) if owner[i] == rank]
+        firsts, packs = self.engine.prefill_export([prompts[i] for i in mine], [sp[i] for i in mine], world,
+                                                   ignore_eos=self.ignore_eos)
+        tp_eng = self.reduce_engine
+        shapes = [tp_eng.import_shape(len(p)) for p in prompts]
+        numel = [math.prod(s) for s in shapes]
+        recv_sizes = [sum(numel[i] for i in range(len(prompts)) if owner[i] == s) for s in range(world)]
+        send = torch.cat(packs) if packs else torch.empty(0, dtype=torch.bfloat16)
+        nccl = dist.get_backend() == "nccl"
+        dev = send.device if nccl else torch.device("cpu")
+        send = send.to(dev)
+        recv = torch.empty(sum(recv_sizes), dtype=send.dtype, device=dev)
+        dist.all_to_all_single(recv, send, recv_sizes, [p.numel() for p in packs])
+        tok = {}
+        for part in pdist.all_gather_json({str(i): int(t) for i, t in zip(mine, firsts)}):
+            tok.update({int(k): v for k, v in part.items()})
+        out, off = {}, 0
+        for s in range(world):
+            for i in range(len(prompts)):
+                if owner[i] == s:
+                    out[i] = ImportedPrefill(tok[i], recv[off:off + numel[i]].view(shapes[i]))
+                    off += numel[i]
+        self.timings["handoff_s"] = self.timings.get("handoff_s", 0.0) + time.perf_counter() - t0
+        return out
 
     def encode_request(self, req: GenRequest) -> List[int]:
         ids = render_chat(self.tokenizer, req.user, req.system)
@@ -246,9 +290,9 @@ class LocalEngineProvider(Provider):
         self.stage_plan.setdefault(stage, {"tp": tp})
         if tp > 1:
             # every rank runs every request on the TP engine; the TP ranks sample identically
-            outs = self.reduce_engine.generate(
-                prompts, [SamplingParams(r.max_tokens, r.temperature, _req_seed(self.seed, r)) for r in reqs],
-                ignore_eos=self.ignore_eos)
+            sp = [SamplingParams(r.max_tokens, r.temperature, _req_seed(self.seed, r)) for r in reqs]
+            imported = self._handoff(prompts, sp) if self.handoff else None
+            outs = self.reduce_engine.generate(prompts, sp, ignore_eos=self.ignore_eos, imported=imported)
             self.timings["generate_s"] += time.perf_counter() - t0
             return [GenResult(self.tokenizer.decode(o.token_ids), o.prompt_len, len(o.token_ids), 0.0,
                               extra={"finish_reason": o.finish_reason}) for o in outs]

@@ -22,6 +22,11 @@ node, so the choice is a cost model whose hardware constants are *measured*:
   inside a replayed hipGraph; one RCCL all-reduce of a prefill-sized activation), MAX-reduced over
   the ranks so every rank takes the same decision.
 
+A TP stage may also prefill *disaggregated* (``handoff``): data-parallel on every rank's full
+TP=1 engine, then one all-to-all moves each prompt's KV heads to their TP owner -- the KV of a
+prompt is 128 KiB/token for Llama-3-8B, far less than the 2 x 32 activation all-reduces of
+8 KiB/token each that a TP prefill forward needs.
+
 The reference has a single form of parallelism, a semaphore-bounded fan-out of HTTPS calls
 (reference llm_executor.py:133-147); this module is the MI355X replacement for choosing how the
 fan-out maps onto GPUs.
@@ -85,21 +90,33 @@ def _lpt(costs: Sequence[int], bins: int) -> List[List[int]]:
     return out
 
 
+def handoff_prefill_s(d: ModelDims, hw: HWModel, prompt_lens: Sequence[int], world: int) -> float:
+    """Disaggregated prefill of a TP=``world`` stage: the prompts are prefilled data-parallel on the
+    ranks' full (TP=1) engines, then every rank sends each TP peer its KV heads (one all-to-all)."""
+    bins = _lpt(list(prompt_lens), world)
+    compute = max(prefill_s(d, hw, sum(prompt_lens[i] for i in b), 1) for b in bins)
+    kv = sum(prompt_lens) * d.kv_bytes_per_token
+    per_rank = kv / world * (world - 1) / world  # what one rank sends (and receives)
+    return compute + per_rank / hw.ar_bw
+
+
 def stage_seconds(d: ModelDims, hw: HWModel, prompt_lens: Sequence[int], max_new: Sequence[int], tp: int,
-                  world: int) -> float:
+                  world: int, handoff: bool = False) -> float:
     """Estimated wall-clock of one stage on ``world`` GPUs as ``world // tp`` replicas of TP=``tp``
-    (requests LPT-balanced over replicas, every generation pinned to its ``max_new``)."""
+    (requests LPT-balanced over replicas, every generation pinned to its ``max_new``).  ``handoff``:
+    a TP=world stage prefills through handoff_prefill_s instead of a TP forward."""
     if not prompt_lens:
         return 0.0
     dp = max(1, world // tp)
     bins = _lpt([p + m for p, m in zip(prompt_lens, max_new)], dp)
+    use_handoff = handoff and tp > 1 and tp == world
     worst = 0.0
     for idx in bins:
         if not idx:
             continue
         pl = [prompt_lens[i] for i in idx]
         mn = [max_new[i] for i in idx]
-        t = prefill_s(d, hw, sum(pl), tp)
+        t = handoff_prefill_s(d, hw, pl, world) if use_handoff else prefill_s(d, hw, sum(pl), tp)
         # sequences retire as they reach their max_new: walk the decode in segments of equal batch
         order = sorted(range(len(idx)), key=lambda k: mn[k])
         done = 0
@@ -115,12 +132,12 @@ def stage_seconds(d: ModelDims, hw: HWModel, prompt_lens: Sequence[int], max_new
 
 
 def choose(d: ModelDims, hw: HWModel, prompt_lens: Sequence[int], max_new: Sequence[int], world: int,
-           candidates: Sequence[int] = ()) -> Dict[str, object]:
+           candidates: Sequence[int] = (), handoff: bool = False) -> Dict[str, object]:
     """Best TP degree for a stage among ``candidates`` (default: 1 and ``world``)."""
     cands = list(candidates) or ([1, world] if world > 1 else [1])
     if not hw.tp_ok:
         cands = [1]
-    est = {tp: stage_seconds(d, hw, prompt_lens, max_new, tp, world) for tp in cands}
+    est = {tp: stage_seconds(d, hw, prompt_lens, max_new, tp, world, handoff) for tp in cands}
     best = min(cands, key=lambda tp: (est[tp], tp))
     return {"tp": best, "estimates_s": {str(k): round(v, 3) for k, v in est.items()}}
 

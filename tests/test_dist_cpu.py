@@ -120,7 +120,10 @@ def test_tp2_matches_tp1():
 
 
 RTP_SCRIPT = SCRIPT.replace('engine_options={"kv_pages": 512, "max_num_seqs": 16})',
-                            'engine_options={"kv_pages": 512, "max_num_seqs": 16}, reduce_tp=True)')
+                            'engine_options={"kv_pages": 512, "max_num_seqs": 16}, reduce_tp=True)').replace(
+    'LocalEngineProvider("tiny", cfg', 'LocalEngineProvider("tiny-gqa4", cfg').replace(
+    '"engine_calls": prov.stats().get("generate_calls", 0)}',
+    '"engine_calls": prov.stats().get("generate_calls", 0), "stage_plan": prov.stats()["stage_plan"]}')
 
 
 @pytest.mark.slow
@@ -136,10 +139,15 @@ def test_dp2_with_tp2_reduce():
         assert p.returncode == 0, err[-3000:]
         outs.append(json.loads([l for l in o.splitlines() if l.startswith("RESULT ")][-1][7:]))
     assert outs[0]["summary"] == outs[1]["summary"] and outs[0]["plan"]["levels"] >= 2
+    sp = outs[0]["stage_plan"]
+    assert sp["map"]["tp"] == 1 and sp["reduce_final"]["tp"] == 2, sp
 
 
 TPALL_SCRIPT = SCRIPT.replace('engine_options={"kv_pages": 512, "max_num_seqs": 16})',
-                              'engine_options={"kv_pages": 512, "max_num_seqs": 16}, parallel="tp")')
+                              'engine_options={"kv_pages": 512, "max_num_seqs": 16}, parallel="tp")').replace(
+    '"engine_calls": prov.stats().get("generate_calls", 0)}',
+    '"engine_calls": 0, "imported": prov.stats()["reduce_engine"].get("imported_prefills", 0)}').replace(
+    'LocalEngineProvider("tiny", cfg', 'LocalEngineProvider("tiny-gqa4", cfg')
 
 
 @pytest.mark.slow
@@ -156,3 +164,4 @@ def test_all_stages_tp2():
         assert p.returncode == 0, err[-3000:]
         outs.append(json.loads([l for l in o.splitlines() if l.startswith("RESULT ")][-1][7:]))
     assert outs[0]["summary"] == outs[1]["summary"] and outs[0]["plan"]["levels"] >= 2
+    assert outs[0]["imported"] > 0  # TP stages prefilled data-parallel and imported their KV

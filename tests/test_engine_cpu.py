@@ -161,3 +161,30 @@ def test_fp8_weights_engine_cpu():
     w = torch.randn(64, 128)
     q = Fp8Weight.quantize(w)
     assert q.q.dtype == torch.float8_e4m3fn and torch.allclose(q.dequant(), w, rtol=0.07, atol=1e-3)
+
+
+def test_prefill_export_import_roundtrip():
+    """Disaggregated prefill: engine A prefills + exports (1 group), engine B imports the KV and first
+    token and decodes -- same tokens as B generating on its own (same seeded weights)."""
+    from llm_map_reduce_summarizer_amd.engine.engine import ImportedPrefill
+    cfg = get_model_config("tiny", init_std=0.05)
+    a = LLMEngine(cfg, device="cpu", max_model_len=512, max_num_seqs=8, kv_pages=64, sync_every=3)
+    b = LLMEngine(cfg, device="cpu", max_model_len=512, max_num_seqs=8, kv_pages=64, sync_every=3)
+    prompts = _prompts(4)
+    ps = [SamplingParams(5 + i, 0.3, 40 + i) for i in range(4)]
+    firsts, packs = a.prefill_export(prompts, ps, groups=1)
+    assert a.kv.alloc.available() == a.kv.num_pages - 1  # exporter's pages released
+    imported, off = {}, 0
+    for i, p in enumerate(prompts):
+        shape = b.import_shape(len(p))
+        n = math.prod(shape)
+        imported[i] = ImportedPrefill(firsts[i], packs[0][off:off + n].view(shape))
+        off += n
+    assert off == packs[0].numel()
+    got = b.generate(prompts, ps, imported=imported)
+    ref = b.generate(prompts, ps)
+    assert [o.token_ids for o in got] == [o.token_ids for o in ref]
+    assert b.stats["imported_prefills"] == 4
+    # a request that is complete after its first token never reaches the decode loop
+    one = b.generate(prompts[:1], [SamplingParams(1, 0.3, 40)], imported={0: ImportedPrefill(firsts[0], None)})
+    assert one[0].token_ids == [firsts[0]] and one[0].finish_reason == "length"
