@@ -333,11 +333,48 @@ __device__ __forceinline__ int dk_off(int row, int chunk) { return row * 256 + (
 __device__ __forceinline__ int dv_off(int row, int chunk) { return row * 256 + ((chunk ^ ((row & 7) << 1)) << 4); }
 }  // namespace
 
-template <int G>
+// ROPE variant (decode): q is not a bf16 row but the QKV GEMM's fp32 split-K slabs ``qkv_parts``
+// [SP, B, (Hq + 2 Hkv) D] -- the workgroup sums its G query heads' slabs, rotates them (RoPE at
+// position ctx - 1) in registers, and the workgroup whose split holds position ctx - 1 also builds
+// the new token's rotated K and V row from the slabs and writes it into the paged cache before
+// streaming (its split is the only reader of that page in this launch: splits are whole pages).
+// This folds the separate rope_kv_parts launch into the attention kernel.
+struct RopeArgs {
+    const float* parts;   // slab 0, row 0
+    size_t slab_stride;   // elements between slabs (B * width)
+    int SP;               // number of slabs
+    int width;            // (Hq + 2 Hkv) * D elements per token row
+    int hq_total;         // Hq of this rank
+    const float2* cos_sin;  // [max_pos, D/2]
+};
+
+// 8 consecutive floats of a token row summed over the SP slabs (batched loads, see rope_kv.hip)
+__device__ __forceinline__ void slab_sum8(const RopeArgs& ra, const float* row, int col, float* f) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = 0.f;
+    for (int s0 = 0; s0 < ra.SP; s0 += 4) {
+        float4 a[4], c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float4* p = reinterpret_cast<const float4*>(row + (size_t)min(s0 + u, ra.SP - 1) * ra.slab_stride + col);
+            a[u] = p[0];
+            c[u] = p[1];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (s0 + u < ra.SP) {
+                f[0] += a[u].x; f[1] += a[u].y; f[2] += a[u].z; f[3] += a[u].w;
+                f[4] += c[u].x; f[5] += c[u].y; f[6] += c[u].z; f[7] += c[u].w;
+            }
+        }
+    }
+}
+
+template <int G, bool ROPE>
 __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
-    const bf16* __restrict__ q, int q_stride, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
+    const bf16* __restrict__ q, int q_stride, bf16* __restrict__ kc, bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ positions,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int S, float scale_log2) {
+    float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int S, float scale_log2, RopeArgs ra) {
     constexpr int D = 128, PG = 64;
     __shared__ __attribute__((aligned(16))) char lds[2 * PG * 256 + 2 * 4 * 16 * 4];
     char* ldsK = lds;
@@ -362,13 +399,38 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
     }
     const int ntiles = (ke - ks + PG - 1) / PG;
 
-    // Q^T fragments (B operand of 16x16x32): lane holds Q[head col][dims 32k + 8grp .. +8]
-    bf16x8 qf[4];
+    const float* prow = ROPE ? ra.parts + (size_t)b * ra.width : nullptr;
+    const float2* cs = ROPE ? ra.cos_sin + (size_t)(ctx - 1) * (D / 2) : nullptr;
+    if constexpr (ROPE) {
+        const int pos = ctx - 1;
+        if (ks <= pos && pos < ke) {
+            // the new token's K (rotated) and V row of this kv head -> paged cache, then visible to
+            // this workgroup's page loads below (drain + workgroup barrier); only this split reads
+            // that page in this launch
+            const int page = block_tables[(size_t)b * bt_stride + pos / PG];
+            const size_t dst = ((size_t)page * Hkv * PG + (size_t)kvh * PG + (pos % PG)) * D;
+            if (tid < 8) {
+                const int c = tid * 8;
+                float lo[8], hi[8], rl[8], rh[8];
+                slab_sum8(ra, prow, (ra.hq_total + kvh) * D + c, lo);
+                slab_sum8(ra, prow, (ra.hq_total + kvh) * D + c + D / 2, hi);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (col < G) v = *reinterpret_cast<const uint4*>(q + (size_t)b * q_stride + (kvh * G + col) * D + 32 * k + 8 * grp);
-        qf[k] = __builtin_bit_cast(bf16x8, v);
+                for (int j = 0; j < 8; ++j) {
+                    const float2 e = cs[c + j];
+                    rl[j] = lo[j] * e.x - hi[j] * e.y;
+                    rh[j] = hi[j] * e.x + lo[j] * e.y;
+                }
+                *reinterpret_cast<uint4*>(kc + dst + c) = pack8(rl);
+                *reinterpret_cast<uint4*>(kc + dst + c + D / 2) = pack8(rh);
+            } else if (tid < 8 + D / 8) {
+                const int c = (tid - 8) * 8;
+                float v[8];
+                slab_sum8(ra, prow, (ra.hq_total + Hkv + kvh) * D + c, v);
+                *reinterpret_cast<uint4*>(vc + dst + c) = pack8(v);
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
     }
 
     const int* bt = block_tables + (size_t)b * bt_stride + ks / PG;
@@ -384,6 +446,41 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
         for (int i = 0; i < 4; ++i) {
             kreg[i] = *reinterpret_cast<const u32x4*>(kc + base + (size_t)16 * i * D);
             vreg[i] = *reinterpret_cast<const u32x4*>(vc + base + (size_t)16 * i * D);
+        }
+    }
+    // Q^T fragments (B operand of 16x16x32): lane holds Q[head col][dims 32k + 8grp .. +8]; built
+    // after the first page's loads are in flight (the ROPE slab sums are an L2 round trip of their own)
+    bf16x8 qf[4];
+    if constexpr (ROPE) {
+        // dims 32k + 8grp + j (k = 0, 1) pair with dims 64 + the same (k = 2, 3): the rotation of a
+        // lane's q values needs only the lane's own values
+        float a[4][8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (col < G) slab_sum8(ra, prow, (kvh * G + col) * D + 32 * k + 8 * grp, a[k]);
+            else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) a[k][j] = 0.f;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            float lo[8], hi[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float2 e = cs[32 * k + 8 * grp + j];
+                lo[j] = a[k][j] * e.x - a[k + 2][j] * e.y;
+                hi[j] = a[k + 2][j] * e.x + a[k][j] * e.y;
+            }
+            qf[k] = __builtin_bit_cast(bf16x8, pack8(lo));
+            qf[k + 2] = __builtin_bit_cast(bf16x8, pack8(hi));
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (col < G) v = *reinterpret_cast<const uint4*>(q + (size_t)b * q_stride + (kvh * G + col) * D + 32 * k + 8 * grp);
+            qf[k] = __builtin_bit_cast(bf16x8, v);
         }
     }
 #pragma unroll
@@ -487,25 +584,31 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
     }
 }
 
-MRSUM_API int mrsum_attn_decode_mfma(const void* q, int q_stride, const void* kcache, const void* vcache,
-                                     const int* block_tables, int bt_stride, const int* positions, void* part_o,
-                                     void* part_ml, void* out, int out_stride, int B, int Hq, int Hkv, int D, int P,
-                                     int S, float scale, hipStream_t s) {
+static int launch_mfma(const void* q, int q_stride, const void* kcache, const void* vcache, const int* block_tables,
+                       int bt_stride, const int* positions, void* part_o, void* part_ml, void* out, int out_stride,
+                       int B, int Hq, int Hkv, int D, int P, int S, float scale, const RopeArgs* rope, hipStream_t s) {
     if (B <= 0) return 0;
     if (D != 128 || P != 64 || Hq % Hkv || Hq / Hkv > 16 || S < 1 || S > MAX_SPLITS) return (int)hipErrorInvalidValue;
     const int G = Hq / Hkv;
     const float sl = scale * 1.4426950408889634f;
     dim3 grid(S, Hkv, B), block(256);
-    auto Qp = (const bf16*)q; auto K = (const bf16*)kcache; auto V = (const bf16*)vcache;
+    auto Qp = (const bf16*)q; auto K = (bf16*)kcache; auto V = (bf16*)vcache;
     auto PO = (float*)part_o; auto PM = (float*)part_ml;
-    switch (G) {
-        case 1: attn_decode_mfma_kernel<1><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, S, sl); break;
-        case 2: attn_decode_mfma_kernel<2><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, S, sl); break;
-        case 4: attn_decode_mfma_kernel<4><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, S, sl); break;
-        case 8: attn_decode_mfma_kernel<8><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, S, sl); break;
-        case 16: attn_decode_mfma_kernel<16><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, S, sl); break;
-        default: return (int)hipErrorInvalidValue;
+    const RopeArgs ra = rope ? *rope : RopeArgs{nullptr, 0, 0, 0, 0, nullptr};
+#define MFMA_L(G_, R_) attn_decode_mfma_kernel<G_, R_><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, \
+                                                                         positions, PO, PM, Hkv, S, sl, ra)
+#define MFMA_G(R_)                            \
+    switch (G) {                              \
+        case 1: MFMA_L(1, R_); break;         \
+        case 2: MFMA_L(2, R_); break;         \
+        case 4: MFMA_L(4, R_); break;         \
+        case 8: MFMA_L(8, R_); break;         \
+        case 16: MFMA_L(16, R_); break;       \
+        default: return (int)hipErrorInvalidValue; \
     }
+    if (rope) { MFMA_G(true) } else { MFMA_G(false) }
+#undef MFMA_G
+#undef MFMA_L
     int e = (int)hipGetLastError();
     if (e) return e;
     switch (G) {
@@ -516,4 +619,25 @@ MRSUM_API int mrsum_attn_decode_mfma(const void* q, int q_stride, const void* kc
         case 16: attn_decode_combine_kernel<16><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
     }
     return (int)hipGetLastError();
+}
+
+MRSUM_API int mrsum_attn_decode_mfma(const void* q, int q_stride, const void* kcache, const void* vcache,
+                                     const int* block_tables, int bt_stride, const int* positions, void* part_o,
+                                     void* part_ml, void* out, int out_stride, int B, int Hq, int Hkv, int D, int P,
+                                     int S, float scale, hipStream_t s) {
+    return launch_mfma(q, q_stride, kcache, vcache, block_tables, bt_stride, positions, part_o, part_ml, out,
+                       out_stride, B, Hq, Hkv, D, P, S, scale, nullptr, s);
+}
+
+// Decode attention straight from the QKV GEMM's fp32 split-K slabs [SP, B, (Hq + 2 Hkv) D]: RoPE on q,
+// the new token's K/V rotated + written into the paged cache, attention, split merge (2 launches).
+MRSUM_API int mrsum_attn_decode_rope(const void* qkv_parts, int SP, const void* cos_sin, void* kcache, void* vcache,
+                                     const int* block_tables, int bt_stride, const int* positions, void* part_o,
+                                     void* part_ml, void* out, int out_stride, int B, int Hq, int Hkv, int D, int P,
+                                     int S, float scale, hipStream_t s) {
+    if (SP < 1 || !qkv_parts || !cos_sin) return (int)hipErrorInvalidValue;
+    const int width = (Hq + 2 * Hkv) * D;
+    const RopeArgs ra{(const float*)qkv_parts, (size_t)B * width, SP, width, Hq, (const float2*)cos_sin};
+    return launch_mfma(nullptr, 0, kcache, vcache, block_tables, bt_stride, positions, part_o, part_ml, out,
+                       out_stride, B, Hq, Hkv, D, P, S, scale, &ra, s);
 }

@@ -201,7 +201,7 @@ class LlamaModel:
         for i, lw in enumerate(self.layers):
             nxt = self.layers[i + 1].ln1 if i + 1 < n else self.final_norm
             qkv = ops.qkv_rope(x, lw.wqkv, positions, seq_idx, block_tables, kcache[i], vcache[i], self.cos_sin,
-                               self.hq, self.hkv, self.hd, page)
+                               self.hq, self.hkv, self.hd, page, defer=decode)
             a = attention(i, qkv)
             x = ops.proj_add_rmsnorm(a, lw.wo, residual, lw.ln2, c.rms_eps, "o", ar)
             act = ops.gate_up_swiglu(x, lw.wgu)

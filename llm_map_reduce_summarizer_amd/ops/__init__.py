@@ -96,6 +96,14 @@ def attn_prefill(qkv, cu_seqlens, hq, hkv, d, scale, out=None, **kw):
 
 
 def attn_decode(q, kcache, vcache, block_tables, positions, hq, hkv, d, page, scale, out=None, workspace=None):
+    """``q``: bf16 rows [B, hq * d] (already rotated, K/V already in the cache) or a QKVParts."""
+    if isinstance(q, QKVParts):
+        from . import hip
+        if workspace is not None and workspace.counters is not None:
+            q = q.materialize()
+        else:
+            return hip.attn_decode_rope(q.parts, q.cos_sin, kcache, vcache, block_tables, positions, hq, hkv, d,
+                                        page, scale, out, workspace=workspace)
     if _use_hip(q):
         from . import hip
         return hip.attn_decode(q, kcache, vcache, block_tables, positions, hq, hkv, d, page, scale, out,
@@ -141,12 +149,36 @@ def _fp8_parts(hip, x, w, role, splits):
     return hip.fp8_linear_parts(x, w, s, nt)
 
 
-def qkv_rope(x, wqkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page):
-    """qkv = x @ wqkv^T, RoPE on Q/K, K/V into the paged cache; returns bf16 qkv rows."""
+class QKVParts:
+    """Deferred decode QKV: the QKV GEMM's fp32 split-K slabs [S, B, (hq + 2 hkv) d], not yet rotated nor
+    written to the cache.  ``attn_decode`` consumes it with the fused RoPE + KV-write attention kernel
+    (ops.hip.attn_decode_rope); ``materialize`` runs the separate rope_kv_parts pass instead."""
+
+    def __init__(self, parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page):
+        self.parts, self.positions, self.seq_idx, self.block_tables = parts, positions, seq_idx, block_tables
+        self.kcache, self.vcache, self.cos_sin = kcache, vcache, cos_sin
+        self.hq, self.hkv, self.d, self.page = hq, hkv, d, page
+
+    def materialize(self):
+        from . import hip
+        return hip.rope_kv_parts(self.parts, self.positions, self.seq_idx, self.block_tables, self.kcache,
+                                 self.vcache, self.cos_sin, self.hq, self.hkv, self.d, self.page)
+
+
+def _defer_ok(hip, defer, x, hq, hkv, d, page):
+    return defer and hip.FUSED_ROPE and d == 128 and page == 64 and hq % hkv == 0 and hq // hkv <= 16 \
+        and hip.DECODE_ATTN_IMPL == "mfma"
+
+
+def qkv_rope(x, wqkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page, defer=False):
+    """qkv = x @ wqkv^T, RoPE on Q/K, K/V into the paged cache; returns bf16 qkv rows -- or, with
+    ``defer`` on the GPU decode path, a QKVParts for attn_decode's fused RoPE + KV write."""
     if _use_hip(x) and isinstance(wqkv, Fp8Weight):
         from . import hip
         if x.shape[0] <= hip.SKINNY_MAX_M:
             parts = _fp8_parts(hip, x, wqkv, "qkv", None)
+            if _defer_ok(hip, defer, x, hq, hkv, d, page):
+                return QKVParts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page)
             return hip.rope_kv_parts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d,
                                      page)
         qkv = hip.fp8_linear(x, wqkv)
@@ -157,6 +189,8 @@ def qkv_rope(x, wqkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin,
         p = hip.plan("qkv", x.shape[0], wqkv.shape[0], wqkv.shape[1])
         if p[0] != "blas":
             parts = _plan_parts(hip, p, x, wqkv, None)
+            if _defer_ok(hip, defer, x, hq, hkv, d, page):
+                return QKVParts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page)
             return hip.rope_kv_parts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv,
                                      d, page)
         qkv = torch.nn.functional.linear(x, wqkv)

@@ -33,6 +33,8 @@ _SIGS = {
                           _c_int, _c_int, _c_int, _c_float, _vp, _vp],
     "mrsum_attn_decode_mfma": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int,
                                _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
+    "mrsum_attn_decode_rope": [_vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int,
+                               _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int,
                          _vp],
@@ -262,6 +264,40 @@ class DecodeWorkspace:
 
 
 DECODE_ATTN_IMPL = os.environ.get("MRSUM_DECODE_ATTN", "mfma")
+FUSED_ROPE = os.environ.get("MRSUM_FUSED_ROPE", "1") == "1"
+
+
+def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
+                     block_tables: torch.Tensor, positions: torch.Tensor, hq: int, hkv: int, d: int, page: int,
+                     scale: float, out: Optional[torch.Tensor] = None,
+                     workspace: Optional[DecodeWorkspace] = None) -> torch.Tensor:
+    """Decode attention from the QKV GEMM's fp32 split-K slabs ``parts`` [S, B, (hq + 2 hkv) d]: RoPE of
+    q and of the new token's k, K/V write into the paged cache and the attention itself in one launch
+    (+ the split merge): the rope_kv_parts kernel of the unfused path disappears."""
+    _req(parts.is_cuda and parts.dtype == torch.float32 and parts.is_contiguous() and parts.dim() == 3,
+         "attn_decode_rope: parts must be fp32 [S, B, width]")
+    SP, B, width = parts.shape
+    _req(width == (hq + 2 * hkv) * d and d == 128 and page == 64 and hq % hkv == 0 and hq // hkv <= 16,
+         "attn_decode_rope: unsupported config")
+    _bf16_cuda(kcache, vcache)
+    _req(tuple(kcache.shape[1:]) == (hkv, page, d) and kcache.is_contiguous() and vcache.is_contiguous(),
+         "attn_decode_rope: cache must be [pages, Hkv, P, D]")
+    _req(cos_sin.dtype == torch.float32 and cos_sin.is_contiguous() and cos_sin.shape[-2:] == (d // 2, 2),
+         "attn_decode_rope: cos_sin [max_pos, d/2, 2] fp32")
+    _i32(block_tables, positions)
+    _req(block_tables.dim() == 2 and block_tables.shape[0] >= B and positions.numel() >= B, "attn_decode_rope: tables")
+    if workspace is None:
+        workspace = DecodeWorkspace(B, hq, d, decode_splits(B, hkv, block_tables.shape[1] * page), parts.device, hkv)
+    _req(workspace.part_o.numel() >= B * hq * workspace.splits * d and workspace.counters is None,
+         "attn_decode_rope: workspace")
+    if out is None:
+        out = torch.empty(B, hq * d, dtype=torch.bfloat16, device=parts.device)
+    _rows_ok(out)
+    _check(_fn("mrsum_attn_decode_rope")(_p(parts), SP, _p(cos_sin), _p(kcache), _p(vcache), _p(block_tables),
+                                         block_tables.stride(0), _p(positions), _p(workspace.part_o),
+                                         _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
+                                         workspace.splits, scale, _stream()), "attn_decode_rope")
+    return out
 
 
 def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, block_tables: torch.Tensor,

@@ -7,6 +7,12 @@ and then sums all peers' buffers directly over xGMI -- one kernel, no host invol
 inside a hipGraph.  Handles are exchanged once through the group (any backend); messages larger
 than ``max_bytes`` or non-fp32 tensors go to ``torch.distributed.all_reduce`` (RCCL).
 
+The decode projections use a second, *push-mode* kernel (``add_rmsnorm``): every rank sums its own
+split-K slabs, writes the row straight into every peer's buffer (posted remote stores -- no remote
+read round trip), flags, and then reduces the rows from LOCAL memory in rank order, adds the
+residual and applies the RMSNorm -- the all-reduce, the split-K reduction and the add_rmsnorm
+kernel of the TP=1 graph in one launch.
+
 The reference has no collective of any kind (its only "communication" is HTTPS, reference
 llm_executor.py:290-297); this is the MI355X replacement for the TP reduce path it implies.
 """
@@ -53,7 +59,9 @@ class CustomAllReduce:
 
     MAX_RANKS = 8
 
-    def __init__(self, group=None, max_bytes: int = 1 << 20):
+    def __init__(self, group=None, max_bytes: int = 2 << 20):
+        """``max_bytes`` bounds one message: the one-shot kernel takes at most 1 MiB of it, the fused
+        add_rmsnorm (push mode) the whole (Llama-3-70B decode rows are 32 KiB of fp32: 64 rows)."""
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -284,7 +292,7 @@ class CustomAllReduce:
             pass
 
 
-def maybe_custom_all_reduce(group=None, max_bytes: int = 1 << 20) -> Optional[CustomAllReduce]:
+def maybe_custom_all_reduce(group=None, max_bytes: int = 2 << 20) -> Optional[CustomAllReduce]:
     """A CustomAllReduce for ``group`` when every rank is on a GPU, else None (RCCL/gloo path)."""
     if not (dist.is_initialized() and torch.cuda.is_available()):
         return None

@@ -342,3 +342,40 @@ def test_fp8_swiglu_and_quant():
     assert torch.allclose(s.cpu(), x.float().abs().amax(1).cpu() / 448, rtol=1e-5)
     assert (q.float() - ref_q.float()).abs().max().item() <= 16.0  # at most one e4m3 ulp at the top binade
     assert (q.float() == ref_q.float()).float().mean().item() > 0.98
+
+
+@pytest.mark.parametrize("hq,hkv,S", [(32, 8, 4), (4, 1, 1), (16, 1, 3), (8, 2, 2)])
+def test_attn_decode_rope_fused(hq, hkv, S):
+    """attn_decode_rope (q/k RoPE + new K/V written into the cache + attention, from the QKV GEMM's
+    fp32 split-K slabs) == reference rope_kv_parts followed by reference attention."""
+    d, page = 128, 64
+    ctxs = [1, 64, 65, 700, 129, 1000]
+    B = len(ctxs)
+    n_pages = 64
+    g = torch.Generator().manual_seed(77)
+    kc0 = torch.randn(n_pages, hkv, page, d, generator=g).to(torch.bfloat16)
+    vc0 = torch.randn(n_pages, hkv, page, d, generator=g).to(torch.bfloat16)
+    perm = torch.randperm(n_pages - 1, generator=g) + 1
+    bt = torch.zeros(B, 20, dtype=torch.int32)
+    used = 0
+    for b, c in enumerate(ctxs):
+        npg = -(-c // page)
+        bt[b, :npg] = perm[used:used + npg]
+        used += npg
+    bt = bt.to(DEV)
+    pos = torch.tensor([c - 1 for c in ctxs], dtype=torch.int32, device=DEV)
+    W = (hq + 2 * hkv) * d
+    parts = (torch.randn(S, B, W, generator=g) * 0.5).to(DEV)
+    cs = reference.rope_cos_sin(2048, d, 500000.0, DEV)
+    sc = 1.0 / math.sqrt(d)
+    sidx = torch.arange(B, dtype=torch.int32, device=DEV)
+    k2, v2 = kc0.clone().to(DEV), vc0.clone().to(DEV)
+    qkv = reference.rope_kv_parts(parts, pos, sidx, bt, k2, v2, cs, hq, hkv, d, page)
+    o2 = reference.attn_decode(qkv, k2, v2, bt, pos, hq, hkv, d, page, sc)
+    k1, v1 = kc0.clone().to(DEV), vc0.clone().to(DEV)
+    ws = hip.DecodeWorkspace(B, hq, d, hip.decode_splits(B, hkv, 20 * page), DEV, hkv)
+    for _ in range(2):  # idempotent: the second call rewrites the same K/V row
+        o1 = hip.attn_decode_rope(parts, cs, k1, v1, bt, pos, hq, hkv, d, page, sc, workspace=ws)
+        _close(o1, o2, 2e-2)
+    _close(k1, k2, 3e-2)
+    _close(v1, v2, 3e-2)
