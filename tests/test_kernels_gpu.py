@@ -379,3 +379,4 @@ def test_attn_decode_rope_fused(hq, hkv, S):
         _close(o1, o2, 2e-2)
     _close(k1, k2, 3e-2)
     _close(v1, v2, 3e-2)
+
