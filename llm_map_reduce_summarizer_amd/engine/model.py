@@ -165,6 +165,9 @@ class LlamaModel:
             if self.custom_ar is not None and self.custom_ar.fits(t):
                 self.custom_ar.all_reduce(t)
             else:
+                if t.is_cuda and torch.cuda.is_current_stream_capturing():
+                    raise RuntimeError("TP all-reduce of %s does not fit the P2P buffers inside a hipGraph "
+                                       "capture (lower the decode batch or raise max_bytes)" % (tuple(t.shape),))
                 torch.distributed.all_reduce(t, group=self.tp_group)
         return t
 

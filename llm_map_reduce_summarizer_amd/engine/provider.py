@@ -66,7 +66,7 @@ class LocalEngineProvider(Provider):
     batched = True
 
     def __init__(self, model: str = "llama3-8b", config: Optional[LLMConfig] = None, device: Optional[str] = None,
-                 tp: int = 1, seed: Optional[int] = None, max_model_len: int = 16384, engine=None,
+                 tp: int = 1, seed: Optional[int] = None, max_model_len: int = 32768, engine=None,
                  engine_options: Optional[Dict[str, Any]] = None, dtype: Optional[str] = None,
                  kv_fraction: Optional[float] = None, use_graphs: bool = True, max_num_seqs: Optional[int] = None,
                  tokenizer: Optional[str] = None, ignore_eos: bool = False, reduce_tp: Optional[bool] = None,
@@ -164,7 +164,7 @@ class LocalEngineProvider(Provider):
             world = self.par.world
             opts = dict(self._engine_options)
             frac = "0.6" if self.parallel == "tp" else "0.35"  # leave HBM for the DP engine
-            opts.update(max_model_len=self.max_model_len, max_num_seqs=64,
+            opts.update(max_model_len=self.max_model_len, max_num_seqs=self.config.ENGINE_MAX_NUM_SEQS,
                         kv_fraction=float(os.environ.get("MRSUM_REDUCE_KV_FRACTION", frac)),
                         eos_ids=self.tokenizer.eos_ids)
             if self._device is None:

@@ -59,9 +59,10 @@ class CustomAllReduce:
 
     MAX_RANKS = 8
 
-    def __init__(self, group=None, max_bytes: int = 2 << 20):
+    def __init__(self, group=None, max_bytes: int = 4 << 20):
         """``max_bytes`` bounds one message: the one-shot kernel takes at most 1 MiB of it, the fused
-        add_rmsnorm (push mode) the whole (Llama-3-70B decode rows are 32 KiB of fp32: 64 rows)."""
+        add_rmsnorm (push mode) the whole: 256 decode rows of Llama-3-8B (16 KiB of fp32 each), 128
+        of Llama-3-70B."""
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -292,7 +293,7 @@ class CustomAllReduce:
             pass
 
 
-def maybe_custom_all_reduce(group=None, max_bytes: int = 2 << 20) -> Optional[CustomAllReduce]:
+def maybe_custom_all_reduce(group=None, max_bytes: int = 4 << 20) -> Optional[CustomAllReduce]:
     """A CustomAllReduce for ``group`` when every rank is on a GPU, else None (RCCL/gloo path)."""
     if not (dist.is_initialized() and torch.cuda.is_available()):
         return None

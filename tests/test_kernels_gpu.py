@@ -380,3 +380,49 @@ def test_attn_decode_rope_fused(hq, hkv, S):
     _close(k1, k2, 3e-2)
     _close(v1, v2, 3e-2)
 
+
+@pytest.mark.parametrize("tp", [2, 4, 8])
+@pytest.mark.parametrize("M", [1, 10, 39, 48, 64])
+def test_tp_shard_decode_blocks(tp, M):
+    """The fused decode blocks (ops.qkv_rope + attn_decode, proj_add_rmsnorm, gate_up_swiglu) at the
+    per-rank shard shapes of Llama-3-8B under TP=tp (e.g. TP=8: 1 KV head, QKV N=768, o K=512, gate_up
+    N=3584, down K=1792) -- whatever GEMM plan they pick -- against the fp32 reference."""
+    from llm_map_reduce_summarizer_amd import ops
+    hid, hd, page = 4096, 128, 64
+    hq, hkv, ffn = 32 // tp, 8 // tp, 14336 // tp
+    sc = 1.0 / math.sqrt(hd)
+    x = _rand(M, hid, seed=70)
+    wqkv = _rand((hq + 2 * hkv) * hd, hid, scale=0.02, seed=71)
+    wo = _rand(hid, hq * hd, scale=0.02, seed=72)
+    wgu = _rand(2 * ffn, hid, scale=0.02, seed=73)
+    wd = _rand(hid, ffn, scale=0.02, seed=74)
+    ln = (torch.rand(hid) + 0.5).to(torch.bfloat16).to(DEV)
+    cs = reference.rope_cos_sin(4096, hd, 500000.0, DEV)
+    n_pages = M * 3 + 1
+    g = torch.Generator().manual_seed(75)
+    k0 = torch.randn(n_pages, hkv, page, hd, generator=g).to(torch.bfloat16)
+    v0 = torch.randn(n_pages, hkv, page, hd, generator=g).to(torch.bfloat16)
+    bt = (1 + torch.arange(M * 3, dtype=torch.int32).view(M, 3)).to(DEV)
+    pos = torch.tensor([(37 * i) % 190 for i in range(M)], dtype=torch.int32, device=DEV)
+    sidx = torch.arange(M, dtype=torch.int32, device=DEV)
+    # attention block: fused GPU path vs reference rope_kv + attention
+    k1, v1 = k0.clone().to(DEV), v0.clone().to(DEV)
+    k2, v2 = k0.clone().to(DEV), v0.clone().to(DEV)
+    q1 = ops.qkv_rope(x, wqkv, pos, sidx, bt, k1, v1, cs, hq, hkv, hd, page, defer=True)
+    a1 = ops.attn_decode(q1, k1, v1, bt, pos, hq, hkv, hd, page, sc)
+    qkv2 = reference.linear(x, wqkv)
+    reference.rope_kv(qkv2, pos, sidx, bt, k2, v2, cs, hq, hkv, hd, page)
+    a2 = reference.attn_decode(qkv2, k2, v2, bt, pos, hq, hkv, hd, page, sc)
+    _close(a1, a2, 3e-2, 5e-2)
+    # o projection + residual + norm, gate_up + SwiGLU, down + residual + norm
+    r1, r2 = x.clone(), x.clone()
+    h1 = ops.proj_add_rmsnorm(a2, wo, r1, ln, 1e-5, "o")
+    h2 = reference.add_rmsnorm(reference.linear(a2, wo), r2, ln, 1e-5)
+    _close(r1, r2, 3e-2)
+    _close(h1, h2, 5e-2, 5e-2)
+    act1 = ops.gate_up_swiglu(h2, wgu)
+    act2 = reference.swiglu(reference.linear(h2, wgu))
+    _close(act1, act2, 3e-2, 5e-2)
+    d1 = ops.proj_add_rmsnorm(act2, wd, r1.copy_(x), ln, 1e-5, "down")
+    d2 = reference.add_rmsnorm(reference.linear(act2, wd), r2.copy_(x), ln, 1e-5)
+    _close(d1, d2, 5e-2, 5e-2)
