@@ -52,7 +52,7 @@ __device__ __forceinline__ void combine_group(const float* part_o, const float* 
             ls = v.y;
         }
         const float M = wave_max(ms);
-        const float w = ms == -INFINITY ? 0.f : exp2f(ms - M);
+        const float w = ms == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms - M);
         const float den = wave_sum(w * ls);
         if (lane < S) sw[g * S + lane] = w;
         if (lane == 0) sden[g] = den;
@@ -220,10 +220,10 @@ __global__ __launch_bounds__(256) void attn_decode_split_kernel(
         for (int g = 0; g < G; ++g) {
             const float mx = fmaxf(fmaxf(s[0][g], s[1][g]), fmaxf(s[2][g], s[3][g]));
             const float mn = fmaxf(m[g], mx);  // finite: key k0 is always valid
-            const float alpha = exp2f(m[g] - mn);
+            const float alpha = __builtin_amdgcn_exp2f(m[g] - mn);
             m[g] = mn;
 #pragma unroll
-            for (int u = 0; u < 4; ++u) pr[u][g] = exp2f(s[u][g] - mn);
+            for (int u = 0; u < 4; ++u) pr[u][g] = __builtin_amdgcn_exp2f(s[u][g] - mn);
             l[g] = l[g] * alpha + (pr[0][g] + pr[1][g]) + (pr[2][g] + pr[3][g]);
 #pragma unroll
             for (int j = 0; j < 8; ++j) o[g][j] *= alpha;
@@ -260,7 +260,7 @@ __global__ __launch_bounds__(256) void attn_decode_split_kernel(
 #pragma unroll
         for (int s2 = 0; s2 < 16; ++s2) {
             const float ms = sm_m[s2][g];
-            const float w = ms == -INFINITY ? 0.f : exp2f(ms - M);
+            const float w = ms == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms - M);
             acc += w * sm_o[s2][g][d];
             L += w * sm_l[s2][g];
         }
@@ -523,9 +523,9 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
             mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
             mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
             const float mn = fmaxf(m, mt);  // finite: key0 < ke is a valid key for every head
-            const float alpha = exp2f(m - mn);
+            const float alpha = __builtin_amdgcn_exp2f(m - mn);
             m = mn;
-            const float p0 = exp2f(s0 - mn), p1 = exp2f(s1 - mn), p2 = exp2f(s2 - mn), p3 = exp2f(s3 - mn);
+            const float p0 = __builtin_amdgcn_exp2f(s0 - mn), p1 = __builtin_amdgcn_exp2f(s1 - mn), p2 = __builtin_amdgcn_exp2f(s2 - mn), p3 = __builtin_amdgcn_exp2f(s3 - mn);
             lsum = lsum * alpha + (p0 + p1) + (p2 + p3);
             const s4v pb = {__builtin_bit_cast(short, (bf16)p0), __builtin_bit_cast(short, (bf16)p1),
                             __builtin_bit_cast(short, (bf16)p2), __builtin_bit_cast(short, (bf16)p3)};
@@ -571,7 +571,7 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
 #pragma unroll
         for (int ww = 0; ww < 4; ++ww) {
             const float mw = sm_ml[ww * 16 + h];
-            const float wt = mw == -INFINITY ? 0.f : exp2f(mw - M);
+            const float wt = mw == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(mw - M);
             acc += wt * sm_o[(ww * D + d) * 16 + h];
             L += wt * sm_ml[64 + ww * 16 + h];
         }
