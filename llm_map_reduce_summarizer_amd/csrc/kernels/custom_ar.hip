@@ -146,8 +146,10 @@ __global__ __launch_bounds__(256) void ar_oneshot_kernel(Peers peers, int rank, 
 // Push-mode fused all-reduce + residual add + RMSNorm (the row-parallel o / down projections of a
 // TP decode step).  One block per row r of the [T, D] output:
 //   1. v = sum_s parts[s][r]                   -- this rank's split-K slabs, fp32, in registers
-//   2. store v into push[(epoch & 1)][me][r] of EVERY rank   -- remote stores over xGMI (posted:
-//      no round trip, unlike reading the peers' copies)
+//   2. store bf16(v) into push[(epoch & 1)][me][r] of EVERY rank   -- remote stores over xGMI
+//      (posted: no round trip, unlike reading the peers' copies).  The payload is bf16 (like a
+//      Megatron bf16 all-reduce): a push sends T x D x (world - 1) elements per rank, so at decode
+//      batches of ~40 rows the xGMI links, not the latency, bound an fp32 payload.
 //   3. release fence (system scope), then flag[r][me] = epoch on every rank
 //   4. wait until my flag[r][p] >= epoch for all p, acquire
 //   5. a = sum_p push[(epoch & 1)][p][r] in rank order from LOCAL memory (every rank adds the same
@@ -186,13 +188,16 @@ __global__ __launch_bounds__(256) void ar_add_rmsnorm_kernel(Peers peers, int ra
     __syncthreads();
     const unsigned epoch = s_epoch;
     const size_t region = push_off(slot_bytes) + (size_t)(epoch & 1) * world * slot_bytes;
-    const size_t mine_off = region + (size_t)rank * slot_bytes + (size_t)row * D * 4;
+    const size_t mine_off = region + (size_t)rank * slot_bytes + (size_t)row * D * 2;
+    uint2 pv[VPT];
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) pv[i] = make_uint2(pack2(v[i].x, v[i].y), pack2(v[i].z, v[i].w));
     for (int p = 0; p < world; ++p) {
-        float4* dst = reinterpret_cast<float4*>(peers.base[p] + mine_off);
+        uint2* dst = reinterpret_cast<uint2*>(peers.base[p] + mine_off);
 #pragma unroll
         for (int i = 0; i < VPT; ++i) {
             const int c = tid + i * 256;
-            if (c < nv) dst[c] = v[i];
+            if (c < nv) dst[c] = pv[i];
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -210,7 +215,7 @@ __global__ __launch_bounds__(256) void ar_add_rmsnorm_kernel(Peers peers, int ra
     }
     __syncthreads();
     // 5 + 6: rank-ordered sum from local memory, residual add (bf16 rounding), RMSNorm
-    const char* base = peers.base[rank] + region + (size_t)row * D * 4;
+    const char* base = peers.base[rank] + region + (size_t)row * D * 2;
     bf16* rrow = residual + (size_t)row * D;
     float ss = 0.f;
     float x[VPT][4];
@@ -220,8 +225,11 @@ __global__ __launch_bounds__(256) void ar_add_rmsnorm_kernel(Peers peers, int ra
         if (c < nv) {
             float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
             for (int p = 0; p < world; ++p) {
-                const float4 a = reinterpret_cast<const float4*>(base + (size_t)p * slot_bytes)[c];
-                acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+                const uint2 a = reinterpret_cast<const uint2*>(base + (size_t)p * slot_bytes)[c];
+                acc.x += __uint_as_float(a.x << 16);
+                acc.y += __uint_as_float(a.x & 0xffff0000u);
+                acc.z += __uint_as_float(a.y << 16);
+                acc.w += __uint_as_float(a.y & 0xffff0000u);
             }
             const uint2 rv = reinterpret_cast<const uint2*>(rrow)[c];
             x[i][0] = (float)(bf16)(__uint_as_float(rv.x << 16) + acc.x);
@@ -336,12 +344,12 @@ MRSUM_API int mrsum_ar_allreduce_max_u64(void* hv, const void* in, void* out, si
 
 
 // residual[T, D] += all-reduce(sum_s parts[s]) ; out = rmsnorm(residual) * w   (push-mode, see above)
-// parts fp32 [S, T, D]; residual, w, out bf16; T <= 256, T * D * 4 <= max_bytes, D % 4 == 0, D <= 8192
+// parts fp32 [S, T, D]; residual, w, out bf16; T <= 256, T * D * 2 <= max_bytes, D % 4 == 0, D <= 8192
 MRSUM_API int mrsum_ar_add_rmsnorm(void* hv, const void* parts, int S, int T, void* residual, const void* w,
                                    void* out, int D, int out_stride, float eps, hipStream_t s) {
     auto h = (ArHandle*)hv;
     if (T <= 0) return 0;
-    if (S < 1 || T > MAX_ROWS || D % 4 || D > 8192 || (size_t)T * D * 4 > h->max_bytes) return (int)hipErrorInvalidValue;
+    if (S < 1 || T > MAX_ROWS || D % 4 || D > 8192 || (size_t)T * D * 2 > h->max_bytes) return (int)hipErrorInvalidValue;
     for (int r = 0; r < h->world; ++r)
         if (!h->peers.base[r]) return (int)hipErrorInvalidValue;
     const int vpt = (D / 4 + 255) / 256;

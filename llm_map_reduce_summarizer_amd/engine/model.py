@@ -65,7 +65,7 @@ class _TPReduce:
     def fused_ok(self, rows: int, hidden: int) -> bool:
         ar = self.model.custom_ar
         return self.fused and rows <= ar.MAX_ROWS and hidden % 4 == 0 and hidden <= 8192 and \
-            rows * hidden * 4 <= ar.max_bytes
+            rows * hidden * 2 <= ar.max_bytes
 
     def add_rmsnorm(self, parts, residual, ln, eps):
         return self.model.custom_ar.add_rmsnorm(parts, residual, ln, eps)

@@ -201,11 +201,11 @@ class LocalEngineProvider(Provider):
             if ar is None or self.parallel != "auto":
                 self.hw = plan.with_measurements(hw, tp_ok=ar is not None)
                 return self.hw
-            lat = ar.measure_latency(rows=16, hidden=eng.cfg.hidden)
+            lat, per_row = ar.measure_latency(rows=(1, 64), hidden=eng.cfg.hidden)
             bw = _rccl_bandwidth(eng.model.tp_group, eng.cfg.hidden, torch.device(self._device))
-            self.hw = plan.with_measurements(hw, ar_lat_s=lat, ar_bw=bw, tp_ok=True)
-            log.info("planner constants: all-reduce latency %.1f us (fused, over the local add_rmsnorm), RCCL "
-                     "all-reduce %.1f GB/s", lat * 1e6, bw / 1e9)
+            self.hw = plan.with_measurements(hw, ar_lat_s=lat, ar_lat_row_s=per_row, ar_bw=bw, tp_ok=True)
+            log.info("planner constants: all-reduce %.1f us + %.3f us/row (fused, over the local add_rmsnorm), "
+                     "RCCL all-reduce %.1f GB/s", lat * 1e6, per_row * 1e6, bw / 1e9)
         return self.hw
 
     def _stage_tp(self, stage: str, prompts: Sequence[Sequence[int]], reqs: Sequence[GenRequest]) -> int:
@@ -336,7 +336,9 @@ class LocalEngineProvider(Provider):
         if self.stage_plan:
             s["stage_plan"] = dict(self.stage_plan)
         if self.hw is not None:
-            s["planner_hw"] = {"ar_lat_us": round(self.hw.ar_lat_s * 1e6, 2), "ar_gbps": round(self.hw.ar_bw / 1e9, 1)}
+            s["planner_hw"] = {"ar_lat_us": round(self.hw.ar_lat_s * 1e6, 2),
+                               "ar_us_per_row": round(self.hw.ar_lat_row_s * 1e6, 4),
+                               "ar_gbps": round(self.hw.ar_bw / 1e9, 1)}
         if self._engine is not None:
             s.update(self._engine.engine_stats())
         if self._reduce_engine is not None:

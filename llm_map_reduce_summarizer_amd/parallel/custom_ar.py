@@ -8,10 +8,10 @@ inside a hipGraph.  Handles are exchanged once through the group (any backend); 
 than ``max_bytes`` or non-fp32 tensors go to ``torch.distributed.all_reduce`` (RCCL).
 
 The decode projections use a second, *push-mode* kernel (``add_rmsnorm``): every rank sums its own
-split-K slabs, writes the row straight into every peer's buffer (posted remote stores -- no remote
-read round trip), flags, and then reduces the rows from LOCAL memory in rank order, adds the
-residual and applies the RMSNorm -- the all-reduce, the split-K reduction and the add_rmsnorm
-kernel of the TP=1 graph in one launch.
+split-K slabs, writes the row (bf16 payload) straight into every peer's buffer (posted remote stores
+-- no remote read round trip), flags, and then reduces the rows from LOCAL memory in rank order in
+fp32, adds the residual and applies the RMSNorm -- the all-reduce, the split-K reduction and the
+add_rmsnorm kernel of the TP=1 graph in one launch.
 
 The reference has no collective of any kind (its only "communication" is HTTPS, reference
 llm_executor.py:290-297); this is the MI355X replacement for the TP reduce path it implies.
@@ -61,8 +61,8 @@ class CustomAllReduce:
 
     def __init__(self, group=None, max_bytes: int = 4 << 20):
         """``max_bytes`` bounds one message: the one-shot kernel takes at most 1 MiB of it, the fused
-        add_rmsnorm (push mode) the whole: 256 decode rows of Llama-3-8B (16 KiB of fp32 each), 128
-        of Llama-3-70B."""
+        add_rmsnorm (push mode, bf16 rows of 8 KiB for Llama-3-8B, 16 KiB for Llama-3-70B) its
+        MAX_ROWS = 256 rows."""
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -112,7 +112,7 @@ class CustomAllReduce:
         if not (parts.is_cuda and parts.dtype == torch.float32 and parts.is_contiguous() and parts.dim() == 3):
             return False
         _, T, D = parts.shape
-        return T <= self.MAX_ROWS and D % 4 == 0 and D <= 8192 and T * D * 4 <= self.max_bytes
+        return T <= self.MAX_ROWS and D % 4 == 0 and D <= 8192 and T * D * 2 <= self.max_bytes
 
     def add_rmsnorm(self, parts: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -235,47 +235,55 @@ class CustomAllReduce:
             ok &= check()
         return ok
 
-    def measure_latency(self, rows: int = 16, hidden: int = 4096, calls: int = 64, reps: int = 3) -> float:
-        """Seconds per fused all-reduce + add_rmsnorm call MINUS a local add_rmsnorm_parts call (what a
-        TP decode step pays per all-reduce over the TP=1 graph), both timed inside replayed hipGraphs.
-        MAX over the ranks, so every rank plans with the same number."""
+    def measure_latency(self, rows=(1, 64), hidden: int = 4096, calls: int = 64, reps: int = 3):
+        """(a, b): a fused all-reduce + add_rmsnorm call costs a + b * rows seconds MORE than the local
+        add_rmsnorm_parts it replaces in a TP=1 graph (least squares over ``rows``; both timed inside
+        replayed hipGraphs).  MAX over the ranks, so every rank plans with the same numbers."""
         from ..ops import hip
         dev = torch.device("cuda", torch.cuda.current_device())
-        rows = max(1, min(rows, self.max_bytes // (hidden * 4), self.MAX_ROWS))
-        parts = torch.zeros(1, rows, hidden, device=dev)
-        res = torch.zeros(rows, hidden, dtype=torch.bfloat16, device=dev)
-        w = torch.ones(hidden, dtype=torch.bfloat16, device=dev)
-        out = torch.empty_like(res)
+        pts = []
+        for r in rows:
+            r = max(1, min(int(r), self.max_bytes // (hidden * 2), self.MAX_ROWS))
+            parts = torch.zeros(1, r, hidden, device=dev)
+            res = torch.zeros(r, hidden, dtype=torch.bfloat16, device=dev)
+            w = torch.ones(hidden, dtype=torch.bfloat16, device=dev)
+            out = torch.empty_like(res)
 
-        def timed(fn) -> float:
-            s = torch.cuda.Stream(device=dev)
-            s.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.stream(s):
-                fn()
-            torch.cuda.synchronize(dev)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s):
-                for _ in range(calls):
+            def timed(fn) -> float:
+                s = torch.cuda.Stream(device=dev)
+                s.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.stream(s):
                     fn()
-            g.replay()
-            torch.cuda.synchronize(dev)
-            best = float("inf")
-            for _ in range(reps):
-                dist.barrier(group=self.group)
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                g.replay()
-                e1.record()
                 torch.cuda.synchronize(dev)
-                best = min(best, e0.elapsed_time(e1) / 1000.0 / calls)
-            return best
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, stream=s):
+                    for _ in range(calls):
+                        fn()
+                g.replay()
+                torch.cuda.synchronize(dev)
+                best = float("inf")
+                for _ in range(reps):
+                    dist.barrier(group=self.group)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    g.replay()
+                    e1.record()
+                    torch.cuda.synchronize(dev)
+                    best = min(best, e0.elapsed_time(e1) / 1000.0 / calls)
+                return best
 
-        t_ar = timed(lambda: self.add_rmsnorm(parts, res, w, 1e-5, out))
-        t_local = timed(lambda: hip.add_rmsnorm_parts(parts, res, w, 1e-5, out))
-        v = torch.tensor([max(0.0, t_ar - t_local)], dtype=torch.float64,
-                         device=dev if dist.get_backend(self.group) == "nccl" else "cpu")
+            t_ar = timed(lambda: self.add_rmsnorm(parts, res, w, 1e-5, out))
+            t_local = timed(lambda: hip.add_rmsnorm_parts(parts, res, w, 1e-5, out))
+            pts.append((r, max(0.0, t_ar - t_local)))
+        n = len(pts)
+        mx = sum(p[0] for p in pts) / n
+        my = sum(p[1] for p in pts) / n
+        var = sum((p[0] - mx) ** 2 for p in pts)
+        b = max(0.0, sum((p[0] - mx) * (p[1] - my) for p in pts) / var) if var else 0.0
+        a = max(0.0, my - b * mx)
+        v = torch.tensor([a, b], dtype=torch.float64, device=dev if dist.get_backend(self.group) == "nccl" else "cpu")
         dist.all_reduce(v, op=dist.ReduceOp.MAX, group=self.group)
-        return float(v.item())
+        return float(v[0].item()), float(v[1].item())
 
     def error(self) -> int:
         """Non-zero if a wait for a peer timed out (the result of that call is garbage)."""

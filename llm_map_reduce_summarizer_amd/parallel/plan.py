@@ -18,9 +18,10 @@ node, so the choice is a cost model whose hardware constants are *measured*:
 * ``hbm_bw``, ``step_floor_s``, ``prefill_flops``: single-GPU decode/prefill measurements of the
   engine (profiles/r1_decode_step_latency.log: B=1/5/10/39 at 4k context fit
   t = (W + B ctx kv) / 5.4 TB/s + 0.96 ms to within 3 %; prefill 72k tok/s of Llama-3-8B);
-* ``ar_lat_s`` and ``ar_bw``: timed at start-up on the job's own GPUs (the custom all-reduce
-  inside a replayed hipGraph; one RCCL all-reduce of a prefill-sized activation), MAX-reduced over
-  the ranks so every rank takes the same decision.
+* ``ar_lat_s`` / ``ar_lat_row_s`` and ``ar_bw``: timed at start-up on the job's own GPUs (the fused
+  all-reduce inside a replayed hipGraph at 1 and 64 rows -- a latency and a per-row link cost; one
+  RCCL all-reduce of a prefill-sized activation), MAX-reduced over the ranks so every rank takes
+  the same decision.
 
 A TP stage may also prefill *disaggregated* (``handoff``): data-parallel on every rank's full
 TP=1 engine, then one all-to-all moves each prompt's KV heads to their TP owner -- the KV of a
@@ -43,7 +44,8 @@ class HWModel:
     hbm_bw: float = 5.4e12          # bytes/s streamed by the decode GEMM + attention kernels
     step_floor_s: float = 0.96e-3   # fixed per-step cost of the decode graph (kernel latencies), 32 layers
     prefill_flops: float = 1.1e15   # effective prefill FLOP/s (hipBLASLt GEMMs + flash attention)
-    ar_lat_s: float = 20e-6         # one decode all-reduce (custom P2P kernel), measured at start-up
+    ar_lat_s: float = 20e-6         # one decode all-reduce (custom P2P kernel), measured at start-up ...
+    ar_lat_row_s: float = 0.0       # ... plus this per decode row (the push sends every row to every peer)
     ar_bw: float = 100e9            # RCCL all-reduce algorithm bandwidth (bytes/s), measured at start-up
     tp_ok: bool = True              # False when the TP engine has no graph-safe all-reduce
 
@@ -70,7 +72,7 @@ def decode_step_s(d: ModelDims, hw: HWModel, batch: int, ctx: float, tp: int) ->
         return 0.0
     stream = (d.weight_bytes + batch * ctx * d.kv_bytes_per_token) / tp / hw.hbm_bw
     floor = hw.step_floor_s * d.n_layers / 32.0
-    comm = (2 * d.n_layers + 1) * hw.ar_lat_s if tp > 1 else 0.0
+    comm = (2 * d.n_layers + 1) * (hw.ar_lat_s + hw.ar_lat_row_s * batch) if tp > 1 else 0.0
     return stream + floor + comm
 
 
@@ -142,10 +144,12 @@ def choose(d: ModelDims, hw: HWModel, prompt_lens: Sequence[int], max_new: Seque
     return {"tp": best, "estimates_s": {str(k): round(v, 3) for k, v in est.items()}}
 
 
-def with_measurements(hw: HWModel, ar_lat_s=None, ar_bw=None, tp_ok=None) -> HWModel:
+def with_measurements(hw: HWModel, ar_lat_s=None, ar_bw=None, tp_ok=None, ar_lat_row_s=None) -> HWModel:
     kw = {}
     if ar_lat_s is not None:
         kw["ar_lat_s"] = float(ar_lat_s)
+    if ar_lat_row_s is not None:
+        kw["ar_lat_row_s"] = float(ar_lat_row_s)
     if ar_bw is not None:
         kw["ar_bw"] = float(ar_bw)
     if tp_ok is not None:

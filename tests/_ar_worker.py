@@ -87,9 +87,9 @@ def main():
         expect = 1.0 + S * sum(r + 1 + it for r in range(world))
         assert torch.equal(res, torch.full_like(res, expect)), "fused graph replay %d" % it
     assert ar.self_test()
-    lat = ar.measure_latency(rows=16, hidden=4096)
-    print("rank %d fused all-reduce latency over local add_rmsnorm: %.2f us (2 ranks sharing one GPU)"
-          % (rank, lat * 1e6), flush=True)
+    lat, per_row = ar.measure_latency(rows=(1, 64), hidden=4096)
+    print("rank %d fused all-reduce cost over local add_rmsnorm: %.2f us + %.4f us/row (2 ranks sharing one GPU)"
+          % (rank, lat * 1e6, per_row * 1e6), flush=True)
     assert ar.error() == 0
     dist.barrier()
     ar.close()

@@ -64,3 +64,12 @@ def test_choice_is_deterministic(world):
     a = plan.choose(D8B, hw, pl, [1000] * 23, world)
     b = plan.choose(D8B, hw, list(pl), [1000] * 23, world)
     assert a == b
+
+
+def test_per_row_all_reduce_cost_penalises_big_tp_batches():
+    base = plan.with_measurements(plan.HWModel(), ar_lat_s=8e-6)
+    rowy = plan.with_measurements(base, ar_lat_row_s=0.25e-6)
+    a = plan.decode_step_s(D8B, base, 48, 4000, 8)
+    b = plan.decode_step_s(D8B, rowy, 48, 4000, 8)
+    assert abs((b - a) - 65 * 48 * 0.25e-6) < 1e-12
+    assert plan.decode_step_s(D8B, rowy, 48, 4000, 1) == plan.decode_step_s(D8B, base, 48, 4000, 1)
