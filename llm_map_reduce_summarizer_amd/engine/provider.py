@@ -208,27 +208,28 @@ class LocalEngineProvider(Provider):
                      "RCCL all-reduce %.1f GB/s", lat * 1e6, per_row * 1e6, bw / 1e9)
         return self.hw
 
-    def _stage_tp(self, stage: str, prompts: Sequence[Sequence[int]], reqs: Sequence[GenRequest]) -> int:
-        """TP degree for this stage's generate: 1 (DP replicas) or world (one sharded engine)."""
+    def _stage_tp(self, stage: str, prompts: Sequence[Sequence[int]], reqs: Sequence[GenRequest]):
+        """(TP degree, disaggregated prefill?) for this stage's generate: TP 1 = DP replicas, world = one
+        sharded engine."""
         world = self.par.world
         if self.parallel != "dp":
             _ = self.reduce_engine  # may fall back to dp (no P2P all-reduce on this node)
         if self.parallel == "dp" or not reqs:
-            return 1
+            return 1, False
         if self.parallel == "tp":
-            return world
+            return world, self.handoff and len(reqs) > 1
         if self.parallel == "reduce_tp":
-            return 1 if stage == "map" else world
+            return (1, False) if stage == "map" else (world, self.handoff and len(reqs) > 1)
         from ..parallel import plan
         hw = self._measure()
         if self.parallel != "auto":  # _measure found no P2P all-reduce and fell back to dp
-            return 1
+            return 1, False
         d = plan.ModelDims.of(self.model_config(),
                               1.0 if self._engine_options.get("weight_dtype") == "fp8" else 2.0)
         choice = plan.choose(d, hw, [len(p) for p in prompts], [r.max_tokens for r in reqs], world,
                              handoff=self.handoff)
         self.stage_plan[stage] = choice
-        return int(choice["tp"])
+        return int(choice["tp"]), bool(choice.get("handoff", False))
 
     def _handoff(self, prompts: Sequence[Sequence[int]], sp) -> Dict[int, Any]:
         """Disaggregated prefill for a TP stage: every rank prefills its LPT share of the prompts on
@@ -286,12 +287,12 @@ class LocalEngineProvider(Provider):
         t0 = time.perf_counter()
         prompts = [self.encode_request(r) for r in reqs]
         stage = reqs[0].stage if reqs else "map"
-        tp = self._stage_tp(stage, prompts, reqs) if self.par.world > 1 and self.tp == 1 else 1
-        self.stage_plan.setdefault(stage, {"tp": tp})
+        tp, handoff = self._stage_tp(stage, prompts, reqs) if self.par.world > 1 and self.tp == 1 else (1, False)
+        self.stage_plan.setdefault(stage, {"tp": tp, "handoff": handoff})
         if tp > 1:
             # every rank runs every request on the TP engine; the TP ranks sample identically
             sp = [SamplingParams(r.max_tokens, r.temperature, _req_seed(self.seed, r)) for r in reqs]
-            imported = self._handoff(prompts, sp) if self.handoff else None
+            imported = self._handoff(prompts, sp) if handoff else None
             outs = self.reduce_engine.generate(prompts, sp, ignore_eos=self.ignore_eos, imported=imported)
             self.timings["generate_s"] += time.perf_counter() - t0
             return [GenResult(self.tokenizer.decode(o.token_ids), o.prompt_len, len(o.token_ids), 0.0,

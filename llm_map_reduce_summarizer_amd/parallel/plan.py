@@ -118,7 +118,9 @@ def stage_seconds(d: ModelDims, hw: HWModel, prompt_lens: Sequence[int], max_new
             continue
         pl = [prompt_lens[i] for i in idx]
         mn = [max_new[i] for i in idx]
-        t = handoff_prefill_s(d, hw, pl, world) if use_handoff else prefill_s(d, hw, sum(pl), tp)
+        t = prefill_s(d, hw, sum(pl), tp)
+        if use_handoff:  # the cheaper of the TP forward and the disaggregated prefill
+            t = min(t, handoff_prefill_s(d, hw, pl, world))
         # sequences retire as they reach their max_new: walk the decode in segments of equal batch
         order = sorted(range(len(idx)), key=lambda k: mn[k])
         done = 0
@@ -141,7 +143,13 @@ def choose(d: ModelDims, hw: HWModel, prompt_lens: Sequence[int], max_new: Seque
         cands = [1]
     est = {tp: stage_seconds(d, hw, prompt_lens, max_new, tp, world, handoff) for tp in cands}
     best = min(cands, key=lambda tp: (est[tp], tp))
-    return {"tp": best, "estimates_s": {str(k): round(v, 3) for k, v in est.items()}}
+    out = {"tp": best, "estimates_s": {str(k): round(v, 3) for k, v in est.items()}}
+    if best > 1 and best == world:
+        # disaggregated prefill only where it beats the TP forward: many prompts split over the ranks
+        # win, one long prompt (the final reduce) prefills faster as one TP forward over all GPUs
+        out["handoff"] = bool(handoff) and handoff_prefill_s(d, hw, prompt_lens, world) < \
+            prefill_s(d, hw, sum(prompt_lens), world)
+    return out
 
 
 def with_measurements(hw: HWModel, ar_lat_s=None, ar_bw=None, tp_ok=None, ar_lat_row_s=None) -> HWModel:

@@ -73,3 +73,14 @@ def test_per_row_all_reduce_cost_penalises_big_tp_batches():
     b = plan.decode_step_s(D8B, rowy, 48, 4000, 8)
     assert abs((b - a) - 65 * 48 * 0.25e-6) < 1e-12
     assert plan.decode_step_s(D8B, rowy, 48, 4000, 1) == plan.decode_step_s(D8B, base, 48, 4000, 1)
+
+
+def test_handoff_for_many_prompts_tp_forward_for_one():
+    hw = plan.with_measurements(plan.HWModel(), ar_lat_s=8e-6, ar_bw=150e9)
+    many = plan.choose(D8B, hw, [3950] * 39, [1000] * 39, 8, handoff=True)
+    one = plan.choose(D8B, hw, [23000], [1000], 8, handoff=True)
+    assert many["tp"] == 8 and many["handoff"] is True
+    assert one["tp"] == 8 and one["handoff"] is False
+    # the handoff option never makes a TP stage look more expensive
+    assert plan.stage_seconds(D8B, hw, [3950] * 39, [1000] * 39, 8, 8, True) <= \
+        plan.stage_seconds(D8B, hw, [3950] * 39, [1000] * 39, 8, 8, False)
