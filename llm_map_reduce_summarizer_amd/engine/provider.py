@@ -181,14 +181,19 @@ class LocalEngineProvider(Provider):
                 self.parallel, self.reduce_tp, self._dp_needed = "dp", False, True
         return self._reduce_engine
 
-    def warm(self) -> None:
-        """Build the engines (and measure the planner's constants) outside any timed region."""
+    def warm(self, capture_batch: Optional[int] = None) -> None:
+        """Build the engines (and measure the planner's constants) outside any timed region; with
+        ``capture_batch``, also capture the decode graphs of every batch bucket up to it."""
         if self.reduce_tp:
             _ = self.reduce_engine
             if self.parallel == "auto":
                 self._measure()
+            if capture_batch and self.reduce_tp:
+                self._reduce_engine.capture_graphs(capture_batch)
         if self._dp_needed:
             _ = self.engine
+            if capture_batch and self.parallel in ("dp", "auto", "reduce_tp"):
+                self._engine.capture_graphs(-(-capture_batch // self.par.dp))
 
     def _measure(self):
         """plan.HWModel with the all-reduce latency / bandwidth of THIS job's GPUs (auto mode)."""
