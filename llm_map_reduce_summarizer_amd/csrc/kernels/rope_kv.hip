@@ -4,7 +4,7 @@
 // qkv      [T, row_stride] bf16: per token [Hq*D | Hkv*D | Hkv*D]; Q and K are
 //          rotated IN PLACE (prefill attention reads them back from here),
 //          rotated K and raw V are also scattered into the paged cache.
-// positions[T] int32, seq_idx[T] int32 (row of block_tables for the token),
+// positions[T] int32, seq_idx[T] int32 (row of block_tables for the token; < 0: not cached),
 // block_tables [*, bt_stride] int32 page ids,
 // cache    K and V: [num_pages, Hkv, P, D] bf16 (one page = P consecutive
 //          positions of one kv head: 16 KiB at P=64, D=128, so a decode
@@ -78,6 +78,8 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
     }
     bf16* row = qkv_out + (size_t)t * row_stride;
     size_t page_base = 0;
+    // seq_idx < 0: a padding token of the prefill batch (engine._prefill) -- rotated, never cached
+    write_cache = write_cache && seq_idx[t] >= 0;
     if (write_cache) {
         const int page = block_tables[(size_t)seq_idx[t] * bt_stride + pos / P];
         page_base = (size_t)page * Hkv * P + (pos % P);

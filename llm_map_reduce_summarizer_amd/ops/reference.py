@@ -65,10 +65,11 @@ def rope_kv(qkv: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, b
     qkv[:, : (hq + hkv) * d] = rot.reshape(T, -1)
     if write_cache:
         rows = seq_idx[:T].long()
-        pages = block_tables[rows, pos // page].long()
-        offs = pos % page
-        k = rot[:, hq:]
-        v = qkv[:, (hq + hkv) * d: (hq + 2 * hkv) * d].view(T, hkv, d)
+        keep = rows >= 0  # seq_idx < 0: prefill padding token, never cached
+        rows, p_, k = rows[keep], pos[keep], rot[:, hq:][keep]
+        pages = block_tables[rows, p_ // page].long()
+        offs = p_ % page
+        v = qkv[:, (hq + hkv) * d: (hq + 2 * hkv) * d].view(T, hkv, d)[keep]
         kcache[pages, :, offs] = k
         vcache[pages, :, offs] = v
 

@@ -66,3 +66,22 @@ def test_many_sequences_compaction(eng):
     outs = eng.generate(prompts, sp)
     assert [len(o.token_ids) for o in outs] == [s.max_new_tokens for s in sp]
     assert eng.kv.alloc.available() == eng.kv.num_pages - 1
+
+
+def test_padded_prefill_matches_unpadded(eng):
+    """Prefill batches padded to a multiple of 4096 tokens (a never-cached padding sequence) generate
+    what the unpadded batch generates."""
+    prompts = [[128000] + [(i * 53 + j * 7) % 120000 + 5 for j in range(n)] for i, n in enumerate((1500, 1200, 1100))]
+    T = sum(len(p) for p in prompts)
+    assert eng._prefill_pad(T) == 4096  # 3803 tokens -> one 293-token padding sequence
+    sp = [SamplingParams(8, 0.0, 0)] * len(prompts)
+    pad0 = eng.stats.get("prefill_pad_tokens", 0)
+    a = eng.generate(prompts, sp)
+    assert eng.stats.get("prefill_pad_tokens", 0) - pad0 == 4096 - T
+    eng.pad_prefill = False
+    try:
+        b = eng.generate(prompts, sp)
+    finally:
+        eng.pad_prefill = True
+    same = sum(x.token_ids == y.token_ids for x, y in zip(a, b))
+    assert same >= len(prompts) - 1  # a bf16 near-tie may flip one sequence
