@@ -103,16 +103,16 @@ class LocalEngineProvider(Provider):
         if parallel == "auto" and not torch.cuda.is_available():
             parallel = "dp"  # the planner's constants are GPU measurements
         self.parallel = parallel if multi else "dp"
-        self.reduce_tp = self.parallel != "dp"  # a TP=world engine exists for some stage
-        self._reduce_engine = None
+        self.use_tp_engine = self.parallel != "dp"  # a TP=world engine exists for some stage
+        self._tp_engine = None
         self._dp_needed = self.parallel != "tp"
         self.hw = None  # plan.HWModel with this job's measured all-reduce constants (auto mode)
         # TP stages prefill data-parallel on the TP=1 engines and move the KV with one all-to-all
-        self.handoff = self.reduce_tp and os.environ.get("MRSUM_HANDOFF", "1") == "1"
+        self.handoff = self.use_tp_engine and os.environ.get("MRSUM_HANDOFF", "1") == "1"
         if self.handoff:
             self._dp_needed = True
         self.stage_plan: Dict[str, Any] = {}
-        if self.reduce_tp:
+        if self.use_tp_engine:
             self._engine_options.setdefault("kv_fraction", float(os.environ.get("MRSUM_DP_KV_FRACTION", "0.5")))
 
     def _tp_world_ok(self) -> bool:
@@ -156,9 +156,9 @@ class LocalEngineProvider(Provider):
         return self._engine
 
     @property
-    def reduce_engine(self):
+    def tp_engine(self):
         """TP=world engine of the same model/seed (the ``tp`` engine of the module docstring)."""
-        if self._reduce_engine is None:
+        if self._tp_engine is None:
             import torch
             from .engine import LLMEngine
             world = self.par.world
@@ -170,26 +170,29 @@ class LocalEngineProvider(Provider):
             if self._device is None:
                 self._device = ("cuda:%d" % (self.par.local_rank % max(1, torch.cuda.device_count()))
                                 if torch.cuda.is_available() else "cpu")
-            self._reduce_engine = LLMEngine(self.model_config(), device=self._device, seed=self.seed,
+            self._tp_engine = LLMEngine(self.model_config(), device=self._device, seed=self.seed,
                                             tp_rank=self.par.rank, tp_size=world,
                                             tp_group=pdist.tp_group_for(world), **opts)
             log.info("TP engine up: %s TP=%d", self.model, world)
-            if self._reduce_engine.model.custom_ar is None and torch.cuda.is_available() \
+            if self._tp_engine.model.custom_ar is None and torch.cuda.is_available() \
                     and self.parallel in ("auto", "reduce_tp"):
-                # every rank built the same engine and got the same collective verdict
+                # every rank built the same engine and got the same collective verdict: drop it (its
+                # decode could not run in hipGraphs) and keep every stage data-parallel
                 log.warning("no P2P all-reduce for the TP engine: every stage stays data-parallel")
-                self.parallel, self.reduce_tp, self._dp_needed = "dp", False, True
-        return self._reduce_engine
+                self.parallel, self.use_tp_engine, self._dp_needed = "dp", False, True
+                self._tp_engine = None
+                torch.cuda.empty_cache()
+        return self._tp_engine
 
     def warm(self, capture_batch: Optional[int] = None) -> None:
         """Build the engines (and measure the planner's constants) outside any timed region; with
         ``capture_batch``, also capture the decode graphs of every batch bucket up to it."""
-        if self.reduce_tp:
-            _ = self.reduce_engine
+        if self.use_tp_engine:
+            _ = self.tp_engine
             if self.parallel == "auto":
                 self._measure()
-            if capture_batch and self.reduce_tp:
-                self._reduce_engine.capture_graphs(capture_batch)
+            if capture_batch and self.use_tp_engine:
+                self._tp_engine.capture_graphs(capture_batch)
         if self._dp_needed:
             _ = self.engine
             if capture_batch and self.parallel in ("dp", "auto", "reduce_tp"):
@@ -201,7 +204,7 @@ class LocalEngineProvider(Provider):
             import torch
             from ..parallel import plan
             hw = plan.HWModel()
-            eng = self.reduce_engine
+            eng = self.tp_engine
             ar = eng.model.custom_ar if eng is not None else None
             if ar is None or self.parallel != "auto":
                 self.hw = plan.with_measurements(hw, tp_ok=ar is not None)
@@ -218,7 +221,7 @@ class LocalEngineProvider(Provider):
         sharded engine."""
         world = self.par.world
         if self.parallel != "dp":
-            _ = self.reduce_engine  # may fall back to dp (no P2P all-reduce on this node)
+            _ = self.tp_engine  # may fall back to dp (no P2P all-reduce on this node)
         if self.parallel == "dp" or not reqs:
             return 1, False
         if self.parallel == "tp":
@@ -252,7 +255,7 @@ class LocalEngineProvider(Provider):
         mine = [i for i in range(len(prompts)) if owner[i] == rank]
         firsts, packs = self.engine.prefill_export([prompts[i] for i in mine], [sp[i] for i in mine], world,
                                                    ignore_eos=self.ignore_eos)
-        tp_eng = self.reduce_engine
+        tp_eng = self.tp_engine
         shapes = [tp_eng.import_shape(len(p)) for p in prompts]
         numel = [math.prod(s) for s in shapes]
         recv_sizes = [sum(numel[i] for i in range(len(prompts)) if owner[i] == s) for s in range(world)]
@@ -298,7 +301,7 @@ class LocalEngineProvider(Provider):
             # every rank runs every request on the TP engine; the TP ranks sample identically
             sp = [SamplingParams(r.max_tokens, r.temperature, _req_seed(self.seed, r)) for r in reqs]
             imported = self._handoff(prompts, sp) if handoff else None
-            outs = self.reduce_engine.generate(prompts, sp, ignore_eos=self.ignore_eos, imported=imported)
+            outs = self.tp_engine.generate(prompts, sp, ignore_eos=self.ignore_eos, imported=imported)
             self.timings["generate_s"] += time.perf_counter() - t0
             return [GenResult(self.tokenizer.decode(o.token_ids), o.prompt_len, len(o.token_ids), 0.0,
                               extra={"finish_reason": o.finish_reason}) for o in outs]
@@ -347,8 +350,8 @@ class LocalEngineProvider(Provider):
                                "ar_gbps": round(self.hw.ar_bw / 1e9, 1)}
         if self._engine is not None:
             s.update(self._engine.engine_stats())
-        if self._reduce_engine is not None:
-            s["reduce_engine"] = self._reduce_engine.engine_stats()
+        if self._tp_engine is not None:
+            s["tp_engine"] = self._tp_engine.engine_stats()
         return s
 
 

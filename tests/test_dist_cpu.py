@@ -146,7 +146,7 @@ def test_dp2_with_tp2_reduce():
 TPALL_SCRIPT = SCRIPT.replace('engine_options={"kv_pages": 512, "max_num_seqs": 16})',
                               'engine_options={"kv_pages": 512, "max_num_seqs": 16}, parallel="tp")').replace(
     '"engine_calls": prov.stats().get("generate_calls", 0)}',
-    '"engine_calls": 0, "imported": prov.stats()["reduce_engine"].get("imported_prefills", 0)}').replace(
+    '"engine_calls": 0, "imported": prov.stats()["tp_engine"].get("imported_prefills", 0)}').replace(
     'LocalEngineProvider("tiny", cfg', 'LocalEngineProvider("tiny-gqa4", cfg')
 
 
