@@ -7,10 +7,10 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -s KILL 60 python3 tools/pmc_kernels.py > gpurun_out/pmc_plain.log 2>&1 || exit $?
 i=0
-for CTRS in "FETCH_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES"; do
+for CTRS in ${PASSES:-"FETCH_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES"}; do
   i=$((i + 1))
   NAME=pmc_pass$i
-  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $CTRS --output-format csv -d /tmp/$NAME -o run -- \
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $(echo $CTRS | tr : " ") --output-format csv -d /tmp/$NAME -o run -- \
     python3 tools/pmc_kernels.py > gpurun_out/$NAME.log 2>&1 || exit $?
   mkdir -p gpurun_out/$NAME
   python3 tools/pmc_summary.py /tmp/$NAME > gpurun_out/$NAME/summary.txt 2>&1
