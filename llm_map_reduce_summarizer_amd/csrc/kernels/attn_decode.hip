@@ -348,35 +348,60 @@ struct RopeArgs {
     const float2* cos_sin;  // [max_pos, D/2]
 };
 
-// 8 consecutive floats of a token row summed over the SP slabs (batched loads, see rope_kv.hip)
-__device__ __forceinline__ void slab_sum8(const RopeArgs& ra, const float* row, int col, float* f) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = 0.f;
-    for (int s0 = 0; s0 < ra.SP; s0 += 4) {
-        float4 a[4], c[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const float4* p = reinterpret_cast<const float4*>(row + (size_t)min(s0 + u, ra.SP - 1) * ra.slab_stride + col);
-            a[u] = p[0];
-            c[u] = p[1];
+// The fp32 slab sums the ROPE variant needs, by all 256 threads: q of the G heads of kv head ``kvh``
+// (G D floats) and, with ``with_kv``, the new token's K and V rows (D floats each), into ``sq``.
+// Work items = float4 columns x slab subsets (NH subsets when there are fewer than 256 columns), so
+// every thread has its loads in flight at once; the subsets are merged through LDS.
+template <int G>
+__device__ __forceinline__ void rope_slab_sums(const RopeArgs& ra, const float* prow, int kvh, int Hkv, bool with_kv,
+                                               float* sq) {
+    constexpr int D = 128;
+    const int tid = threadIdx.x;
+    const int nq = G * D / 4;                    // q float4 columns
+    const int nv = nq + (with_kv ? 2 * D / 4 : 0);
+    const int nh = nv >= 256 ? 1 : 256 / nv;
+    float4* red = reinterpret_cast<float4*>(sq) + nv;  // [nh][nv] partials after the [nv] result
+    for (int it = tid; it < nv * nh; it += 256) {
+        const int item = it % nv, h = it / nv;
+        int colf;
+        if (item < nq) colf = kvh * G * D + 4 * item;
+        else if (item < nq + D / 4) colf = (ra.hq_total + kvh) * D + 4 * (item - nq);
+        else colf = (ra.hq_total + Hkv + kvh) * D + 4 * (item - nq - D / 4);
+        const float* src = prow + colf;
+        float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+        for (int s2 = h; s2 < ra.SP; s2 += nh) {
+            const float4 v = *reinterpret_cast<const float4*>(src + (size_t)s2 * ra.slab_stride);
+            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            if (s0 + u < ra.SP) {
-                f[0] += a[u].x; f[1] += a[u].y; f[2] += a[u].z; f[3] += a[u].w;
-                f[4] += c[u].x; f[5] += c[u].y; f[6] += c[u].z; f[7] += c[u].w;
-            }
-        }
+        red[it] = acc;
     }
+    __syncthreads();
+    float4* out = reinterpret_cast<float4*>(sq);
+    for (int item = tid; item < nv; item += 256) {
+        float4 acc = red[item];
+        for (int h = 1; h < nh; ++h) {
+            const float4 v = red[h * nv + item];
+            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+        out[item] = acc;
+    }
+    __syncthreads();
 }
 
 template <int G, bool ROPE>
 __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
     const bf16* __restrict__ q, int q_stride, bf16* __restrict__ kc, bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ positions,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int S, float scale_log2, RopeArgs ra) {
+    float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int S, float scale_log2, RopeArgs ra,
+    int* __restrict__ counters, bf16* __restrict__ out, int out_stride) {
     constexpr int D = 128, PG = 64;
     __shared__ __attribute__((aligned(16))) char lds[2 * PG * 256 + 2 * 4 * 16 * 4];
+    __shared__ __attribute__((aligned(16))) bf16 lds_new[2 * D];  // ROPE: the new token's K | V row (bf16)
+    // fused split merge (``counters``): weights [G][MAX_SPLITS] + denominators + last flag, aliasing lds
+    float* c_sw = reinterpret_cast<float*>(lds);
+    float* c_den = c_sw + G * MAX_SPLITS;
+    int* c_last = reinterpret_cast<int*>(c_den + 16);
     char* ldsK = lds;
     char* ldsV = lds + PG * 256;
     float* sm_ml = reinterpret_cast<float*>(lds + 2 * PG * 256);  // [2][4 waves][16 heads]
@@ -395,41 +420,49 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
             part_ml[(ml_base + (size_t)tid * S) * 2 + 0] = -INFINITY;
             part_ml[(ml_base + (size_t)tid * S) * 2 + 1] = 0.f;
         }
+        if (counters) combine_if_last<G>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, c_last, c_sw, c_den);
         return;
     }
     const int ntiles = (ke - ks + PG - 1) / PG;
 
     const float* prow = ROPE ? ra.parts + (size_t)b * ra.width : nullptr;
     const float2* cs = ROPE ? ra.cos_sin + (size_t)(ctx - 1) * (D / 2) : nullptr;
+    // ROPE: the q rows of this group (and, for the split holding the new token, its K and V rows)
+    // summed over the SP slabs by ALL 256 threads in one round of independent loads into an fp32
+    // LDS image (aliasing the K/V tile buffers, which are first written after it is consumed):
+    // q at [0, G D), K at [G D, G D + D), V after it.  A per-lane serial sum cost SP / 4 dependent
+    // L2/MALL round trips per operand (22 us per layer at TP = 8, SP = 16).
+    float* sq = reinterpret_cast<float*>(lds);
+    const bool has_pos = ROPE && ks <= ctx - 1 && ctx - 1 < ke;
     if constexpr (ROPE) {
-        const int pos = ctx - 1;
-        if (ks <= pos && pos < ke) {
-            // the new token's K (rotated) and V row of this kv head -> paged cache, then visible to
-            // this workgroup's page loads below (drain + workgroup barrier); only this split reads
-            // that page in this launch
+        if (has_pos) {
+            rope_slab_sums<G>(ra, prow, kvh, Hkv, true, sq);
+            // the new token's K (rotated) and V row of this kv head -> paged cache for the next steps;
+            // THIS launch never reads it back from memory (no store drain on the critical path): the
+            // staging of the page that holds it patches the row into LDS from the fp32 image
+            // (lds_new); only this split reads that page in this launch
+            const int pos = ctx - 1;
             const int page = block_tables[(size_t)b * bt_stride + pos / PG];
             const size_t dst = ((size_t)page * Hkv * PG + (size_t)kvh * PG + (pos % PG)) * D;
-            if (tid < 8) {
-                const int c = tid * 8;
-                float lo[8], hi[8], rl[8], rh[8];
-                slab_sum8(ra, prow, (ra.hq_total + kvh) * D + c, lo);
-                slab_sum8(ra, prow, (ra.hq_total + kvh) * D + c + D / 2, hi);
+            const float* kr = sq + G * D;
+            if (tid < D / 8) {  // rotated K chunk tid (8 dims), into the cache and the LDS patch row
+                const int c = tid * 8, cl = c & (D / 2 - 1);
+                float kv[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const float2 e = cs[c + j];
-                    rl[j] = lo[j] * e.x - hi[j] * e.y;
-                    rh[j] = hi[j] * e.x + lo[j] * e.y;
+                    const float2 e = cs[cl + j];
+                    const float lo = kr[cl + j], hi = kr[cl + j + D / 2];
+                    kv[j] = c < D / 2 ? lo * e.x - hi * e.y : hi * e.x + lo * e.y;
                 }
-                *reinterpret_cast<uint4*>(kc + dst + c) = pack8(rl);
-                *reinterpret_cast<uint4*>(kc + dst + c + D / 2) = pack8(rh);
-            } else if (tid < 8 + D / 8) {
-                const int c = (tid - 8) * 8;
-                float v[8];
-                slab_sum8(ra, prow, (ra.hq_total + Hkv + kvh) * D + c, v);
-                *reinterpret_cast<uint4*>(vc + dst + c) = pack8(v);
+                const uint4 pk = pack8(kv);
+                *reinterpret_cast<uint4*>(kc + dst + c) = pk;
+                *reinterpret_cast<uint4*>(lds_new + c) = pk;
+            } else if (tid < D / 4) {
+                const int c = (tid - D / 8) * 8;
+                const uint4 pv = pack8(kr + D + c);
+                *reinterpret_cast<uint4*>(vc + dst + c) = pv;
+                *reinterpret_cast<uint4*>(lds_new + D + c) = pv;
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
         }
     }
 
@@ -454,14 +487,12 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
     if constexpr (ROPE) {
         // dims 32k + 8grp + j (k = 0, 1) pair with dims 64 + the same (k = 2, 3): the rotation of a
         // lane's q values needs only the lane's own values
+        if (!has_pos) rope_slab_sums<G>(ra, prow, kvh, Hkv, false, sq);  // overlaps the first page's loads
         float a[4][8];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            if (col < G) slab_sum8(ra, prow, (kvh * G + col) * D + 32 * k + 8 * grp, a[k]);
-            else {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) a[k][j] = 0.f;
-            }
+            for (int j = 0; j < 8; ++j) a[k][j] = col < G ? sq[col * D + 32 * k + 8 * grp + j] : 0.f;
         }
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -483,10 +514,18 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
             qf[k] = __builtin_bit_cast(bf16x8, v);
         }
     }
+    // the new token's row (row pr of tile ptile) is staged from lds_new, not from the page loads
+    const int ptile = has_pos ? (ctx - 1 - ks) / PG : -1;
+    const int pr = (ctx - 1 - ks) % PG;
+    const bool patcher = has_pos && st_row == (pr & 15);
+    if constexpr (ROPE) {
+        __syncthreads();  // every lane has its q out of the fp32 image the tiles overwrite
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        *reinterpret_cast<u32x4*>(ldsK + dk_off(st_row + 16 * i, st_chunk)) = kreg[i];
-        *reinterpret_cast<u32x4*>(ldsV + dv_off(st_row + 16 * i, st_chunk)) = vreg[i];
+        const bool pt = ROPE && ptile == 0 && patcher && i == (pr >> 4);
+        *reinterpret_cast<u32x4*>(ldsK + dk_off(st_row + 16 * i, st_chunk)) = pt ? *reinterpret_cast<const u32x4*>(lds_new + st_chunk * 8) : kreg[i];
+        *reinterpret_cast<u32x4*>(ldsV + dv_off(st_row + 16 * i, st_chunk)) = pt ? *reinterpret_cast<const u32x4*>(lds_new + D + st_chunk * 8) : vreg[i];
     }
 
     f32x4 o[8];
@@ -542,8 +581,9 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
         if (t + 1 < ntiles) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                *reinterpret_cast<u32x4*>(ldsK + dk_off(st_row + 16 * i, st_chunk)) = kreg[i];
-                *reinterpret_cast<u32x4*>(ldsV + dv_off(st_row + 16 * i, st_chunk)) = vreg[i];
+                const bool pt = ROPE && ptile == t + 1 && patcher && i == (pr >> 4);
+                *reinterpret_cast<u32x4*>(ldsK + dk_off(st_row + 16 * i, st_chunk)) = pt ? *reinterpret_cast<const u32x4*>(lds_new + st_chunk * 8) : kreg[i];
+                *reinterpret_cast<u32x4*>(ldsV + dv_off(st_row + 16 * i, st_chunk)) = pt ? *reinterpret_cast<const u32x4*>(lds_new + D + st_chunk * 8) : vreg[i];
             }
             __syncthreads();
         }
@@ -582,11 +622,13 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
             part_ml[pi * 2 + 1] = L;
         }
     }
+    if (counters) combine_if_last<G>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, c_last, c_sw, c_den);
 }
 
 static int launch_mfma(const void* q, int q_stride, const void* kcache, const void* vcache, const int* block_tables,
                        int bt_stride, const int* positions, void* part_o, void* part_ml, void* out, int out_stride,
-                       int B, int Hq, int Hkv, int D, int P, int S, float scale, const RopeArgs* rope, hipStream_t s) {
+                       int B, int Hq, int Hkv, int D, int P, int S, float scale, const RopeArgs* rope, int* counters,
+                       hipStream_t s) {
     if (B <= 0) return 0;
     if (D != 128 || P != 64 || Hq % Hkv || Hq / Hkv > 16 || S < 1 || S > MAX_SPLITS) return (int)hipErrorInvalidValue;
     const int G = Hq / Hkv;
@@ -596,7 +638,8 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
     auto PO = (float*)part_o; auto PM = (float*)part_ml;
     const RopeArgs ra = rope ? *rope : RopeArgs{nullptr, 0, 0, 0, 0, nullptr};
 #define MFMA_L(G_, R_) attn_decode_mfma_kernel<G_, R_><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, \
-                                                                         positions, PO, PM, Hkv, S, sl, ra)
+                                                                         positions, PO, PM, Hkv, S, sl, ra, counters, \
+                                                                         (bf16*)out, out_stride)
 #define MFMA_G(R_)                            \
     switch (G) {                              \
         case 1: MFMA_L(1, R_); break;         \
@@ -610,7 +653,7 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
 #undef MFMA_G
 #undef MFMA_L
     int e = (int)hipGetLastError();
-    if (e) return e;
+    if (e || counters) return e;
     switch (G) {
         case 1: attn_decode_combine_kernel<1><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
         case 2: attn_decode_combine_kernel<2><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
@@ -624,9 +667,9 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
 MRSUM_API int mrsum_attn_decode_mfma(const void* q, int q_stride, const void* kcache, const void* vcache,
                                      const int* block_tables, int bt_stride, const int* positions, void* part_o,
                                      void* part_ml, void* out, int out_stride, int B, int Hq, int Hkv, int D, int P,
-                                     int S, float scale, hipStream_t s) {
+                                     int S, float scale, int* counters, hipStream_t s) {
     return launch_mfma(q, q_stride, kcache, vcache, block_tables, bt_stride, positions, part_o, part_ml, out,
-                       out_stride, B, Hq, Hkv, D, P, S, scale, nullptr, s);
+                       out_stride, B, Hq, Hkv, D, P, S, scale, nullptr, counters, s);
 }
 
 // Decode attention straight from the QKV GEMM's fp32 split-K slabs [SP, B, (Hq + 2 Hkv) D]: RoPE on q,
@@ -634,10 +677,10 @@ MRSUM_API int mrsum_attn_decode_mfma(const void* q, int q_stride, const void* kc
 MRSUM_API int mrsum_attn_decode_rope(const void* qkv_parts, int SP, const void* cos_sin, void* kcache, void* vcache,
                                      const int* block_tables, int bt_stride, const int* positions, void* part_o,
                                      void* part_ml, void* out, int out_stride, int B, int Hq, int Hkv, int D, int P,
-                                     int S, float scale, hipStream_t s) {
+                                     int S, float scale, int* counters, hipStream_t s) {
     if (SP < 1 || !qkv_parts || !cos_sin) return (int)hipErrorInvalidValue;
     const int width = (Hq + 2 * Hkv) * D;
     const RopeArgs ra{(const float*)qkv_parts, (size_t)B * width, SP, width, Hq, (const float2*)cos_sin};
     return launch_mfma(nullptr, 0, kcache, vcache, block_tables, bt_stride, positions, part_o, part_ml, out,
-                       out_stride, B, Hq, Hkv, D, P, S, scale, &ra, s);
+                       out_stride, B, Hq, Hkv, D, P, S, scale, &ra, counters, s);
 }

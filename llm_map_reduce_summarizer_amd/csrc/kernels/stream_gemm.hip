@@ -25,7 +25,7 @@
 #include "common.h"
 
 namespace {
-enum { EPI_BF16 = 0, EPI_F32_PARTIAL = 1, EPI_SWIGLU = 2 };
+enum { EPI_BF16 = 0, EPI_F32_PARTIAL = 1, EPI_SWIGLU = 2, EPI_SWIGLU_SPLIT = 3 };
 constexpr int KBLK = 128;
 constexpr int LDS_BUDGET = 160 * 1024 - 1024;  // one KiB scratch for the dummy x pieces
 
@@ -57,7 +57,8 @@ __device__ __forceinline__ void glds16(const void* g, char* lds) {
 template <int MT, int EPI, int WPB>
 __global__ __launch_bounds__(64 * WPB, 1) void stream_gemm_kernel(const bf16* __restrict__ x, int ldx,
                                                                   const bf16* __restrict__ W, int K, int M,
-                                                                  void* __restrict__ out, int ldo, int kper) {
+                                                                  void* __restrict__ out, int ldo, int kper,
+                                                                  float* __restrict__ parts, int* __restrict__ counters) {
     constexpr int R = 16 * WPB, BM = 16 * MT;
     constexpr int WBYTES = R * 256, SLOT = WBYTES + BM * 256;
     constexpr int D = (LDS_BUDGET / SLOT) < 6 ? (LDS_BUDGET / SLOT) : 6;
@@ -156,28 +157,77 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_gemm_kernel(const bf16* __
                 o.x = pack2(acc[m][0], acc[m][1]);
                 o.y = pack2(acc[m][2], acc[m][3]);
                 *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + nw + 4 * g) = o;
-            } else {
+            } else if constexpr (EPI == EPI_F32_PARTIAL) {
                 float* o = reinterpret_cast<float*>(out) + ((size_t)blockIdx.y * M + mm) * ldo + nw + 4 * g;
+                *reinterpret_cast<float4*>(o) = make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
+            } else {
+                float* o = parts + ((size_t)blockIdx.y * M + mm) * (gridDim.x * R) + nw + 4 * g;
                 *reinterpret_cast<float4*>(o) = make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
             }
         }
+    }
+    if constexpr (EPI == EPI_SWIGLU_SPLIT) {
+        // split-K SwiGLU: the last of the gridDim.y split workgroups of this column tile to arrive sums
+        // the fp32 partial tiles and applies silu(gate) * up (same publish / ticket / acquire protocol as
+        // attn_decode.hip combine_if_last; the ticket is re-armed for the next launch / graph replay).
+        // Lets a narrow gate_up projection (TP shards: N = 3584) fill the chip with split-K instead of
+        // streaming its weights through N / (16 WPB) CUs.
+        __shared__ int s_last;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const int prev = __hip_atomic_fetch_add(counters + blockIdx.x, 1, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+            s_last = prev == (int)gridDim.y - 1;
+        }
+        __syncthreads();
+        if (!s_last) return;
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        const int S = gridDim.y;
+        const size_t ncols = (size_t)gridDim.x * R;
+        // item = (row, 16-row block, half): 4 features = gate rows n0 + 16 bl + 4 hf .. +4, up rows + 8
+        for (int it = tid; it < M * 2 * WPB; it += 64 * WPB) {
+            const int mm = it / (2 * WPB), q = it % (2 * WPB), bl = q >> 1, hf = q & 1;
+            const float* pg = parts + (size_t)mm * ncols + n0 + 16 * bl + 4 * hf;
+            float4 gs = make_float4(0.f, 0.f, 0.f, 0.f), us = gs;
+#pragma unroll 4
+            for (int sp = 0; sp < S; ++sp) {
+                const float4 a = *reinterpret_cast<const float4*>(pg + (size_t)sp * M * ncols);
+                const float4 u = *reinterpret_cast<const float4*>(pg + (size_t)sp * M * ncols + 8);
+                gs.x += a.x; gs.y += a.y; gs.z += a.z; gs.w += a.w;
+                us.x += u.x; us.y += u.y; us.z += u.z; us.w += u.w;
+            }
+            uint2 o;
+            o.x = pack2(gs.x / (1.f + __expf(-gs.x)) * us.x, gs.y / (1.f + __expf(-gs.y)) * us.y);
+            o.y = pack2(gs.z / (1.f + __expf(-gs.z)) * us.z, gs.w / (1.f + __expf(-gs.w)) * us.w);
+            *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + (n0 >> 1) + 8 * bl + 4 * hf) = o;
+        }
+        if (tid == 0) __hip_atomic_store(counters + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
 // out: bf16 [M, ldo] (EPI_BF16), fp32 slabs [splits, M, ldo] (EPI_F32_PARTIAL) or bf16 [M, ldo] of
 // N/2 SwiGLU features (EPI_SWIGLU, splits = 1).  N % (16 wpb) == 0, wpb in {4, 5, 6, 7, 8}.
-MRSUM_API int mrsum_stream_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
-                                int epi, int splits, int wpb, hipStream_t s) {
+static int launch_stream_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
+                              int epi, int splits, int wpb, float* parts, int* counters, hipStream_t s) {
     if (M <= 0) return 0;
     if (wpb < 4 || wpb > 8 || M > 64 || K % KBLK || N % (16 * wpb) || splits < 1 || (K / KBLK) % splits)
         return (int)hipErrorInvalidValue;
-    if (epi != EPI_F32_PARTIAL && splits != 1) return (int)hipErrorInvalidValue;
+    if (epi != EPI_F32_PARTIAL && epi != EPI_SWIGLU_SPLIT && splits != 1) return (int)hipErrorInvalidValue;
+    if (epi == EPI_SWIGLU_SPLIT && (!parts || !counters)) return (int)hipErrorInvalidValue;
     const int kper = K / splits;
     const int mt = (M + 15) / 16;
     dim3 grid(N / (16 * wpb), splits), block(64 * wpb);
     auto X = (const bf16*)x;
     auto Wp = (const bf16*)W;
-#define L(MT_, EPI_, WPB_) stream_gemm_kernel<MT_, EPI_, WPB_><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper)
+#define L(MT_, EPI_, WPB_) \
+    stream_gemm_kernel<MT_, EPI_, WPB_><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, parts, counters)
 #define BY_WPB(MT_, EPI_)                          \
     switch (wpb) {                                 \
         case 4: L(MT_, EPI_, 4); break;            \
@@ -189,7 +239,8 @@ MRSUM_API int mrsum_stream_gemm(const void* x, int ldx, const void* W, int N, in
 #define BY_EPI(MT_)                                                           \
     if (epi == EPI_BF16) { BY_WPB(MT_, EPI_BF16) }                            \
     else if (epi == EPI_F32_PARTIAL) { BY_WPB(MT_, EPI_F32_PARTIAL) }         \
-    else { BY_WPB(MT_, EPI_SWIGLU) }
+    else if (epi == EPI_SWIGLU) { BY_WPB(MT_, EPI_SWIGLU) }                   \
+    else { BY_WPB(MT_, EPI_SWIGLU_SPLIT) }
     switch (mt) {
         case 1: BY_EPI(1); break;
         case 2: BY_EPI(2); break;
@@ -200,4 +251,20 @@ MRSUM_API int mrsum_stream_gemm(const void* x, int ldx, const void* W, int N, in
 #undef BY_WPB
 #undef L
     return (int)hipGetLastError();
+}
+
+MRSUM_API int mrsum_stream_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
+                                int epi, int splits, int wpb, hipStream_t s) {
+    if (epi == EPI_SWIGLU_SPLIT) return (int)hipErrorInvalidValue;
+    return launch_stream_gemm(x, ldx, W, N, K, M, out, ldo, epi, splits, wpb, nullptr, nullptr, s);
+}
+
+// out [M, ldo] bf16 = SwiGLU of the blocked gate_up product, split-K over ``splits`` workgroups per
+// column tile: ``parts`` fp32 [splits, M, N] scratch, ``counters`` >= N / (16 wpb) ints, zero on the
+// first call (every launch leaves them zero again).
+MRSUM_API int mrsum_stream_gemm_swiglu_split(const void* x, int ldx, const void* W, int N, int K, int M, void* out,
+                                             int ldo, int splits, int wpb, void* parts, int* counters,
+                                             hipStream_t s) {
+    return launch_stream_gemm(x, ldx, W, N, K, M, out, ldo, EPI_SWIGLU_SPLIT, splits, wpb, (float*)parts, counters,
+                              s);
 }

@@ -178,9 +178,10 @@ class LLMEngine:
             return None
         ws = self._workspaces.get(B)
         if ws is None:
-            from ..ops.hip import DecodeWorkspace, decode_splits
-            s = decode_splits(B, self.model.hkv, self.max_model_len)
-            ws = DecodeWorkspace(B, self.model.hq, self.cfg.head_dim, s, self.device, self.model.hkv)
+            from ..ops.hip import DecodeWorkspace, decode_attn_plan
+            s, fused = decode_attn_plan(B, self.model.hkv, self.max_model_len)
+            ws = DecodeWorkspace(B, self.model.hq, self.cfg.head_dim, s, self.device, self.model.hkv,
+                                 fused_combine=fused)
             self._workspaces[B] = ws
         return ws
 

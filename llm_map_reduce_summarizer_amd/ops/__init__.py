@@ -99,11 +99,8 @@ def attn_decode(q, kcache, vcache, block_tables, positions, hq, hkv, d, page, sc
     """``q``: bf16 rows [B, hq * d] (already rotated, K/V already in the cache) or a QKVParts."""
     if isinstance(q, QKVParts):
         from . import hip
-        if workspace is not None and workspace.counters is not None:
-            q = q.materialize()
-        else:
-            return hip.attn_decode_rope(q.parts, q.cos_sin, kcache, vcache, block_tables, positions, hq, hkv, d,
-                                        page, scale, out, workspace=workspace)
+        return hip.attn_decode_rope(q.parts, q.cos_sin, kcache, vcache, block_tables, positions, hq, hkv, d,
+                                    page, scale, out, workspace=workspace)
     if _use_hip(q):
         from . import hip
         return hip.attn_decode(q, kcache, vcache, block_tables, positions, hq, hkv, d, page, scale, out,
@@ -262,6 +259,8 @@ def gate_up_swiglu(x, wgu):
         p = hip.plan("gate_up", x.shape[0], wgu.shape[0], wgu.shape[1])
         if p[0] == "stream":
             return hip.linear_swiglu(x, wgu, kernel="stream", wpb=p[1])
+        if p[0] == "stream_split":
+            return hip.linear_swiglu(x, wgu, kernel="stream_split", wpb=p[1], splits=p[2])
         if p[0] != "blas":
             return hip.linear_swiglu(x, wgu, kernel=p[0])
         return hip.swiglu(torch.nn.functional.linear(x, wgu))

@@ -32,13 +32,15 @@ _SIGS = {
     "mrsum_attn_decode": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
                           _c_int, _c_int, _c_int, _c_float, _vp, _vp],
     "mrsum_attn_decode_mfma": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int,
-                               _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
+                               _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp],
     "mrsum_attn_decode_rope": [_vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int,
-                               _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
+                               _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp],
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int,
                          _vp],
     "mrsum_stream_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
+    "mrsum_stream_gemm_swiglu_split": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _vp,
+                                       _vp, _vp],
     "mrsum_skinny_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_quant_fp8_rows": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
@@ -247,6 +249,24 @@ def decode_splits(batch: int, hkv: int, max_ctx: int, target_wgs: int = 1024, ma
     return s
 
 
+FUSED_COMBINE = os.environ.get("MRSUM_FUSED_COMBINE", "0")
+
+
+def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
+    """(splits, fused_combine) of the decode attention of ``batch`` sequences x ``hkv`` kv heads.
+
+    The in-launch merge by the last arriving split (MRSUM_FUSED_COMBINE=1, or "auto": at most 12
+    (sequence, kv head) groups, 16 splits) wins in isolation (tools/bench_tp_shard.py, attention + merge
+    per call at 4k context: TP=8 B=1 14.8 vs 17.8 us, TP=1 B=1 14.9 vs 18.0) but LOSES inside the decode
+    graph (step at 4k context: TP=8 B=1 1.555 vs 1.502 ms, TP=1 B=1 3.765 vs 3.715 ms): the agent-scope
+    release of every split writes back an L2 full of the preceding GEMMs' dirty slabs.  Off by default."""
+    fused = (batch * hkv <= 12) if FUSED_COMBINE == "auto" else FUSED_COMBINE == "1"
+    splits = decode_splits(batch, hkv, max_ctx)
+    if fused:
+        splits = min(splits, 16)
+    return splits, fused
+
+
 class DecodeWorkspace:
     """Split-K partial buffers + per-(seq, kv head) arrival counters for attn_decode
     (allocated once per batch bucket; counters start at 0 and every launch re-arms them)."""
@@ -288,7 +308,8 @@ def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.T
     _req(block_tables.dim() == 2 and block_tables.shape[0] >= B and positions.numel() >= B, "attn_decode_rope: tables")
     if workspace is None:
         workspace = DecodeWorkspace(B, hq, d, decode_splits(B, hkv, block_tables.shape[1] * page), parts.device, hkv)
-    _req(workspace.part_o.numel() >= B * hq * workspace.splits * d and workspace.counters is None,
+    _req(workspace.part_o.numel() >= B * hq * workspace.splits * d and workspace.part_ml.numel() >=
+         B * hq * workspace.splits * 2 and (workspace.counters is None or workspace.counters.numel() >= B * hkv),
          "attn_decode_rope: workspace")
     if out is None:
         out = torch.empty(B, hq * d, dtype=torch.bfloat16, device=parts.device)
@@ -296,7 +317,8 @@ def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.T
     _check(_fn("mrsum_attn_decode_rope")(_p(parts), SP, _p(cos_sin), _p(kcache), _p(vcache), _p(block_tables),
                                          block_tables.stride(0), _p(positions), _p(workspace.part_o),
                                          _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
-                                         workspace.splits, scale, _stream()), "attn_decode_rope")
+                                         workspace.splits, scale, _p(workspace.counters), _stream()),
+           "attn_decode_rope")
     return out
 
 
@@ -323,11 +345,12 @@ def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, blo
         out = torch.empty(B, hq * d, dtype=q.dtype, device=q.device)
     _rows_ok(out)
     impl = impl or DECODE_ATTN_IMPL
-    if impl == "mfma" and page == 64 and hq // hkv <= 16 and workspace.counters is None:
+    if impl == "mfma" and page == 64 and hq // hkv <= 16:
         _check(_fn("mrsum_attn_decode_mfma")(_p(q), q.stride(0), _p(kcache), _p(vcache), _p(block_tables),
                                              block_tables.stride(0), _p(positions), _p(workspace.part_o),
                                              _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
-                                             workspace.splits, scale, _stream()), "attn_decode_mfma")
+                                             workspace.splits, scale, _p(workspace.counters), _stream()),
+               "attn_decode_mfma")
         return out
     _check(_fn("mrsum_attn_decode")(_p(q), q.stride(0), _p(kcache), _p(vcache), _p(block_tables),
                                     block_tables.stride(0), _p(positions), _p(workspace.part_o),
@@ -466,8 +489,43 @@ def linear_parts(x: torch.Tensor, w: torch.Tensor, splits: Optional[int] = None,
     return _skinny(x, w, out, EPI_F32_PARTIAL, nt, splits, N)
 
 
+_TILE_COUNTERS = {}
+
+
+def _tile_counters(device, n: int) -> torch.Tensor:
+    """Per-device arrival tickets of the split-K SwiGLU GEMM (one per column tile, zero between
+    launches: the last arriver of every tile re-arms its ticket).  One buffer serves every launch on
+    the device's decode stream -- launches on one stream never overlap."""
+    key = (str(device), n)
+    t = _TILE_COUNTERS.get(key)
+    if t is None:
+        # must outlive any graph: never allocate inside a capture (the engine's eager warm-up step
+        # before every capture allocates it)
+        _req(not torch.cuda.is_current_stream_capturing(), "split-K SwiGLU tickets first used inside a capture")
+        t = _TILE_COUNTERS[key] = torch.zeros(max(n, 1024), dtype=torch.int32, device=device)
+    return t
+
+
+def stream_swiglu_split(x: torch.Tensor, w_gu: torch.Tensor, out: torch.Tensor, wpb: int, splits: int) -> torch.Tensor:
+    """SwiGLU of the gate_up GEMM split-K over ``splits`` workgroups per column tile; the last split
+    of a tile to finish sums the fp32 partial tiles and applies silu(gate) * up (stream_gemm.hip)."""
+    _bf16_cuda(x, w_gu)
+    _rows_ok(x)
+    M, K = x.shape
+    N = w_gu.shape[0]
+    _req(w_gu.is_contiguous() and w_gu.shape[1] == K, "stream_swiglu_split: weight must be [N, K] contiguous")
+    _req(1 <= M <= SKINNY_MAX_M and K % 128 == 0 and 4 <= wpb <= 8 and N % (16 * wpb) == 0 and splits >= 1
+         and (K // 128) % splits == 0 and out.is_contiguous() and out.shape == (M, N // 2),
+         "stream_swiglu_split: unsupported shape M=%d N=%d K=%d S=%d wpb=%d" % (M, N, K, splits, wpb))
+    parts = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
+    cnt = _tile_counters(x.device, N // (16 * wpb))
+    _check(_fn("mrsum_stream_gemm_swiglu_split")(_p(x), x.stride(0), _p(w_gu), N, K, M, _p(out), out.stride(0),
+                                                 splits, wpb, _p(parts), _p(cnt), _stream()), "stream_swiglu_split")
+    return out
+
+
 def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tensor] = None,
-                  kernel: str = "skinny", wpb: int = 4) -> torch.Tensor:
+                  kernel: str = "skinny", wpb: int = 4, splits: int = 1) -> torch.Tensor:
     """silu(gate) * up straight out of the gate_up GEMM (blocked [8 gate | 8 up] weight rows)."""
     M = x.shape[0]
     F2 = w_gu.shape[0]
@@ -478,6 +536,8 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tenso
     _req(out.is_contiguous() and out.shape == (M, F2 // 2), "linear_swiglu: bad out")
     if kernel == "stream":
         return _stream_gemm(x, w_gu, out, EPI_SWIGLU, 1, F2 // 2, wpb)
+    if kernel == "stream_split":
+        return stream_swiglu_split(x, w_gu, out, wpb, splits)
     if kernel == "lds":
         return _skinny_lds(x, w_gu, out, EPI_SWIGLU, 1, F2 // 2)
     return _skinny(x, w_gu, out, EPI_SWIGLU, 1, 1, F2 // 2)
@@ -544,6 +604,13 @@ def plan(role: str, M: int, N: int, K: int, splits: Optional[int] = None, stream
     cfg = stream_config(N, K, swiglu=(role == "gate_up"), splits=splits) if stream and STREAM_GEMM else None
     if cfg is not None:
         return ("stream",) + cfg
+    if role == "gate_up" and stream and STREAM_GEMM and SWIGLU_SPLIT and M > 16 and N % 128 == 0 \
+            and (K // 128) % 4 == 0:
+        # narrow gate_up (TP shards, N = 3584 / 7168) at M > 16: split-K over the column tiles, SwiGLU by the
+        # last split to arrive (tools/bench_tp_shard.py, us: TP=4 M=39 23.8 vs hipBLASLt + SwiGLU 28.2 vs
+        # register-streaming 29.4; TP=8 M=39 15.4 vs 15.7).  At M <= 16 the register-streaming kernel
+        # wins (TP=8 M=1 9.7 vs 11.5; M=10 9.9 vs 12.2; the LDS-x kernel took 39).
+        return ("stream_split", 8, 4)
     blocks = K // 128
 
     def div(s):
@@ -564,15 +631,14 @@ def plan(role: str, M: int, N: int, K: int, splits: Optional[int] = None, stream
             return ("blas",)
         return ("lds", splits or div(8))
     if role == "gate_up":
-        if M <= 8:
+        if M <= 16:
             return ("skinny", 1, 1)
-        if M <= 16 and N % 64 == 0:
-            return ("lds", 1)
         return ("blas",)
     return ("blas",)
 
 
 STREAM_GEMM = os.environ.get("MRSUM_STREAM_GEMM", "1") == "1"
+SWIGLU_SPLIT = os.environ.get("MRSUM_SWIGLU_SPLIT", "1") == "1"
 
 
 # ------------------------------------------------------------------ FP8 (e4m3fn) weights

@@ -109,11 +109,11 @@ def test_attn_prefill_spike():
 
 @pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (4, 4), (16, 1)])
 @pytest.mark.parametrize("splits", [1, 3, 16])
-@pytest.mark.parametrize("impl", ["mfma", "valu", "valu_fused"])
+@pytest.mark.parametrize("impl", ["mfma", "mfma_fused", "valu", "valu_fused"])
 def test_attn_decode(hq, hkv, splits, impl):
-    if impl != "mfma" and hq // hkv == 16:
+    if impl.startswith("valu") and hq // hkv == 16:
         pytest.skip("valu kernel supports G <= 8")
-    fused = impl == "valu_fused"
+    fused = impl.endswith("_fused")
     d, page = 128, 64
     ctxs = [1, 65, 700, 129, 64, 1000]
     B = len(ctxs)
@@ -309,6 +309,32 @@ def test_stream_gemm(M, wpb, K):
            g * torch.sigmoid(g) * u, 2e-2)
 
 
+@pytest.mark.parametrize("M", [1, 10, 39, 64])
+@pytest.mark.parametrize("N,K,wpb,S", [(3584, 4096, 7, 8), (7168, 4096, 7, 4), (448, 1024, 4, 2), (896, 512, 8, 4)])
+def test_stream_swiglu_split(M, N, K, wpb, S):
+    """split-K SwiGLU (last arriving split of a column tile applies silu(gate) * up): vs fp32, and the
+    arrival tickets re-arm (repeated launches and a replayed hipGraph give the same answer)."""
+    x = _rand(M, K, seed=64)
+    wg = _rand(N // 2, K, scale=0.05, seed=65)
+    wu = _rand(N // 2, K, scale=0.05, seed=66)
+    g, u = x.float() @ wg.float().t(), x.float() @ wu.float().t()
+    ref = g * torch.sigmoid(g) * u
+    w = reference.interleave_gate_up(wg, wu).contiguous()
+    out = torch.empty(M, N // 2, dtype=torch.bfloat16, device=DEV)
+    for _ in range(3):
+        out.zero_()
+        _close(hip.stream_swiglu_split(x, w, out, wpb, S), ref, 2e-2)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        hip.stream_swiglu_split(x, w, out, wpb, S)
+    for _ in range(3):
+        out.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        _close(out, ref, 2e-2)
+    assert int(hip._tile_counters(x.device, N // (16 * wpb))[: N // (16 * wpb)].abs().sum()) == 0
+
+
 @pytest.mark.parametrize("M", [1, 5, 17, 48, 64, 200])
 @pytest.mark.parametrize("N,K", [(1280, 8192), (512, 3584)])
 def test_fp8_linear(M, N, K):
@@ -344,8 +370,9 @@ def test_fp8_swiglu_and_quant():
     assert (q.float() == ref_q.float()).float().mean().item() > 0.98
 
 
-@pytest.mark.parametrize("hq,hkv,S", [(32, 8, 4), (4, 1, 1), (16, 1, 3), (8, 2, 2)])
-def test_attn_decode_rope_fused(hq, hkv, S):
+@pytest.mark.parametrize("hq,hkv,S", [(32, 8, 4), (4, 1, 1), (16, 1, 3), (8, 2, 2), (4, 1, 16)])
+@pytest.mark.parametrize("fused_combine", [False, True])
+def test_attn_decode_rope_fused(hq, hkv, S, fused_combine):
     """attn_decode_rope (q/k RoPE + new K/V written into the cache + attention, from the QKV GEMM's
     fp32 split-K slabs) == reference rope_kv_parts followed by reference attention."""
     d, page = 128, 64
@@ -373,10 +400,12 @@ def test_attn_decode_rope_fused(hq, hkv, S):
     qkv = reference.rope_kv_parts(parts, pos, sidx, bt, k2, v2, cs, hq, hkv, d, page)
     o2 = reference.attn_decode(qkv, k2, v2, bt, pos, hq, hkv, d, page, sc)
     k1, v1 = kc0.clone().to(DEV), vc0.clone().to(DEV)
-    ws = hip.DecodeWorkspace(B, hq, d, hip.decode_splits(B, hkv, 20 * page), DEV, hkv)
-    for _ in range(2):  # idempotent: the second call rewrites the same K/V row
+    ws = hip.DecodeWorkspace(B, hq, d, hip.decode_splits(B, hkv, 20 * page), DEV, hkv, fused_combine=fused_combine)
+    for _ in range(3):  # idempotent: later calls rewrite the same K/V row (and re-armed merge tickets)
         o1 = hip.attn_decode_rope(parts, cs, k1, v1, bt, pos, hq, hkv, d, page, sc, workspace=ws)
         _close(o1, o2, 2e-2)
+    if fused_combine:
+        assert int(ws.counters.abs().sum()) == 0
     _close(k1, k2, 3e-2)
     _close(v1, v2, 3e-2)
 

@@ -18,15 +18,24 @@ def main():
     ap.add_argument("--batches", default="1,5,10,39")
     ap.add_argument("--ctx", type=int, default=4000)
     ap.add_argument("--new", type=int, default=256)
+    ap.add_argument("--tp-shard", type=int, default=1,
+                    help="run ONE rank's shard shapes of TP=K (heads, ffn and vocab / K) on this GPU with no "
+                         "all-reduce: the compute + launch floor of a TP=K decode step")
     a = ap.parse_args()
     import torch
     from llm_map_reduce_summarizer_amd.engine.config import get_model_config
     from llm_map_reduce_summarizer_amd.engine.engine import LLMEngine, SamplingParams
-    eng = LLMEngine(get_model_config(a.model), device="cuda:0", max_model_len=a.ctx + a.new + 64,
+    cfg = get_model_config(a.model)
+    if a.tp_shard > 1:
+        k = a.tp_shard
+        cfg = get_model_config(a.model, n_heads=cfg.n_heads // k, n_kv_heads=cfg.n_kv_heads // k,
+                               ffn=cfg.ffn // k, vocab_size=cfg.vocab_size // k)
+    eng = LLMEngine(cfg, device="cuda:0", max_model_len=a.ctx + a.new + 64,
                     max_num_seqs=64, kv_fraction=0.5, weight_dtype=a.dtype, sync_every=32)
     res = []
     for B in (int(b) for b in a.batches.split(",")):
-        prompts = [[128000] + [(i * 7919 + j * 31) % 120000 + 10 for j in range(a.ctx)] for i in range(B)]
+        V = cfg.vocab_size
+        prompts = [[1] + [(i * 7919 + j * 31) % (V - 20) + 10 for j in range(a.ctx)] for i in range(B)]
         sp = [SamplingParams(a.new, 0.3, i) for i in range(B)]
         eng.generate(prompts, [SamplingParams(8, 0.3, i) for i in range(B)], ignore_eos=True)  # capture/warm
         s0 = dict(eng.stats)
@@ -37,7 +46,7 @@ def main():
         st = eng.stats
         steps = st["decode_steps"] - s0["decode_steps"]
         dec = st["decode_s"] - s0["decode_s"]
-        res.append({"B": B, "ctx": a.ctx, "decode_ms_per_step": round(1000 * dec / max(1, steps), 3),
+        res.append({"B": B, "ctx": a.ctx, "tp_shard": a.tp_shard, "decode_ms_per_step": round(1000 * dec / max(1, steps), 3),
                     "prefill_s": round(st["prefill_s"] - s0["prefill_s"], 3), "wall_s": round(wall, 3)})
         print(json.dumps(res[-1]), flush=True)
 
