@@ -27,7 +27,8 @@ def test_tp_divides_streams_and_adds_all_reduces():
     t1 = plan.decode_step_s(D8B, hw, 8, 4000, 1)
     t8 = plan.decode_step_s(D8B, hw, 8, 4000, 8)
     floor = hw.step_floor_s
-    assert abs((t8 - floor) * 8 - (t1 - floor)) < 1e-9
+    tp_floor = floor + hw.tp_floor_s + hw.tp_row_s * 8  # a TP shard's fixed cost grows with the rows
+    assert abs((t8 - tp_floor) * 8 - (t1 - floor)) < 1e-9
     hw2 = plan.with_measurements(hw, ar_lat_s=10e-6)
     assert abs(plan.decode_step_s(D8B, hw2, 8, 4000, 8) - t8 - 65 * 10e-6) < 1e-12
 
