@@ -62,6 +62,8 @@ def main() -> int:
                          "tensor-parallel over all ranks; tp: every stage on one engine sharded over all ranks; "
                          "auto: per stage, the cheaper of dp / tp under parallel/plan.py's cost model fed with the "
                          "all-reduce latency and bandwidth measured on these GPUs at start-up")
+    ap.add_argument("--no-hierarchical", action="store_true",
+                    help="single-pass reduce over every summary (use a long-context model, e.g. llama3.1-8b)")
     ap.add_argument("--profile", default=None, metavar="DIR", help="torch.profiler trace of the timed steps")
     ap.add_argument("--log-level", default="WARNING")
     args = ap.parse_args()
@@ -89,7 +91,8 @@ def main() -> int:
     provider = LocalEngineProvider(args.model, cfg, use_graphs=not args.no_graphs, ignore_eos=not args.stop_at_eos,
                                    parallel=args.parallel)
     executor = LLMExecutor(config=cfg, provider_obj=provider)
-    summarizer = TranscriptSummarizer(executor=executor, max_tokens_per_chunk=args.chunk_tokens)
+    summarizer = TranscriptSummarizer(executor=executor, max_tokens_per_chunk=args.chunk_tokens,
+                                      hierarchical_aggregation=not args.no_hierarchical)
     transcript = synthetic_transcript(args.hours, seed=0)
     # weight init, KV allocation, planner measurements and the decode graphs of every batch bucket a
     # stage of this transcript can use: engine start-up, outside the timed region
@@ -125,7 +128,10 @@ def main() -> int:
     value = n_chunks / (ms / 1000.0)
     eng = rep.get("engine", {})
     out = {
-        "metric": "chunks/sec (whole node) + end-to-end wall-clock, 10h transcript, Llama-3-8B",
+        "metric": "chunks/sec (whole node) + end-to-end wall-clock, 10h transcript, Llama-3-8B"
+                  + ("" if args.model == "llama3-8b" and args.hours == 10.0 and not args.no_hierarchical
+                     else " [variant: %s, %gh%s]" % (args.model, args.hours,
+                                                     ", single-pass reduce" if args.no_hierarchical else "")),
         "value": round(value, 4),
         "unit": "chunks/s",
         "n_gpus": world,

@@ -68,6 +68,9 @@ def build_parser() -> argparse.ArgumentParser:
     e.add_argument("--seed", type=int, default=None)
     e.add_argument("--kv-fraction", type=float, default=None, help="fraction of free HBM for the KV cache")
     e.add_argument("--no-graphs", action="store_true", help="disable hipGraph capture of decode steps")
+    e.add_argument("--max-model-len", type=int, default=None,
+                   help="context budget per request (default: 32k for llama3-*, the model window for llama3.1-*); "
+                        "longer prompts are truncated with a warning")
     e.add_argument("--tokenizer", default=None, help="tiktoken-format vocabulary file (default: bundled)")
     e.add_argument("--weights", default=os.environ.get("MRSUM_WEIGHTS"),
                    help="Hugging Face Llama safetensors checkpoint (file or dir) for the map model; "
@@ -129,6 +132,8 @@ async def async_main(args: argparse.Namespace) -> int:
                       "max_num_seqs": args.max_concurrent_requests, "reduce_tp": args.reduce_tp,
                       "parallel": args.parallel,
                       "weights": args.weights})
+        if args.max_model_len:
+            popts["max_model_len"] = args.max_model_len
     agg_executor = None
     if args.aggregator_model:
         if provider != "local":
@@ -137,7 +142,7 @@ async def async_main(args: argparse.Namespace) -> int:
         if popts.get("kv_fraction") is None:
             popts["kv_fraction"] = 0.3  # leave HBM for the second engine
         aopts = dict(popts, dtype=args.aggregator_dtype, tp=args.aggregator_tp or args.tp, kv_fraction=0.6,
-                     max_model_len=40960, weights=args.aggregator_weights)
+                     max_model_len=args.max_model_len or 40960, weights=args.aggregator_weights)
         agg_executor = LLMExecutor(config=cfg, provider="local", model=args.aggregator_model, **aopts)
     executor = LLMExecutor(config=cfg, provider=provider, model=args.model,
                            max_concurrent_requests=args.max_concurrent_requests, **popts)

@@ -12,6 +12,7 @@ for) so CPU tests and GPU smoke runs exercise the same code paths.
 from __future__ import annotations
 
 from dataclasses import dataclass, replace
+from typing import Optional, Tuple
 
 
 @dataclass(frozen=True)
@@ -28,6 +29,9 @@ class ModelConfig:
     rms_eps: float = 1e-5
     max_position: int = 40960
     init_std: float = 0.02
+    # Llama-3.1 "llama3" RoPE frequency scaling: (factor, low_freq_factor, high_freq_factor,
+    # original_max_position_embeddings); None = plain RoPE
+    rope_scaling: Optional[Tuple[float, float, float, int]] = None
 
     @property
     def qkv_dim(self) -> int:
@@ -45,6 +49,11 @@ class ModelConfig:
 PRESETS = {
     "llama3-8b": ModelConfig("llama3-8b"),
     "llama3-70b": ModelConfig("llama3-70b", hidden=8192, n_layers=80, n_heads=64, n_kv_heads=8, ffn=28672),
+    # Llama-3.1: same shapes, 128k positions with the "llama3" RoPE scaling -- the model for a single-pass
+    # reduce over a whole day of summaries (--no-hierarchical on 24 h: ~100k-token prompt)
+    "llama3.1-8b": ModelConfig("llama3.1-8b", max_position=131072, rope_scaling=(8.0, 1.0, 4.0, 8192)),
+    "llama3.1-70b": ModelConfig("llama3.1-70b", hidden=8192, n_layers=80, n_heads=64, n_kv_heads=8, ffn=28672,
+                                max_position=131072, rope_scaling=(8.0, 1.0, 4.0, 8192)),
     # test / smoke configs (real vocab, head_dim 128)
     "tiny": ModelConfig("tiny", hidden=256, n_layers=2, n_heads=2, n_kv_heads=1, ffn=512, max_position=8192),
     "tiny-gqa4": ModelConfig("tiny-gqa4", hidden=512, n_layers=2, n_heads=8, n_kv_heads=2, ffn=1024,

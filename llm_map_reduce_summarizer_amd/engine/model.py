@@ -109,7 +109,8 @@ class LlamaModel:
             load_hf(self, weights_path)
         else:
             self._init_weights(seed)
-        self.cos_sin = rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, self.device)
+        self.cos_sin = rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, self.device,
+                                    scaling=cfg.rope_scaling)
         self.vocab_offset = tp_rank * self.vocab_local
         # TP on GPUs: decode all-reduces (fp32 split-K slabs, <= 1 MiB) and the sampler's key max go
         # through the one-shot P2P kernel (parallel/custom_ar.py); larger messages through RCCL

@@ -66,7 +66,7 @@ class LocalEngineProvider(Provider):
     batched = True
 
     def __init__(self, model: str = "llama3-8b", config: Optional[LLMConfig] = None, device: Optional[str] = None,
-                 tp: int = 1, seed: Optional[int] = None, max_model_len: int = 32768, engine=None,
+                 tp: int = 1, seed: Optional[int] = None, max_model_len: Optional[int] = None, engine=None,
                  engine_options: Optional[Dict[str, Any]] = None, dtype: Optional[str] = None,
                  kv_fraction: Optional[float] = None, use_graphs: bool = True, max_num_seqs: Optional[int] = None,
                  tokenizer: Optional[str] = None, ignore_eos: bool = False, reduce_tp: Optional[bool] = None,
@@ -78,13 +78,21 @@ class LocalEngineProvider(Provider):
         self.tp = tp
         self.ignore_eos = ignore_eos
         self.seed = self.config.ENGINE_SEED if seed is None else seed
-        self.max_model_len = max_model_len
         self._engine = engine
         self._device = device
         self._engine_options = dict(engine_options or {})
         self._engine_options.setdefault("use_graphs", use_graphs)
         if weights:  # HF safetensors checkpoint (engine/weights.py); else seeded random init
             self._engine_options.setdefault("weights_path", weights)
+        # context budget: 32k for the Llama-3 presets (map prompts ~4k, reduce prompts <= ~12k), the
+        # model's full window for long-context models (Llama-3.1: 128k, a single-pass reduce of a day)
+        if max_model_len is None:
+            try:
+                mp = self.model_config().max_position
+            except Exception:  # noqa: BLE001 -- unknown model: the engine reports it when built
+                mp = 32768
+            max_model_len = mp if mp > 40960 else min(mp, 32768)
+        self.max_model_len = max_model_len
         if dtype == "fp8":
             self._engine_options.setdefault("weight_dtype", "fp8")
         if kv_fraction is not None:

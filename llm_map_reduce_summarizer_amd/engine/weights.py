@@ -116,7 +116,12 @@ def save_hf(model, path: str) -> None:
                    "num_attention_heads": cfg.n_heads, "num_key_value_heads": cfg.n_kv_heads,
                    "head_dim": cfg.head_dim, "rope_theta": cfg.rope_theta, "rms_norm_eps": cfg.rms_eps,
                    "vocab_size": cfg.vocab_size, "max_position_embeddings": cfg.max_position,
-                   "torch_dtype": "bfloat16"}, fh, indent=1)
+                   "torch_dtype": "bfloat16",
+                   **({"rope_scaling": {"rope_type": "llama3", "factor": cfg.rope_scaling[0],
+                                        "low_freq_factor": cfg.rope_scaling[1],
+                                        "high_freq_factor": cfg.rope_scaling[2],
+                                        "original_max_position_embeddings": cfg.rope_scaling[3]}}
+                      if cfg.rope_scaling else {})}, fh, indent=1)
 
 
 def config_from_hf(path: str, name: str = "hf"):
@@ -126,7 +131,15 @@ def config_from_hf(path: str, name: str = "hf"):
     with open(f) as fh:
         c = json.load(fh)
     heads = c["num_attention_heads"]
-    return ModelConfig(name, vocab_size=c["vocab_size"], hidden=c["hidden_size"], n_layers=c["num_hidden_layers"],
+    rs = c.get("rope_scaling") or None
+    scaling = None
+    if rs:
+        kind = rs.get("rope_type", rs.get("type"))
+        if kind != "llama3":
+            raise ValueError("unsupported rope_scaling %r (only Llama-3.1 'llama3' scaling)" % kind)
+        scaling = (float(rs["factor"]), float(rs.get("low_freq_factor", 1.0)), float(rs.get("high_freq_factor", 4.0)),
+                   int(rs.get("original_max_position_embeddings", 8192)))
+    return ModelConfig(name, rope_scaling=scaling, vocab_size=c["vocab_size"], hidden=c["hidden_size"], n_layers=c["num_hidden_layers"],
                        n_heads=heads, n_kv_heads=c.get("num_key_value_heads", heads),
                        head_dim=c.get("head_dim", c["hidden_size"] // heads), ffn=c["intermediate_size"],
                        rope_theta=float(c.get("rope_theta", 500000.0)), rms_eps=float(c.get("rms_norm_eps", 1e-5)),

@@ -40,8 +40,26 @@ def add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: f
     return rmsnorm(residual, w, eps, out)
 
 
-def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None) -> torch.Tensor:
+def rope_inv_freq(head_dim: int, theta: float, scaling=None) -> torch.Tensor:
+    """RoPE inverse frequencies (float64); ``scaling`` = (factor, low_freq_factor, high_freq_factor,
+    original_max_position) applies Llama-3.1's "llama3" rule: wavelengths longer than
+    orig / low_freq_factor are divided by ``factor``, shorter than orig / high_freq_factor kept, and the
+    band between interpolated smoothly."""
     inv = 1.0 / (theta ** (torch.arange(0, head_dim, 2, dtype=torch.float64) / head_dim))
+    if scaling is None:
+        return inv
+    factor, low, high, orig = scaling
+    wavelen = 2 * math.pi / inv
+    low_wl, high_wl = orig / low, orig / high
+    smooth = ((orig / wavelen) - low) / (high - low)
+    mid = (1 - smooth) * inv / factor + smooth * inv
+    out = torch.where(wavelen > low_wl, inv / factor, inv)
+    band = (wavelen <= low_wl) & (wavelen >= high_wl)
+    return torch.where(band, mid, out)
+
+
+def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None, scaling=None) -> torch.Tensor:
+    inv = rope_inv_freq(head_dim, theta, scaling)
     t = torch.arange(max_pos, dtype=torch.float64)
     ang = torch.outer(t, inv)
     return torch.stack([ang.cos(), ang.sin()], dim=-1).float().contiguous().to(device)
