@@ -40,10 +40,27 @@ __device__ __forceinline__ void combine_group(const float* part_o, const float* 
                                               int b, int kvh, int Hq, int S, float* sw /* [G][S] LDS */,
                                               float* sden /* [G] */) {
     constexpr int D = 128;
+    constexpr int NV = G * D / 4;                 // float4 output items
+    constexpr int NH = NV >= 256 ? 1 : 256 / NV;  // interleaved split subsets per item
+    constexpr int NR = NV > 256 ? NV / 256 : 1;   // item rounds (G = 16: 2)
+    constexpr int PRE = 16 / NR;                  // partial loads per thread issued up front
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const size_t bh0 = (size_t)b * Hq + (size_t)kvh * G;
-    // split weights: one wave per head, one lane per split (S <= MAX_SPLITS = 64), all loads issued
-    // at once -- a serial per-head loop over S dependent L2 loads cost ~5 us at S = 32
+    // 1. the first PRE partial slabs of every (item, subset) are loaded BEFORE the split weights are
+    //    known, so the slab loads and the (max, sum) loads share one memory round trip
+    float4 pre[NR][PRE];
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+        const int t = r * 256 + tid, item = t % NV, h = t / NV;
+        const int g = item / (D / 4), d4 = item % (D / 4);
+        const float4* po = reinterpret_cast<const float4*>(part_o + (bh0 + g) * S * D) + d4;
+#pragma unroll
+        for (int j = 0; j < PRE; ++j) {
+            const int sp = h + j * NH;
+            pre[r][j] = (h < NH && sp < S) ? po[(size_t)sp * (D / 4)] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+    // 2. split weights: one wave per head, one lane per split (S <= MAX_SPLITS = 64)
     for (int g = wv; g < G; g += 4) {
         float ms = -INFINITY, ls = 0.f;
         if (lane < S) {
@@ -58,24 +75,28 @@ __device__ __forceinline__ void combine_group(const float* part_o, const float* 
         if (lane == 0) sden[g] = den;
     }
     __syncthreads();
-    // weighted slab sum: float4 items (G * 32 of them) x NH interleaved split subsets, so every thread
-    // has <= S / NH independent 16-B loads in flight at once; subsets merged through LDS
-    constexpr int NV = G * D / 4;
-    constexpr int NH = NV >= 256 ? 1 : 256 / NV;
+    // 3. weighted sums (the rare splits beyond the preloaded ones loaded now), subsets merged through LDS
     __shared__ float4 red[NH > 1 ? 256 : 1];
 #pragma unroll
-    for (int i0 = 0; i0 < (NV > 256 ? NV : 256); i0 += 256) {  // G = 16: two item rounds
-        const int t = i0 + tid;
-        const int item = t % NV, h = t / NV;
+    for (int r = 0; r < NR; ++r) {
+        const int t = r * 256 + tid, item = t % NV, h = t / NV;
         const int g = item / (D / 4), d4 = item % (D / 4);
+        const float* w = sw + g * S;
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
         if (h < NH) {
+#pragma unroll
+            for (int j = 0; j < PRE; ++j) {
+                const int sp = h + j * NH;
+                const float ws = sp < S ? w[sp] : 0.f;
+                acc.x += ws * pre[r][j].x;
+                acc.y += ws * pre[r][j].y;
+                acc.z += ws * pre[r][j].z;
+                acc.w += ws * pre[r][j].w;
+            }
             const float4* po = reinterpret_cast<const float4*>(part_o + (bh0 + g) * S * D) + d4;
-            const float* w = sw + g * S;
-#pragma unroll 8
-            for (int s = h; s < S; s += NH) {
-                const float4 v = po[(size_t)s * (D / 4)];
-                const float ws = w[s];
+            for (int sp = h + PRE * NH; sp < S; sp += NH) {
+                const float4 v = po[(size_t)sp * (D / 4)];
+                const float ws = w[sp];
                 acc.x += ws * v.x;
                 acc.y += ws * v.y;
                 acc.z += ws * v.z;

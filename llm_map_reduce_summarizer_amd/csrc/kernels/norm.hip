@@ -100,26 +100,48 @@ __global__ __launch_bounds__(256) void add_rmsnorm_parts_kernel(const float* __r
     uint4 wv[VPT];  // norm weights fetched up front, off the reduction's critical path
 #pragma unroll
     for (int i = 0; i < VPT; ++i) wv[i] = wr[min((int)threadIdx.x + i * 256, nvec - 1)];
+    // every load of the first 4 slabs (and the residual) of all VPT vectors is issued before any is
+    // consumed: one memory round trip for S <= 4 instead of one per vector
+    uint4 rv[VPT];
+    float4 a[VPT][4], bq[VPT][4];
+#pragma unroll
+    for (int i = 0; i < VPT; ++i) {
+        const int c = min((int)threadIdx.x + i * 256, nvec - 1);
+        rv[i] = rr[c];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float4* p = reinterpret_cast<const float4*>(parts + ((size_t)min(u, S - 1) * T + row) * D + c * 8);
+            a[i][u] = p[0];
+            bq[i][u] = p[1];
+        }
+    }
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
         const int c = threadIdx.x + i * 256;
+        unpack8(rv[i], v[i]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (u < S) {
+                v[i][0] += a[i][u].x; v[i][1] += a[i][u].y; v[i][2] += a[i][u].z; v[i][3] += a[i][u].w;
+                v[i][4] += bq[i][u].x; v[i][5] += bq[i][u].y; v[i][6] += bq[i][u].z; v[i][7] += bq[i][u].w;
+            }
+        }
         if (c < nvec) {
-            unpack8(rr[c], v[i]);
-            // slabs in batches of 4, all loads of a batch in flight together (see rope_kv.hip)
-            for (int s0 = 0; s0 < S; s0 += 4) {
-                float4 a[4], b[4];
+            // slabs beyond the first 4 in batches of 4, all loads of a batch in flight together
+            for (int s0 = 4; s0 < S; s0 += 4) {
+                float4 x0[4], x1[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const float4* p = reinterpret_cast<const float4*>(
                         parts + ((size_t)min(s0 + u, S - 1) * T + row) * D + c * 8);
-                    a[u] = p[0];
-                    b[u] = p[1];
+                    x0[u] = p[0];
+                    x1[u] = p[1];
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     if (s0 + u < S) {
-                        v[i][0] += a[u].x; v[i][1] += a[u].y; v[i][2] += a[u].z; v[i][3] += a[u].w;
-                        v[i][4] += b[u].x; v[i][5] += b[u].y; v[i][6] += b[u].z; v[i][7] += b[u].w;
+                        v[i][0] += x0[u].x; v[i][1] += x0[u].y; v[i][2] += x0[u].z; v[i][3] += x0[u].w;
+                        v[i][4] += x1[u].x; v[i][5] += x1[u].y; v[i][6] += x1[u].z; v[i][7] += x1[u].w;
                     }
                 }
             }
