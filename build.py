@@ -103,6 +103,18 @@ def build_runtime(force: bool = False) -> str:
     return out
 
 
+def build_sanitized_stress(sanitizer: str, out_dir: str = None) -> str:
+    """Host runtime (csrc/runtime/*.cpp) + csrc/tests/runtime_stress.cpp as one executable under
+    ``-fsanitize=<sanitizer>`` (host code only: "address,undefined" or "thread")."""
+    srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp"))) + [os.path.join(CSRC, "tests", "runtime_stress.cpp")]
+    tag = sanitizer.replace(",", "_")
+    out = os.path.join(out_dir or NATIVE, "runtime_stress_%s" % tag)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    _run([CXX, "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=%s" % sanitizer, "-pthread"]
+         + srcs + ["-o", out])
+    return out
+
+
 def build_all(force: bool = False, jobs: int = 8, kernels: bool = True) -> None:
     build_runtime(force)
     if kernels:

@@ -62,6 +62,9 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--profile", default=None, metavar="DIR",
                    help="torch.profiler trace of the run: DIR/trace_rank{r}.json + top-kernel table")
     g.add_argument("--log-level", default=os.environ.get("MRSUM_LOG_LEVEL", "INFO"))
+    g.add_argument("--debug-sync", action="store_true",
+                   help="debug mode: serialised kernels (AMD_SERIALIZE_KERNEL=3, HIP_LAUNCH_BLOCKING=1) and a "
+                        "device sync + error check after every HIP kernel launch, so a fault names its op")
     e = p.add_argument_group("local engine")
     e.add_argument("--dtype", choices=["bf16", "fp8"], default=None)
     e.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (ranks per model replica)")
@@ -192,6 +195,8 @@ async def async_main(args: argparse.Namespace) -> int:
 
 def main(argv: Optional[List[str]] = None) -> int:
     args = build_parser().parse_args(argv)
+    if args.debug_sync:  # must precede the first HIP call of the process
+        os.environ.update(AMD_SERIALIZE_KERNEL="3", HIP_LAUNCH_BLOCKING="1", MRSUM_DEBUG_SYNC="1")
     setup_logging(args.log_level)
     from .parallel.dist import init_distributed_from_env, shutdown
     init_distributed_from_env()

@@ -72,9 +72,19 @@ def _p(t: Optional[torch.Tensor]) -> Optional[int]:
     return None if t is None else t.data_ptr()
 
 
+DEBUG_SYNC = os.environ.get("MRSUM_DEBUG_SYNC", "0") == "1"
+
+
 def _check(rc: int, name: str) -> None:
     if rc != 0:
         raise RuntimeError("%s launch failed: hipError %d" % (name, rc))
+    if DEBUG_SYNC and not torch.cuda.is_current_stream_capturing():
+        # debug mode (cli --debug-sync): wait for the kernel so an asynchronous fault is reported here,
+        # against the op that caused it, instead of at some later synchronisation point
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:
+            raise RuntimeError("%s: device error after the launch: %s" % (name, e)) from e
 
 
 def _req(cond: bool, msg: str) -> None:

@@ -29,6 +29,20 @@ def _close(a, b, atol, rtol=2e-2):
     assert bad == 0, "max err %.4g (%d bad of %d)" % (err.max().item(), bad, a.numel())
 
 
+def test_debug_sync_mode(monkeypatch):
+    """--debug-sync: every launch is followed by a device sync + error check (and stays capturable)."""
+    monkeypatch.setattr(hip, "DEBUG_SYNC", True)
+    x, w = _rand(3, 512, seed=1), _rand(512, seed=2)
+    _close(hip.rmsnorm(x, w, 1e-5), reference.rmsnorm(x, w, 1e-5), 2e-2)
+    g = torch.cuda.CUDAGraph()
+    out = torch.empty_like(x)
+    with torch.cuda.graph(g):
+        hip.rmsnorm(x, w, 1e-5, out=out)
+    g.replay()
+    torch.cuda.synchronize()
+    _close(out, reference.rmsnorm(x, w, 1e-5), 2e-2)
+
+
 @pytest.mark.parametrize("T,D", [(1, 4096), (5, 4096), (3, 8192), (2, 256)])
 def test_rmsnorm(T, D):
     x = _rand(T, D, seed=1)
