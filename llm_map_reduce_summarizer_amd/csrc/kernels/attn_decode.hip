@@ -31,6 +31,13 @@
 
 constexpr int MAX_SPLITS = 64;
 
+// partial-result store: agent-scope atomic (global_store sc1, write-through) when a last-arriving
+// workgroup of another XCD will read it in the same launch (combine_if_last<G, true>), else plain
+__device__ __forceinline__ void st_part(float* p, float v, bool wt) {
+    if (wt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
 // Merge the S split partials of one (b, kv head) group -- G query heads x D -- with all 256
 // threads: the (max, sum) pairs are read in parallel into LDS and turned into per-split weights
 // once, then each output element sums S slabs with independent (unrolled) loads, so the merge
@@ -129,7 +136,11 @@ __device__ __forceinline__ void combine_group(const float* part_o, const float* 
 }
 
 // Publish this workgroup's partials and, if it is the last split of (b, kvh) to arrive, merge all S.
-template <int G>
+// WT (write-through publish): the partials were stored with agent-scope atomic stores (global_store sc1,
+// coherent at the device level once drained), so no release fence is needed -- the fence is a
+// buffer_wbl2 that writes back EVERY dirty line of this XCD's L2, i.e. the preceding GEMMs' split-K
+// slabs too, which is what made the fenced form lose inside the decode graph.
+template <int G, bool WT = false>
 __device__ __forceinline__ void combine_if_last(const float* part_o, const float* part_ml, int* counters,
                                                 bf16* out, int out_stride, int b, int kvh, int Hq, int Hkv, int S,
                                                 int* s_last, float* sw, float* sden) {
@@ -137,7 +148,7 @@ __device__ __forceinline__ void combine_if_last(const float* part_o, const float
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its slab stores
     __syncthreads();
     if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if constexpr (!WT) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const int prev = __hip_atomic_fetch_add(counters + b * Hkv + kvh, 1, __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT);
@@ -438,10 +449,10 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
     const size_t ml_base = ((size_t)b * Hq + (size_t)kvh * G) * S + split;
     if (ks >= ke) {
         if (tid < G) {
-            part_ml[(ml_base + (size_t)tid * S) * 2 + 0] = -INFINITY;
-            part_ml[(ml_base + (size_t)tid * S) * 2 + 1] = 0.f;
+            st_part(part_ml + (ml_base + (size_t)tid * S) * 2 + 0, -INFINITY, counters != nullptr);
+            st_part(part_ml + (ml_base + (size_t)tid * S) * 2 + 1, 0.f, counters != nullptr);
         }
-        if (counters) combine_if_last<G>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, c_last, c_sw, c_den);
+        if (counters) combine_if_last<G, true>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, c_last, c_sw, c_den);
         return;
     }
     const int ntiles = (ke - ks + PG - 1) / PG;
@@ -637,13 +648,13 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
             L += wt * sm_ml[64 + ww * 16 + h];
         }
         const size_t pi = ml_base + (size_t)h * S;
-        part_o[pi * D + d] = acc;
+        st_part(part_o + pi * D + d, acc, counters != nullptr);
         if (d == 0) {
-            part_ml[pi * 2 + 0] = M;
-            part_ml[pi * 2 + 1] = L;
+            st_part(part_ml + pi * 2 + 0, M, counters != nullptr);
+            st_part(part_ml + pi * 2 + 1, L, counters != nullptr);
         }
     }
-    if (counters) combine_if_last<G>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, c_last, c_sw, c_den);
+    if (counters) combine_if_last<G, true>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, c_last, c_sw, c_den);
 }
 
 static int launch_mfma(const void* q, int q_stride, const void* kcache, const void* vcache, const int* block_tables,

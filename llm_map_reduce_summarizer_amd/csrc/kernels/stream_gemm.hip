@@ -160,24 +160,24 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_gemm_kernel(const bf16* __
             } else if constexpr (EPI == EPI_F32_PARTIAL) {
                 float* o = reinterpret_cast<float*>(out) + ((size_t)blockIdx.y * M + mm) * ldo + nw + 4 * g;
                 *reinterpret_cast<float4*>(o) = make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
-            } else {
+            } else {  // write-through (global_store sc1): read by another XCD's last arriver, no release fence
                 float* o = parts + ((size_t)blockIdx.y * M + mm) * (gridDim.x * R) + nw + 4 * g;
-                *reinterpret_cast<float4*>(o) = make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+                    __hip_atomic_store(o + jj, acc[m][jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
     }
     if constexpr (EPI == EPI_SWIGLU_SPLIT) {
         // split-K SwiGLU: the last of the gridDim.y split workgroups of this column tile to arrive sums
-        // the fp32 partial tiles and applies silu(gate) * up (same publish / ticket / acquire protocol as
-        // attn_decode.hip combine_if_last; the ticket is re-armed for the next launch / graph replay).
+        // the fp32 partial tiles and applies silu(gate) * up (write-through publish / ticket / acquire, as
+        // attn_decode.hip combine_if_last<G, true>; the ticket is re-armed for the next launch / replay).
         // Lets a narrow gate_up projection (TP shards: N = 3584) fill the chip with split-K instead of
         // streaming its weights through N / (16 WPB) CUs.
         __shared__ int s_last;
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (tid == 0) {  // partials are write-through stores, drained above: no release fence (buffer_wbl2)
             const int prev = __hip_atomic_fetch_add(counters + blockIdx.x, 1, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT);
             s_last = prev == (int)gridDim.y - 1;

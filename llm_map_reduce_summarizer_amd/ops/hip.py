@@ -259,18 +259,20 @@ def decode_splits(batch: int, hkv: int, max_ctx: int, target_wgs: int = 1024, ma
     return s
 
 
-FUSED_COMBINE = os.environ.get("MRSUM_FUSED_COMBINE", "0")
+FUSED_COMBINE = os.environ.get("MRSUM_FUSED_COMBINE", "auto")
 
 
 def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
     """(splits, fused_combine) of the decode attention of ``batch`` sequences x ``hkv`` kv heads.
 
-    The in-launch merge by the last arriving split (MRSUM_FUSED_COMBINE=1, or "auto": at most 12
-    (sequence, kv head) groups, 16 splits) wins in isolation (tools/bench_tp_shard.py, attention + merge
-    per call at 4k context: TP=8 B=1 14.8 vs 17.8 us, TP=1 B=1 14.9 vs 18.0) but LOSES inside the decode
-    graph (step at 4k context: TP=8 B=1 1.555 vs 1.502 ms, TP=1 B=1 3.765 vs 3.715 ms): the agent-scope
-    release of every split writes back an L2 full of the preceding GEMMs' dirty slabs.  Off by default."""
-    fused = (batch * hkv <= 12) if FUSED_COMBINE == "auto" else FUSED_COMBINE == "1"
+    Fused = the split merge runs in the attention launch, by the last split of each (sequence, kv head)
+    to arrive; the splits publish their partials with write-through (sc1) stores, so no agent-scope
+    release fence is needed (the fenced form wrote back the whole L2, full of the preceding GEMMs'
+    slabs, and lost inside the decode graph: TP=8 B=1 1.555 vs 1.502 ms per step).  Write-through,
+    in the decode graph at 4k context (ms per step, fused vs separate merge kernel): TP=8 shard B=10
+    1.714 vs 1.772, B=39 2.391 vs 2.471; TP=1 B=1 / B=10 equal within noise.  "auto": fused for at most
+    64 (sequence, kv head) groups, capped at 16 splits (the merging workgroup reads S partials)."""
+    fused = (batch * hkv <= 64) if FUSED_COMBINE == "auto" else FUSED_COMBINE == "1"
     splits = decode_splits(batch, hkv, max_ctx)
     if fused:
         splits = min(splits, 16)
