@@ -447,10 +447,26 @@ class LLMEngine:
         s.imported = None  # release the staging buffer
         self.stats["imported_prefills"] = self.stats.get("imported_prefills", 0) + 1
 
+    def _prefill_isolated(self, batch: List[_Seq]) -> None:
+        """Prefill ``batch``; on a device out-of-memory error (activations of a long packed batch), retry
+        it as two halves, down to single sequences (SURVEY §5.3 failure isolation).  TP engines never
+        split: their ranks must issue the same collectives."""
+        try:
+            self._prefill(batch)
+            self._sync()
+        except torch.OutOfMemoryError:
+            if len(batch) == 1 or self.model.tp_size > 1:
+                raise
+            torch.cuda.empty_cache()
+            self.stats["prefill_oom_splits"] = self.stats.get("prefill_oom_splits", 0) + 1
+            log.warning("prefill of %d sequences ran out of device memory: retrying as two halves", len(batch))
+            half = len(batch) // 2
+            self._prefill_isolated(batch[:half])
+            self._prefill_isolated(batch[half:])
+
     def _run_prefill(self, batch: List[_Seq], active: List[_Seq]) -> None:
         t0 = time.perf_counter()
-        self._prefill(batch)
-        self._sync()
+        self._prefill_isolated(batch)
         self.stats["prefill_s"] += time.perf_counter() - t0
         active.extend(batch)
         if self._on_prefill is not None:

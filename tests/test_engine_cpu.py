@@ -188,3 +188,33 @@ def test_prefill_export_import_roundtrip():
     # a request that is complete after its first token never reaches the decode loop
     one = b.generate(prompts[:1], [SamplingParams(1, 0.3, 40)], imported={0: ImportedPrefill(firsts[0], None)})
     assert one[0].token_ids == [firsts[0]] and one[0].finish_reason == "length"
+
+
+def test_prefill_oom_is_isolated(monkeypatch):
+    """A device OOM in a packed prefill is retried as halves (down to one sequence) with the same
+    results; a single sequence that still does not fit re-raises."""
+    e = LLMEngine(get_model_config("tiny", init_std=0.05), device="cpu", max_model_len=512, max_num_seqs=8,
+                  kv_pages=64, sync_every=3, max_prefill_tokens=4096)
+    ps = [SamplingParams(4, 0.3, 20 + i) for i in range(5)]
+    ref = e.generate(_prompts(), ps)
+    real = e._prefill
+    calls = []
+
+    def flaky(seqs):
+        calls.append(len(seqs))
+        if len(seqs) > 2:
+            raise torch.OutOfMemoryError("simulated HIP out of memory")
+        return real(seqs)
+
+    monkeypatch.setattr(e, "_prefill", flaky)
+    got = e.generate(_prompts(), ps)
+    assert [o.token_ids for o in got] == [o.token_ids for o in ref]
+    assert calls[:3] == [5, 2, 3] and e.stats["prefill_oom_splits"] == 2  # 5 -> 2 + 3 -> 2 + (1 + 2)
+    assert e.kv.alloc.available() == e.kv.num_pages - 1
+
+    def always(seqs):
+        raise torch.OutOfMemoryError("simulated HIP out of memory")
+
+    monkeypatch.setattr(e, "_prefill", always)
+    with pytest.raises(torch.OutOfMemoryError):
+        e.generate(_prompts(1), ps[:1])
