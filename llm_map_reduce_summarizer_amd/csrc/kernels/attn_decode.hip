@@ -421,7 +421,14 @@ __device__ __forceinline__ void rope_slab_sums(const RopeArgs& ra, const float* 
     __syncthreads();
 }
 
-template <int G, bool ROPE>
+// KV page loads: nontemporal (each page is read once per step by one workgroup) when NT
+template <bool NT>
+__device__ __forceinline__ u32x4 ld_kv(const bf16* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    else return *reinterpret_cast<const u32x4*>(p);
+}
+
+template <int G, bool ROPE, bool NT = false>
 __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
     const bf16* __restrict__ q, int q_stride, bf16* __restrict__ kc, bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ positions,
@@ -509,8 +516,8 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
         const size_t base = (size_t)bt[0] * Hkv * PG * D + head_off;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            kreg[i] = *reinterpret_cast<const u32x4*>(kc + base + (size_t)16 * i * D);
-            vreg[i] = *reinterpret_cast<const u32x4*>(vc + base + (size_t)16 * i * D);
+            kreg[i] = ld_kv<NT>(kc + base + (size_t)16 * i * D);
+            vreg[i] = ld_kv<NT>(vc + base + (size_t)16 * i * D);
         }
     }
     // Q^T fragments (B operand of 16x16x32): lane holds Q[head col][dims 32k + 8grp .. +8]; built
@@ -573,8 +580,8 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
             const size_t base = (size_t)bt[tn] * Hkv * PG * D + head_off;
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                kreg[i] = *reinterpret_cast<const u32x4*>(kc + base + (size_t)16 * i * D);
-                vreg[i] = *reinterpret_cast<const u32x4*>(vc + base + (size_t)16 * i * D);
+                kreg[i] = ld_kv<NT>(kc + base + (size_t)16 * i * D);
+                vreg[i] = ld_kv<NT>(vc + base + (size_t)16 * i * D);
             }
         }
         const int key0 = ks + t * PG + 16 * w;  // this wave's 16 keys
@@ -657,6 +664,13 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
     if (counters) combine_if_last<G, true>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, c_last, c_sw, c_den);
 }
 
+static int g_attn_nt = 2;
+
+// KV page load policy of the MFMA decode attention: 0 default, 1 nontemporal, 2 (auto) nontemporal for
+// >= 64 (sequence, kv head) groups -- measured, step at 4k context: B=39 x 8 kv heads 7.02-7.05 vs
+// 7.18-7.26 ms; B <= 10 0.7-1 % slower with nt (profiles/r1_decode_nt_ab.jsonl)
+MRSUM_API void mrsum_attn_decode_set_nt(int mode) { g_attn_nt = mode; }
+
 static int launch_mfma(const void* q, int q_stride, const void* kcache, const void* vcache, const int* block_tables,
                        int bt_stride, const int* positions, void* part_o, void* part_ml, void* out, int out_stride,
                        int B, int Hq, int Hkv, int D, int P, int S, float scale, const RopeArgs* rope, int* counters,
@@ -669,9 +683,17 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
     auto Qp = (const bf16*)q; auto K = (bf16*)kcache; auto V = (bf16*)vcache;
     auto PO = (float*)part_o; auto PM = (float*)part_ml;
     const RopeArgs ra = rope ? *rope : RopeArgs{nullptr, 0, 0, 0, 0, nullptr};
-#define MFMA_L(G_, R_) attn_decode_mfma_kernel<G_, R_><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, \
+#define MFMA_L(G_, R_)                                                                                        \
+    do {                                                                                                      \
+        if (g_attn_nt == 1 || (g_attn_nt == 2 && B * Hkv >= 64))                                            \
+            attn_decode_mfma_kernel<G_, R_, true><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, \
                                                                          positions, PO, PM, Hkv, S, sl, ra, counters, \
-                                                                         (bf16*)out, out_stride)
+                                                                         (bf16*)out, out_stride);             \
+        else                                                                                                  \
+            attn_decode_mfma_kernel<G_, R_, false><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, \
+                                                                          positions, PO, PM, Hkv, S, sl, ra, counters, \
+                                                                          (bf16*)out, out_stride);            \
+    } while (0)
 #define MFMA_G(R_)                            \
     switch (G) {                              \
         case 1: MFMA_L(1, R_); break;         \

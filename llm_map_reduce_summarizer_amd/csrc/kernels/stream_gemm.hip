@@ -48,13 +48,17 @@ __device__ __forceinline__ int img_off(int row, int chunk) {
     return (((row >> 3) << 1) + (chunk >> 3)) * 1024 + ((row & 7) << 7) + ((((chunk & 7) ^ (row & 7))) << 4);
 }
 
+template <int AUX = 0>
 __device__ __forceinline__ void glds16(const void* g, char* lds) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
-                                     (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+                                     (__attribute__((address_space(3))) void*)lds, 16, 0, AUX);
 }
 }  // namespace
 
-template <int MT, int EPI, int WPB>
+// NTW: weight pieces loaded with the nontemporal policy (aux = 2): decode weights are read once per
+// step by one CU (MI355X_MICROARCH.md "nt-weights"); the x pieces keep the default policy (re-read by
+// every column tile from L2).
+template <int MT, int EPI, int WPB, bool NTW>
 __global__ __launch_bounds__(64 * WPB, 1) void stream_gemm_kernel(const bf16* __restrict__ x, int ldx,
                                                                   const bf16* __restrict__ W, int K, int M,
                                                                   void* __restrict__ out, int ldo, int kper,
@@ -96,7 +100,7 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_gemm_kernel(const bf16* __
 #define ISSUE(slot, kb)                                                                              \
     {                                                                                                \
         char* base = lds + (slot) * SLOT;                                                            \
-        _Pragma("unroll") for (int p = 0; p < 4; ++p) glds16(wsrc[p] + (kb), base + (4 * w + p) * 1024); \
+        _Pragma("unroll") for (int p = 0; p < 4; ++p) glds16<NTW ? 2 : 0>(wsrc[p] + (kb), base + (4 * w + p) * 1024); \
         _Pragma("unroll") for (int i = 0; i < XI; ++i)                                               \
             glds16(xsrc[i] + (kb), xdst[i] >= 0 ? base + xdst[i] : lds + D * SLOT);                  \
     }
@@ -214,6 +218,11 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_gemm_kernel(const bf16* __
 
 // out: bf16 [M, ldo] (EPI_BF16), fp32 slabs [splits, M, ldo] (EPI_F32_PARTIAL) or bf16 [M, ldo] of
 // N/2 SwiGLU features (EPI_SWIGLU, splits = 1).  N % (16 wpb) == 0, wpb in {4, 5, 6, 7, 8}.
+static int g_stream_nt = 1;
+
+// 1: nontemporal weight loads (default), 0: default cache policy (A/B switch for tools/ and tests)
+MRSUM_API void mrsum_stream_gemm_set_nt(int on) { g_stream_nt = on ? 1 : 0; }
+
 static int launch_stream_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
                               int epi, int splits, int wpb, float* parts, int* counters, hipStream_t s) {
     if (M <= 0) return 0;
@@ -226,8 +235,15 @@ static int launch_stream_gemm(const void* x, int ldx, const void* W, int N, int 
     dim3 grid(N / (16 * wpb), splits), block(64 * wpb);
     auto X = (const bf16*)x;
     auto Wp = (const bf16*)W;
-#define L(MT_, EPI_, WPB_) \
-    stream_gemm_kernel<MT_, EPI_, WPB_><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, parts, counters)
+#define L(MT_, EPI_, WPB_)                                                                                   \
+    do {                                                                                                     \
+        if (g_stream_nt)                                                                                     \
+            stream_gemm_kernel<MT_, EPI_, WPB_, true><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, \
+                                                                             parts, counters);               \
+        else                                                                                                 \
+            stream_gemm_kernel<MT_, EPI_, WPB_, false><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, \
+                                                                              parts, counters);              \
+    } while (0)
 #define BY_WPB(MT_, EPI_)                          \
     switch (wpb) {                                 \
         case 4: L(MT_, EPI_, 4); break;            \

@@ -51,12 +51,23 @@ _SIGS = {
 }
 
 _fns = {}
+# stream GEMM weight loads with the nontemporal policy (1, default) or the default policy (0)
+STREAM_NT = os.environ.get("MRSUM_STREAM_NT", "1") == "1"
+# decode attention KV page loads: 0 default policy, 1 nontemporal, 2 nontemporal for >= 64 groups (auto)
+ATTN_NT = int(os.environ.get("MRSUM_ATTN_NT", "2"))
 
 
 def _fn(name: str):
     f = _fns.get(name)
     if f is None:
         lib = kernels_lib()
+        if not _fns:  # first use of the library in this process: apply the launch-policy switches
+            lib.mrsum_stream_gemm_set_nt.argtypes = [_c_int]
+            lib.mrsum_stream_gemm_set_nt.restype = None
+            lib.mrsum_stream_gemm_set_nt(1 if STREAM_NT else 0)
+            lib.mrsum_attn_decode_set_nt.argtypes = [_c_int]
+            lib.mrsum_attn_decode_set_nt.restype = None
+            lib.mrsum_attn_decode_set_nt(ATTN_NT)
         f = getattr(lib, name)
         f.argtypes = _SIGS[name]
         f.restype = ctypes.c_int
