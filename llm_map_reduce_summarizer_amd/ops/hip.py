@@ -627,13 +627,16 @@ def plan(role: str, M: int, N: int, K: int, splits: Optional[int] = None, stream
     cfg = stream_config(N, K, swiglu=(role == "gate_up"), splits=splits) if stream and STREAM_GEMM else None
     if cfg is not None:
         return ("stream",) + cfg
-    if role == "gate_up" and stream and STREAM_GEMM and SWIGLU_SPLIT and M > 16 and N % 128 == 0 \
-            and (K // 128) % 4 == 0:
-        # narrow gate_up (TP shards, N = 3584 / 7168) at M > 16: split-K over the column tiles, SwiGLU by the
-        # last split to arrive (tools/bench_tp_shard.py, us: TP=4 M=39 23.8 vs hipBLASLt + SwiGLU 28.2 vs
-        # register-streaming 29.4; TP=8 M=39 15.4 vs 15.7).  At M <= 16 the register-streaming kernel
-        # wins (TP=8 M=1 9.7 vs 11.5; M=10 9.9 vs 12.2; the LDS-x kernel took 39).
-        return ("stream_split", 8, 4)
+    if role == "gate_up" and stream and STREAM_GEMM and SWIGLU_SPLIT and (K // 128) % 4 == 0:
+        # narrow gate_up (TP shards) that the one-tile-per-CU stream kernel cannot fill: split-K over the
+        # column tiles, SwiGLU by the last split to arrive -- where it beats the register-streaming kernel
+        # (tools/bench_tp_shard.py with write-through partials, us: TP=4 N=7168 M=10 15.7 vs 17.0, M=39
+        # 21.2 vs 29.4 (M=1 14.9 vs 14.4: skinny); TP=8 N=3584 M=39 15.2 vs 15.8, M <= 10 12.2-12.8 vs
+        # 10.3: skinny)
+        if N >= 7168 and N % 112 == 0 and M > 8:
+            return ("stream_split", 7, 4)
+        if N % 64 == 0 and M > 32:
+            return ("stream_split", 4, 4)
     blocks = K // 128
 
     def div(s):

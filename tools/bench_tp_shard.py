@@ -31,10 +31,11 @@ def main():
     dev = "cuda:0"
     tps = [int(t) for t in os.environ.get("TPS", "8,4,1").split(",")]
     do_gemm = os.environ.get("GEMM", "1") == "1"
+    do_attn = os.environ.get("ATTN", "1") == "1"
     ctx = int(os.environ.get("CTX", "4000"))
     for tp in tps:
         hq, hkv, d, page = 32 // tp, 8 // tp, 128, 64
-        for B in (1, 10, 39):
+        for B in ((1, 10, 39) if do_attn else ()):
             npg = -(-ctx // page) + 1
             n_pages = B * npg + 1
             kc = torch.randn(n_pages, hkv, page, d, device=dev, dtype=torch.bfloat16)
