@@ -26,7 +26,7 @@ import math
 import os
 import time
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from typing import Tuple, Dict, List, Optional, Sequence
 
 import torch
 
@@ -159,10 +159,13 @@ class LLMEngine:
             # replay them eagerly instead (RCCL stays outside any capture)
             log.warning("TP=%d without the custom all-reduce: decode hipGraphs disabled", self.model.tp_size)
             self.use_graphs = False
-        self._graphs: Dict[int, "torch.cuda.CUDAGraph"] = {}
+        # decode graphs / attention workspaces per (batch bucket, context class): the attention's split
+        # plan depends on how long the contexts get (ops.hip.decode_attn_plan)
+        self._graphs: Dict[Tuple[int, int], "torch.cuda.CUDAGraph"] = {}
+        self._ctx_cls = 0
         self._on_prefill = None
         self.pad_prefill = os.environ.get("MRSUM_PAD_PREFILL", "1") == "1"
-        self._workspaces: Dict[int, object] = {}
+        self._workspaces: Dict[Tuple[int, int], object] = {}
         self.stats = {"prefill_tokens": 0, "prefill_s": 0.0, "decode_steps": 0, "decode_tokens": 0,
                       "decode_s": 0.0, "generate_calls": 0, "graph_captures": 0, "peak_active": 0}
 
@@ -173,16 +176,22 @@ class LLMEngine:
                 return min(b, self.max_num_seqs)
         return self.max_num_seqs
 
+    def _ctx_classes(self) -> int:
+        """Number of context classes this engine can reach (ops.hip.CTX_CLASSES up to max_model_len)."""
+        from ..ops.hip import ctx_class
+        return ctx_class(self.max_model_len) + 1
+
     def _workspace(self, B: int):
         if self.device.type != "cuda":
             return None
-        ws = self._workspaces.get(B)
+        key = (B, self._ctx_cls)
+        ws = self._workspaces.get(key)
         if ws is None:
-            from ..ops.hip import DecodeWorkspace, decode_attn_plan
-            s, fused = decode_attn_plan(B, self.model.hkv, self.max_model_len)
+            from ..ops.hip import CTX_CLASSES, DecodeWorkspace, decode_attn_plan
+            s, fused = decode_attn_plan(B, self.model.hkv, min(CTX_CLASSES[self._ctx_cls], self.max_model_len))
             ws = DecodeWorkspace(B, self.model.hq, self.cfg.head_dim, s, self.device, self.model.hkv,
                                  fused_combine=fused)
-            self._workspaces[B] = ws
+            self._workspaces[key] = ws
         return ws
 
     def _sync(self) -> None:
@@ -262,7 +271,7 @@ class LLMEngine:
             for _ in range(steps):
                 self._decode_once(B)
             return
-        g = self._graphs.get(B)
+        g = self._graphs.get((B, self._ctx_cls))
         if g is None:
             g = self._capture(B)
         for _ in range(steps):
@@ -275,12 +284,20 @@ class LLMEngine:
         if not self.use_graphs:
             return 0
         n = 0
-        for B in BUCKETS:
-            if B > min(max_batch or self.max_num_seqs, self.max_num_seqs):
-                break
-            if B not in self._graphs:
-                self._capture(B)
-                n += 1
+        keep = self._ctx_cls
+        try:
+            for B in BUCKETS:
+                if B > min(max_batch or self.max_num_seqs, self.max_num_seqs):
+                    break
+                # every context class for single-sequence steps (a final reduce over a long prompt), the
+                # short class for batches
+                for cls in range(self._ctx_classes() if B == 1 else 1):
+                    self._ctx_cls = cls
+                    if (B, cls) not in self._graphs:
+                        self._capture(B)
+                        n += 1
+        finally:
+            self._ctx_cls = keep
         self._sync()
         return n
 
@@ -302,7 +319,7 @@ class LLMEngine:
         # capture does not execute; restore anyway in case the backend ran the work
         for f, t in snap.items():
             getattr(st, f)[:B].copy_(t)
-        self._graphs[B] = g
+        self._graphs[(B, self._ctx_cls)] = g
         self.stats["graph_captures"] += 1
         return g
 
@@ -355,6 +372,9 @@ class LLMEngine:
             waiting.append(s)
         # longest first: better packing and no late long straggler
         waiting.sort(key=lambda s: -(len(s.prompt) + s.params.max_new_tokens))
+        if waiting and self.device.type == "cuda":
+            from ..ops.hip import ctx_class
+            self._ctx_cls = ctx_class(len(waiting[0].prompt) + waiting[0].params.max_new_tokens)
         active: List[_Seq] = []
         st = self.state
         while waiting or active:

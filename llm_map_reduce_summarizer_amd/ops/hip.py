@@ -273,18 +273,37 @@ def decode_splits(batch: int, hkv: int, max_ctx: int, target_wgs: int = 1024, ma
 FUSED_COMBINE = os.environ.get("MRSUM_FUSED_COMBINE", "auto")
 
 
-def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
-    """(splits, fused_combine) of the decode attention of ``batch`` sequences x ``hkv`` kv heads.
+CTX_CLASSES = (6144, 12288, 32768, 1 << 30)  # decode context classes (tokens): graphs / split plans per class
 
-    Fused = the split merge runs in the attention launch, by the last split of each (sequence, kv head)
-    to arrive; the splits publish their partials with write-through (sc1) stores, so no agent-scope
-    release fence is needed (the fenced form wrote back the whole L2, full of the preceding GEMMs'
-    slabs, and lost inside the decode graph: TP=8 B=1 1.555 vs 1.502 ms per step).  Write-through,
-    in the decode graph at 4k context (ms per step, fused vs separate merge kernel): TP=8 shard B=10
-    1.714 vs 1.772, B=39 2.391 vs 2.471; TP=1 B=1 / B=10 equal within noise.  "auto": fused for at most
-    64 (sequence, kv head) groups, capped at 16 splits (the merging workgroup reads S partials)."""
-    fused = (batch * hkv <= 64) if FUSED_COMBINE == "auto" else FUSED_COMBINE == "1"
-    splits = decode_splits(batch, hkv, max_ctx)
+
+def ctx_class(ctx: int) -> int:
+    """Index of the context class holding ``ctx`` tokens (0: <= 6k, 1: <= 12k, 2: <= 32k, 3: longer)."""
+    for i, c in enumerate(CTX_CLASSES):
+        if ctx <= c:
+            return i
+    return len(CTX_CLASSES) - 1
+
+
+def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
+    """(splits, fused_combine) of the decode attention of ``batch`` sequences x ``hkv`` kv heads whose
+    contexts reach ``max_ctx`` tokens (the engine passes its context class's upper bound).
+
+    Splits: enough (sequence, kv head, split) workgroups to fill the chip (~1024), about 4 pages per split
+    (each workgroup walks its pages serially: at B=1 and ~11k context 16 splits of 11 pages ran at
+    1.7 TB/s), at most 64.  Fused = the split merge runs in the attention launch, by the last split of
+    each (sequence, kv head) to arrive, with write-through (sc1) partial stores and no release fence
+    (the fenced form wrote back the whole L2, full of the preceding GEMMs' slabs, and lost in the decode
+    graph: TP=8 B=1 1.555 vs 1.502 ms per step); write-through, in the decode graph at 4k context (ms
+    per step, fused vs separate merge kernel): TP=8 shard B=10 1.714 vs 1.772, B=39 2.391 vs 2.471,
+    TP=1 B=1 / B=10 equal within noise.  "auto": fused for at most 64 (sequence, kv head) groups and at
+    most 24 splits (the merging workgroup reads every split's partials)."""
+    pages = max(1, -(-max_ctx // 64))
+    groups = max(1, batch * hkv)
+    splits = max(1, min(-(-1024 // groups), -(-pages // 4), 64))
+    if FUSED_COMBINE == "auto":
+        fused = groups <= 64 and splits <= 24
+    else:
+        fused = FUSED_COMBINE == "1"
     if fused:
         splits = min(splits, 16)
     return splits, fused
