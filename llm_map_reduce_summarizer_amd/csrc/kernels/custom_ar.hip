@@ -52,6 +52,22 @@ __device__ __forceinline__ void st_release_sys(unsigned* p, unsigned v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Write-through publish (WT): payload stored with system-scope relaxed atomic stores (global_store
+// sc0 sc1: coherent at system scope once acknowledged), every store drained (s_waitcnt vmcnt(0)),
+// then a relaxed system-scope flag store.  The fenced form (release fence + release flag store)
+// emits two buffer_wbl2, each writing back EVERY dirty line of this XCD's L2 -- inside a decode graph
+// the preceding GEMM's split-K slabs -- for a payload that lives in uncached memory and never
+// touches L2.  (The same drained-payload-then-flag hand-off as attn_decode.hip's write-through merge;
+// cdna_hip_programming.md / MI355X_MICROARCH.md "handoff-flag".)
+__device__ __forceinline__ void st_wt8(void* p, unsigned long long v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void st_flag(unsigned* p, unsigned v, bool wt) {
+    if (wt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else st_release_sys(p, v);
+}
+
 // Spin (relaxed system-scope loads, s_sleep between polls) until *f >= epoch, bounded in WALL time by
 // the 100 MHz s_memrealtime counter: ranks are launched by independent host threads and may lag each
 // other by host-side jitter (GC, logging, a first hipBLASLt call), so the bound is generous (4 s) but
@@ -77,7 +93,7 @@ enum { OP_SUM_F32 = 0, OP_MAX_U64 = 1 };
 
 // Block b always owns bytes [b * CH, (b + 1) * CH) of a message, whatever the op and size, so the
 // slot-reuse argument above holds per block across calls of different kinds.
-template <int OP>
+template <int OP, bool WT>
 __global__ __launch_bounds__(256) void ar_oneshot_kernel(Peers peers, int rank, int world, size_t slot_bytes,
                                                          const char* __restrict__ in, char* __restrict__ out,
                                                          size_t nbytes, unsigned* __restrict__ epochs,
@@ -94,17 +110,24 @@ __global__ __launch_bounds__(256) void ar_oneshot_kernel(Peers peers, int rank, 
     // 1. my slice -> my slot
     char* mine = peers.base[rank] + off;
     for (size_t i = b0 + (size_t)tid * VB; i < b1; i += 256 * VB) {
-        if constexpr (VB == 16) *reinterpret_cast<float4*>(mine + i) = *reinterpret_cast<const float4*>(in + i);
-        else *reinterpret_cast<unsigned long long*>(mine + i) = *reinterpret_cast<const unsigned long long*>(in + i);
+        if constexpr (WT) {
+            const unsigned long long* src = reinterpret_cast<const unsigned long long*>(in + i);
+#pragma unroll
+            for (int k = 0; k < VB / 8; ++k) st_wt8(mine + i + 8 * k, src[k]);
+        } else if constexpr (VB == 16) {
+            *reinterpret_cast<float4*>(mine + i) = *reinterpret_cast<const float4*>(in + i);
+        } else {
+            *reinterpret_cast<unsigned long long*>(mine + i) = *reinterpret_cast<const unsigned long long*>(in + i);
+        }
     }
     // every wave retires its own slot stores at system scope before the flag can be published
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if constexpr (!WT) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // 2. announce to every rank
     if (tid < world) {
         unsigned* f = reinterpret_cast<unsigned*>(peers.base[tid]) + b * MAX_RANKS + rank;
-        st_release_sys(f, epoch);
+        st_flag(f, epoch, WT);
     }
     // 3. wait for every rank's slice b (relaxed polling, one acquire after: the invalidate it
     //    implies runs once, and covers the whole block's later reads through the barrier)
@@ -161,7 +184,7 @@ __global__ __launch_bounds__(256) void ar_oneshot_kernel(Peers peers, int rank, 
 // passing call e+1's wait for row r, which needs my flag of call e+1, i.e. my call e is complete.
 constexpr size_t push_off(size_t slot_bytes) { return HDR + 2 * slot_bytes; }
 
-template <int VPT>  // float4 vectors per thread: D <= 1024 * VPT
+template <int VPT, bool WT>  // float4 vectors per thread: D <= 1024 * VPT
 __global__ __launch_bounds__(256) void ar_add_rmsnorm_kernel(Peers peers, int rank, int world, size_t slot_bytes,
                                                              const float* __restrict__ parts, int S, int T,
                                                              bf16* __restrict__ residual, const bf16* __restrict__ w,
@@ -197,15 +220,18 @@ __global__ __launch_bounds__(256) void ar_add_rmsnorm_kernel(Peers peers, int ra
 #pragma unroll
         for (int i = 0; i < VPT; ++i) {
             const int c = tid + i * 256;
-            if (c < nv) dst[c] = pv[i];
+            if (c < nv) {
+                if constexpr (WT) st_wt8(dst + c, __builtin_bit_cast(unsigned long long, pv[i]));
+                else dst[c] = pv[i];
+            }
         }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if constexpr (!WT) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid < world) {
         unsigned* f = reinterpret_cast<unsigned*>(peers.base[tid] + PUSH_FLAGS) + row * MAX_RANKS + rank;
-        st_release_sys(f, epoch);
+        st_flag(f, epoch, WT);
     }
     if (tid < world) {
         const unsigned* f = reinterpret_cast<const unsigned*>(peers.base[rank] + PUSH_FLAGS) + row * MAX_RANKS + tid;
@@ -258,18 +284,28 @@ __global__ __launch_bounds__(256) void ar_add_rmsnorm_kernel(Peers peers, int ra
     if (tid == 0) epochs[row] = epoch;
 }
 
+static int g_ar_wt = 1;
+
+// 1 (default): write-through publish (no release fences), 0: fenced publish (A/B switch)
+MRSUM_API void mrsum_ar_set_wt(int on) { g_ar_wt = on ? 1 : 0; }
+
 static int launch_ar(ArHandle* h, int op, const void* in, void* out, size_t nbytes, hipStream_t s) {
     if (nbytes == 0) return 0;
     if (nbytes > h->max_bytes || nbytes > (size_t)MAX_BLOCKS * CH) return (int)hipErrorInvalidValue;
     for (int r = 0; r < h->world; ++r)
         if (!h->peers.base[r]) return (int)hipErrorInvalidValue;
     const int nblk = (int)((nbytes + CH - 1) / CH);
-    if (op == OP_SUM_F32)
-        ar_oneshot_kernel<OP_SUM_F32><<<nblk, 256, 0, s>>>(h->peers, h->rank, h->world, h->max_bytes,
-                                                           (const char*)in, (char*)out, nbytes, h->epochs, h->error);
-    else
-        ar_oneshot_kernel<OP_MAX_U64><<<nblk, 256, 0, s>>>(h->peers, h->rank, h->world, h->max_bytes,
-                                                           (const char*)in, (char*)out, nbytes, h->epochs, h->error);
+#define AR_ONE(OP_, WT_)                                                                                 \
+    ar_oneshot_kernel<OP_, WT_><<<nblk, 256, 0, s>>>(h->peers, h->rank, h->world, h->max_bytes, (const char*)in, \
+                                                     (char*)out, nbytes, h->epochs, h->error)
+    if (op == OP_SUM_F32) {
+        if (g_ar_wt) AR_ONE(OP_SUM_F32, true);
+        else AR_ONE(OP_SUM_F32, false);
+    } else {
+        if (g_ar_wt) AR_ONE(OP_MAX_U64, true);
+        else AR_ONE(OP_MAX_U64, false);
+    }
+#undef AR_ONE
     return (int)hipGetLastError();
 }
 
@@ -354,13 +390,20 @@ MRSUM_API int mrsum_ar_add_rmsnorm(void* hv, const void* parts, int S, int T, vo
         if (!h->peers.base[r]) return (int)hipErrorInvalidValue;
     const int vpt = (D / 4 + 255) / 256;
     auto P = (const float*)parts; auto R = (bf16*)residual; auto W = (const bf16*)w; auto O = (bf16*)out;
-#define AR_NORM(V) ar_add_rmsnorm_kernel<V><<<T, 256, 0, s>>>(h->peers, h->rank, h->world, h->max_bytes, P, S, T, R, \
-                                                            W, O, D, out_stride, eps, h->push_epochs, h->error)
+#define AR_NORM_(V, WT_)                                                                                     \
+    ar_add_rmsnorm_kernel<V, WT_><<<T, 256, 0, s>>>(h->peers, h->rank, h->world, h->max_bytes, P, S, T, R, W, O, D, \
+                                                    out_stride, eps, h->push_epochs, h->error)
+#define AR_NORM(V)                  \
+    do {                            \
+        if (g_ar_wt) AR_NORM_(V, true); \
+        else AR_NORM_(V, false);    \
+    } while (0)
     if (vpt <= 1) AR_NORM(1);
     else if (vpt <= 2) AR_NORM(2);
     else if (vpt <= 4) AR_NORM(4);
     else AR_NORM(8);
 #undef AR_NORM
+#undef AR_NORM_
     return (int)hipGetLastError();
 }
 
