@@ -26,7 +26,7 @@ import math
 import os
 import time
 from dataclasses import dataclass, field
-from typing import Tuple, Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
