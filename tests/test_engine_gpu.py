@@ -85,3 +85,16 @@ def test_padded_prefill_matches_unpadded(eng):
         eng.pad_prefill = True
     same = sum(x.token_ids == y.token_ids for x, y in zip(a, b))
     assert same >= len(prompts) - 1  # a bf16 near-tie may flip one sequence
+
+
+def test_long_context_class_graphs():
+    """Prompts in the 6k-12k and 12k-32k context classes run on their own decode graphs (attention split
+    plans per class) and agree with teacher-forced prefill, like the short class."""
+    e = LLMEngine(get_model_config("tiny-gqa4", init_std=0.05, max_position=40960), device="cuda:0",
+                  max_model_len=40960, max_num_seqs=4, kv_pages=1400, sync_every=8)
+    for n in (7000, 20000):
+        p = [128000] + [(j * 29 + n) % 120000 + 5 for j in range(n)]
+        out = e.generate([p], [SamplingParams(6, 0.0, 0)])[0]
+        assert (1, 1 if n < 12288 else 2) in e._graphs
+        nxt = e.generate([p + out.token_ids[:-1]], [SamplingParams(1, 0.0, 0)])[0].token_ids[0]
+        assert nxt == out.token_ids[-1]
