@@ -53,6 +53,9 @@ _SIGS = {
 _fns = {}
 # stream GEMM weight loads with the nontemporal policy (1, default) or the default policy (0)
 STREAM_NT = os.environ.get("MRSUM_STREAM_NT", "1") == "1"
+# prefill attention softmax in packed fp32 (v_pk_fma_f32 / v_pk_add_f32) (1) or scalar (0, default: packed
+# measured 1-3 % slower, profiles/r1_prefill_packed_softmax_ab.jsonl -- the kernel is not VALU-issue bound)
+PREFILL_PK = os.environ.get("MRSUM_PREFILL_PK", "0") == "1"
 # decode attention KV page loads: 0 default policy, 1 nontemporal, 2 nontemporal for >= 64 groups (auto)
 ATTN_NT = int(os.environ.get("MRSUM_ATTN_NT", "2"))
 
@@ -68,6 +71,9 @@ def _fn(name: str):
             lib.mrsum_attn_decode_set_nt.argtypes = [_c_int]
             lib.mrsum_attn_decode_set_nt.restype = None
             lib.mrsum_attn_decode_set_nt(ATTN_NT)
+            lib.mrsum_attn_prefill_set_pk.argtypes = [_c_int]
+            lib.mrsum_attn_prefill_set_pk.restype = None
+            lib.mrsum_attn_prefill_set_pk(1 if PREFILL_PK else 0)
         f = getattr(lib, name)
         f.argtypes = _SIGS[name]
         f.restype = ctypes.c_int

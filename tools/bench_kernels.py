@@ -64,7 +64,7 @@ def main():
         del ws
     # decode attention: B seqs x ctx, Llama-3-8B kv layout
     hq, hkv, d, page = 32, 8, 128, 64
-    for B, ctx in ((1, 8192), (8, 4096), (39, 4400), (64, 2048)):
+    for B, ctx in (((1, 8192), (8, 4096), (39, 4400), (64, 2048)) if os.environ.get("DECODE", "1") == "1" else ()):
         npg = -(-ctx // page)
         kc = torch.randn(B * npg + 1, hkv, page, d, device=dev, dtype=torch.bfloat16)
         vc = torch.randn_like(kc)
@@ -82,7 +82,7 @@ def main():
                                            "TBps": round(gb / t / 1e3, 2)})
                 print(json.dumps(res["attn_decode"][-1]), flush=True)
     # prefill attention
-    for nseq, L in ((1, 4096), (8, 4096), (4, 8192)):
+    for nseq, L in ((1, 4096), (8, 4096), (4, 8192), (1, 32768)):
         T = nseq * L
         qkv = torch.randn(T, (hq + 2 * hkv) * d, device=dev, dtype=torch.bfloat16)
         cu = torch.arange(0, T + 1, L, dtype=torch.int32, device=dev)
@@ -90,7 +90,8 @@ def main():
         t = timeit(lambda: hip.attn_prefill(qkv, cu, hq, hkv, d, 1 / math.sqrt(d), items=items, seqlens=[L] * nseq),
                    iters=20)
         fl = nseq * 4 * L * L / 2 * d * hq
-        res["attn_prefill"].append({"nseq": nseq, "L": L, "ms": round(t * 1e3, 3), "TFLOPs": round(fl / t / 1e12, 1)})
+        res["attn_prefill"].append({"nseq": nseq, "L": L, "ms": round(t * 1e3, 3), "TFLOPs": round(fl / t / 1e12, 1),
+                                    "packed_softmax": hip.PREFILL_PK})
         print(json.dumps(res["attn_prefill"][-1]), flush=True)
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/bench_kernels.json", "w") as f:
