@@ -708,6 +708,13 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
 #undef MFMA_L
     int e = (int)hipGetLastError();
     if (e || counters) return e;
+    if (S > 16) {
+        // many splits (long contexts): one merge workgroup per query head instead of per kv-head group,
+        // G x more workgroups with G x fewer partial loads each (B=1, 11k context, S=48: 8 workgroups
+        // took 10 us)
+        attn_decode_combine_kernel<1><<<B * Hq, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hq, S);
+        return (int)hipGetLastError();
+    }
     switch (G) {
         case 1: attn_decode_combine_kernel<1><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
         case 2: attn_decode_combine_kernel<2><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;

@@ -122,7 +122,7 @@ def test_attn_prefill_spike():
 
 
 @pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (4, 4), (16, 1)])
-@pytest.mark.parametrize("splits", [1, 3, 16])
+@pytest.mark.parametrize("splits", [1, 3, 16, 48])
 @pytest.mark.parametrize("impl", ["mfma", "mfma_fused", "valu", "valu_fused"])
 def test_attn_decode(hq, hkv, splits, impl):
     if impl.startswith("valu") and hq // hkv == 16:
