@@ -37,7 +37,8 @@ def main():
         bt = (1 + torch.arange(B * 64, dtype=torch.int32, device=dev).view(B, 64) % (n_pages - 1))
         pos = torch.full((B,), 4095, dtype=torch.int32, device=dev)
         q = torch.randn(B, 48 * hd, **bf)
-        ws = hip.DecodeWorkspace(B, 32, hd, hip.decode_splits(B, 8, 64 * page), dev, 8)
+        S, fused = hip.decode_attn_plan(B, 8, 64 * page)  # the engine's plan for this batch / context
+        ws = hip.DecodeWorkspace(B, 32, hd, S, dev, 8, fused_combine=fused)
         for _ in range(3):
             hip.attn_decode(q, kc, vc, bt, pos, 32, 8, hd, page, 1 / math.sqrt(hd), workspace=ws)
     # prefill attention: 4 sequences x 4096 tokens
