@@ -466,6 +466,23 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
 
     const float* prow = ROPE ? ra.parts + (size_t)b * ra.width : nullptr;
     const float2* cs = ROPE ? ra.cos_sin + (size_t)(ctx - 1) * (D / 2) : nullptr;
+    const int* bt = block_tables + (size_t)b * bt_stride + ks / PG;
+    const int st_row = tid >> 4, st_chunk = tid & 15;
+    const size_t head_off = (size_t)kvh * PG * D + (size_t)st_row * D + st_chunk * 8;
+    // staging registers are plain named arrays indexed only by unrolled constants (a lambda
+    // capturing them by reference put them in scratch), and the prefetch is unconditional
+    // (the last tile is re-read instead of branching) so hipcc keeps the loads in flight.
+    // (issued first by every split, the one holding the new token included: its new K/V row reaches
+    // the tile through the LDS patch, so the page loads need not wait for the slab sums)
+    u32x4 kreg[4], vreg[4];
+    {
+        const size_t base = (size_t)bt[0] * Hkv * PG * D + head_off;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            kreg[i] = ld_kv<NT>(kc + base + (size_t)16 * i * D);
+            vreg[i] = ld_kv<NT>(vc + base + (size_t)16 * i * D);
+        }
+    }
     // ROPE: the q rows of this group (and, for the split holding the new token, its K and V rows)
     // summed over the SP slabs by ALL 256 threads in one round of independent loads into an fp32
     // LDS image (aliasing the K/V tile buffers, which are first written after it is consumed):
@@ -505,21 +522,6 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
         }
     }
 
-    const int* bt = block_tables + (size_t)b * bt_stride + ks / PG;
-    const int st_row = tid >> 4, st_chunk = tid & 15;
-    const size_t head_off = (size_t)kvh * PG * D + (size_t)st_row * D + st_chunk * 8;
-    // staging registers are plain named arrays indexed only by unrolled constants (a lambda
-    // capturing them by reference put them in scratch), and the prefetch is unconditional
-    // (the last tile is re-read instead of branching) so hipcc keeps the loads in flight.
-    u32x4 kreg[4], vreg[4];
-    {
-        const size_t base = (size_t)bt[0] * Hkv * PG * D + head_off;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            kreg[i] = ld_kv<NT>(kc + base + (size_t)16 * i * D);
-            vreg[i] = ld_kv<NT>(vc + base + (size_t)16 * i * D);
-        }
-    }
     // Q^T fragments (B operand of 16x16x32): lane holds Q[head col][dims 32k + 8grp .. +8]; built
     // after the first page's loads are in flight (the ROPE slab sums are an L2 round trip of their own)
     bf16x8 qf[4];

@@ -29,7 +29,9 @@ import threading
 from typing import Optional
 
 NATIVE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native")
-KERNELS_SO = os.path.join(NATIVE_DIR, "libmrsum_kernels.so")
+# MRSUM_KERNELS_SO: an alternative build of the kernel library (A/B experiments of two kernel versions
+# in one process tree); default the in-tree build
+KERNELS_SO = os.environ.get("MRSUM_KERNELS_SO") or os.path.join(NATIVE_DIR, "libmrsum_kernels.so")
 RUNTIME_SO = os.path.join(NATIVE_DIR, "libmrsum_runtime.so")
 
 _lock = threading.Lock()
