@@ -52,6 +52,7 @@ class ResultAggregator:
         self.tokenizer = tokenizer
         self.hierarchical = hierarchical
         self.max_levels = max_levels
+        self.level_seconds: List[float] = []
         self.reserved_tokens = reserved_tokens
         self.max_batch_size = max_batch_size
         self.last_plan: Dict[str, Any] = {}
@@ -109,15 +110,20 @@ class ResultAggregator:
             else:
                 log.warning("chunk %s has no summary", c.get("chunk_index", "?"))
         log.info("aggregating %d summaries", len(summaries))
+        self.level_seconds = []
         if not self.hierarchical or self._total_tokens(summaries) <= self.max_tokens_per_batch:
             self.last_plan = {"levels": 1, "calls": [1]}
+            t1 = time.perf_counter()
             final = await self._single_aggregation(summaries, prompt_template, metadata)
+            self.level_seconds.append(time.perf_counter() - t1)
         else:
             final = await self._hierarchical_aggregation(summaries, prompt_template, metadata)
         dt = time.perf_counter() - t0
         log.info("aggregation done in %.2f s (%s)", dt, self.last_plan)
+        plan = dict(self.last_plan)
+        plan["seconds"] = [round(x, 3) for x in self.level_seconds]  # wall-clock of every reduce level
         return {"summary": final, "chunks_aggregated": len(processed_chunks), "processing_time": dt,
-                "plan": dict(self.last_plan)}
+                "plan": plan}
 
     async def _hierarchical_aggregation(self, summaries: List[str], prompt_template: Optional[str] = None,
                                         metadata: Optional[Dict[str, Any]] = None) -> str:
@@ -137,7 +143,9 @@ class ResultAggregator:
                 reqs.append(self._request(b, AGG_BATCH_PROMPT, meta, "reduce_l%d" % level))
             log.info("reduce level %d: %d summaries -> %d batches of <=%d", level, len(current), n, bs)
             before = self._total_tokens(current) if self.max_levels is None else 0
+            t1 = time.perf_counter()
             current = await self._run(reqs, "reduce_l%d" % level)
+            self.level_seconds.append(time.perf_counter() - t1)
             calls.append(n)
             if len(current) == 1:
                 self.last_plan = {"levels": len(calls), "calls": calls}
@@ -152,7 +160,10 @@ class ResultAggregator:
         template = prompt_template or AGG_FINAL_PROMPT
         calls.append(1)
         self.last_plan = {"levels": len(calls), "calls": calls}
-        return (await self._run([self._request(current, template, metadata, "reduce_final")], "reduce_final"))[0]
+        t1 = time.perf_counter()
+        out = (await self._run([self._request(current, template, metadata, "reduce_final")], "reduce_final"))[0]
+        self.level_seconds.append(time.perf_counter() - t1)
+        return out
 
 
 def aggregate_results(processed_chunks: List[Dict[str, Any]], prompt_template: Optional[str] = None,

@@ -71,7 +71,8 @@ def test_aggregator_single_vs_hierarchical():
     agg = ResultAggregator(executor=ex)
     chunks = [dict(c, summary="short summary %d" % c["chunk_index"]) for c in _chunks(5)]
     r = asyncio.run(agg.aggregate(chunks, metadata={"File": "x"}))
-    assert r["plan"] == {"levels": 1, "calls": [1]} and r["chunks_aggregated"] == 5
+    assert {k: r["plan"][k] for k in ("levels", "calls")} == {"levels": 1, "calls": [1]}
+    assert r["chunks_aggregated"] == 5 and len(r["plan"]["seconds"]) == 1
     assert "[Time: 00:00 - 01:00]" in prov.reqs[-1].user and "File: x" in prov.reqs[-1].user
     assert prov.reqs[-1].temperature == pytest.approx(0.2)
 
@@ -82,6 +83,7 @@ def test_aggregator_single_vs_hierarchical():
     n_tok = agg.tokenizer.count("[Time: 00:00 - 01:00]\n" + long)
     bs = min(10, max(1, int(5000 / n_tok)))
     assert r["plan"]["levels"] == 2 and r["plan"]["calls"] == [-(-23 // bs), 1]
+    assert len(r["plan"]["seconds"]) == 2 and all(t >= 0 for t in r["plan"]["seconds"])
     assert "Batch: 1/%d" % r["plan"]["calls"][0] in prov.reqs[0].user
 
 
