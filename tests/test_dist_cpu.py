@@ -74,7 +74,7 @@ def test_dp2_equals_single_process():
     assert single["plan"]["levels"] >= 2  # exercises the hierarchical reduce
     for r in dp:
         assert r["summary"] == single["summary"]
-        assert r["plan"] == single["plan"]
+        assert {k: r["plan"][k] for k in ("levels", "calls")} == {k: single["plan"][k] for k in ("levels", "calls")}
 
 
 TP_SCRIPT = textwrap.dedent("""
