@@ -284,3 +284,178 @@ MRSUM_API int mrsum_stream_gemm_swiglu_split(const void* x, int ldx, const void*
     return launch_stream_gemm(x, ldx, W, N, K, M, out, ldo, EPI_SWIGLU_SPLIT, splits, wpb, (float*)parts, counters,
                               s);
 }
+
+// ---------------------------------------------------------------------------------------------
+// W8A16 (OCP e4m3fn weights, per-row fp32 scales) variant for the fp8 Llama-3-70B decode.  The ring is
+// bound by its slot rate (~1 us per slot at full chip load, profiles/r1_fp8_stream_gemm_experiment.txt:
+// a 128-wide fp8 slot carried half the bf16 bytes and halved the bandwidth), so an fp8 slot spans 256
+// k: the SAME 256 B per weight row as a bf16 slot (same pieces, same swizzle), twice the x bytes (two
+// bf16 images of 128 k).  A fragments: 8 fp8 per lane per 32-k MFMA step (ds_read_b64), converted
+// exactly by v_cvt_scalef32_pk_bf16_fp8; the row scale multiplies the fp32 accumulator in the epilogue
+// (before SwiGLU for gate / up rows).
+namespace {
+constexpr int KB8 = 256;
+
+__device__ __forceinline__ bf16x8 fp8x8_bf16(uint2 d) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    const bf16x2 a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d.x, 1.0f, false);
+    const bf16x2 b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d.x, 1.0f, true);
+    const bf16x2 c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d.y, 1.0f, false);
+    const bf16x2 e = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(d.y, 1.0f, true);
+    return bf16x8{a[0], a[1], b[0], b[1], c[0], c[1], e[0], e[1]};
+}
+}  // namespace
+
+template <int MT, int EPI, int WPB>
+__global__ __launch_bounds__(64 * WPB, 1) void stream_fp8_kernel(const bf16* __restrict__ x, int ldx,
+                                                                 const unsigned char* __restrict__ W,
+                                                                 const float* __restrict__ wscale, int K, int M,
+                                                                 void* __restrict__ out, int ldo, int kper) {
+    constexpr int R = 16 * WPB, BM = 16 * MT;
+    constexpr int WBYTES = R * 256, XBYTES = BM * 256, SLOT = WBYTES + 2 * XBYTES;
+    constexpr int D = (LDS_BUDGET / SLOT) < 6 ? (LDS_BUDGET / SLOT) : 6;
+    static_assert(D >= 2, "ring too shallow");
+    constexpr int XP = 2 * (2 * BM / 8);         // x pieces per slot: two 128-k images
+    constexpr int XI = (XP + WPB - 1) / WPB;
+    constexpr int NI = 4 + XI;
+    __shared__ __attribute__((aligned(1024))) char lds[D * SLOT + 1024];
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int n0 = blockIdx.x * R;
+    const int ks = blockIdx.y * kper;
+    const int nkb = kper / KB8;
+    const int prow = lane >> 3, pslot = lane & 7;
+    const unsigned char* wsrc[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int q = 4 * w + p;
+        const int row = 8 * (q >> 1) + prow;
+        wsrc[p] = W + (size_t)(n0 + row) * K + ks + 16 * (8 * (q & 1) + (pslot ^ prow));
+    }
+    // x piece q: image q / (2 BM / 8) (k half of the 256-wide block), then the bf16 piece layout
+    constexpr int XPI = 2 * BM / 8;  // pieces per image
+    const bf16* xsrc[XI];
+    int xdst[XI];
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+        const int q = w + WPB * i;
+        const int qq = q < XP ? q : 0;
+        const int img = qq / XPI, qi = qq % XPI;
+        const int row = 8 * (qi >> 1) + prow;
+        xsrc[i] = x + (size_t)min(row, M - 1) * ldx + ks + 128 * img + 8 * (8 * (qi & 1) + (pslot ^ prow));
+        xdst[i] = q < XP ? WBYTES + img * XBYTES + qi * 1024 : -1;
+    }
+#define ISSUE8(slot, kb)                                                                             \
+    {                                                                                                \
+        char* base = lds + (slot) * SLOT;                                                            \
+        _Pragma("unroll") for (int p = 0; p < 4; ++p) glds16<2>(wsrc[p] + (kb), base + (4 * w + p) * 1024); \
+        _Pragma("unroll") for (int i = 0; i < XI; ++i)                                               \
+            glds16(xsrc[i] + (kb), xdst[i] >= 0 ? base + xdst[i] : lds + D * SLOT);                  \
+    }
+    f32x4 acc[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < D - 1; ++s) ISSUE8(s, min(s, nkb - 1) * KB8);
+
+    const int r = lane & 15, g = lane >> 4;
+    for (int j = 0; j < nkb; ++j) {
+        if (j + D - 2 < nkb) wait_vmcnt<NI * (D - 2)>();
+        else wait_vmcnt<0>();
+        raw_barrier();
+        if (j + D - 1 < nkb) ISSUE8((j + D - 1) % D, (j + D - 1) * KB8);
+        const char* wl = lds + (j % D) * SLOT;
+        const char* xl = wl + WBYTES;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {  // 32-k MFMA steps: fp8 bytes 32 i + 8 g .. +8 of the row
+            const uint2 araw = *reinterpret_cast<const uint2*>(wl + img_off(16 * w + r, 2 * i + (g >> 1)) + 8 * (g & 1));
+            const bf16x8 av = fp8x8_bf16(araw);
+#pragma unroll
+            for (int m = 0; m < MT; ++m) {
+                const u32x4 bv = *reinterpret_cast<const u32x4*>(xl + (i >> 2) * XBYTES +
+                                                                 img_off(16 * m + r, 4 * (i & 3) + g));
+                acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, bv), acc[m], 0, 0, 0);
+            }
+        }
+    }
+#undef ISSUE8
+
+    // C: lane holds out^T[n = n0 + 16w + 4g + jj][m = 16 mt + r]; scale rows first
+    const int nw = n0 + 16 * w;
+    const float4 sc = *reinterpret_cast<const float4*>(wscale + nw + 4 * g);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        acc[m][0] *= sc.x;
+        acc[m][1] *= sc.y;
+        acc[m][2] *= sc.z;
+        acc[m][3] *= sc.w;
+        const int mm = 16 * m + r;
+        if constexpr (EPI == EPI_SWIGLU) {
+            f32x4 up;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) up[jj] = __shfl_xor(acc[m][jj], 32, 64);
+            if (g < 2 && mm < M) {
+                float rr[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const float gv = acc[m][jj];
+                    rr[jj] = gv / (1.f + __expf(-gv)) * up[jj];
+                }
+                uint2 o;
+                o.x = pack2(rr[0], rr[1]);
+                o.y = pack2(rr[2], rr[3]);
+                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + (nw >> 1) + 4 * g) = o;
+            }
+        } else if (mm < M) {
+            if constexpr (EPI == EPI_BF16) {
+                uint2 o;
+                o.x = pack2(acc[m][0], acc[m][1]);
+                o.y = pack2(acc[m][2], acc[m][3]);
+                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + nw + 4 * g) = o;
+            } else {
+                float* o = reinterpret_cast<float*>(out) + ((size_t)blockIdx.y * M + mm) * ldo + nw + 4 * g;
+                *reinterpret_cast<float4*>(o) = make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
+            }
+        }
+    }
+}
+
+// out: bf16 [M, ldo] (EPI_BF16), fp32 slabs [splits, M, ldo] (EPI_F32_PARTIAL) or bf16 [M, ldo] SwiGLU of the
+// blocked gate/up rows (EPI_SWIGLU, splits = 1).  W e4m3fn [N, K] row-major, wscale fp32 [N];
+// K % 256 == 0, (K / 256) % splits == 0, N % (16 wpb) == 0, wpb in 4..8, M <= 64.
+MRSUM_API int mrsum_stream_fp8(const void* x, int ldx, const void* W, const float* wscale, int N, int K, int M,
+                               void* out, int ldo, int epi, int splits, int wpb, hipStream_t s) {
+    if (M <= 0) return 0;
+    if (wpb < 4 || wpb > 8 || M > 64 || K % KB8 || N % (16 * wpb) || splits < 1 || (K / KB8) % splits ||
+        epi < EPI_BF16 || epi > EPI_SWIGLU)
+        return (int)hipErrorInvalidValue;
+    if (epi != EPI_F32_PARTIAL && splits != 1) return (int)hipErrorInvalidValue;
+    const int kper = K / splits;
+    const int mt = (M + 15) / 16;
+    dim3 grid(N / (16 * wpb), splits), block(64 * wpb);
+    auto X = (const bf16*)x;
+    auto Wp = (const unsigned char*)W;
+#define L8(MT_, EPI_, WPB_) stream_fp8_kernel<MT_, EPI_, WPB_><<<grid, block, 0, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper)
+#define BY_WPB8(MT_, EPI_)                          \
+    switch (wpb) {                                  \
+        case 4: L8(MT_, EPI_, 4); break;            \
+        case 5: L8(MT_, EPI_, 5); break;            \
+        case 6: L8(MT_, EPI_, 6); break;            \
+        case 7: L8(MT_, EPI_, 7); break;            \
+        default: L8(MT_, EPI_, 8); break;           \
+    }
+#define BY_EPI8(MT_)                                                      \
+    if (epi == EPI_BF16) { BY_WPB8(MT_, EPI_BF16) }                       \
+    else if (epi == EPI_F32_PARTIAL) { BY_WPB8(MT_, EPI_F32_PARTIAL) }    \
+    else { BY_WPB8(MT_, EPI_SWIGLU) }
+    switch (mt) {
+        case 1: BY_EPI8(1); break;
+        case 2: BY_EPI8(2); break;
+        case 3: BY_EPI8(3); break;
+        default: BY_EPI8(4); break;
+    }
+#undef BY_EPI8
+#undef BY_WPB8
+#undef L8
+    return (int)hipGetLastError();
+}

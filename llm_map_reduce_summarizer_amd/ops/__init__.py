@@ -137,7 +137,11 @@ def _plan_parts(hip, p, x, w, splits):
 
 
 def _fp8_parts(hip, x, w, role, splits):
-    """Split-K fp32 slabs from the fp8 weight-streaming kernel (decode) -- same plan shapes as bf16."""
+    """Split-K fp32 slabs from an fp8 weight-streaming kernel (decode): the LDS-DMA stream kernel when
+    it fills the chip, else the register-streaming kernel with the bf16 plan shapes."""
+    cfg = hip.stream_config_fp8(w.shape[0], w.shape[1], splits=splits, M=x.shape[0])
+    if cfg is not None:
+        return hip.fp8_linear_parts(x, w, cfg[1], stream_wpb=cfg[0])
     p = hip.plan(role, x.shape[0], w.shape[0], w.shape[1], stream=False)
     nt = p[1] if p[0] == "skinny" else 1
     s = splits or (p[2] if p[0] == "skinny" else (p[1] if p[0] == "lds" else 1))

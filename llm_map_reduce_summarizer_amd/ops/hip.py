@@ -41,6 +41,7 @@ _SIGS = {
     "mrsum_stream_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_stream_gemm_swiglu_split": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _vp,
                                        _vp, _vp],
+    "mrsum_stream_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_skinny_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_quant_fp8_rows": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
@@ -720,23 +721,62 @@ def _skinny_fp8(x, w, out, epi, nt, splits, ldo):
     return out
 
 
+STREAM_FP8 = os.environ.get("MRSUM_STREAM_FP8", "1") == "1"
+
+
+def stream_config_fp8(N: int, K: int, swiglu: bool = False, splits: Optional[int] = None, M: int = 1):
+    """(wpb, S) for the fp8 stream GEMM (256-wide k slots), or None (register-streaming skinny_fp8).
+
+    Measured (tools/bench_fp8_gemm.py, us, stream vs skinny): Llama-3-70B TP=1 at M=1 the skinny kernel
+    wins (gate_up 103 vs 92, down 66 vs 51, qkv 24 vs 20) -- at M=16/40 the stream kernel does (gate_up
+    110 / 138 vs 158 / 312, down 67 / 88 vs 66 / 161); TP=8 shards (<= 64 M weights) the stream kernel at
+    every M (o 12.9 vs 22.7, qkv 13.4 vs 18.1, down 13.7 vs 15.3 at M=1)."""
+    if not STREAM_FP8 or K % 256 or (M <= 8 and N * K > (64 << 20)):
+        return None
+    return stream_config(N, K // 2, swiglu=swiglu, splits=splits)  # K/256 slots == (K/2)/128 blocks
+
+
+def _stream_fp8(x, w, out, epi, splits, ldo, wpb):
+    """fp8 (e4m3fn, per-row scale) LDS-DMA weight-ring decode GEMM (stream_gemm.hip stream_fp8_kernel)."""
+    _bf16_cuda(x)
+    _rows_ok(x)
+    M, K = x.shape
+    N = w.q.shape[0]
+    _req(w.q.is_cuda and w.q.dtype == torch.float8_e4m3fn and w.q.is_contiguous() and w.q.shape[1] == K,
+         "stream_fp8: weight must be e4m3fn [N, K] contiguous")
+    _req(w.scale.dtype == torch.float32 and w.scale.numel() == N and w.scale.is_contiguous(), "stream_fp8: scale")
+    _req(1 <= M <= SKINNY_MAX_M and K % 256 == 0 and 4 <= wpb <= 8 and N % (16 * wpb) == 0
+         and (K // 256) % splits == 0, "stream_fp8: unsupported shape M=%d N=%d K=%d S=%d wpb=%d"
+         % (M, N, K, splits, wpb))
+    _check(_fn("mrsum_stream_fp8")(_p(x), x.stride(0), _p(w.q), _p(w.scale), N, K, M, _p(out), ldo, epi, splits, wpb,
+                                   _stream()), "stream_fp8")
+    return out
+
+
 def fp8_linear(x: torch.Tensor, w, out_dtype=torch.bfloat16) -> torch.Tensor:
     """x @ (scale * W8)^T for any M: MFMA W8A16 weight-streaming kernel at decode sizes, hipBLASLt fp8
     (torch._scaled_mm, row-wise activation x column-wise weight scales) at prefill sizes."""
     M = x.shape[0]
     N = w.q.shape[0]
     if M <= SKINNY_MAX_M:
-        nt = 2 if N % 32 == 0 and N >= 16384 else 1
         out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+        cfg = stream_config_fp8(N, x.shape[1], splits=1, M=M)
+        if cfg is not None:
+            return _stream_fp8(x, w, out, EPI_BF16, 1, N, cfg[0])
+        nt = 2 if N % 32 == 0 and N >= 16384 else 1
         return _skinny_fp8(x, w, out, EPI_BF16, nt, 1, N)
     xq, xs = quant_fp8_rows(x)
     return torch._scaled_mm(xq, w.q.t(), scale_a=xs.view(-1, 1), scale_b=w.scale.view(1, -1), out_dtype=out_dtype)
 
 
-def fp8_linear_parts(x: torch.Tensor, w, splits: int, nt: int = 1) -> torch.Tensor:
+def fp8_linear_parts(x: torch.Tensor, w, splits: int, nt: int = 1, stream_wpb: Optional[int] = None) -> torch.Tensor:
+    """fp32 split-K slabs [splits, M, N] of x @ (scale * W8)^T: the fp8 stream GEMM when ``stream_wpb`` is
+    given (its own split count), else the register-streaming kernel."""
     M, K = x.shape
     N = w.q.shape[0]
     out = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
+    if stream_wpb is not None:
+        return _stream_fp8(x, w, out, EPI_F32_PARTIAL, splits, N, stream_wpb)
     return _skinny_fp8(x, w, out, EPI_F32_PARTIAL, nt, splits, N)
 
 
@@ -746,4 +786,7 @@ def fp8_linear_swiglu(x: torch.Tensor, w) -> torch.Tensor:
     if M > SKINNY_MAX_M:
         return swiglu(fp8_linear(x, w))
     out = torch.empty(M, F2 // 2, dtype=torch.bfloat16, device=x.device)
+    cfg = stream_config_fp8(F2, x.shape[1], swiglu=True, M=M)
+    if cfg is not None:
+        return _stream_fp8(x, w, out, EPI_SWIGLU, 1, F2 // 2, cfg[0])
     return _skinny_fp8(x, w, out, EPI_SWIGLU, 1, 1, F2 // 2)

@@ -98,3 +98,17 @@ def test_long_context_class_graphs():
         assert (1, 1 if n < 12288 else 2) in e._graphs
         nxt = e.generate([p + out.token_ids[:-1]], [SamplingParams(1, 0.0, 0)])[0].token_ids[0]
         assert nxt == out.token_ids[-1]
+
+
+def test_fp8_engine_decode_matches_prefill():
+    """fp8 (e4m3fn) weights: decode GEMMs on the fp8 stream / register-streaming kernels, prefill on
+    hipBLASLt fp8 -- greedy decode agrees with teacher-forced prefill."""
+    e = LLMEngine(get_model_config("tiny-gqa4", init_std=0.05), device="cuda:0", max_model_len=2048,
+                  max_num_seqs=16, kv_pages=256, sync_every=8, weight_dtype="fp8")
+    prompts = _prompts()
+    outs = e.generate(prompts, [SamplingParams(8, 0.0, 0)] * len(prompts))
+    agree = 0
+    for p, o in zip(prompts, outs):
+        nxt = e.generate([p + o.token_ids[:-1]], [SamplingParams(1, 0.0, 0)])[0].token_ids[0]
+        agree += nxt == o.token_ids[-1]
+    assert agree >= len(prompts) - 1

@@ -368,6 +368,26 @@ def test_fp8_linear(M, N, K):
         _close(parts.sum(0), ref[:min(M, 64)], 2e-3, 2e-3)
 
 
+@pytest.mark.parametrize("M", [1, 9, 17, 40, 64])
+@pytest.mark.parametrize("N,K,wpb,S", [(640, 1024, 5, 1), (512, 2048, 4, 2), (896, 768, 7, 3), (1024, 512, 8, 2)])
+def test_stream_fp8(M, N, K, wpb, S):
+    """fp8 LDS-DMA stream GEMM (256-wide k slots): bf16 out, split-K fp32 slabs and SwiGLU vs fp32 of the
+    dequantised weights."""
+    from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight
+    x = _rand(M, K, seed=80)
+    w = Fp8Weight.quantize(_rand(N, K, scale=0.05, seed=81))
+    ref = x.float() @ w.dequant().t()
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    _close(hip._stream_fp8(x, w, out, hip.EPI_BF16, 1, N, wpb), ref, 2e-2)
+    parts = torch.empty(S, M, N, dtype=torch.float32, device=DEV)
+    _close(hip._stream_fp8(x, w, parts, hip.EPI_F32_PARTIAL, S, N, wpb).sum(0), ref, 2e-3, 2e-3)
+    wg, wu = _rand(N // 2, K, scale=0.05, seed=82), _rand(N // 2, K, scale=0.05, seed=83)
+    wgu = Fp8Weight.quantize(reference.interleave_gate_up(wg, wu).contiguous())
+    g, u = reference.split_gate_up(x.float() @ wgu.dequant().t())
+    act = torch.empty(M, N // 2, dtype=torch.bfloat16, device=DEV)
+    _close(hip._stream_fp8(x, wgu, act, hip.EPI_SWIGLU, 1, N // 2, wpb), g * torch.sigmoid(g) * u, 3e-2)
+
+
 def test_fp8_swiglu_and_quant():
     from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight
     M, F, K = 9, 512, 1024
