@@ -62,6 +62,9 @@ class LLMConfig:
         "LOCAL_MODEL": ("llama3-8b", str), "ENGINE_DTYPE": ("bf16", str), "ENGINE_SEED": ("0", int),
         "ENGINE_MAX_NUM_SEQS": ("256", int), "ENGINE_KV_FRACTION": ("0.6", float),
         "REDUCE_TEMPERATURE": ("0.2", float),
+        # hosted-provider endpoints (new): point the adapters at any compatible server
+        "OPENAI_BASE_URL": ("https://api.openai.com/v1", str),
+        "ANTHROPIC_BASE_URL": ("https://api.anthropic.com/v1", str),
     }
 
     def __init__(self, **overrides):

@@ -141,7 +141,12 @@ class MockProvider(Provider):
 
 
 class _HTTPProvider(Provider):
-    url = ""
+    path = ""
+
+    @property
+    def url(self) -> str:
+        base = self.config.OPENAI_BASE_URL if self.name == "openai" else self.config.ANTHROPIC_BASE_URL
+        return base.rstrip("/") + self.path
 
     def _key(self) -> str:
         return self.config.api_key(self.name)
@@ -151,7 +156,10 @@ class _HTTPProvider(Provider):
         timeout = aiohttp.ClientTimeout(total=self.config.REQUEST_TIMEOUT)
         async with aiohttp.ClientSession(timeout=timeout) as session:
             async with session.post(self.url, headers=headers, json=body) as resp:
-                data = await resp.json()
+                try:
+                    data = await resp.json(content_type=None)
+                except ValueError:
+                    data = {"error": {"message": (await resp.text())[:200]}}
                 if resp.status != 200:
                     msg = (data.get("error") or {}).get("message", "Unknown error") if isinstance(data, dict) else data
                     raise ProviderError("%s API Error: %s" % (self.name, msg))
@@ -160,7 +168,7 @@ class _HTTPProvider(Provider):
 
 class OpenAIProvider(_HTTPProvider):
     name = "openai"
-    url = "https://api.openai.com/v1/chat/completions"
+    path = "/chat/completions"  # reference llm_executor.py:292
 
     async def generate(self, req: GenRequest) -> GenResult:
         if not self._key():
@@ -182,7 +190,7 @@ class OpenAIProvider(_HTTPProvider):
 
 class AnthropicProvider(_HTTPProvider):
     name = "anthropic"
-    url = "https://api.anthropic.com/v1/messages"
+    path = "/messages"
 
     async def generate(self, req: GenRequest) -> GenResult:
         if not self._key():
