@@ -278,6 +278,8 @@ def decode_splits(batch: int, hkv: int, max_ctx: int, target_wgs: int = 1024, ma
 
 
 FUSED_COMBINE = os.environ.get("MRSUM_FUSED_COMBINE", "auto")
+ATTN_PAGES_PER_SPLIT = int(os.environ.get("MRSUM_ATTN_PPS", "2"))
+ATTN_FUSED_MAX_SPLITS = int(os.environ.get("MRSUM_ATTN_FUSED_MAX", "32"))
 
 
 CTX_CLASSES = (6144, 12288, 32768, 1 << 30)  # decode context classes (tokens): graphs / split plans per class
@@ -295,7 +297,7 @@ def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
     """(splits, fused_combine) of the decode attention of ``batch`` sequences x ``hkv`` kv heads whose
     contexts reach ``max_ctx`` tokens (the engine passes its context class's upper bound).
 
-    Splits: enough (sequence, kv head, split) workgroups to fill the chip (~1024), about 4 pages per split
+    Splits: enough (sequence, kv head, split) workgroups to fill the chip (~1024), about 2 pages per split
     (each workgroup walks its pages serially: at B=1 and ~11k context 16 splits of 11 pages ran at
     1.7 TB/s), at most 64.  Fused = the split merge runs in the attention launch, by the last split of
     each (sequence, kv head) to arrive, with write-through (sc1) partial stores and no release fence
@@ -303,16 +305,18 @@ def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
     graph: TP=8 B=1 1.555 vs 1.502 ms per step); write-through, in the decode graph at 4k context (ms
     per step, fused vs separate merge kernel): TP=8 shard B=10 1.714 vs 1.772, B=39 2.391 vs 2.471,
     TP=1 B=1 / B=10 equal within noise.  "auto": fused for at most 64 (sequence, kv head) groups and at
-    most 24 splits (the merging workgroup reads every split's partials)."""
+    most 32 splits (the merging workgroup reads every split's partials).  2 pages / split with up to 32
+    fused splits vs 4 / 16 (ms per step, profiles/r1_attn_splits_ab.jsonl): B=1 4k 3.508 vs 3.539, B=1 10k
+    3.615 vs 3.683, B=10 / B=39 within noise; 1 page / split lost (B=1 4k 3.806)."""
     pages = max(1, -(-max_ctx // 64))
     groups = max(1, batch * hkv)
-    splits = max(1, min(-(-1024 // groups), -(-pages // 4), 64))
+    splits = max(1, min(-(-1024 // groups), -(-pages // ATTN_PAGES_PER_SPLIT), 64))
     if FUSED_COMBINE == "auto":
-        fused = groups <= 64 and splits <= 24
+        fused = groups <= 64 and splits <= max(24, ATTN_FUSED_MAX_SPLITS)
     else:
         fused = FUSED_COMBINE == "1"
     if fused:
-        splits = min(splits, 16)
+        splits = min(splits, ATTN_FUSED_MAX_SPLITS)
     return splits, fused
 
 
