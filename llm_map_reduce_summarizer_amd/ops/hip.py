@@ -733,9 +733,9 @@ def stream_config_fp8(N: int, K: int, swiglu: bool = False, splits: Optional[int
 
     Measured (tools/bench_fp8_gemm.py, us, stream vs skinny): Llama-3-70B TP=1 at M=1 the skinny kernel
     wins (gate_up 103 vs 92, down 66 vs 51, qkv 24 vs 20) -- at M=16/40 the stream kernel does (gate_up
-    110 / 138 vs 158 / 312, down 67 / 88 vs 66 / 161); TP=8 shards (<= 64 M weights) the stream kernel at
+    110 / 138 vs 158 / 312, down 67 / 88 vs 66 / 161); TP=8 shards (< 64 M weights) the stream kernel at
     every M (o 12.9 vs 22.7, qkv 13.4 vs 18.1, down 13.7 vs 15.3 at M=1)."""
-    if not STREAM_FP8 or K % 256 or (M <= 8 and N * K > (64 << 20)):
+    if not STREAM_FP8 or K % 256 or (M <= 8 and N * K >= (64 << 20)):
         return None
     return stream_config(N, K // 2, swiglu=swiglu, splits=splits)  # K/256 slots == (K/2)/128 blocks
 
