@@ -96,3 +96,15 @@ def test_handoff_for_many_prompts_tp_forward_for_one():
     # the handoff option never makes a TP stage look more expensive
     assert plan.stage_seconds(D8B, hw, [3950] * 39, [1000] * 39, 8, 8, True) <= \
         plan.stage_seconds(D8B, hw, [3950] * 39, [1000] * 39, 8, 8, False)
+
+
+@pytest.mark.parametrize("ar_lat_us", [8.0, 15.0])
+def test_full_tp_beats_intermediate_layouts_for_10h_stages(ar_lat_us):
+    """Why ``auto`` only weighs TP=1 against TP=N: for the 10 h headline's three stages on 8 GPUs the
+    cost model ranks TP=8 ahead of every TP x DP layout (TP=2 x DP=4, TP=4 x DP=2) and of DP=8."""
+    hw = plan.with_measurements(plan.HWModel(), ar_lat_s=ar_lat_us * 1e-6, ar_bw=150e9, ar_lat_row_s=0.03e-6)
+    for prompts in ([4000] * 39, [10500] * 10, [10500]):
+        new = [1000] * len(prompts)
+        est = {tp: plan.stage_seconds(D8B, hw, prompts, new, tp, 8, handoff=True) for tp in (1, 2, 4, 8)}
+        assert min(est, key=est.get) == 8, est
+        assert est[8] < est[4] < est[2] < est[1], est
