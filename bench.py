@@ -31,6 +31,9 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# RCCL and the custom all-reduce share device memory across processes through dmabuf IPC, the only
+# IPC mode the host driver supports; set before anything initialises HIP
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 BASELINE_VALUE = None  # the reference publishes no number
 
