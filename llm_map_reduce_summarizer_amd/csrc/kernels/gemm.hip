@@ -1,0 +1,316 @@
+// Large-M GEMM on the matrix cores (prefill projections, LM head over many rows):
+//
+//     C[M, N] = X[M, K] . W[N, K]^T            X = activations, W = weights, both K-contiguous
+//
+//   * bf16 x bf16 on v_mfma_f32_16x16x32_bf16, or
+//   * OCP e4m3fn x e4m3fn on v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales (E8M0 127): the
+//     block-scaled form runs at twice the bf16 rate (MI355X_MICROARCH.md "Matrix cores"), so the plain
+//     per-row quantisation (activation row scale sx[m] x weight row scale sw[n]) is applied in the
+//     epilogue and the MX block scales stay 1.0.
+//
+// Structure (cdna_hip_programming.md §5 "The 256^2 8-phase template", re-derived for this layout):
+//   * one 256 x 256 output tile per 512-thread workgroup (8 waves, one workgroup per CU), K-tiles of 128
+//     bytes per row (64 bf16 | 128 e4m3); the XCD-aware bijective tile remap + grouped raster keeps
+//     the ~32 tiles an XCD runs at a time on 4 X row-panels x 8 W row-panels (L2 reuse).
+//   * LDS: 2 buffers x 4 half-tile images of 128 rows x 128 B (X rows 0-127, W rows 0-127, W rows
+//     128-255, X rows 128-255 -- the order the phases first read them) = 128 KiB in ONE __shared__
+//     array.  Half-tiles arrive by LDS-DMA (buffer_load ... lds, 16 B per lane, one 1 KiB piece = 8
+//     rows per wave instruction) from a tile-local buffer descriptor: rows past M / N are dropped by
+//     the descriptor's range check (their LDS rows hold stale bytes that only feed masked outputs).
+//     The bank swizzle is applied on the SOURCE address (rule 21): 16-B chunk c of row r sits at
+//     chunk position c ^ ((r >> 1) & 7), which makes every ds_read_b128 fragment read conflict-free
+//     (each 16-lane group covers the 16 slots of a bank row).
+//   * wave (wr, wc) owns 128 x 64 outputs split into four 64 x 32 quadrants; quadrant (qm, qn) reads
+//     X half qm and W half qn, so the four phases of a K-tile need the half-tiles in the order
+//     X0 W0 | W1 | X1 | -- and a half-tile can be staged LOOK = 6 half-tiles (1.5 K-tiles) ahead of
+//     the phase that first reads it.  Per phase: R = fragment ds_reads + stage one half-tile (2 DMA
+//     per lane) + counted s_waitcnt vmcnt(8) (never 0 in the main loop), raw s_barrier, M = 16 bf16 (8
+//     fp8) MFMAs between s_setprio(1/0), raw s_barrier.  With STAGGER, waves 4-7 run one barrier
+//     (half a phase) behind waves 0-3, so one wave of each SIMD reads LDS while its partner computes.
+//   * hazards (derived for the staggered schedule, which is the stricter one): the wait at the end of
+//     R_P covers every half-tile phase P+1 reads, before the barrier the lagging group passes ahead
+//     of its R_P; a half-tile is restaged >= 2 phases after the last phase that read its region
+//     (reads are retired by the lgkmcnt wait ahead of that phase's MFMAs, which precede the barrier
+//     the restaging wave passes).
+//   * the MFMA computes the transposed tile (A = W fragment, B = X fragment) so each lane ends with 4
+//     consecutive output columns of one row: 8-byte bf16 stores, and the fused SwiGLU epilogue of the
+//     [8 gate | 8 up]-interleaved gate_up weight is a lane-xor-32 exchange.
+#include "common.h"
+
+#include <type_traits>
+
+namespace {
+constexpr int HALF = 16384;
+constexpr int TILE = 4 * HALF;
+constexpr int LOOK = 6;
+
+enum { GEPI_BF16 = 0, GEPI_SWIGLU = 1 };
+
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+struct GemmArgs {
+    const char* x;
+    const char* w;
+    void* c;
+    const float* sx;  // fp8: per-row activation scale [M]
+    const float* sw;  // fp8: per-row weight scale [N]
+    int ldx_b, ldw_b, ldc;  // X / W row strides in bytes, C row stride in elements
+    int M, N, kb;           // kb = K-tiles (128 bytes of every row each)
+    int tiles_m, tiles_n, group_m;
+};
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+__device__ __forceinline__ void vm_wait_rt(int n) {
+    if (n >= 8) vm_wait<8>();
+    else if (n >= 6) vm_wait<6>();
+    else if (n >= 4) vm_wait<4>();
+    else if (n >= 2) vm_wait<2>();
+    else vm_wait<0>();
+}
+
+__device__ __forceinline__ void bar() {
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* dst, int voff, int soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)dst, 16, voff, soff, 0, 0);
+}
+
+// bijective XCD remap (blocks b, b+8, ... share an XCD) then a grouped raster of group_m tile rows
+__device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles_n, int group_m, int& tm, int& tn) {
+    const int xcd = bid & 7, local = bid >> 3, q = nwg >> 3, r = nwg & 7;
+    const int p = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+    const int gsz = group_m * tiles_n;
+    const int g = p / gsz, first = g * group_m;
+    const int gm = min(tiles_m - first, group_m);
+    const int within = p - g * gsz;
+    tm = first + within % gm;
+    tn = within / gm;
+}
+}  // namespace
+
+template <bool FP8, int EPI, bool STAGGER>
+__global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
+    __shared__ __attribute__((aligned(1024))) char lds[2 * TILE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wr = w >> 2, wc = w & 3;
+    int tm, tn;
+    tile_of(blockIdx.x, gridDim.x, a.tiles_m, a.tiles_n, a.group_m, tm, tn);
+    const int m0 = tm * 256, n0 = tn * 256;
+    const int xrows = min(a.M - m0, 256), wrows = min(a.N - n0, 256);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.x + (size_t)m0 * a.ldx_b), (short)0, xrows * a.ldx_b, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.w + (size_t)n0 * a.ldw_b), (short)0, wrows * a.ldw_b, 0x00020000);
+
+    // staging: this lane's source offsets for the 2 pieces (8 rows each) of every half-tile it fills
+    const int srow = 16 * w + (lane >> 3);
+    const int ch0 = ((lane & 7) ^ ((lane >> 4) & 7)) << 4;
+    const int ch1 = ((lane & 7) ^ ((4 + (lane >> 4)) & 7)) << 4;
+    const int vx0 = srow * a.ldx_b + ch0, vx1 = (srow + 8) * a.ldx_b + ch1;
+    const int vw0 = srow * a.ldw_b + ch0, vw1 = (srow + 8) * a.ldw_b + ch1;
+    const int xh = 128 * a.ldx_b, wh = 128 * a.ldw_b;
+    const int nk = a.kb, htot = 4 * nk;
+
+    auto stage = [&](int part, int kt) {
+        char* dst = lds + (kt & 1) * TILE + part * HALF + w * 2048;
+        const int soff = kt * 128;
+        if (part == 0 || part == 3) {
+            const int o = part == 3 ? xh : 0;
+            dma16(rx, dst, vx0 + o, soff);
+            dma16(rx, dst + 1024, vx1 + o, soff);
+        } else {
+            const int o = part == 2 ? wh : 0;
+            dma16(rw, dst, vw0 + o, soff);
+            dma16(rw, dst + 1024, vw1 + o, soff);
+        }
+    };
+
+    // fragment reads: row (lane & 15) of a 16-row block, chunk (lane >> 4) (k-step 0) or 4 + (lane >> 4)
+    const int lo0 = (lane & 15) * 128 + (((lane >> 4) ^ ((lane >> 1) & 7)) << 4);
+    const int lo1 = (lane & 15) * 128 + (((4 + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4);
+    const int xbase = (64 * wr) * 128, wbase = (32 * wc) * 128;
+
+    f32x4 acc[2][4][2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) acc[i][b][j][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+    u32x4 xf[4][2], wf0[2][2], wf1[2][2];
+
+    // prologue: half-tiles 0 .. LOOK-1 in flight, wait for the two phase 0 reads
+#pragma unroll
+    for (int h = 0; h < LOOK; ++h)
+        if (h < htot) stage(h & 3, h >> 2);
+    vm_wait_rt(2 * (min(LOOK - 1, htot - 1) - 1));
+    bar();
+    if (STAGGER && wr == 1) bar();
+
+    auto read_x = [&](const char* base) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            xf[b][0] = *reinterpret_cast<const u32x4*>(base + xbase + b * 2048 + lo0);
+            xf[b][1] = *reinterpret_cast<const u32x4*>(base + xbase + b * 2048 + lo1);
+        }
+    };
+    auto read_w = [&](const char* base, u32x4 (&wf)[2][2]) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            wf[i][0] = *reinterpret_cast<const u32x4*>(base + wbase + i * 2048 + lo0);
+            wf[i][1] = *reinterpret_cast<const u32x4*>(base + wbase + i * 2048 + lo1);
+        }
+    };
+    auto mfma_q = [&](int qm, int qn, const u32x4 (&wf)[2][2]) {
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                if constexpr (FP8) {
+                    const i32x8 av = {(int)wf[i][0][0], (int)wf[i][0][1], (int)wf[i][0][2], (int)wf[i][0][3],
+                                      (int)wf[i][1][0], (int)wf[i][1][1], (int)wf[i][1][2], (int)wf[i][1][3]};
+                    const i32x8 bv = {(int)xf[b][0][0], (int)xf[b][0][1], (int)xf[b][0][2], (int)xf[b][0][3],
+                                      (int)xf[b][1][0], (int)xf[b][1][1], (int)xf[b][1][2], (int)xf[b][1][3]};
+                    acc[qm][b][qn][i] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                        av, bv, acc[qm][b][qn][i], 0, 0, 0, 127, 0, 127);
+                } else {
+#pragma unroll
+                    for (int ks = 0; ks < 2; ++ks)
+                        acc[qm][b][qn][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                            __builtin_bit_cast(bf16x8, wf[i][ks]), __builtin_bit_cast(bf16x8, xf[b][ks]),
+                            acc[qm][b][qn][i], 0, 0, 0);
+                }
+            }
+        __builtin_amdgcn_s_setprio(0);
+    };
+    // stage the half-tile LOOK ahead of phase P = 4 kt + p, then wait for what phase P + 1 reads.  In the
+    // steady state (TAIL false: kt < nk - 2) the stage always exists and the wait is vmcnt(2 (LOOK - 2)).
+    auto stage_and_wait = [&](int kt, int p, auto tail) {
+        const int P = 4 * kt + p, h = P + LOOK;
+        if constexpr (decltype(tail)::value) {
+            if (h < htot) stage(h & 3, h >> 2);
+            const int rem = htot - 1 - P;
+            vm_wait_rt(rem >= LOOK ? 2 * (LOOK - 2) : 2 * (rem - 2));
+        } else {
+            stage(h & 3, h >> 2);
+            vm_wait<2 * (LOOK - 2)>();
+        }
+    };
+    auto ktile = [&](int kt, auto tail) {
+        const char* buf = lds + (kt & 1) * TILE;
+        // phase 0: quadrant (0, 0) -- X0, W0
+        read_x(buf + 0 * HALF);
+        read_w(buf + 1 * HALF, wf0);
+        stage_and_wait(kt, 0, tail);
+        bar();
+        mfma_q(0, 0, wf0);
+        bar();
+        // phase 1: quadrant (0, 1) -- W1
+        read_w(buf + 2 * HALF, wf1);
+        stage_and_wait(kt, 1, tail);
+        bar();
+        mfma_q(0, 1, wf1);
+        bar();
+        // phase 2: quadrant (1, 1) -- X1
+        read_x(buf + 3 * HALF);
+        stage_and_wait(kt, 2, tail);
+        bar();
+        mfma_q(1, 1, wf1);
+        bar();
+        // phase 3: quadrant (1, 0) -- registers only
+        stage_and_wait(kt, 3, tail);
+        bar();
+        mfma_q(1, 0, wf0);
+        bar();
+    };
+    int kt = 0;
+    for (; kt < nk - 2; ++kt) ktile(kt, std::false_type{});
+    for (; kt < nk; ++kt) ktile(kt, std::true_type{});
+    if (STAGGER && wr == 0) bar();
+
+    // epilogue: lane holds C[m][n .. n+3] of every 16 x 16 block, m = .. + (lane & 15), n = .. + 4 (lane >> 4)
+    const int g4 = lane >> 4;
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const int m = m0 + 128 * qm + 64 * wr + 16 * b + (lane & 15);
+            float rs = 1.f;
+            if constexpr (FP8) rs = a.sx[min(m, a.M - 1)];
+#pragma unroll
+            for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    const int nb = n0 + 128 * qn + 32 * wc + 16 * i;  // 16-column block
+                    const int n = nb + 4 * g4;
+                    f32x4 v = acc[qm][b][qn][i];
+                    if constexpr (FP8) {
+                        const int nn = min(n, a.N - 4);
+                        const float4 s4 = *reinterpret_cast<const float4*>(a.sw + nn);
+                        v[0] *= rs * s4.x; v[1] *= rs * s4.y; v[2] *= rs * s4.z; v[3] *= rs * s4.w;
+                    }
+                    if constexpr (EPI == GEPI_SWIGLU) {
+                        f32x4 up;
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) up[j] = __shfl_xor(v[j], 32, 64);
+                        if (g4 < 2 && m < a.M && nb < a.N) {
+                            float r[4];
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) r[j] = v[j] / (1.f + __expf(-v[j])) * up[j];
+                            bf16* o = reinterpret_cast<bf16*>(a.c) + (size_t)m * a.ldc + (nb >> 1) + 4 * g4;
+                            *reinterpret_cast<uint2*>(o) = make_uint2(pack2(r[0], r[1]), pack2(r[2], r[3]));
+                        }
+                    } else {
+                        if (m < a.M && n < a.N) {
+                            bf16* o = reinterpret_cast<bf16*>(a.c) + (size_t)m * a.ldc + n;
+                            *reinterpret_cast<uint2*>(o) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+                        }
+                    }
+                }
+        }
+}
+
+// x [M, K] (row stride ldx elements), w [N, K] (ldw), c [M, N] bf16 (ldc) -- or [M, N / 2] for
+// epi 1 (SwiGLU of the [8 gate | 8 up]-interleaved gate_up rows).  fp8: x, w are e4m3fn bytes,
+// sx [M] / sw [N] fp32 row scales.  Requirements (checked by the Python wrapper too): K % 64 (bf16) /
+// K % 128 (fp8), N % 16, 16-byte aligned rows.
+MRSUM_API int mrsum_gemm(const void* x, int ldx, const void* w, int ldw, void* c, int ldc, int M, int N, int K,
+                         int fp8, int epi, const float* sx, const float* sw, int stagger, int group_m,
+                         hipStream_t s) {
+    if (M <= 0 || N <= 0) return 0;
+    const int es = fp8 ? 1 : 2;
+    if ((K * es) % 128 || N % 16 || (ldx * es) % 16 || (ldw * es) % 16 || ldc % 4) return (int)hipErrorInvalidValue;
+    if ((size_t)256 * ldx * es >= (1u << 31) || (size_t)256 * ldw * es >= (1u << 31)) return (int)hipErrorInvalidValue;
+    if (fp8 && (!sx || !sw)) return (int)hipErrorInvalidValue;
+    GemmArgs a;
+    a.x = (const char*)x; a.w = (const char*)w; a.c = c; a.sx = sx; a.sw = sw;
+    a.ldx_b = ldx * es; a.ldw_b = ldw * es; a.ldc = ldc;
+    a.M = M; a.N = N; a.kb = K * es / 128;
+    a.tiles_m = ceil_div(M, 256); a.tiles_n = ceil_div(N, 256);
+    a.group_m = group_m > 0 ? group_m : 4;
+    const dim3 grid(a.tiles_m * a.tiles_n), block(512);
+#define GEMM_LAUNCH(F, E, ST) gemm_kernel<F, E, ST><<<grid, block, 0, s>>>(a)
+    if (fp8) {
+        if (epi == GEPI_SWIGLU) { if (stagger) GEMM_LAUNCH(true, GEPI_SWIGLU, true); else GEMM_LAUNCH(true, GEPI_SWIGLU, false); }
+        else { if (stagger) GEMM_LAUNCH(true, GEPI_BF16, true); else GEMM_LAUNCH(true, GEPI_BF16, false); }
+    } else {
+        if (epi == GEPI_SWIGLU) { if (stagger) GEMM_LAUNCH(false, GEPI_SWIGLU, true); else GEMM_LAUNCH(false, GEPI_SWIGLU, false); }
+        else { if (stagger) GEMM_LAUNCH(false, GEPI_BF16, true); else GEMM_LAUNCH(false, GEPI_BF16, false); }
+    }
+#undef GEMM_LAUNCH
+    return (int)hipGetLastError();
+}

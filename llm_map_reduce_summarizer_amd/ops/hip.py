@@ -47,6 +47,8 @@ _SIGS = {
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_sample_keys": [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
     "mrsum_sample_finish": [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
+    "mrsum_gemm": [_vp, _c_int, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int,
+                   _c_int, _vp],
     "mrsum_sample": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp,
                      _c_int, _vp],
 }
@@ -441,6 +443,68 @@ def sample_tp(logits: torch.Tensor, st, tok_offset: int, max_reduce) -> None:
     _check(_fn("mrsum_sample_finish")(_p(st.result), _p(st.next_ids), _p(st.positions), _p(st.gen_count),
                                       _p(st.max_new), _p(st.out_tokens), st.out_tokens.stride(0), _p(st.done),
                                       _p(st.eos), st.n_eos, B, _stream()), "sample_finish")
+
+
+# ------------------------------------------------------------------ large-M GEMM (prefill, M > 64)
+GEMM_STAGGER = int(os.environ.get("MRSUM_GEMM_STAGGER", "1"))
+GEMM_GROUP_M = int(os.environ.get("MRSUM_GEMM_GROUP_M", "4"))
+GEMM_EPI_BF16, GEMM_EPI_SWIGLU = 0, 1
+
+
+def _gemm(xp, ldx, wp, ldw, out, M, N, K, fp8, epi, sx, sw, stagger, group_m):
+    _req(out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 8 == 0, "gemm: bad out layout")
+    _check(_fn("mrsum_gemm")(xp, ldx, wp, ldw, _p(out), out.stride(0), M, N, K, fp8, epi, sx, sw,
+                             GEMM_STAGGER if stagger is None else stagger,
+                             GEMM_GROUP_M if group_m is None else group_m, _stream()), "gemm")
+    return out
+
+
+def gemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, swiglu: bool = False,
+         stagger: Optional[int] = None, group_m: Optional[int] = None) -> torch.Tensor:
+    """x [M, K] @ w [N, K]^T in bf16 on the 256 x 256-tile MFMA kernel (csrc/kernels/gemm.hip), any M.
+    ``swiglu``: w is the [8 gate | 8 up]-interleaved gate_up weight and the result is silu(gate) * up
+    [M, N / 2]."""
+    _bf16_cuda(x, w)
+    _rows_ok(x)
+    _rows_ok(w)
+    M, K = x.shape
+    N = w.shape[0]
+    _req(w.shape[1] == K and K % 64 == 0 and N % (32 if swiglu else 16) == 0,
+         "gemm: unsupported shape M=%d N=%d K=%d" % (M, N, K))
+    n_out = N // 2 if swiglu else N
+    if out is None:
+        out = torch.empty(M, n_out, dtype=torch.bfloat16, device=x.device)
+    _bf16_cuda(out)
+    _req(out.shape == (M, n_out), "gemm: bad out shape")
+    if M == 0:
+        return out
+    return _gemm(_p(x), x.stride(0), _p(w), w.stride(0), out, M, N, K, 0,
+                 GEMM_EPI_SWIGLU if swiglu else GEMM_EPI_BF16, None, None, stagger, group_m)
+
+
+def gemm_fp8(xq: torch.Tensor, xs: torch.Tensor, w, out: Optional[torch.Tensor] = None, swiglu: bool = False,
+             stagger: Optional[int] = None, group_m: Optional[int] = None) -> torch.Tensor:
+    """(xs[:, None] * xq) @ (w.scale[:, None] * w.q)^T on the fp8 MFMA path of the same kernel
+    (v_mfma_scale_f32_16x16x128_f8f6f4, OCP e4m3fn operands), bf16 out."""
+    _req(xq.is_cuda and xq.dtype == torch.float8_e4m3fn and xq.dim() == 2 and xq.stride(1) == 1
+         and xq.stride(0) % 16 == 0 and xq.data_ptr() % 16 == 0, "gemm_fp8: x must be e4m3fn rows, 16-B aligned")
+    M, K = xq.shape
+    q, sc = w.q, w.scale
+    N = q.shape[0]
+    _req(q.is_cuda and q.dtype == torch.float8_e4m3fn and q.is_contiguous() and q.shape[1] == K,
+         "gemm_fp8: weight must be e4m3fn [N, K] contiguous")
+    _req(xs.dtype == torch.float32 and xs.is_contiguous() and xs.numel() >= M and sc.dtype == torch.float32
+         and sc.is_contiguous() and sc.numel() == N, "gemm_fp8: scales")
+    _req(K % 128 == 0 and N % (32 if swiglu else 16) == 0, "gemm_fp8: unsupported shape M=%d N=%d K=%d" % (M, N, K))
+    n_out = N // 2 if swiglu else N
+    if out is None:
+        out = torch.empty(M, n_out, dtype=torch.bfloat16, device=xq.device)
+    _bf16_cuda(out)
+    _req(out.shape == (M, n_out), "gemm_fp8: bad out shape")
+    if M == 0:
+        return out
+    return _gemm(_p(xq), xq.stride(0), _p(q), K, out, M, N, K, 1, GEMM_EPI_SWIGLU if swiglu else GEMM_EPI_BF16,
+                 _p(xs), _p(sc), stagger, group_m)
 
 
 # ------------------------------------------------------------------ decode GEMMs (M <= 64)
