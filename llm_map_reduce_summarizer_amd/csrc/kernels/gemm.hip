@@ -66,7 +66,9 @@ __device__ __forceinline__ void vm_wait() {
 }
 
 __device__ __forceinline__ void vm_wait_rt(int n) {
-    if (n >= 8) vm_wait<8>();
+    if (n >= 12) vm_wait<12>();
+    else if (n >= 10) vm_wait<10>();
+    else if (n >= 8) vm_wait<8>();
     else if (n >= 6) vm_wait<6>();
     else if (n >= 4) vm_wait<4>();
     else if (n >= 2) vm_wait<2>();
@@ -98,9 +100,14 @@ __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles
 }
 }  // namespace
 
-template <bool FP8, int EPI, bool STAGGER>
+template <bool FP8, int EPI, bool STAGGER, int NS, bool LEPI>
 __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
-    __shared__ __attribute__((aligned(1024))) char lds[2 * TILE];
+    // NS = half-tile slots of the LDS ring: half-tile h (K-tile h / 4, part h % 4) lives in slot h % NS.
+    // NS = 8 (128 KiB, 2 K-tiles): staged LK = 6 ahead; NS = 10 (160 KiB): LK = 8 ahead.  A slot is
+    // restaged at phase h + NS - LK >= 2 phases after the last phase that read half-tile h (<= h).
+    constexpr int LK = NS - 2;
+    static_assert(NS * HALF <= 160 * 1024 && NS * HALF >= 2 * TILE, "LDS ring size");
+    __shared__ __attribute__((aligned(1024))) char lds[NS * HALF];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wr = w >> 2, wc = w & 3;
@@ -123,7 +130,7 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
     const int nk = a.kb, htot = 4 * nk;
 
     auto stage = [&](int part, int kt) {
-        char* dst = lds + (kt & 1) * TILE + part * HALF + w * 2048;
+        char* dst = lds + ((4 * kt + part) % NS) * HALF + w * 2048;
         const int soff = kt * 128;
         if (part == 0 || part == 3) {
             const int o = part == 3 ? xh : 0;
@@ -152,11 +159,11 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
                 for (int k = 0; k < 2; ++k) acc[i][b][j][k] = f32x4{0.f, 0.f, 0.f, 0.f};
     u32x4 xf[4][2], wf0[2][2], wf1[2][2];
 
-    // prologue: half-tiles 0 .. LOOK-1 in flight, wait for the two phase 0 reads
+    // prologue: half-tiles 0 .. LK-1 in flight, wait for the phase 0 reads (h <= 1 | h <= 2)
 #pragma unroll
-    for (int h = 0; h < LOOK; ++h)
+    for (int h = 0; h < LK; ++h)
         if (h < htot) stage(h & 3, h >> 2);
-    vm_wait_rt(2 * (min(LOOK - 1, htot - 1) - 1));
+    vm_wait_rt(2 * (min(LK - 1, htot - 1) - 1));
     bar();
     if (STAGGER && wr == 1) bar();
 
@@ -197,36 +204,36 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
             }
         __builtin_amdgcn_s_setprio(0);
     };
-    // stage the half-tile LOOK ahead of phase P = 4 kt + p, then wait for what phase P + 1 reads.  In the
-    // steady state (TAIL false: kt < nk - 2) the stage always exists and the wait is vmcnt(2 (LOOK - 2)).
+    // stage the half-tile LK ahead of phase P = 4 kt + p, then wait for what phase P + 1 reads.  In the
+    // steady state (TAIL false: kt < nk - LK / 4) the stage always exists and the wait is vmcnt(2 (LK - 2)).
     auto stage_and_wait = [&](int kt, int p, auto tail) {
-        const int P = 4 * kt + p, h = P + LOOK;
+        const int P = 4 * kt + p, h = P + LK;
         if constexpr (decltype(tail)::value) {
             if (h < htot) stage(h & 3, h >> 2);
             const int rem = htot - 1 - P;
-            vm_wait_rt(rem >= LOOK ? 2 * (LOOK - 2) : 2 * (rem - 2));
+            vm_wait_rt(rem >= LK ? 2 * (LK - 2) : 2 * (rem - 2));
         } else {
             stage(h & 3, h >> 2);
-            vm_wait<2 * (LOOK - 2)>();
+            vm_wait<2 * (LK - 2)>();
         }
     };
+    auto slot = [&](int kt, int part) -> const char* { return lds + ((4 * kt + part) % NS) * HALF; };
     auto ktile = [&](int kt, auto tail) {
-        const char* buf = lds + (kt & 1) * TILE;
         // phase 0: quadrant (0, 0) -- X0, W0
-        read_x(buf + 0 * HALF);
-        read_w(buf + 1 * HALF, wf0);
+        read_x(slot(kt, 0));
+        read_w(slot(kt, 1), wf0);
         stage_and_wait(kt, 0, tail);
         bar();
         mfma_q(0, 0, wf0);
         bar();
         // phase 1: quadrant (0, 1) -- W1
-        read_w(buf + 2 * HALF, wf1);
+        read_w(slot(kt, 2), wf1);
         stage_and_wait(kt, 1, tail);
         bar();
         mfma_q(0, 1, wf1);
         bar();
         // phase 2: quadrant (1, 1) -- X1
-        read_x(buf + 3 * HALF);
+        read_x(slot(kt, 3));
         stage_and_wait(kt, 2, tail);
         bar();
         mfma_q(1, 1, wf1);
@@ -237,25 +244,32 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
         mfma_q(1, 0, wf0);
         bar();
     };
+    // steady state while every phase's stage exists: P + LK < htot for P <= 4 kt + 3
     int kt = 0;
-    for (; kt < nk - 2; ++kt) ktile(kt, std::false_type{});
+    for (; kt < nk - (LK + 3) / 4; ++kt) ktile(kt, std::false_type{});
     for (; kt < nk; ++kt) ktile(kt, std::true_type{});
     if (STAGGER && wr == 0) bar();
 
-    // epilogue: lane holds C[m][n .. n+3] of every 16 x 16 block, m = .. + (lane & 15), n = .. + 4 (lane >> 4)
+    // epilogue: lane holds C[m][n .. n+3] of every 16 x 16 block, m = .. + (lane & 15), n = .. + 4 (lane >> 4).
+    // LEPI: every wave writes its bf16 results into a [256 rows][RB bytes] LDS image of the whole tile
+    // (16-B unit u of row r at u ^ (r & 7): 2-way ds_write_b64, conflict-free ds_read_b128), then each
+    // wave stores 32 whole rows with 16-B lanes (full-row segments instead of 32-B pieces per row).
+    constexpr int RB = EPI == GEPI_SWIGLU ? 256 : 512;
     const int g4 = lane >> 4;
 #pragma unroll
     for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-            const int m = m0 + 128 * qm + 64 * wr + 16 * b + (lane & 15);
+            const int rl = 128 * qm + 64 * wr + 16 * b + (lane & 15);  // row within the tile
+            const int m = m0 + rl;
             float rs = 1.f;
             if constexpr (FP8) rs = a.sx[min(m, a.M - 1)];
 #pragma unroll
             for (int qn = 0; qn < 2; ++qn)
 #pragma unroll
                 for (int i = 0; i < 2; ++i) {
-                    const int nb = n0 + 128 * qn + 32 * wc + 16 * i;  // 16-column block
+                    const int cb = 128 * qn + 32 * wc + 16 * i;  // 16-column block within the tile
+                    const int nb = n0 + cb;
                     const int n = nb + 4 * g4;
                     f32x4 v = acc[qm][b][qn][i];
                     if constexpr (FP8) {
@@ -263,25 +277,47 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
                         const float4 s4 = *reinterpret_cast<const float4*>(a.sw + nn);
                         v[0] *= rs * s4.x; v[1] *= rs * s4.y; v[2] *= rs * s4.z; v[3] *= rs * s4.w;
                     }
+                    uint2 pk;
+                    int cbyte;  // byte offset of this lane's 4 outputs within the tile row
+                    bool have;
                     if constexpr (EPI == GEPI_SWIGLU) {
                         f32x4 up;
 #pragma unroll
                         for (int j = 0; j < 4; ++j) up[j] = __shfl_xor(v[j], 32, 64);
-                        if (g4 < 2 && m < a.M && nb < a.N) {
-                            float r[4];
+                        float r[4];
 #pragma unroll
-                            for (int j = 0; j < 4; ++j) r[j] = v[j] / (1.f + __expf(-v[j])) * up[j];
-                            bf16* o = reinterpret_cast<bf16*>(a.c) + (size_t)m * a.ldc + (nb >> 1) + 4 * g4;
-                            *reinterpret_cast<uint2*>(o) = make_uint2(pack2(r[0], r[1]), pack2(r[2], r[3]));
-                        }
+                        for (int j = 0; j < 4; ++j) r[j] = v[j] / (1.f + __expf(-v[j])) * up[j];
+                        pk = make_uint2(pack2(r[0], r[1]), pack2(r[2], r[3]));
+                        cbyte = ((cb >> 1) + 4 * g4) * 2;
+                        have = g4 < 2;
                     } else {
-                        if (m < a.M && n < a.N) {
-                            bf16* o = reinterpret_cast<bf16*>(a.c) + (size_t)m * a.ldc + n;
-                            *reinterpret_cast<uint2*>(o) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-                        }
+                        pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+                        cbyte = (cb + 4 * g4) * 2;
+                        have = true;
+                    }
+                    if constexpr (LEPI) {
+                        if (have)
+                            *reinterpret_cast<uint2*>(lds + rl * RB + (((cbyte >> 4) ^ (rl & 7)) << 4) + (cbyte & 15)) = pk;
+                    } else if (have && m < a.M && nb < a.N) {
+                        char* o = reinterpret_cast<char*>(a.c) + ((size_t)m * a.ldc) * 2 +
+                                  (EPI == GEPI_SWIGLU ? n0 : 2 * n0) + cbyte;
+                        *reinterpret_cast<uint2*>(o) = pk;
                     }
                 }
         }
+    if constexpr (LEPI) {
+        __syncthreads();
+        constexpr int UPR = RB / 16, RPI = 1024 / RB;
+#pragma unroll
+        for (int it = 0; it < 32 / RPI; ++it) {
+            const int rl = 32 * w + RPI * it + lane / UPR, u = lane % UPR;
+            const u32x4 val = *reinterpret_cast<const u32x4*>(lds + rl * RB + ((u ^ (rl & 7)) << 4));
+            const int m = m0 + rl;
+            const int col = (EPI == GEPI_SWIGLU ? (n0 >> 1) : n0) + 8 * u;  // output column of the unit
+            const bool ok = m < a.M && (EPI == GEPI_SWIGLU ? 2 * col : col) < a.N;
+            if (ok) *reinterpret_cast<u32x4*>(reinterpret_cast<bf16*>(a.c) + (size_t)m * a.ldc + col) = val;
+        }
+    }
 }
 
 // x [M, K] (row stride ldx elements), w [N, K] (ldw), c [M, N] bf16 (ldc) -- or [M, N / 2] for
@@ -303,13 +339,23 @@ MRSUM_API int mrsum_gemm(const void* x, int ldx, const void* w, int ldw, void* c
     a.tiles_m = ceil_div(M, 256); a.tiles_n = ceil_div(N, 256);
     a.group_m = group_m > 0 ? group_m : 4;
     const dim3 grid(a.tiles_m * a.tiles_n), block(512);
-#define GEMM_LAUNCH(F, E, ST) gemm_kernel<F, E, ST><<<grid, block, 0, s>>>(a)
+    // variant flags (A/B): bit 0 stagger, bit 1 10-slot LDS ring (8 half-tiles ahead), bit 2 LDS-staged epilogue
+    if ((stagger & 4) && (ldc % 8 || (uintptr_t)c % 16)) stagger &= ~4;
+#define GEMM_LAUNCH(F, E)                                                                 \
+    switch (stagger & 7) {                                                                \
+        case 0: gemm_kernel<F, E, false, 8, false><<<grid, block, 0, s>>>(a); break;      \
+        case 1: gemm_kernel<F, E, true, 8, false><<<grid, block, 0, s>>>(a); break;       \
+        case 2: gemm_kernel<F, E, false, 10, false><<<grid, block, 0, s>>>(a); break;     \
+        case 3: gemm_kernel<F, E, true, 10, false><<<grid, block, 0, s>>>(a); break;      \
+        case 4: gemm_kernel<F, E, false, 8, true><<<grid, block, 0, s>>>(a); break;       \
+        case 5: gemm_kernel<F, E, true, 8, true><<<grid, block, 0, s>>>(a); break;        \
+        case 6: gemm_kernel<F, E, false, 10, true><<<grid, block, 0, s>>>(a); break;      \
+        default: gemm_kernel<F, E, true, 10, true><<<grid, block, 0, s>>>(a); break;      \
+    }
     if (fp8) {
-        if (epi == GEPI_SWIGLU) { if (stagger) GEMM_LAUNCH(true, GEPI_SWIGLU, true); else GEMM_LAUNCH(true, GEPI_SWIGLU, false); }
-        else { if (stagger) GEMM_LAUNCH(true, GEPI_BF16, true); else GEMM_LAUNCH(true, GEPI_BF16, false); }
+        if (epi == GEPI_SWIGLU) GEMM_LAUNCH(true, GEPI_SWIGLU) else GEMM_LAUNCH(true, GEPI_BF16)
     } else {
-        if (epi == GEPI_SWIGLU) { if (stagger) GEMM_LAUNCH(false, GEPI_SWIGLU, true); else GEMM_LAUNCH(false, GEPI_SWIGLU, false); }
-        else { if (stagger) GEMM_LAUNCH(false, GEPI_BF16, true); else GEMM_LAUNCH(false, GEPI_BF16, false); }
+        if (epi == GEPI_SWIGLU) GEMM_LAUNCH(false, GEPI_SWIGLU) else GEMM_LAUNCH(false, GEPI_BF16)
     }
 #undef GEMM_LAUNCH
     return (int)hipGetLastError();

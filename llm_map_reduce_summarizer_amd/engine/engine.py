@@ -164,7 +164,6 @@ class LLMEngine:
         self._graphs: Dict[Tuple[int, int], "torch.cuda.CUDAGraph"] = {}
         self._ctx_cls = 0
         self._on_prefill = None
-        self.pad_prefill = os.environ.get("MRSUM_PAD_PREFILL", "1") == "1"
         self._workspaces: Dict[Tuple[int, int], object] = {}
         self.stats = {"prefill_tokens": 0, "prefill_s": 0.0, "decode_steps": 0, "decode_tokens": 0,
                       "decode_s": 0.0, "generate_calls": 0, "graph_captures": 0, "peak_active": 0}
@@ -213,14 +212,6 @@ class LLMEngine:
             lens.append(n)
         T = len(ids)
         att_lens = list(lens)
-        pad = self._prefill_pad(T) - T
-        if pad:  # a padding "sequence": attends to itself only, rotated but never written to the cache
-            ids.extend([0] * pad)
-            pos.extend(range(pad))
-            sidx.extend([-1] * pad)
-            cu.append(cu[-1] + pad)
-            att_lens.append(pad)
-            self.stats["prefill_pad_tokens"] = self.stats.get("prefill_pad_tokens", 0) + pad
         h = lambda x: torch.tensor(x, dtype=torch.int32).to(dev, non_blocking=True)  # noqa: E731
         ids_t, pos_t, sidx_t, cu_t = h(ids), h(pos), h(sidx), h(cu)
         last_t = torch.tensor(last, dtype=torch.long).to(dev, non_blocking=True)
@@ -237,20 +228,6 @@ class LLMEngine:
         v.positions.copy_(h([n - 1 for n in lens]))
         self._sample(logits, v)
         self.stats["prefill_tokens"] += T
-
-    PAD_QUANTUM = 4096
-    PAD_MAX_WASTE = 0.08
-
-    def _prefill_pad(self, T: int) -> int:
-        """Packed prefill length to run: T rounded up to a multiple of 4096 when that costs <= 8 % extra
-        tokens (GPU only).  hipBLASLt's projection GEMMs are shape-sensitive: at M = 16384 the four
-        Llama-3-8B projections run at 1.62 PFLOP/s vs 1.26-1.56 at the M between multiples of 4096
-        that a packed batch of prompts lands on (profiles/r1_prefill_gemm_m_sweep.txt)."""
-        if self.device.type != "cuda" or not self.pad_prefill:
-            return T
-        q = self.PAD_QUANTUM
-        Tp = -(-T // q) * q
-        return Tp if Tp - T <= self.PAD_MAX_WASTE * T else T
 
     # ------------------------------------------------------------------ decode
     def _sample(self, logits: torch.Tensor, st_view) -> None:

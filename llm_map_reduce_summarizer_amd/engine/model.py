@@ -13,7 +13,7 @@ parallelism so a model is bit-identical for every TP degree.  Fused layouts:
 
 One residual block (both phases)::
 
-    qkv = x @ wqkv^T                 hipBLASLt GEMM
+    qkv = x @ wqkv^T                 HIP MFMA GEMM (stream / skinny decode kernels, 256^2 prefill)
     rope_kv(qkv -> Q,K rotated; K,V -> paged cache)     HIP
     a   = attention(qkv)             HIP: flash prefill | paged split-K decode
     o   = a @ wo^T  (+ TP all-reduce over RCCL)
@@ -31,7 +31,6 @@ from dataclasses import dataclass
 from typing import Callable, List, Optional
 
 import torch
-import torch.nn.functional as F
 
 from .. import ops
 from ..ops.reference import Fp8Weight, interleave_gate_up, rope_cos_sin
@@ -213,7 +212,9 @@ class LlamaModel:
         return x
 
     def logits(self, x: torch.Tensor, gather: bool = True) -> torch.Tensor:
-        local = F.linear(x, self.lm_head)  # hipBLASLt streams the 1 GB head at ~5.4 TB/s
+        # decode rows: the LDS-DMA weight-ring stream GEMM (the 1 GB head read once); more rows: the
+        # 256 x 256 MFMA GEMM (ops.linear -> ops.hip.linear)
+        local = ops.linear(x, self.lm_head)
         return self._gather_vocab(local) if gather else local
 
     def prefill(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, cu_seqlens: torch.Tensor,

@@ -6,9 +6,11 @@ to the hand-written gfx950 kernels in ``ops.hip`` (and fail loudly if
 ``ops.reference`` (the numerics oracle, also what CPU-only tests run).
 ``MRSUM_OPS=torch`` forces the reference on the GPU for debugging only.
 
-Plain dense GEMMs (projections, LM head) are ``torch.matmul`` -> hipBLASLt;
-every fused / non-GEMM hot op (norms, RoPE + KV write, SwiGLU, embedding,
-flash prefill attention, paged decode attention, sampling) is ours.
+Every GPU op is a hand-written gfx950 kernel, GEMMs included: decode-shaped
+projections on the weight-streaming MFMA kernels (stream_gemm.hip /
+skinny_gemm.hip, fused split-K / SwiGLU / RoPE epilogues), everything with
+more rows (prefill projections, the LM head over many rows) on the 256 x 256
+MFMA GEMM (gemm.hip; bf16 or OCP fp8).  No vendor BLAS on the hot path.
 """
 
 from __future__ import annotations
@@ -58,8 +60,8 @@ def swiglu(gu, out=None):
 
 
 def linear(x, w):
-    """x @ w^T (bf16).  GPU: MFMA weight-streaming kernel for decode shapes, hipBLASLt otherwise;
-    ``w`` may be an Fp8Weight (W8A16 decode kernel / hipBLASLt fp8 prefill)."""
+    """x @ w^T (bf16).  GPU: MFMA weight-streaming kernels for decode shapes, the 256 x 256 MFMA GEMM
+    otherwise; ``w`` may be an Fp8Weight (W8A16 decode kernel / fp8 MFMA GEMM at prefill sizes)."""
     if isinstance(w, Fp8Weight):
         if _use_hip(x):
             from . import hip
@@ -124,9 +126,10 @@ def sample_tp(logits, st, tok_offset, max_reduce):
 
 
 # ---------------------------------------------------------------- fused projection blocks
-# The model calls these; each picks (on the GPU) between our MFMA weight-streaming kernel
-# with a fused epilogue and hipBLASLt + a separate HIP kernel, per the measured plan table
-# (ops.hip.plan).  On the CPU they are the reference composition.
+# The model calls these; each picks (on the GPU) between our MFMA weight-streaming kernels
+# with a fused epilogue (decode rows) and the 256 x 256 MFMA GEMM + a separate HIP kernel
+# (prefill rows), per the measured plan table (ops.hip.plan).  On the CPU they are the
+# reference composition.
 
 def _plan_parts(hip, p, x, w, splits):
     if p[0] == "stream":
@@ -188,13 +191,13 @@ def qkv_rope(x, wqkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin,
     if _use_hip(x):
         from . import hip
         p = hip.plan("qkv", x.shape[0], wqkv.shape[0], wqkv.shape[1])
-        if p[0] != "blas":
+        if p[0] != "gemm":
             parts = _plan_parts(hip, p, x, wqkv, None)
             if _defer_ok(hip, defer, x, hq, hkv, d, page):
                 return QKVParts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page)
             return hip.rope_kv_parts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv,
                                      d, page)
-        qkv = torch.nn.functional.linear(x, wqkv)
+        qkv = hip.gemm(x, wqkv)
         hip.rope_kv(qkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page)
         return qkv
     qkv = reference.linear(x, wqkv)
@@ -236,14 +239,14 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
         fused = _fused_ar(all_reduce, a.shape[0], residual.shape[1])
         one = 1 if (all_reduce and not fused) else None  # a plain all-reduce takes one slab
         p = hip.plan(role, a.shape[0], w.shape[0], w.shape[1], splits=one)
-        if p[0] != "blas":
+        if p[0] != "gemm":
             parts = _plan_parts(hip, p, a, w, one)
             if fused:
                 return fused(parts, residual, ln, eps)
             if all_reduce:
                 all_reduce(parts)
             return hip.add_rmsnorm_parts(parts, residual, ln, eps)
-        o = torch.nn.functional.linear(a, w)
+        o = hip.gemm(a, w)
         if all_reduce:
             all_reduce(o)
         return hip.add_rmsnorm(o, residual, ln, eps)
@@ -265,7 +268,5 @@ def gate_up_swiglu(x, wgu):
             return hip.linear_swiglu(x, wgu, kernel="stream", wpb=p[1])
         if p[0] == "stream_split":
             return hip.linear_swiglu(x, wgu, kernel="stream_split", wpb=p[1], splits=p[2])
-        if p[0] != "blas":
-            return hip.linear_swiglu(x, wgu, kernel=p[0])
-        return hip.swiglu(torch.nn.functional.linear(x, wgu))
+        return hip.linear_swiglu(x, wgu, kernel=p[0])
     return reference.swiglu(reference.linear(x, wgu))

@@ -575,15 +575,22 @@ def _stream_gemm(x, w, out, epi, splits, ldo, wpb):
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """x @ w^T, bf16 out; MFMA weight-streaming kernel for M <= 64, hipBLASLt above."""
-    M = x.shape[0]
-    if M > SKINNY_MAX_M or M == 0:
-        return torch.nn.functional.linear(x, w, out=out) if out is not None else torch.nn.functional.linear(x, w)
+    """x @ w^T, bf16 out: the 256 x 256-tile MFMA GEMM for M > 64 (or shapes the decode kernels do not
+    take), else the LDS-DMA weight-ring stream GEMM when it fills the chip (the LM head), else the
+    register-streaming skinny kernel."""
+    M, K = x.shape
     N = w.shape[0]
-    nt = 2 if N % 32 == 0 and N >= 16384 else 1
+    if M > SKINNY_MAX_M or M == 0 or K % 128:
+        return gemm(x, w, out=out)
     if out is None:
         out = torch.empty(M, N, dtype=x.dtype, device=x.device)
     _req(out.is_contiguous() and out.shape == (M, N), "linear: bad out")
+    cfg = stream_config(N, K, splits=1) if STREAM_GEMM else None
+    if cfg is not None:
+        return _stream_gemm(x, w, out, EPI_BF16, 1, N, cfg[0])
+    nt = 2 if N % 32 == 0 and N >= 16384 else 1
+    if N % (16 * nt):
+        return gemm(x, w, out=out)
     return _skinny(x, w, out, EPI_BF16, nt, 1, N)
 
 
@@ -646,8 +653,8 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tenso
     """silu(gate) * up straight out of the gate_up GEMM (blocked [8 gate | 8 up] weight rows)."""
     M = x.shape[0]
     F2 = w_gu.shape[0]
-    if M > SKINNY_MAX_M:
-        return swiglu(torch.nn.functional.linear(x, w_gu), out)
+    if M > SKINNY_MAX_M or kernel == "gemm":
+        return gemm(x, w_gu, out=out, swiglu=True)
     if out is None:
         out = torch.empty(M, F2 // 2, dtype=x.dtype, device=x.device)
     _req(out.is_contiguous() and out.shape == (M, F2 // 2), "linear_swiglu: bad out")
@@ -686,7 +693,7 @@ def add_rmsnorm_parts(parts: torch.Tensor, residual: torch.Tensor, w: torch.Tens
 #   hipBLASLt                              M=39 qkv 19.9 | o 19.7 | gate_up 49.8 (+SwiGLU) | down 36.3
 # The stream kernel is flat in M up to 64 and best on grids of exactly one workgroup per CU.
 # Streaming floor (probe): qkv 9.5, o 7.6, down 20.1, gate_up 39.1.
-# Plan = ("stream", wpb, S) | ("skinny", nt, S) | ("lds", S) | ("blas",)
+# Plan = ("stream", wpb, S) | ("skinny", nt, S) | ("lds", S) | ("gemm",) (the 256 x 256-tile kernel)
 N_CU = 256
 
 
@@ -717,7 +724,7 @@ def stream_config(N: int, K: int, swiglu: bool = False, splits: Optional[int] = 
 
 def plan(role: str, M: int, N: int, K: int, splits: Optional[int] = None, stream: bool = True):
     if M > SKINNY_MAX_M or K % 128:
-        return ("blas",)
+        return ("gemm",)
     cfg = stream_config(N, K, swiglu=(role == "gate_up"), splits=splits) if stream and STREAM_GEMM else None
     if cfg is not None:
         return ("stream",) + cfg
@@ -743,18 +750,18 @@ def plan(role: str, M: int, N: int, K: int, splits: Optional[int] = None, stream
             return ("skinny", 1, splits or div(2))
         if M <= 16:
             return ("skinny", 2, splits or div(4)) if N % 32 == 0 else ("skinny", 1, splits or div(2))
-        return ("lds", splits or div(8)) if N % 64 == 0 else ("blas",)
+        return ("lds", splits or div(8)) if N % 64 == 0 else ("gemm",)
     if role in ("o", "down"):
         if M <= 16:
             return ("skinny", 2, splits or div(2)) if N % 32 == 0 else ("skinny", 1, splits or div(4))
         if N % 64:
-            return ("blas",)
+            return ("gemm",)
         return ("lds", splits or div(8))
     if role == "gate_up":
         if M <= 16:
             return ("skinny", 1, 1)
-        return ("blas",)
-    return ("blas",)
+        return ("gemm",)
+    return ("gemm",)
 
 
 STREAM_GEMM = os.environ.get("MRSUM_STREAM_GEMM", "1") == "1"
@@ -821,9 +828,10 @@ def _stream_fp8(x, w, out, epi, splits, ldo, wpb):
     return out
 
 
-def fp8_linear(x: torch.Tensor, w, out_dtype=torch.bfloat16) -> torch.Tensor:
-    """x @ (scale * W8)^T for any M: MFMA W8A16 weight-streaming kernel at decode sizes, hipBLASLt fp8
-    (torch._scaled_mm, row-wise activation x column-wise weight scales) at prefill sizes."""
+def fp8_linear(x: torch.Tensor, w, swiglu: bool = False) -> torch.Tensor:
+    """x @ (scale * W8)^T for any M: MFMA W8A16 weight-streaming kernel at decode sizes; at prefill sizes
+    row-wise e4m3fn activation quantisation + the fp8 MFMA GEMM (gemm.hip, per-row activation x
+    per-row weight scales in the epilogue)."""
     M = x.shape[0]
     N = w.q.shape[0]
     if M <= SKINNY_MAX_M:
@@ -834,7 +842,7 @@ def fp8_linear(x: torch.Tensor, w, out_dtype=torch.bfloat16) -> torch.Tensor:
         nt = 2 if N % 32 == 0 and N >= 16384 else 1
         return _skinny_fp8(x, w, out, EPI_BF16, nt, 1, N)
     xq, xs = quant_fp8_rows(x)
-    return torch._scaled_mm(xq, w.q.t(), scale_a=xs.view(-1, 1), scale_b=w.scale.view(1, -1), out_dtype=out_dtype)
+    return gemm_fp8(xq, xs, w, swiglu=swiglu)
 
 
 def fp8_linear_parts(x: torch.Tensor, w, splits: int, nt: int = 1, stream_wpb: Optional[int] = None) -> torch.Tensor:
@@ -852,7 +860,7 @@ def fp8_linear_swiglu(x: torch.Tensor, w) -> torch.Tensor:
     M = x.shape[0]
     F2 = w.q.shape[0]
     if M > SKINNY_MAX_M:
-        return swiglu(fp8_linear(x, w))
+        return fp8_linear(x, w, swiglu=True)
     out = torch.empty(M, F2 // 2, dtype=torch.bfloat16, device=x.device)
     cfg = stream_config_fp8(F2, x.shape[1], swiglu=True, M=M)
     if cfg is not None:

@@ -68,21 +68,13 @@ def test_many_sequences_compaction(eng):
     assert eng.kv.alloc.available() == eng.kv.num_pages - 1
 
 
-def test_padded_prefill_matches_unpadded(eng):
-    """Prefill batches padded to a multiple of 4096 tokens (a never-cached padding sequence) generate
-    what the unpadded batch generates."""
+def test_packed_prefill_matches_single(eng):
+    """A packed varlen prefill of ragged prompts (3803 rows: no 256-multiple, no padding) generates what
+    each prompt generates on its own."""
     prompts = [[128000] + [(i * 53 + j * 7) % 120000 + 5 for j in range(n)] for i, n in enumerate((1500, 1200, 1100))]
-    T = sum(len(p) for p in prompts)
-    assert eng._prefill_pad(T) == 4096  # 3803 tokens -> one 293-token padding sequence
     sp = [SamplingParams(8, 0.0, 0)] * len(prompts)
-    pad0 = eng.stats.get("prefill_pad_tokens", 0)
     a = eng.generate(prompts, sp)
-    assert eng.stats.get("prefill_pad_tokens", 0) - pad0 == 4096 - T
-    eng.pad_prefill = False
-    try:
-        b = eng.generate(prompts, sp)
-    finally:
-        eng.pad_prefill = True
+    b = [eng.generate([p], [s])[0] for p, s in zip(prompts, sp)]
     same = sum(x.token_ids == y.token_ids for x, y in zip(a, b))
     assert same >= len(prompts) - 1  # a bf16 near-tie may flip one sequence
 
@@ -102,7 +94,7 @@ def test_long_context_class_graphs():
 
 def test_fp8_engine_decode_matches_prefill():
     """fp8 (e4m3fn) weights: decode GEMMs on the fp8 stream / register-streaming kernels, prefill on
-    hipBLASLt fp8 -- greedy decode agrees with teacher-forced prefill."""
+    the fp8 MFMA GEMM (gemm.hip) -- greedy decode agrees with teacher-forced prefill."""
     e = LLMEngine(get_model_config("tiny-gqa4", init_std=0.05), device="cuda:0", max_model_len=2048,
                   max_num_seqs=16, kv_pages=256, sync_every=8, weight_dtype="fp8")
     prompts = _prompts()

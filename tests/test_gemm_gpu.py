@@ -33,7 +33,7 @@ def _check(out, ref, tol=2e-2):
 
 @pytest.mark.parametrize("M,N,K", [(65, 256, 128), (1000, 1280, 4096), (4097, 6144, 4096),
                                    (300, 16032, 1024), (16384 + 13, 4096, 1024), (257, 4096, 14336)])
-@pytest.mark.parametrize("stagger", [0, 1])
+@pytest.mark.parametrize("stagger", [0, 1, 3, 5, 6, 7])
 def test_gemm_bf16(M, N, K, stagger):
     x = _rand(M, K, seed=1, scale=0.5, offset=0.05)
     w = _rand(N, K, seed=2, scale=0.02, offset=0.001)
@@ -58,20 +58,22 @@ def test_gemm_strided_input_and_out():
     big = _rand(M, K + 64, seed=3, scale=0.3)
     x = big[:, 32:32 + K]
     w = _rand(N, K, seed=4, scale=0.05)
-    out_big = torch.zeros(M, N + 16, dtype=torch.bfloat16, device=DEV)
-    hip.gemm(x, w, out=out_big[:, :N])
-    torch.cuda.synchronize()
-    _check(out_big[:, :N], x.float() @ w.float().t())
-    assert float(out_big[:, N:].abs().max()) == 0.0, "wrote past the output view"
+    for flags in (1, 7):
+        out_big = torch.zeros(M, N + 16, dtype=torch.bfloat16, device=DEV)
+        hip.gemm(x, w, out=out_big[:, :N], stagger=flags)
+        torch.cuda.synchronize()
+        _check(out_big[:, :N], x.float() @ w.float().t())
+        assert float(out_big[:, N:].abs().max()) == 0.0, "wrote past the output view"
 
 
 @pytest.mark.parametrize("M", [100, 3000])
-def test_gemm_swiglu(M):
+@pytest.mark.parametrize("flags", [1, 7])
+def test_gemm_swiglu(M, flags):
     K, F = 4096, 1792
     x = _rand(M, K, seed=5, scale=0.5)
     wg, wu = _rand(F, K, seed=6, scale=0.03), _rand(F, K, seed=7, scale=0.03)
     wgu = reference.interleave_gate_up(wg, wu).contiguous()
-    out = hip.gemm(x, wgu, swiglu=True)
+    out = hip.gemm(x, wgu, swiglu=True, stagger=flags)
     torch.cuda.synchronize()
     g, u = x.float() @ wg.float().t(), x.float() @ wu.float().t()
     _check(out, torch.nn.functional.silu(g) * u, tol=3e-2)
@@ -79,11 +81,12 @@ def test_gemm_swiglu(M):
 
 @pytest.mark.parametrize("M,N,K", [(77, 1280, 8192), (2049, 7168, 8192), (513, 16032, 1024)])
 @pytest.mark.parametrize("swiglu", [False, True])
-def test_gemm_fp8(M, N, K, swiglu):
+@pytest.mark.parametrize("flags", [1, 7])
+def test_gemm_fp8(M, N, K, swiglu, flags):
     x = _rand(M, K, seed=8, scale=0.5, offset=0.02)
     w = Fp8Weight.quantize(_rand(N, K, seed=9, scale=0.02))
     xq, xs = hip.quant_fp8_rows(x)
-    out = hip.gemm_fp8(xq, xs, w, swiglu=swiglu)
+    out = hip.gemm_fp8(xq, xs, w, swiglu=swiglu, stagger=flags)
     torch.cuda.synchronize()
     xd = xq.float() * xs[:, None]
     ref = xd @ w.dequant().t()
