@@ -429,7 +429,7 @@ __device__ __forceinline__ u32x4 ld_kv(const bf16* p) {
 }
 
 template <int G, bool ROPE, bool NT = false>
-__global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
+__global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     const bf16* __restrict__ q, int q_stride, bf16* __restrict__ kc, bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ positions,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int S, float scale_log2, RopeArgs ra,
@@ -474,15 +474,19 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
     // (the last tile is re-read instead of branching) so hipcc keeps the loads in flight.
     // (issued first by every split, the one holding the new token included: its new K/V row reaches
     // the tile through the LDS patch, so the page loads need not wait for the slab sums)
-    u32x4 kreg[4], vreg[4];
-    {
-        const size_t base = (size_t)bt[0] * Hkv * PG * D + head_off;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            kreg[i] = ld_kv<NT>(kc + base + (size_t)16 * i * D);
-            vreg[i] = ld_kv<NT>(vc + base + (size_t)16 * i * D);
-        }
+    // TWO tiles in flight: register sets A (kreg/vreg) and B (kreg2/vreg2) alternate; loads past the
+    // last tile re-read it (clamped, unconditional).
+    u32x4 kreg[4], vreg[4], kreg2[4], vreg2[4];
+#define KV_ISSUE(KR, VR, TILE)                                                          \
+    {                                                                                   \
+        const size_t base_ = (size_t)bt[min((TILE), ntiles - 1)] * Hkv * PG * D + head_off; \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                 \
+            KR[i] = ld_kv<NT>(kc + base_ + (size_t)16 * i * D);                         \
+            VR[i] = ld_kv<NT>(vc + base_ + (size_t)16 * i * D);                         \
+        }                                                                               \
     }
+    KV_ISSUE(kreg, vreg, 0)
+    KV_ISSUE(kreg2, vreg2, 1)
     // ROPE: the q rows of this group (and, for the split holding the new token, its K and V rows)
     // summed over the SP slabs by ALL 256 threads in one round of independent loads into an fp32
     // LDS image (aliasing the K/V tile buffers, which are first written after it is consumed):
@@ -562,12 +566,16 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
     if constexpr (ROPE) {
         __syncthreads();  // every lane has its q out of the fp32 image the tiles overwrite
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const bool pt = ROPE && ptile == 0 && patcher && i == (pr >> 4);
-        *reinterpret_cast<u32x4*>(ldsK + dk_off(st_row + 16 * i, st_chunk)) = pt ? *reinterpret_cast<const u32x4*>(lds_new + st_chunk * 8) : kreg[i];
-        *reinterpret_cast<u32x4*>(ldsV + dv_off(st_row + 16 * i, st_chunk)) = pt ? *reinterpret_cast<const u32x4*>(lds_new + D + st_chunk * 8) : vreg[i];
+#define KV_WRITE(KR, VR, TILE)                                                                                  \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                             \
+        const bool pt = ROPE && ptile == (TILE) && patcher && i == (pr >> 4);                                   \
+        *reinterpret_cast<u32x4*>(ldsK + dk_off(st_row + 16 * i, st_chunk)) =                                   \
+            pt ? *reinterpret_cast<const u32x4*>(lds_new + st_chunk * 8) : KR[i];                               \
+        *reinterpret_cast<u32x4*>(ldsV + dv_off(st_row + 16 * i, st_chunk)) =                                   \
+            pt ? *reinterpret_cast<const u32x4*>(lds_new + D + st_chunk * 8) : VR[i];                           \
     }
+    KV_WRITE(kreg, vreg, 0)
+    KV_ISSUE(kreg, vreg, 2)
 
     f32x4 o[8];
 #pragma unroll
@@ -576,16 +584,7 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
     const int q4 = col >> 2, p4 = col & 3;
     __syncthreads();
 
-    for (int t = 0; t < ntiles; ++t) {
-        {
-            const int tn = min(t + 1, ntiles - 1);
-            const size_t base = (size_t)bt[tn] * Hkv * PG * D + head_off;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                kreg[i] = ld_kv<NT>(kc + base + (size_t)16 * i * D);
-                vreg[i] = ld_kv<NT>(vc + base + (size_t)16 * i * D);
-            }
-        }
+    auto compute = [&](int t) {
         const int key0 = ks + t * PG + 16 * w;  // this wave's 16 keys
         if (key0 < ke) {
             f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
@@ -618,17 +617,27 @@ __global__ __launch_bounds__(256, 4) void attn_decode_mfma_kernel(
                 o[dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pb, o[dt], 0, 0, 0);
             }
         }
+    };
+    // LDS holds tile t; set B carries tile t + 1 and set A tile t + 2 (two tiles in flight while a tile
+    // is scored); unrolled by two so every register array is indexed statically.
+    for (int t = 0; t < ntiles; t += 2) {
+        compute(t);
         __syncthreads();
         if (t + 1 < ntiles) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const bool pt = ROPE && ptile == t + 1 && patcher && i == (pr >> 4);
-                *reinterpret_cast<u32x4*>(ldsK + dk_off(st_row + 16 * i, st_chunk)) = pt ? *reinterpret_cast<const u32x4*>(lds_new + st_chunk * 8) : kreg[i];
-                *reinterpret_cast<u32x4*>(ldsV + dv_off(st_row + 16 * i, st_chunk)) = pt ? *reinterpret_cast<const u32x4*>(lds_new + D + st_chunk * 8) : vreg[i];
-            }
+            KV_WRITE(kreg2, vreg2, t + 1)
+            KV_ISSUE(kreg2, vreg2, t + 3)
+            __syncthreads();
+            compute(t + 1);
+            __syncthreads();
+        }
+        if (t + 2 < ntiles) {
+            KV_WRITE(kreg, vreg, t + 2)
+            KV_ISSUE(kreg, vreg, t + 4)
             __syncthreads();
         }
     }
+#undef KV_ISSUE
+#undef KV_WRITE
 
     // merge the 4 waves: lane (grp, col) holds O^T[d = 16dt + 4grp + j][head col]
     lsum += __shfl_xor(lsum, 16, 64);

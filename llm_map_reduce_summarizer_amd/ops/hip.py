@@ -295,24 +295,24 @@ def ctx_class(ctx: int) -> int:
     return len(CTX_CLASSES) - 1
 
 
+ATTN_SLOTS = int(os.environ.get("MRSUM_ATTN_SLOTS", "768"))
+
+
 def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
     """(splits, fused_combine) of the decode attention of ``batch`` sequences x ``hkv`` kv heads whose
     contexts reach ``max_ctx`` tokens (the engine passes its context class's upper bound).
 
-    Splits: enough (sequence, kv head, split) workgroups to fill the chip (~1024), about 2 pages per split
-    (each workgroup walks its pages serially: at B=1 and ~11k context 16 splits of 11 pages ran at
-    1.7 TB/s), at most 64.  Fused = the split merge runs in the attention launch, by the last split of
-    each (sequence, kv head) to arrive, with write-through (sc1) partial stores and no release fence
-    (the fenced form wrote back the whole L2, full of the preceding GEMMs' slabs, and lost in the decode
-    graph: TP=8 B=1 1.555 vs 1.502 ms per step); write-through, in the decode graph at 4k context (ms
-    per step, fused vs separate merge kernel): TP=8 shard B=10 1.714 vs 1.772, B=39 2.391 vs 2.471,
-    TP=1 B=1 / B=10 equal within noise.  "auto": fused for at most 64 (sequence, kv head) groups and at
-    most 32 splits (the merging workgroup reads every split's partials).  2 pages / split with up to 32
-    fused splits vs 4 / 16 (ms per step, profiles/r1_attn_splits_ab.jsonl): B=1 4k 3.508 vs 3.539, B=1 10k
-    3.615 vs 3.683, B=10 / B=39 within noise; 1 page / split lost (B=1 4k 3.806)."""
+    Splits: as many (sequence, kv head, split) workgroups as fit on the chip AT ONCE (ATTN_SLOTS = 3
+    resident workgroups per CU x 256 CUs: the kernel keeps two 32 KiB K+V tiles in flight per
+    workgroup in registers, 162 VGPRs) -- never more, so all splits run in one round (at B=39 x 8 kv
+    heads the previous ceil(1024 / groups) = 4 splits made 1248 workgroups = two rounds) -- and at
+    least ATTN_PAGES_PER_SPLIT pages each, at most 64.  Fused = the split merge runs in the attention
+    launch, by the last split of each (sequence, kv head) to arrive, with write-through (sc1) partial
+    stores and no release fence; "auto": fused for at most 64 (sequence, kv head) groups and at most
+    32 splits (the merging workgroup reads every split's partials)."""
     pages = max(1, -(-max_ctx // 64))
     groups = max(1, batch * hkv)
-    splits = max(1, min(-(-1024 // groups), -(-pages // ATTN_PAGES_PER_SPLIT), 64))
+    splits = max(1, min(ATTN_SLOTS // groups, -(-pages // ATTN_PAGES_PER_SPLIT), 64))
     if FUSED_COMBINE == "auto":
         fused = groups <= 64 and splits <= max(24, ATTN_FUSED_MAX_SPLITS)
     else:
