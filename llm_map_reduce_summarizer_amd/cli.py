@@ -16,6 +16,10 @@ go to stderr through one logging setup (Q11), the summary to stdout.
 
 from __future__ import annotations
 
+import os as _os
+
+_os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL, P2P all-reduce), before HIP init
+
 import argparse
 import asyncio
 import json

@@ -17,6 +17,16 @@ stage, data-parallel over the ranks of the job:
 Sampling seeds are derived from the request content, so a summary does not
 depend on which rank produced it or how the batch was formed.
 
+Failures are collective-safe: an engine error on one rank is caught there,
+the rank still enters the stage's all-gather (with error records for its
+requests), and every rank ends the stage with the SAME results -- so the
+executor's retry loop (reference ``llm_executor.py:196-228``) retries the same
+requests on every rank, re-balanced over the replicas (a request that failed
+on a sick replica may land on a healthy one).  TP stages agree on an ok/error
+vector before and after the sharded generate.  ``MRSUM_FAULT_INJECT=
+"rank:count"`` (or ``fault_inject=``) raises in the engine call of ``rank``
+for its first ``count`` calls (-1: every call) -- the test hook.
+
 With several GPUs a stage may instead run on ONE engine sharded over all of
 them (TP = world): decode is bound by streaming weights + KV from HBM, which
 DP replicas do not shorten and TP divides.  ``parallel`` selects the policy:
@@ -70,8 +80,11 @@ class LocalEngineProvider(Provider):
                  engine_options: Optional[Dict[str, Any]] = None, dtype: Optional[str] = None,
                  kv_fraction: Optional[float] = None, use_graphs: bool = True, max_num_seqs: Optional[int] = None,
                  tokenizer: Optional[str] = None, ignore_eos: bool = False, reduce_tp: Optional[bool] = None,
-                 weights: Optional[str] = None, parallel: Optional[str] = None, **_ignored):
+                 weights: Optional[str] = None, parallel: Optional[str] = None,
+                 fault_inject: Optional[str] = None, **_ignored):
         super().__init__(model, config)
+        spec = fault_inject or os.environ.get("MRSUM_FAULT_INJECT", "")
+        self._fault_rank, self._fault_left = (int(x) for x in spec.split(":")) if spec else (-1, 0)
         self.tokenizer = get_tokenizer(tokenizer)
         if dtype not in (None, "bf16", "fp8"):
             raise ValueError("dtype must be bf16 or fp8, got %s" % dtype)
@@ -120,6 +133,7 @@ class LocalEngineProvider(Provider):
         if self.handoff:
             self._dp_needed = True
         self.stage_plan: Dict[str, Any] = {}
+        self.owner_maps: Dict[str, List[List[int]]] = {}  # stage -> replica of every request, per call
         if self.use_tp_engine:
             self._engine_options.setdefault("kv_fraction", float(os.environ.get("MRSUM_DP_KV_FRACTION", "0.5")))
 
@@ -261,21 +275,36 @@ class LocalEngineProvider(Provider):
         world, rank = self.par.world, self.par.rank
         owner = assign_balanced([len(p) for p in prompts], world)
         mine = [i for i in range(len(prompts)) if owner[i] == rank]
-        firsts, packs = self.engine.prefill_export([prompts[i] for i in mine], [sp[i] for i in mine], world,
-                                                   ignore_eos=self.ignore_eos)
         tp_eng = self.tp_engine
         shapes = [tp_eng.import_shape(len(p)) for p in prompts]
         numel = [math.prod(s) for s in shapes]
         recv_sizes = [sum(numel[i] for i in range(len(prompts)) if owner[i] == s) for s in range(world)]
-        send = torch.cat(packs) if packs else torch.empty(0, dtype=torch.bfloat16)
         nccl = dist.get_backend() == "nccl"
+        err = None
+        try:
+            self._maybe_fault()
+            firsts, packs = self.engine.prefill_export([prompts[i] for i in mine], [sp[i] for i in mine], world,
+                                                       ignore_eos=self.ignore_eos)
+            send = torch.cat(packs) if packs else torch.empty(0, dtype=torch.bfloat16)
+            send_sizes = [p.numel() for p in packs]
+        except Exception as e:  # noqa: BLE001 -- still enter the all-to-all with the sizes the peers expect
+            err = "rank %d prefill: %s: %s" % (rank, type(e).__name__, e)
+            log.error("%s", err)
+            firsts = [0] * len(mine)
+            send_sizes = [sum(numel[i] for i in mine)] * world
+            send = torch.zeros(sum(send_sizes), dtype=torch.bfloat16,
+                               device=torch.device(self._device) if nccl else "cpu")
         dev = send.device if nccl else torch.device("cpu")
         send = send.to(dev)
         recv = torch.empty(sum(recv_sizes), dtype=send.dtype, device=dev)
-        dist.all_to_all_single(recv, send, recv_sizes, [p.numel() for p in packs])
-        tok = {}
-        for part in pdist.all_gather_json({str(i): int(t) for i, t in zip(mine, firsts)}):
-            tok.update({int(k): v for k, v in part.items()})
+        dist.all_to_all_single(recv, send, recv_sizes, send_sizes)
+        tok, errs = {}, []
+        for part in pdist.all_gather_json({"tok": {str(i): int(t) for i, t in zip(mine, firsts)}, "err": err}):
+            tok.update({int(k): v for k, v in part["tok"].items()})
+            if part["err"]:
+                errs.append(part["err"])
+        if errs:  # every rank raises the same error: the stage fails as a whole, consistently
+            raise RuntimeError("; ".join(errs))
         out, off = {}, 0
         for s in range(world):
             for i in range(len(prompts)):
@@ -295,8 +324,40 @@ class LocalEngineProvider(Provider):
         return ids
 
     # ------------------------------------------------------------------ API
+    def _maybe_fault(self) -> None:
+        """Test hook (MRSUM_FAULT_INJECT / fault_inject="rank:count"): raise on this rank's engine call."""
+        if self._fault_left != 0 and self.par.rank == self._fault_rank:
+            if self._fault_left > 0:
+                self._fault_left -= 1
+            raise RuntimeError("injected engine fault on rank %d" % self.par.rank)
+
     async def generate(self, req: GenRequest) -> GenResult:
         return (await self.generate_batch([req]))[0]
+
+    def _generate_tp(self, prompts, reqs, handoff: bool) -> List[GenResult]:
+        """One TP=world engine over every request; ranks agree on ok / error before and after, so a
+        rank-local error (raised before the sharded forward) fails the stage on every rank alike."""
+        from .engine import SamplingParams
+        sp = [SamplingParams(r.max_tokens, r.temperature, _req_seed(self.seed, r)) for r in reqs]
+        err = None
+        try:
+            self._maybe_fault()  # (the TP engine itself was built by _stage_tp, collectively)
+        except Exception as e:  # noqa: BLE001
+            err = "rank %d: %s: %s" % (self.par.rank, type(e).__name__, e)
+        errs = [x for x in pdist.all_gather_json(err) if x]
+        outs = None
+        if not errs:
+            try:
+                imported = self._handoff(prompts, sp) if handoff else None
+                outs = self.tp_engine.generate(prompts, sp, ignore_eos=self.ignore_eos, imported=imported)
+            except Exception as e:  # noqa: BLE001 -- deterministic (SPMD) errors are raised on every rank
+                err = "rank %d: %s: %s" % (self.par.rank, type(e).__name__, e)
+            errs = [x for x in pdist.all_gather_json(err) if x]
+        if errs:
+            log.error("TP stage failed: %s", "; ".join(errs))
+            return [GenResult("", error="; ".join(errs)) for _ in reqs]
+        return [GenResult(self.tokenizer.decode(o.token_ids), o.prompt_len, len(o.token_ids), 0.0,
+                          extra={"finish_reason": o.finish_reason}) for o in outs]
 
     async def generate_batch(self, reqs: Sequence[GenRequest]) -> List[GenResult]:
         from .engine import SamplingParams
@@ -307,24 +368,43 @@ class LocalEngineProvider(Provider):
         self.stage_plan.setdefault(stage, {"tp": tp, "handoff": handoff})
         if tp > 1:
             # every rank runs every request on the TP engine; the TP ranks sample identically
-            sp = [SamplingParams(r.max_tokens, r.temperature, _req_seed(self.seed, r)) for r in reqs]
-            imported = self._handoff(prompts, sp) if handoff else None
-            outs = self.tp_engine.generate(prompts, sp, ignore_eos=self.ignore_eos, imported=imported)
+            res = self._generate_tp(prompts, reqs, handoff)
             self.timings["generate_s"] += time.perf_counter() - t0
-            return [GenResult(self.tokenizer.decode(o.token_ids), o.prompt_len, len(o.token_ids), 0.0,
-                              extra={"finish_reason": o.finish_reason}) for o in outs]
+            return res
         dp, dp_rank = self.par.dp, self.par.dp_rank
         owner = assign_balanced([len(p) + r.max_tokens for p, r in zip(prompts, reqs)], dp)
+        self.owner_maps.setdefault(stage, []).append(owner)
         mine = [i for i in range(len(reqs)) if owner[i] == dp_rank]
         local: List[Dict[str, Any]] = []
-        if mine:
-            outs = self.engine.generate(
-                [prompts[i] for i in mine],
-                [SamplingParams(reqs[i].max_tokens, reqs[i].temperature, _req_seed(self.seed, reqs[i])) for i in mine],
-                ignore_eos=self.ignore_eos)
-            for i, o in zip(mine, outs):
-                local.append({"i": i, "text": self.tokenizer.decode(o.token_ids), "pt": o.prompt_len,
-                              "ct": len(o.token_ids), "fr": o.finish_reason})
+        pre_err = None
+        if self.par.tp > 1:
+            # TP replicas: agree on local pre-checks first, so no TP rank of a replica enters the sharded
+            # forward (all-reduces) while a peer of the same replica has already given up
+            try:
+                self._maybe_fault()
+            except Exception as e:  # noqa: BLE001
+                pre_err = "rank %d: %s: %s" % (self.par.rank, type(e).__name__, e)
+            errs = pdist.all_gather_json(pre_err)
+            g0 = dp_rank * self.par.tp
+            pre_err = next((x for x in errs[g0:g0 + self.par.tp] if x), None)
+        if mine and pre_err:
+            local = [{"i": i, "err": pre_err} for i in mine]
+        elif mine:
+            try:
+                if self.par.tp == 1:
+                    self._maybe_fault()
+                outs = self.engine.generate(
+                    [prompts[i] for i in mine],
+                    [SamplingParams(reqs[i].max_tokens, reqs[i].temperature, _req_seed(self.seed, reqs[i]))
+                     for i in mine],
+                    ignore_eos=self.ignore_eos)
+                for i, o in zip(mine, outs):
+                    local.append({"i": i, "text": self.tokenizer.decode(o.token_ids), "pt": o.prompt_len,
+                                  "ct": len(o.token_ids), "fr": o.finish_reason})
+            except Exception as e:  # noqa: BLE001 -- never skip the all-gather below: the peers are in it
+                msg = "rank %d: %s: %s" % (self.par.rank, type(e).__name__, e)
+                log.error("engine failed on %d requests: %s", len(mine), msg)
+                local = [{"i": i, "err": msg} for i in mine]
         t1 = time.perf_counter()
         self.timings["generate_s"] += t1 - t0
         if pdist.is_initialized():  # also at world 1 under torchrun: same RCCL code path as N > 1
@@ -343,6 +423,8 @@ class LocalEngineProvider(Provider):
             r = merged.get(i)
             if r is None:
                 results.append(GenResult("", error="request %d produced no result" % i))
+            elif "err" in r:
+                results.append(GenResult("", error=r["err"]))
             else:
                 results.append(GenResult(r["text"], r["pt"], r["ct"], 0.0, extra={"finish_reason": r["fr"]}))
         return results

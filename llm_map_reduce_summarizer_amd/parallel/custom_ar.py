@@ -313,9 +313,13 @@ def maybe_custom_all_reduce(group=None, max_bytes: int = 4 << 20) -> Optional[Cu
     """A CustomAllReduce for ``group`` when every rank is on a GPU, else None (RCCL/gloo path)."""
     if not (dist.is_initialized() and torch.cuda.is_available()):
         return None
+    from .. import IPC_MODE_TOO_LATE
     try:
         ar = CustomAllReduce(group, max_bytes)
     except Exception as e:  # no IPC (e.g. container without dmabuf): fall back to RCCL
+        if IPC_MODE_TOO_LATE:
+            log.error("custom all-reduce: HIP was initialised before HSA_ENABLE_IPC_MODE_LEGACY=0 was set "
+                      "(set it in the environment before the first GPU call); dmabuf IPC is unavailable")
         log.warning("custom all-reduce unavailable, using RCCL: %s", e)
         return None
     if not ar.self_test():

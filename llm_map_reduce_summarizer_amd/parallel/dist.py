@@ -13,8 +13,17 @@ on a single node, and data-parallel replicas are the TP groups.
 The map-reduce pipeline only needs tiny DP collectives:
 variable-length UTF-8 payloads (summaries, token counts) are all-gathered as
 ``uint8`` device tensors after an all-gather of their lengths -- one RCCL
-all-gather of ``world x max_len`` bytes per phase.  TP all-reduces live in
-``parallel/tp.py``.
+all-gather of ``world x max_len`` bytes per phase.  TP all-reduces are issued
+by the model (``engine/model.py: LlamaModel._all_reduce``: the one-shot P2P
+kernel of ``parallel/custom_ar.py`` for decode-sized messages, RCCL above).
+
+Failure discipline: a rank-local error must never make one rank skip a
+collective its peers enter.  Stage-level code (``engine/provider.py``) catches
+engine errors locally, still enters every collective of the stage, and turns
+the error into records that the all-gather hands to EVERY rank, so retry
+decisions are identical everywhere.  The process-group timeout
+(``MRSUM_DIST_TIMEOUT`` seconds, default 600) bounds what cannot be caught that
+way (a rank dying inside a TP all-reduce).
 """
 
 from __future__ import annotations
@@ -56,7 +65,7 @@ def is_initialized() -> bool:
     return dist.is_available() and dist.is_initialized()
 
 
-def init_distributed_from_env(backend: Optional[str] = None, timeout_s: float = 1800.0) -> bool:
+def init_distributed_from_env(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> bool:
     """Initialise the default group when launched by torchrun (WORLD_SIZE > 1)."""
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     force = os.environ.get("MRSUM_FORCE_DIST", "0") == "1" and "RANK" in os.environ  # world-1 RCCL rehearsal
@@ -64,6 +73,8 @@ def init_distributed_from_env(backend: Optional[str] = None, timeout_s: float = 
         return is_initialized()
     if backend is None:
         backend = os.environ.get("MRSUM_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("MRSUM_DIST_TIMEOUT", "600"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     kwargs = {}
     if backend == "nccl":

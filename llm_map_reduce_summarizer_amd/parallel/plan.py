@@ -49,7 +49,7 @@ class HWModel:
     step_floor_s: float = 0.96e-3   # fixed per-step cost of the decode graph (kernel latencies), 32 layers
     tp_floor_s: float = 0.08e-3     # extra fixed cost of a TP shard's decode graph per log2(TP) (32 layers) ...
     tp_row_s: float = 3e-6          # ... plus this per decode row per log2(TP) (few-kv-head attention is latency-bound)
-    prefill_flops: float = 1.1e15   # effective prefill FLOP/s (hipBLASLt GEMMs + flash attention)
+    prefill_flops: float = 1.1e15   # effective prefill FLOP/s (MFMA GEMMs + flash attention)
     ar_lat_s: float = 20e-6         # one decode all-reduce (custom P2P kernel), measured at start-up ...
     ar_lat_row_s: float = 0.0       # ... plus this per decode row (the push sends every row to every peer)
     ar_bw: float = 100e9            # RCCL all-reduce algorithm bandwidth (bytes/s), measured at start-up
@@ -112,12 +112,13 @@ def stage_seconds(d: ModelDims, hw: HWModel, prompt_lens: Sequence[int], max_new
                   world: int, handoff: bool = False) -> float:
     """Estimated wall-clock of one stage on ``world`` GPUs as ``world // tp`` replicas of TP=``tp``
     (requests LPT-balanced over replicas, every generation pinned to its ``max_new``).  ``handoff``:
-    a TP=world stage prefills through handoff_prefill_s instead of a TP forward."""
+    a TP stage may prefill through handoff_prefill_s inside its own TP group (the cheaper of the two),
+    whatever the group size -- so TP=world is not favoured over intermediate TP x DP layouts."""
     if not prompt_lens:
         return 0.0
     dp = max(1, world // tp)
     bins = _lpt([p + m for p, m in zip(prompt_lens, max_new)], dp)
-    use_handoff = handoff and tp > 1 and tp == world
+    use_handoff = handoff and tp > 1
     worst = 0.0
     for idx in bins:
         if not idx:
@@ -126,7 +127,7 @@ def stage_seconds(d: ModelDims, hw: HWModel, prompt_lens: Sequence[int], max_new
         mn = [max_new[i] for i in idx]
         t = prefill_s(d, hw, sum(pl), tp)
         if use_handoff:  # the cheaper of the TP forward and the disaggregated prefill
-            t = min(t, handoff_prefill_s(d, hw, pl, world))
+            t = min(t, handoff_prefill_s(d, hw, pl, tp))
         # sequences retire as they reach their max_new: walk the decode in segments of equal batch
         order = sorted(range(len(idx)), key=lambda k: mn[k])
         done = 0

@@ -56,6 +56,7 @@ class LLMExecutor:
         self.total_cost = 0.0
         self.total_requests = 0
         self.failed_requests = 0
+        self.retried_requests = 0  # failed attempts that were retried (final failures: failed_requests)
         self.phase_seconds: Dict[str, float] = {}
 
     @property
@@ -76,6 +77,7 @@ class LLMExecutor:
                     log.warning("request failed (attempt %d/%d): %s", attempt, attempts, e)
                     if attempt == attempts:
                         return GenResult("", error=str(e))
+                    self.retried_requests += 1
                     await asyncio.sleep(self.config.RETRY_DELAY)
         raise AssertionError("unreachable")
 
@@ -103,6 +105,7 @@ class LLMExecutor:
                 log.warning("%d/%d requests failed (attempt %d/%d)", len(nxt), len(reqs), attempt, attempts)
                 pending = nxt
                 if attempt < attempts:
+                    self.retried_requests += len(nxt)
                     await asyncio.sleep(self.config.RETRY_DELAY)
             final = [r for r in results if r is not None]
         else:

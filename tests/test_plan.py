@@ -100,8 +100,10 @@ def test_handoff_for_many_prompts_tp_forward_for_one():
 
 @pytest.mark.parametrize("ar_lat_us", [8.0, 15.0])
 def test_full_tp_beats_intermediate_layouts_for_10h_stages(ar_lat_us):
-    """Why ``auto`` only weighs TP=1 against TP=N: for the 10 h headline's three stages on 8 GPUs the
-    cost model ranks TP=8 ahead of every TP x DP layout (TP=2 x DP=4, TP=4 x DP=2) and of DP=8."""
+    """A property of the COST MODEL (not a hardware measurement -- no 8-GPU run backs it yet): with every
+    TP layout allowed the same hand-off prefill inside its own group, the model ranks TP=8 ahead of
+    TP=2 x DP=4, TP=4 x DP=2 and DP=8 for the 10 h headline's three stages.  This is why ``auto``
+    weighs TP=1 against TP=N only; an 8-GPU measurement may overturn it."""
     hw = plan.with_measurements(plan.HWModel(), ar_lat_s=ar_lat_us * 1e-6, ar_bw=150e9, ar_lat_row_s=0.03e-6)
     for prompts in ([4000] * 39, [10500] * 10, [10500]):
         new = [1000] * len(prompts)
