@@ -308,17 +308,22 @@ def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
     heads the previous ceil(1024 / groups) = 4 splits made 1248 workgroups = two rounds) -- and at
     least ATTN_PAGES_PER_SPLIT pages each, at most 64.  Fused = the split merge runs in the attention
     launch, by the last split of each (sequence, kv head) to arrive, with write-through (sc1) partial
-    stores and no release fence; "auto": fused for at most 64 (sequence, kv head) groups and at most
-    32 splits (the merging workgroup reads every split's partials)."""
+    stores and no release fence; "auto": fused up to 128 (sequence, kv head) groups with at most 16
+    splits (<= 16 groups) or 4 splits (the merging workgroup reads every split's partials)."""
     pages = max(1, -(-max_ctx // 64))
     groups = max(1, batch * hkv)
     splits = max(1, min(ATTN_SLOTS // groups, -(-pages // ATTN_PAGES_PER_SPLIT), 64))
     if FUSED_COMBINE == "auto":
-        fused = groups <= 64 and splits <= max(24, ATTN_FUSED_MAX_SPLITS)
+        # measured at 4k context (tools/bench_attn_decode.py, profiles/r2_attn_decode_splits_fused_sweep.jsonl):
+        # B=1 fused 16 splits 16.1 us vs 32 unfused 19.0; B=10 fused 4 splits 37.5 us vs 9 unfused 40.1;
+        # B=39 unfused 2-4 splits 113 us vs fused 116-118
+        fused = groups <= 128
+        if fused:
+            splits = min(splits, 16 if groups <= 16 else 4)
     else:
         fused = FUSED_COMBINE == "1"
-    if fused:
-        splits = min(splits, ATTN_FUSED_MAX_SPLITS)
+        if fused:
+            splits = min(splits, ATTN_FUSED_MAX_SPLITS)
     return splits, fused
 
 
