@@ -28,6 +28,12 @@
 //                   XOR-swizzled by (row&3)<<2 so the four rows of one
 //                   transposed read land on four different 64-B bank ranges.
 //
+// PAGED (chunked prefill): the packed rows are SLICES of prompts whose first prefix[seq] tokens are
+// already in the paged KV cache (rope_kv wrote this slice's K/V there too, before this launch).  Keys
+// are then read from the cache -- one 64-key tile is exactly one page of one kv head, 16 KiB
+// contiguous -- for positions [0, prefix + slice), and query row qi sits at absolute position
+// prefix + qi (causal offset).  With prefix = 0 it is the same attention as the contiguous path.
+//
 // Numerics: bf16 inputs, fp32 accumulation and softmax, bf16 output.
 #include "common.h"
 
@@ -48,12 +54,21 @@ __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast
 
 // PK: the softmax's per-score FMA (scale, -max) and running-sum adds as packed fp32 pairs
 // (v_pk_fma_f32 / v_pk_add_f32: two scores per VALU instruction)
-template <bool PK>
+struct PagedKV {
+    const bf16* kc;            // [pages, Hkv, 64, D]
+    const bf16* vc;
+    const int* block_tables;   // [slots, bt_stride]
+    int bt_stride;
+    const int* seq_slot;       // [nseq] decode slot (block-table row) of every packed sequence
+    const int* prefix;         // [nseq] tokens already cached before this slice
+};
+
+template <bool PK, bool PAGED>
 __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __restrict__ qkv, int row_stride,
                                                               const int* __restrict__ cu_seqlens,
                                                               const int2* __restrict__ items,
                                                               bf16* __restrict__ out, int out_stride, int Hq,
-                                                              int Hkv, float scale_log2) {
+                                                              int Hkv, float scale_log2, PagedKV pk) {
     // one stage of [K tile | V tile]; a 2-stage ring with one barrier per tile measured 2-4 % slower
     // (its tile writes land between other waves' tile reads instead of behind a barrier)
     __shared__ __attribute__((aligned(16))) char lds[1][2 * BN * 256];
@@ -65,6 +80,10 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5, r32 = lane & 31;
     const bf16* base = qkv + (size_t)s0 * row_stride;
     const int kcol = (Hq + kvh) * D, vcol = (Hq + Hkv + kvh) * D;
+    // keys live at absolute positions [0, pre + len); query row qi at pre + qi
+    const int pre = PAGED ? pk.prefix[seq] : 0;
+    const int* btab = PAGED ? pk.block_tables + (size_t)pk.seq_slot[seq] * pk.bt_stride : nullptr;
+    const size_t head_pg = (size_t)kvh * BN * D;  // this kv head's 64-row slab inside a page
 
     // Q^T fragments: lane holds Q[row r32][dims 16ks + 8half .. +8] for ks = 0..7
     const int qi = qblock + 32 * w + r32;
@@ -80,7 +99,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
         }
     }
 
-    const int kend = min(len, qblock + BM);
+    const int kend = pre + min(len, qblock + BM);
     const int ntiles = (kend + BN - 1) / BN;
 
     // staging: thread loads rows tid/16 + 16i (i<4), chunk tid%16.  Named u32x4 registers and
@@ -90,11 +109,19 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
     const int st_chunk = tid & 15, st_row0 = tid >> 4;
     u32x4 kreg[4], vreg[4];
 #define LOAD_TILE(t)                                                                              \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                               \
-        const int key = min((t) * BN + st_row0 + 16 * i, len - 1);                               \
-        const bf16* p = base + (size_t)key * row_stride + st_chunk * 8;                          \
-        kreg[i] = *reinterpret_cast<const u32x4*>(p + kcol);                                     \
-        vreg[i] = *reinterpret_cast<const u32x4*>(p + vcol);                                     \
+    if constexpr (PAGED) {                                                                        \
+        const size_t pg = (size_t)btab[t] * Hkv * BN * D + head_pg + st_chunk * 8;                \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                           \
+            kreg[i] = *reinterpret_cast<const u32x4*>(pk.kc + pg + (size_t)(st_row0 + 16 * i) * D); \
+            vreg[i] = *reinterpret_cast<const u32x4*>(pk.vc + pg + (size_t)(st_row0 + 16 * i) * D); \
+        }                                                                                         \
+    } else {                                                                                      \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                           \
+            const int key = min((t) * BN + st_row0 + 16 * i, len - 1);                           \
+            const bf16* p = base + (size_t)key * row_stride + st_chunk * 8;                      \
+            kreg[i] = *reinterpret_cast<const u32x4*>(p + kcol);                                 \
+            vreg[i] = *reinterpret_cast<const u32x4*>(p + vcol);                                 \
+        }                                                                                         \
     }
 #define STORE_TILE(stage)                                                                         \
     _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                               \
@@ -112,7 +139,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
     STORE_TILE(0);
     __syncthreads();
 
-    const int wave_last_q = qblock + 32 * w + 31;
+    const int wave_last_q = pre + qblock + 32 * w + 31;  // absolute position of the wave's last row
     const char* ldsK = lds[0];
     const char* ldsV = ldsK + BN * 256;
     for (int t = 0; t < ntiles; ++t) {
@@ -135,8 +162,8 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
             // end (wave-uniform test); scores stay unscaled until the exponent, which is one FMA:
             // p = 2^(s * scale_log2 - m), with the raw v_exp_f32 (no denormal range reduction: the
             // library exp2f costs 4 extra VALU ops per score).
-            const int kmax = min(qi, len - 1) - kv0 - 4 * half;  // last valid key offset for row qi
-            if (kv0 + BN - 1 > qblock + 32 * w || kv0 + BN > len) {
+            const int kmax = pre + min(qi, len - 1) - kv0 - 4 * half;  // last valid key offset for row qi
+            if (kv0 + BN - 1 > pre + qblock + 32 * w || kv0 + BN > pre + len) {
 #pragma unroll
                 for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -154,6 +181,8 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
             // deferred rescale: the running max m only moves (and o, l are rescaled) when some row's
             // max grew by more than RESCALE_LOG2 -- until then p <= 2^RESCALE_LOG2, harmless in fp32
             // and in the bf16 P operand.  Key 0 is valid for every row, so m is finite after tile 0.
+            // (PAGED: rows past the slice end see keys up to pre + len - 1 only; stale page rows past
+            // that are masked like any key beyond the causal limit.)
             const float mc = mt * scale_log2;
             if (__ballot(mc > m + RESCALE_LOG2)) {
                 const float mn = fmaxf(m, mc);
@@ -251,18 +280,39 @@ static int g_prefill_pk = 0;
 // 1: packed-fp32 softmax, 0: scalar (default; packed measured 1-3 % slower) -- A/B switch
 MRSUM_API void mrsum_attn_prefill_set_pk(int on) { g_prefill_pk = on ? 1 : 0; }
 
-MRSUM_API int mrsum_attn_prefill(const void* qkv, int row_stride, const int* cu_seqlens, const int* items,
-                                 int n_items, void* out, int out_stride, int Hq, int Hkv, int Dh, float scale,
-                                 hipStream_t s) {
+static int launch_prefill(const void* qkv, int row_stride, const int* cu_seqlens, const int* items, int n_items,
+                          void* out, int out_stride, int Hq, int Hkv, int Dh, float scale, const PagedKV* pk,
+                          hipStream_t s) {
     if (n_items <= 0) return 0;
     if (Dh != D || Hq % Hkv) return (int)hipErrorInvalidValue;
     dim3 grid(n_items, Hq), block(256);
-    if (g_prefill_pk)
-        attn_prefill_kernel<true><<<grid, block, 0, s>>>((const bf16*)qkv, row_stride, cu_seqlens, (const int2*)items,
-                                                         (bf16*)out, out_stride, Hq, Hkv, scale * 1.4426950408889634f);
-    else
-        attn_prefill_kernel<false><<<grid, block, 0, s>>>((const bf16*)qkv, row_stride, cu_seqlens,
-                                                          (const int2*)items, (bf16*)out, out_stride, Hq, Hkv,
-                                                          scale * 1.4426950408889634f);
+    const float sl = scale * 1.4426950408889634f;
+    auto Q = (const bf16*)qkv;
+    auto IT = (const int2*)items;
+    const PagedKV p = pk ? *pk : PagedKV{nullptr, nullptr, nullptr, 0, nullptr, nullptr};
+    if (pk) {
+        if (g_prefill_pk) attn_prefill_kernel<true, true><<<grid, block, 0, s>>>(Q, row_stride, cu_seqlens, IT, (bf16*)out, out_stride, Hq, Hkv, sl, p);
+        else attn_prefill_kernel<false, true><<<grid, block, 0, s>>>(Q, row_stride, cu_seqlens, IT, (bf16*)out, out_stride, Hq, Hkv, sl, p);
+    } else {
+        if (g_prefill_pk) attn_prefill_kernel<true, false><<<grid, block, 0, s>>>(Q, row_stride, cu_seqlens, IT, (bf16*)out, out_stride, Hq, Hkv, sl, p);
+        else attn_prefill_kernel<false, false><<<grid, block, 0, s>>>(Q, row_stride, cu_seqlens, IT, (bf16*)out, out_stride, Hq, Hkv, sl, p);
+    }
     return (int)hipGetLastError();
+}
+
+MRSUM_API int mrsum_attn_prefill(const void* qkv, int row_stride, const int* cu_seqlens, const int* items,
+                                 int n_items, void* out, int out_stride, int Hq, int Hkv, int Dh, float scale,
+                                 hipStream_t s) {
+    return launch_prefill(qkv, row_stride, cu_seqlens, items, n_items, out, out_stride, Hq, Hkv, Dh, scale, nullptr, s);
+}
+
+// Chunked-prefill attention: q rows of the packed slices (qkv, cu_seqlens), keys / values from the paged
+// cache for absolute positions [0, prefix[seq] + slice length) of every sequence (page size 64).
+MRSUM_API int mrsum_attn_prefill_paged(const void* qkv, int row_stride, const int* cu_seqlens, const int* items,
+                                       int n_items, void* out, int out_stride, int Hq, int Hkv, int Dh, float scale,
+                                       const void* kcache, const void* vcache, const int* block_tables,
+                                       int bt_stride, const int* seq_slot, const int* prefix, hipStream_t s) {
+    if (!kcache || !vcache || !block_tables || !seq_slot || !prefix) return (int)hipErrorInvalidValue;
+    const PagedKV pk{(const bf16*)kcache, (const bf16*)vcache, block_tables, bt_stride, seq_slot, prefix};
+    return launch_prefill(qkv, row_stride, cu_seqlens, items, n_items, out, out_stride, Hq, Hkv, Dh, scale, &pk, s);
 }

@@ -95,8 +95,10 @@ class PagedKVCache:
         self.page = page
         self.num_pages = num_pages
         shape = (n_layers, num_pages, n_kv_heads, page, head_dim)
-        self.k = torch.empty(shape, dtype=dtype, device=device)
-        self.v = torch.empty(shape, dtype=dtype, device=device)
+        # zeroed, not empty: attention kernels read whole pages and mask the scores of rows past a
+        # sequence's end (p = 0), and 0 x a stale NaN bit pattern in such a V row would still be NaN
+        self.k = torch.zeros(shape, dtype=dtype, device=device)
+        self.v = torch.zeros(shape, dtype=dtype, device=device)
         self.alloc = PageAllocator(num_pages)
         log.info("KV cache: %d pages x %d tokens (%.1f GiB)", num_pages, page,
                  2 * self.k.numel() * self.k.element_size() / 2 ** 30)

@@ -220,17 +220,22 @@ class LlamaModel:
     def prefill(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, cu_seqlens: torch.Tensor,
                 last_rows: torch.Tensor, block_tables: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
                 seqlens: Optional[List[int]] = None, items: Optional[torch.Tensor] = None,
-                gather: bool = True) -> torch.Tensor:
+                gather: bool = True, paged=None, logits: bool = True) -> Optional[torch.Tensor]:
         """Packed varlen prefill; returns logits of each sequence's last token [nseq, vocab]
-        (this rank's vocab shard [nseq, vocab / tp] when ``gather`` is False)."""
+        (this rank's vocab shard [nseq, vocab / tp] when ``gather`` is False).  ``paged``
+        (ops.PagedPrefill): the rows are prompt SLICES that attend to their sequence's cached prefix
+        (chunked prefill); ``logits=False`` skips the LM head (a non-final slice)."""
         kw = {}
         if ids.is_cuda:
             kw = {"seqlens": seqlens, "items": items}
 
         def attention(i, qkv):
-            return ops.attn_prefill(qkv, cu_seqlens, self.hq, self.hkv, self.hd, self.scale, **kw)
+            pp = paged.layer(kcache[i], vcache[i]) if paged is not None else None
+            return ops.attn_prefill(qkv, cu_seqlens, self.hq, self.hkv, self.hd, self.scale, paged=pp, **kw)
 
         x = self.run_layers(ids, positions, seq_idx, block_tables, kcache, vcache, attention)
+        if not logits:
+            return None
         return self.logits(x.index_select(0, last_rows), gather)
 
     def decode(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, block_tables: torch.Tensor,

@@ -90,10 +90,27 @@ def embed(ids, table, out=None):
     return _impl(table).embed(ids, table, out)
 
 
-def attn_prefill(qkv, cu_seqlens, hq, hkv, d, scale, out=None, **kw):
+class PagedPrefill:
+    """Chunked-prefill context of a packed batch of prompt slices: sequence i's slice starts at absolute
+    position ``prefix[i]`` of the sequence in decode slot ``seq_slot[i]`` (block-table row); its keys
+    are read from the paged cache (``kcache`` / ``vcache`` of one layer) -- see ops.hip.attn_prefill."""
+
+    def __init__(self, block_tables, seq_slot, prefix, slot_host, prefix_host, kcache=None, vcache=None):
+        self.block_tables, self.seq_slot, self.prefix = block_tables, seq_slot, prefix
+        self.slot_host, self.prefix_host = list(slot_host), list(prefix_host)
+        self.kcache, self.vcache = kcache, vcache
+
+    def layer(self, kcache, vcache) -> "PagedPrefill":
+        return PagedPrefill(self.block_tables, self.seq_slot, self.prefix, self.slot_host, self.prefix_host,
+                            kcache, vcache)
+
+
+def attn_prefill(qkv, cu_seqlens, hq, hkv, d, scale, out=None, paged=None, **kw):
     if _use_hip(qkv):
         from . import hip
-        return hip.attn_prefill(qkv, cu_seqlens, hq, hkv, d, scale, out, **kw)
+        return hip.attn_prefill(qkv, cu_seqlens, hq, hkv, d, scale, out, paged=paged, **kw)
+    if paged is not None:
+        return reference.attn_prefill_paged(qkv, cu_seqlens, hq, hkv, d, scale, paged, out)
     return reference.attn_prefill(qkv, cu_seqlens, hq, hkv, d, scale, out)
 
 

@@ -29,6 +29,8 @@ _SIGS = {
     "mrsum_swiglu": [_vp, _vp, _c_int, _c_int, _vp],
     "mrsum_embed": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _vp],
     "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
+    "mrsum_attn_prefill_paged": [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp,
+                                 _vp, _vp, _c_int, _vp, _vp, _vp],
     "mrsum_attn_decode": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
                           _c_int, _c_int, _c_int, _c_float, _vp, _vp],
     "mrsum_attn_decode_mfma": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int,
@@ -248,7 +250,9 @@ def prefill_items(seqlens, block_m: int = 128) -> torch.Tensor:
 
 def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int, d: int, scale: float,
                  out: Optional[torch.Tensor] = None, items: Optional[torch.Tensor] = None,
-                 seqlens=None) -> torch.Tensor:
+                 seqlens=None, paged=None) -> torch.Tensor:
+    """Causal varlen prefill attention.  ``paged`` (ops.PagedPrefill): the packed rows are slices whose
+    keys are read from the paged cache for positions [0, prefix + slice length) -- chunked prefill."""
     _bf16_cuda(qkv)
     _rows_ok(qkv)
     _req(d == 128 and hq % hkv == 0 and qkv.shape[1] >= (hq + 2 * hkv) * d, "attn_prefill: bad head config")
@@ -265,6 +269,22 @@ def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int,
         out = torch.empty(T, hq * d, dtype=qkv.dtype, device=qkv.device)
     _rows_ok(out)
     _req(out.shape[0] >= T and out.shape[1] >= hq * d, "attn_prefill: bad out")
+    if paged is not None:
+        kc, vc, bt = paged.kcache, paged.vcache, paged.block_tables
+        _bf16_cuda(kc, vc)
+        _req(kc.is_contiguous() and vc.is_contiguous() and tuple(kc.shape[1:]) == (hkv, 64, d),
+             "attn_prefill: paged cache must be [pages, Hkv, 64, D]")
+        _i32(bt, paged.seq_slot, paged.prefix)
+        _req(bt.dim() == 2 and len(paged.prefix_host) == len(seqlens) == paged.seq_slot.numel(),
+             "attn_prefill: paged tables")
+        for pre, n, slot in zip(paged.prefix_host, seqlens, paged.slot_host):
+            _req(0 <= slot < bt.shape[0] and pre >= 0 and pre + n <= bt.shape[1] * 64,
+                 "attn_prefill: slice [%d, %d) beyond block table" % (pre, pre + n))
+        _check(_fn("mrsum_attn_prefill_paged")(_p(qkv), qkv.stride(0), _p(cu_seqlens), _p(items), items.shape[0],
+                                               _p(out), out.stride(0), hq, hkv, d, scale, _p(kc), _p(vc), _p(bt),
+                                               bt.stride(0), _p(paged.seq_slot), _p(paged.prefix), _stream()),
+               "attn_prefill_paged")
+        return out
     _check(_fn("mrsum_attn_prefill")(_p(qkv), qkv.stride(0), _p(cu_seqlens), _p(items), items.shape[0], _p(out),
                                      out.stride(0), hq, hkv, d, scale, _stream()), "attn_prefill")
     return out

@@ -215,6 +215,38 @@ def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int,
     return out
 
 
+def attn_prefill_paged(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int, d: int, scale: float,
+                       paged, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Chunked prefill: slice rows of every packed sequence attend to the cached positions
+    [0, prefix) of that sequence (paged cache, already holding this slice's K/V too) and causally
+    within the slice."""
+    T = qkv.shape[0]
+    if out is None:
+        out = torch.empty(T, hq * d, dtype=qkv.dtype, device=qkv.device)
+    cu = cu_seqlens.tolist()
+    g = hq // hkv
+    P = paged.kcache.shape[2]
+    for i in range(len(cu) - 1):
+        s, e = cu[i], cu[i + 1]
+        if e <= s:
+            continue
+        n, pre, slot = e - s, paged.prefix_host[i], paged.slot_host[i]
+        tot = pre + n
+        pages = paged.block_tables[slot, : -(-tot // P)].long()
+        k = paged.kcache.index_select(0, pages).permute(1, 0, 2, 3).reshape(hkv, -1, d)[:, :tot].float()
+        v = paged.vcache.index_select(0, pages).permute(1, 0, 2, 3).reshape(hkv, -1, d)[:, :tot].float()
+        q = qkv[s:e, : hq * d].view(n, hq, d).float().transpose(0, 1)
+        k = k.repeat_interleave(g, dim=0)
+        v = v.repeat_interleave(g, dim=0)
+        sc = torch.matmul(q, k.transpose(1, 2)) * scale
+        qpos = torch.arange(pre, tot, device=qkv.device)[:, None]
+        kpos = torch.arange(tot, device=qkv.device)[None, :]
+        sc.masked_fill_(kpos > qpos, float("-inf"))
+        p = torch.softmax(sc, dim=-1)
+        out[s:e] = torch.matmul(p, v).transpose(0, 1).reshape(n, hq * d).to(out.dtype)
+    return out
+
+
 def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, block_tables: torch.Tensor,
                 positions: torch.Tensor, hq: int, hkv: int, d: int, page: int, scale: float,
                 out: Optional[torch.Tensor] = None, num_splits: int = 1) -> torch.Tensor:

@@ -218,3 +218,22 @@ def test_prefill_oom_is_isolated(monkeypatch):
     monkeypatch.setattr(e, "_prefill", always)
     with pytest.raises(torch.OutOfMemoryError):
         e.generate(_prompts(1), ps[:1])
+
+
+@pytest.mark.parametrize("chunk", [64, 192])
+def test_chunked_prefill_equals_one_pass(chunk):
+    """Prompts cut into end-aligned slices that attend to their cached prefix through the paged cache
+    (ops.attn_prefill paged path) generate exactly what one-pass prefill generates (greedy, fp32 CPU)."""
+    from llm_map_reduce_summarizer_amd.engine.config import get_model_config
+    from llm_map_reduce_summarizer_amd.engine.engine import LLMEngine, SamplingParams
+    cfg = get_model_config("tiny-gqa4", init_std=0.05)
+    prompts = [[128000] + [(i * 31 + j * 7) % 9000 + 5 for j in range(n)] for i, n in enumerate((450, 130, 61, 300))]
+    sp = [SamplingParams(6, 0.0, i) for i in range(len(prompts))]
+    outs = {}
+    for c in (0, chunk):
+        eng = LLMEngine(cfg, device="cpu", dtype=torch.float32, max_model_len=1024, max_num_seqs=8, kv_pages=96,
+                        sync_every=3, prefill_chunk=c)
+        outs[c] = [o.token_ids for o in eng.generate(prompts, sp)]
+        if c:
+            assert eng.stats["prefill_slices"] > len(prompts)
+    assert outs[0] == outs[chunk]

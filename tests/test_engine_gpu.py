@@ -79,6 +79,23 @@ def test_packed_prefill_matches_single(eng):
     assert same >= len(prompts) - 1  # a bf16 near-tie may flip one sequence
 
 
+def test_chunked_prefill_matches_one_pass():
+    """Chunked prefill (end-aligned slices through the paged cache) generates what one-pass prefill does
+    (greedy; a bf16 near-tie may flip one sequence)."""
+    cfg = get_model_config("tiny-gqa4", init_std=0.05)
+    prompts = [[128000] + [(i * 53 + j * 7) % 120000 + 5 for j in range(n)] for i, n in enumerate((1500, 700, 2600, 90))]
+    sp = [SamplingParams(8, 0.0, 0)] * len(prompts)
+    res = {}
+    for c in (0, 512):
+        e = LLMEngine(cfg, device="cuda:0", max_model_len=4096, max_num_seqs=8, kv_pages=256, sync_every=8,
+                      prefill_chunk=c)
+        res[c] = [o.token_ids for o in e.generate(prompts, sp)]
+        if c:
+            assert e.stats["prefill_slices"] > len(prompts)
+    same = sum(a == b for a, b in zip(res[0], res[512]))
+    assert same >= len(prompts) - 1, (res[0], res[512])
+
+
 def test_long_context_class_graphs():
     """Prompts in the 6k-12k and 12k-32k context classes run on their own decode graphs (attention split
     plans per class) and agree with teacher-forced prefill, like the short class."""

@@ -107,6 +107,35 @@ def test_attn_prefill(hq, hkv, seqlens):
     _close(o1, o2, 2e-2)
 
 
+@pytest.mark.parametrize("hq,hkv", [(4, 1), (8, 2)])
+@pytest.mark.parametrize("spans", [[(0, 200)], [(130, 300), (0, 77), (1000, 1129)], [(64, 128), (2047, 2048)]])
+def test_attn_prefill_paged(hq, hkv, spans):
+    """Chunked-prefill attention: slice rows attend to [0, prefix + slice) of their sequence read from the
+    paged cache (random non-contiguous pages, stale rows past the slice end), vs the fp32 reference."""
+    from llm_map_reduce_summarizer_amd.ops import PagedPrefill
+    d, page = 128, 64
+    g = torch.Generator().manual_seed(21)
+    n_pages, maxp = 160, 40
+    kc = (torch.randn(n_pages, hkv, page, d, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
+    vc = torch.randn(n_pages, hkv, page, d, generator=g).to(torch.bfloat16).to(DEV)
+    nseq = len(spans)
+    perm = torch.randperm(n_pages - 1, generator=g)[: nseq * maxp] + 1
+    bt = perm.view(nseq, maxp).to(torch.int32).to(DEV)
+    lens = [e - b for b, e in spans]
+    T = sum(lens)
+    qkv = _rand(T, (hq + 2 * hkv) * d, seed=22)
+    cu = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)), dtype=torch.int32, device=DEV)
+    slots = list(range(nseq))[::-1]  # sequence i uses block-table row nseq-1-i
+    bt = bt.flip(0).contiguous()
+    pre = [b for b, _ in spans]
+    i32 = lambda x: torch.tensor(x, dtype=torch.int32, device=DEV)  # noqa: E731
+    pp = PagedPrefill(bt, i32(slots), i32(pre), slots, pre, kc, vc)
+    sc = 1.0 / math.sqrt(d)
+    o1 = hip.attn_prefill(qkv, cu, hq, hkv, d, sc, paged=pp)
+    o2 = reference.attn_prefill_paged(qkv, cu, hq, hkv, d, sc, pp)
+    _close(o1, o2, 2e-2)
+
+
 def test_attn_prefill_spike():
     """A key far larger than the rest forces the online-softmax rescale path mid-sequence."""
     hq, hkv, d = 4, 1, 128
