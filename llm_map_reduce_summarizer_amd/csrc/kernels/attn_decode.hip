@@ -6,15 +6,10 @@
 // byte is read from HBM exactly once per step (the op is HBM bound: at B=44,
 // 4.5k context, Llama-3-8B reads ~26 GB of KV per step).
 //
-// Lane layout: 16 "key slots" x 16 lanes; lane (slot, dp) owns dims
-// [8dp, 8dp+8) of every key  slot, slot+16, ... of the split, i.e. one 16-B
-// K load + one 16-B V load per key, 4 keys unrolled => 128 B in flight per
-// lane.  Consecutive slots read consecutive rows of a page (one page = P rows
-// of one head, contiguous), so a workgroup step reads 16 x 256 B contiguous.
-// q.k partial dots are reduced over the 16 lanes of a slot with xor
-// shuffles; each slot keeps its own online-softmax state (m, l, o) which the
-// workgroup merges through LDS at the end.  Scores are in the log2 domain
-// (q pre-scaled by log2(e)/sqrt(D)) so the exponentials are exp2.
+// The workgroup stages 64-key pages of K and V through LDS and scores them on
+// MFMA (attn_decode_mfma_kernel below); its 4 waves merge their online-softmax
+// states through LDS at the end.  Scores are in the log2 domain (scale folded
+// with log2(e)) so the exponentials are exp2.
 //
 // Output: unnormalised partials part_o [B, Hq, S, D] f32 and part_ml
 // [B, Hq, S, 2] = (running max, running sum), merged into out [B, Hq*D] bf16
@@ -166,147 +161,6 @@ __device__ __forceinline__ void combine_if_last(const float* part_o, const float
 }
 
 template <int G>
-__global__ __launch_bounds__(256) void attn_decode_split_kernel(
-    const bf16* __restrict__ q, int q_stride, const bf16* __restrict__ kc, const bf16* __restrict__ vc,
-    const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ positions,
-    float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int P, int S, float scale_log2,
-    int* __restrict__ counters, bf16* __restrict__ out, int out_stride) {
-    constexpr int D = 128;
-    const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
-    const int Hq = Hkv * G;
-    const int tid = threadIdx.x, slot = tid >> 4, dp = tid & 15;
-    const int ctx = positions[b] + 1;
-    int chunk = (ctx + S - 1) / S;
-    chunk = (chunk + 15) & ~15;
-    const int ks = split * chunk;
-    const int ke = min(ctx, ks + chunk);
-
-    __shared__ float sm_o[16][G][D];
-    __shared__ float sm_m[16][G];
-    __shared__ float sm_l[16][G];
-    __shared__ int s_last;
-    __shared__ float s_w[G * MAX_SPLITS];
-    __shared__ float s_den[G];
-
-    const size_t ml_base = ((size_t)b * Hq + (size_t)kvh * G) * S + split;
-    if (ks >= ke) {
-        if (tid < G) {
-            part_ml[(ml_base + (size_t)tid * S) * 2 + 0] = -INFINITY;
-            part_ml[(ml_base + (size_t)tid * S) * 2 + 1] = 0.f;
-        }
-        if (counters) combine_if_last<G>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, &s_last, s_w, s_den);
-        return;
-    }
-
-    float qf[G][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        const uint4 v = *reinterpret_cast<const uint4*>(q + (size_t)b * q_stride + (kvh * G + g) * D + dp * 8);
-        unpack8(v, qf[g]);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) qf[g][j] *= scale_log2;
-    }
-    float m[G], l[G], o[G][8];
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-        m[g] = -INFINITY;
-        l[g] = 0.f;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[g][j] = 0.f;
-    }
-    const int* bt = block_tables + (size_t)b * bt_stride;
-    const size_t head_off = (size_t)kvh * P * D + dp * 8;
-
-    for (int k0 = ks + slot; k0 < ke; k0 += 64) {
-        uint4 kr[4], vr[4];
-        bool valid[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int k = k0 + 16 * u;
-            valid[u] = k < ke;
-            const int kk = valid[u] ? k : k0;
-            const int page = bt[kk / P];
-            const size_t off = ((size_t)page * Hkv * P + (kk % P)) * D + head_off;
-            kr[u] = *reinterpret_cast<const uint4*>(kc + off);
-            vr[u] = *reinterpret_cast<const uint4*>(vc + off);
-        }
-        float s[4][G];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            float kf[8];
-            unpack8(kr[u], kf);
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-                float acc = 0.f;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) acc += qf[g][j] * kf[j];
-                acc += __shfl_xor(acc, 1, 64);
-                acc += __shfl_xor(acc, 2, 64);
-                acc += __shfl_xor(acc, 4, 64);
-                acc += __shfl_xor(acc, 8, 64);
-                s[u][g] = valid[u] ? acc : -INFINITY;
-            }
-        }
-        float pr[4][G];
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            const float mx = fmaxf(fmaxf(s[0][g], s[1][g]), fmaxf(s[2][g], s[3][g]));
-            const float mn = fmaxf(m[g], mx);  // finite: key k0 is always valid
-            const float alpha = __builtin_amdgcn_exp2f(m[g] - mn);
-            m[g] = mn;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) pr[u][g] = __builtin_amdgcn_exp2f(s[u][g] - mn);
-            l[g] = l[g] * alpha + (pr[0][g] + pr[1][g]) + (pr[2][g] + pr[3][g]);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) o[g][j] *= alpha;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            float vf[8];
-            unpack8(vr[u], vf);
-#pragma unroll
-            for (int g = 0; g < G; ++g) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) o[g][j] += pr[u][g] * vf[j];
-            }
-        }
-    }
-
-    // merge the 16 slots
-#pragma unroll
-    for (int g = 0; g < G; ++g) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) sm_o[slot][g][dp * 8 + j] = o[g][j];
-        if (dp == 0) {
-            sm_m[slot][g] = m[g];
-            sm_l[slot][g] = l[g];
-        }
-    }
-    __syncthreads();
-    for (int i = tid; i < G * D; i += 256) {
-        const int g = i / D, d = i % D;
-        float M = -INFINITY;
-#pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) M = fmaxf(M, sm_m[s2][g]);
-        float acc = 0.f, L = 0.f;
-#pragma unroll
-        for (int s2 = 0; s2 < 16; ++s2) {
-            const float ms = sm_m[s2][g];
-            const float w = ms == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms - M);
-            acc += w * sm_o[s2][g][d];
-            L += w * sm_l[s2][g];
-        }
-        const size_t pi = ml_base + (size_t)g * S;
-        part_o[pi * D + d] = acc;
-        if (d == 0) {
-            part_ml[pi * 2 + 0] = M;
-            part_ml[pi * 2 + 1] = L;
-        }
-    }
-    if (counters) combine_if_last<G>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, &s_last, s_w, s_den);
-}
-
-template <int G>
 __global__ __launch_bounds__(256) void attn_decode_combine_kernel(const float* __restrict__ part_o,
                                                                   const float* __restrict__ part_ml,
                                                                   bf16* __restrict__ out, int out_stride, int Hq,
@@ -314,35 +168,6 @@ __global__ __launch_bounds__(256) void attn_decode_combine_kernel(const float* _
     __shared__ float s_w[G * MAX_SPLITS];
     __shared__ float s_den[G];
     combine_group<G>(part_o, part_ml, out, out_stride, blockIdx.x / Hkv, blockIdx.x % Hkv, Hq, S, s_w, s_den);
-}
-
-MRSUM_API int mrsum_attn_decode(const void* q, int q_stride, const void* kcache, const void* vcache,
-                                const int* block_tables, int bt_stride, const int* positions, void* part_o,
-                                void* part_ml, void* out, int out_stride, int B, int Hq, int Hkv, int D, int P,
-                                int S, float scale, int* counters, hipStream_t s) {
-    if (B <= 0) return 0;
-    if (D != 128 || Hq % Hkv || S < 1 || S > MAX_SPLITS || P % 16) return (int)hipErrorInvalidValue;
-    const int G = Hq / Hkv;
-    const float sl = scale * 1.4426950408889634f;
-    dim3 grid(S, Hkv, B), block(256);
-    auto Qp = (const bf16*)q; auto K = (const bf16*)kcache; auto V = (const bf16*)vcache;
-    auto PO = (float*)part_o; auto PM = (float*)part_ml;
-    switch (G) {
-        case 1: attn_decode_split_kernel<1><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl, counters, (bf16*)out, out_stride); break;
-        case 2: attn_decode_split_kernel<2><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl, counters, (bf16*)out, out_stride); break;
-        case 4: attn_decode_split_kernel<4><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl, counters, (bf16*)out, out_stride); break;
-        case 8: attn_decode_split_kernel<8><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, positions, PO, PM, Hkv, P, S, sl, counters, (bf16*)out, out_stride); break;
-        default: return (int)hipErrorInvalidValue;
-    }
-    int e = (int)hipGetLastError();
-    if (e || counters) return e;
-    switch (G) {
-        case 1: attn_decode_combine_kernel<1><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
-        case 2: attn_decode_combine_kernel<2><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
-        case 4: attn_decode_combine_kernel<4><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
-        case 8: attn_decode_combine_kernel<8><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
-    }
-    return (int)hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -675,12 +500,10 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     if (counters) combine_if_last<G, true>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, c_last, c_sw, c_den);
 }
 
-static int g_attn_nt = 2;
-
-// KV page load policy of the MFMA decode attention: 0 default, 1 nontemporal, 2 (auto) nontemporal for
-// >= 64 (sequence, kv head) groups -- measured, step at 4k context: B=39 x 8 kv heads 7.02-7.05 vs
-// 7.18-7.26 ms; B <= 10 0.7-1 % slower with nt (profiles/r1_decode_nt_ab.jsonl)
-MRSUM_API void mrsum_attn_decode_set_nt(int mode) { g_attn_nt = mode; }
+// KV page loads are nontemporal from 64 (sequence, kv head) groups up -- measured, step at 4k context:
+// B=39 x 8 kv heads 7.02-7.05 vs 7.18-7.26 ms with the default policy; B <= 10 0.7-1 % slower with nt
+// (profiles/r1_decode_nt_ab.jsonl)
+constexpr int NT_MIN_GROUPS = 64;
 
 static int launch_mfma(const void* q, int q_stride, const void* kcache, const void* vcache, const int* block_tables,
                        int bt_stride, const int* positions, void* part_o, void* part_ml, void* out, int out_stride,
@@ -696,7 +519,7 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
     const RopeArgs ra = rope ? *rope : RopeArgs{nullptr, 0, 0, 0, 0, nullptr};
 #define MFMA_L(G_, R_)                                                                                        \
     do {                                                                                                      \
-        if (g_attn_nt == 1 || (g_attn_nt == 2 && B * Hkv >= 64))                                            \
+        if (B * Hkv >= NT_MIN_GROUPS)                                                                       \
             attn_decode_mfma_kernel<G_, R_, true><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, \
                                                                          positions, PO, PM, Hkv, S, sl, ra, counters, \
                                                                          (bf16*)out, out_stride);             \

@@ -52,8 +52,6 @@ __device__ __forceinline__ int v_off(int row, int chunk) { return row * 256 + ((
 __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
 }  // namespace
 
-// PK: the softmax's per-score FMA (scale, -max) and running-sum adds as packed fp32 pairs
-// (v_pk_fma_f32 / v_pk_add_f32: two scores per VALU instruction)
 struct PagedKV {
     const bf16* kc;            // [pages, Hkv, 64, D]
     const bf16* vc;
@@ -63,7 +61,7 @@ struct PagedKV {
     const int* prefix;         // [nseq] tokens already cached before this slice
 };
 
-template <bool PK, bool PAGED>
+template <bool PAGED>
 __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __restrict__ qkv, int row_stride,
                                                               const int* __restrict__ cu_seqlens,
                                                               const int2* __restrict__ items,
@@ -194,32 +192,13 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
             }
             float ls = 0.f;
             bf16x8 pf[2][2];
-            if constexpr (PK) {
-                typedef float f2v __attribute__((ext_vector_type(2)));
-                const f2v sc2 = {scale_log2, scale_log2}, nm2 = {-m, -m};
-                f2v ls2 = {0.f, 0.f};
 #pragma unroll
-                for (int kt = 0; kt < 2; ++kt) {
+            for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
-                    for (int i = 0; i < 16; i += 2) {
-                        const f2v s2 = {sacc[kt][i], sacc[kt][i + 1]};
-                        const f2v x = __builtin_elementwise_fma(s2, sc2, nm2);
-                        const f2v p = {__builtin_amdgcn_exp2f(x.x), __builtin_amdgcn_exp2f(x.y)};
-                        ls2 += p;
-                        pf[kt][i >> 3][i & 7] = (bf16)p.x;
-                        pf[kt][i >> 3][(i & 7) + 1] = (bf16)p.y;
-                    }
-                }
-                ls = ls2.x + ls2.y;
-            } else {
-#pragma unroll
-                for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kt][i], scale_log2, -m));
-                        ls += p;
-                        pf[kt][i >> 3][i & 7] = (bf16)p;
-                    }
+                for (int i = 0; i < 16; ++i) {
+                    const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kt][i], scale_log2, -m));
+                    ls += p;
+                    pf[kt][i >> 3][i & 7] = (bf16)p;
                 }
             }
             l += ls;
@@ -275,11 +254,6 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
     }
 }
 
-static int g_prefill_pk = 0;
-
-// 1: packed-fp32 softmax, 0: scalar (default; packed measured 1-3 % slower) -- A/B switch
-MRSUM_API void mrsum_attn_prefill_set_pk(int on) { g_prefill_pk = on ? 1 : 0; }
-
 static int launch_prefill(const void* qkv, int row_stride, const int* cu_seqlens, const int* items, int n_items,
                           void* out, int out_stride, int Hq, int Hkv, int Dh, float scale, const PagedKV* pk,
                           hipStream_t s) {
@@ -290,13 +264,8 @@ static int launch_prefill(const void* qkv, int row_stride, const int* cu_seqlens
     auto Q = (const bf16*)qkv;
     auto IT = (const int2*)items;
     const PagedKV p = pk ? *pk : PagedKV{nullptr, nullptr, nullptr, 0, nullptr, nullptr};
-    if (pk) {
-        if (g_prefill_pk) attn_prefill_kernel<true, true><<<grid, block, 0, s>>>(Q, row_stride, cu_seqlens, IT, (bf16*)out, out_stride, Hq, Hkv, sl, p);
-        else attn_prefill_kernel<false, true><<<grid, block, 0, s>>>(Q, row_stride, cu_seqlens, IT, (bf16*)out, out_stride, Hq, Hkv, sl, p);
-    } else {
-        if (g_prefill_pk) attn_prefill_kernel<true, false><<<grid, block, 0, s>>>(Q, row_stride, cu_seqlens, IT, (bf16*)out, out_stride, Hq, Hkv, sl, p);
-        else attn_prefill_kernel<false, false><<<grid, block, 0, s>>>(Q, row_stride, cu_seqlens, IT, (bf16*)out, out_stride, Hq, Hkv, sl, p);
-    }
+    if (pk) attn_prefill_kernel<true><<<grid, block, 0, s>>>(Q, row_stride, cu_seqlens, IT, (bf16*)out, out_stride, Hq, Hkv, sl, p);
+    else attn_prefill_kernel<false><<<grid, block, 0, s>>>(Q, row_stride, cu_seqlens, IT, (bf16*)out, out_stride, Hq, Hkv, sl, p);
     return (int)hipGetLastError();
 }
 

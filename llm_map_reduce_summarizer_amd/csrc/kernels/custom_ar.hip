@@ -284,10 +284,10 @@ __global__ __launch_bounds__(256) void ar_add_rmsnorm_kernel(Peers peers, int ra
     if (tid == 0) epochs[row] = epoch;
 }
 
-static int g_ar_wt = 1;
-
-// 1 (default): write-through publish (no release fences), 0: fenced publish (A/B switch)
-MRSUM_API void mrsum_ar_set_wt(int on) { g_ar_wt = on ? 1 : 0; }
+// Publish form: write-through (sc1) payload stores, no release fence -- the fenced form (buffer_wbl2 of
+// the whole XCD L2, full of the preceding GEMMs' slabs) measured slower inside the decode graph
+// (profiles/r1_custom_ar_wt_ab.jsonl); the template keeps both forms for the record.
+constexpr bool AR_WT = true;
 
 static int launch_ar(ArHandle* h, int op, const void* in, void* out, size_t nbytes, hipStream_t s) {
     if (nbytes == 0) return 0;
@@ -298,13 +298,8 @@ static int launch_ar(ArHandle* h, int op, const void* in, void* out, size_t nbyt
 #define AR_ONE(OP_, WT_)                                                                                 \
     ar_oneshot_kernel<OP_, WT_><<<nblk, 256, 0, s>>>(h->peers, h->rank, h->world, h->max_bytes, (const char*)in, \
                                                      (char*)out, nbytes, h->epochs, h->error)
-    if (op == OP_SUM_F32) {
-        if (g_ar_wt) AR_ONE(OP_SUM_F32, true);
-        else AR_ONE(OP_SUM_F32, false);
-    } else {
-        if (g_ar_wt) AR_ONE(OP_MAX_U64, true);
-        else AR_ONE(OP_MAX_U64, false);
-    }
+    if (op == OP_SUM_F32) AR_ONE(OP_SUM_F32, AR_WT);
+    else AR_ONE(OP_MAX_U64, AR_WT);
 #undef AR_ONE
     return (int)hipGetLastError();
 }
@@ -393,11 +388,7 @@ MRSUM_API int mrsum_ar_add_rmsnorm(void* hv, const void* parts, int S, int T, vo
 #define AR_NORM_(V, WT_)                                                                                     \
     ar_add_rmsnorm_kernel<V, WT_><<<T, 256, 0, s>>>(h->peers, h->rank, h->world, h->max_bytes, P, S, T, R, W, O, D, \
                                                     out_stride, eps, h->push_epochs, h->error)
-#define AR_NORM(V)                  \
-    do {                            \
-        if (g_ar_wt) AR_NORM_(V, true); \
-        else AR_NORM_(V, false);    \
-    } while (0)
+#define AR_NORM(V) AR_NORM_(V, AR_WT)
     if (vpt <= 1) AR_NORM(1);
     else if (vpt <= 2) AR_NORM(2);
     else if (vpt <= 4) AR_NORM(4);

@@ -25,8 +25,8 @@
 //     X0 W0 | W1 | X1 | -- and a half-tile can be staged LOOK = 6 half-tiles (1.5 K-tiles) ahead of
 //     the phase that first reads it.  Per phase: R = fragment ds_reads + stage one half-tile (2 DMA
 //     per lane) + counted s_waitcnt vmcnt(8) (never 0 in the main loop), raw s_barrier, M = 16 bf16 (8
-//     fp8) MFMAs between s_setprio(1/0), raw s_barrier.  With STAGGER, waves 4-7 run one barrier
-//     (half a phase) behind waves 0-3, so one wave of each SIMD reads LDS while its partner computes.
+//     fp8) MFMAs between s_setprio(1/0), raw s_barrier.  Waves 4-7 run one barrier (half a phase)
+//     behind waves 0-3 (stagger), so one wave of each SIMD reads LDS while its partner computes.
 //   * hazards (derived for the staggered schedule, which is the stricter one): the wait at the end of
 //     R_P covers every half-tile phase P+1 reads, before the barrier the lagging group passes ahead
 //     of its R_P; a half-tile is restaged >= 2 phases after the last phase that read its region
@@ -100,7 +100,7 @@ __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles
 }
 }  // namespace
 
-template <bool FP8, int EPI, bool STAGGER, int NS, bool LEPI>
+template <bool FP8, int EPI, int NS, bool LEPI>
 __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
     // NS = half-tile slots of the LDS ring: half-tile h (K-tile h / 4, part h % 4) lives in slot h % NS.
     // NS = 8 (128 KiB, 2 K-tiles): staged LK = 6 ahead; NS = 10 (160 KiB): LK = 8 ahead.  A slot is
@@ -165,7 +165,7 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
         if (h < htot) stage(h & 3, h >> 2);
     vm_wait_rt(2 * (min(LK - 1, htot - 1) - 1));
     bar();
-    if (STAGGER && wr == 1) bar();
+    if (wr == 1) bar();  // stagger: waves 4-7 run one barrier (half a phase) behind waves 0-3
 
     auto read_x = [&](const char* base) {
 #pragma unroll
@@ -248,7 +248,7 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
     int kt = 0;
     for (; kt < nk - (LK + 3) / 4; ++kt) ktile(kt, std::false_type{});
     for (; kt < nk; ++kt) ktile(kt, std::true_type{});
-    if (STAGGER && wr == 0) bar();
+    if (wr == 0) bar();
 
     // epilogue: lane holds C[m][n .. n+3] of every 16 x 16 block, m = .. + (lane & 15), n = .. + 4 (lane >> 4).
     // LEPI: every wave writes its bf16 results into a [256 rows][RB bytes] LDS image of the whole tile
@@ -325,8 +325,7 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
 // sx [M] / sw [N] fp32 row scales.  Requirements (checked by the Python wrapper too): K % 64 (bf16) /
 // K % 128 (fp8), N % 16, 16-byte aligned rows.
 MRSUM_API int mrsum_gemm(const void* x, int ldx, const void* w, int ldw, void* c, int ldc, int M, int N, int K,
-                         int fp8, int epi, const float* sx, const float* sw, int stagger, int group_m,
-                         hipStream_t s) {
+                         int fp8, int epi, const float* sx, const float* sw, int group_m, hipStream_t s) {
     if (M <= 0 || N <= 0) return 0;
     const int es = fp8 ? 1 : 2;
     if ((K * es) % 128 || N % 16 || (ldx * es) % 16 || (ldw * es) % 16 || ldc % 4) return (int)hipErrorInvalidValue;
@@ -339,23 +338,18 @@ MRSUM_API int mrsum_gemm(const void* x, int ldx, const void* w, int ldw, void* c
     a.tiles_m = ceil_div(M, 256); a.tiles_n = ceil_div(N, 256);
     a.group_m = group_m > 0 ? group_m : 4;
     const dim3 grid(a.tiles_m * a.tiles_n), block(512);
-    // variant flags (A/B): bit 0 stagger, bit 1 10-slot LDS ring (8 half-tiles ahead), bit 2 LDS-staged epilogue
-    if ((stagger & 4) && (ldc % 8 || (uintptr_t)c % 16)) stagger &= ~4;
-#define GEMM_LAUNCH(F, E)                                                                 \
-    switch (stagger & 7) {                                                                \
-        case 0: gemm_kernel<F, E, false, 8, false><<<grid, block, 0, s>>>(a); break;      \
-        case 1: gemm_kernel<F, E, true, 8, false><<<grid, block, 0, s>>>(a); break;       \
-        case 2: gemm_kernel<F, E, false, 10, false><<<grid, block, 0, s>>>(a); break;     \
-        case 3: gemm_kernel<F, E, true, 10, false><<<grid, block, 0, s>>>(a); break;      \
-        case 4: gemm_kernel<F, E, false, 8, true><<<grid, block, 0, s>>>(a); break;       \
-        case 5: gemm_kernel<F, E, true, 8, true><<<grid, block, 0, s>>>(a); break;        \
-        case 6: gemm_kernel<F, E, false, 10, true><<<grid, block, 0, s>>>(a); break;      \
-        default: gemm_kernel<F, E, true, 10, true><<<grid, block, 0, s>>>(a); break;      \
-    }
+    // measured (profiles/r2_gemm_variants_ab.jsonl, r2_gemm_ring10_ab.jsonl): the staggered 8-slot ring
+    // (LOOK 6) with the LDS-staged epilogue is the fastest; the 2-phase / 10-slot rings and the
+    // unstaggered schedule lost 5-25 %.  The register epilogue remains for outputs that are not 16-B
+    // aligned (strided views).
+    const bool lepi = ldc % 8 == 0 && (uintptr_t)c % 16 == 0;
+#define GEMM_LAUNCH(F, E)                                                          \
+    if (lepi) gemm_kernel<F, E, 8, true><<<grid, block, 0, s>>>(a);               \
+    else gemm_kernel<F, E, 8, false><<<grid, block, 0, s>>>(a);
     if (fp8) {
-        if (epi == GEPI_SWIGLU) GEMM_LAUNCH(true, GEPI_SWIGLU) else GEMM_LAUNCH(true, GEPI_BF16)
+        if (epi == GEPI_SWIGLU) { GEMM_LAUNCH(true, GEPI_SWIGLU) } else { GEMM_LAUNCH(true, GEPI_BF16) }
     } else {
-        if (epi == GEPI_SWIGLU) GEMM_LAUNCH(false, GEPI_SWIGLU) else GEMM_LAUNCH(false, GEPI_BF16)
+        if (epi == GEPI_SWIGLU) { GEMM_LAUNCH(false, GEPI_SWIGLU) } else { GEMM_LAUNCH(false, GEPI_BF16) }
     }
 #undef GEMM_LAUNCH
     return (int)hipGetLastError();

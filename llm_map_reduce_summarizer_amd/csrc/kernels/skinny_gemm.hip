@@ -339,8 +339,9 @@ __global__ __launch_bounds__(512) void skinny_lds_kernel(const bf16* __restrict_
 }
 
 // Same contract as mrsum_skinny_gemm; N % (16 wpb) == 0, 16 < M <= 64 (also valid for M <= 16).
+// W is prefetched two 128-wide k blocks ahead (depth 1 measured slower; profiles/r1_decode_gemm_sweep.txt)
 MRSUM_API int mrsum_skinny_lds(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
-                               int epi, int splits, int depth, int wpb, hipStream_t s) {
+                               int epi, int splits, int wpb, hipStream_t s) {
     if (M <= 0) return 0;
     if (wpb < 4 || wpb > 8) return (int)hipErrorInvalidValue;
     if (M > 64 || K % KB || N % (16 * wpb) || splits < 1 || (K / KB) % splits) return (int)hipErrorInvalidValue;
@@ -349,9 +350,7 @@ MRSUM_API int mrsum_skinny_lds(const void* x, int ldx, const void* W, int N, int
     const int mt = (M + 15) / 16;
     dim3 grid(N / (16 * wpb), splits), block(64 * wpb);
     auto X = (const bf16*)x; auto Wp = (const bf16*)W;
-#define L(MT_, EPI_)                                                                                 \
-    if (depth == 2) skinny_lds_kernel<MT_, EPI_, 2><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper); \
-    else skinny_lds_kernel<MT_, EPI_, 1><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper)
+#define L(MT_, EPI_) skinny_lds_kernel<MT_, EPI_, 2><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper)
 #define BY_EPI(MT_) \
     if (epi == EPI_BF16) { L(MT_, EPI_BF16); } else if (epi == EPI_F32_PARTIAL) { L(MT_, EPI_F32_PARTIAL); } \
     else { L(MT_, EPI_SWIGLU); }

@@ -218,10 +218,8 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_gemm_kernel(const bf16* __
 
 // out: bf16 [M, ldo] (EPI_BF16), fp32 slabs [splits, M, ldo] (EPI_F32_PARTIAL) or bf16 [M, ldo] of
 // N/2 SwiGLU features (EPI_SWIGLU, splits = 1).  N % (16 wpb) == 0, wpb in {4, 5, 6, 7, 8}.
-static int g_stream_nt = 1;
-
-// 1: nontemporal weight loads (default), 0: default cache policy (A/B switch for tools/ and tests)
-MRSUM_API void mrsum_stream_gemm_set_nt(int on) { g_stream_nt = on ? 1 : 0; }
+// decode weights are streamed with nontemporal loads (each weight row read once per step by one CU:
+// MI355X_MICROARCH.md "nt-weights"; profiles/r1_decode_nt_ab.jsonl)
 
 static int launch_stream_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
                               int epi, int splits, int wpb, float* parts, int* counters, hipStream_t s) {
@@ -236,14 +234,7 @@ static int launch_stream_gemm(const void* x, int ldx, const void* W, int N, int 
     auto X = (const bf16*)x;
     auto Wp = (const bf16*)W;
 #define L(MT_, EPI_, WPB_)                                                                                   \
-    do {                                                                                                     \
-        if (g_stream_nt)                                                                                     \
-            stream_gemm_kernel<MT_, EPI_, WPB_, true><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, \
-                                                                             parts, counters);               \
-        else                                                                                                 \
-            stream_gemm_kernel<MT_, EPI_, WPB_, false><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, \
-                                                                              parts, counters);              \
-    } while (0)
+    stream_gemm_kernel<MT_, EPI_, WPB_, true><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, parts, counters)
 #define BY_WPB(MT_, EPI_)                          \
     switch (wpb) {                                 \
         case 4: L(MT_, EPI_, 4); break;            \

@@ -246,10 +246,10 @@ class LocalEngineProvider(Provider):
             _ = self.tp_engine  # may fall back to dp (no P2P all-reduce on this node)
         if self.parallel == "dp" or not reqs:
             return 1, False
-        if self.parallel == "tp":
-            return world, self.handoff and len(reqs) > 1
-        if self.parallel == "reduce_tp":
-            return (1, False) if stage == "map" else (world, self.handoff and len(reqs) > 1)
+        if self.parallel in ("tp", "reduce_tp"):
+            if self.parallel == "reduce_tp" and stage == "map":
+                return 1, False
+            return world, self._handoff_pays(prompts, reqs)
         from ..parallel import plan
         hw = self._measure()
         if self.parallel != "auto":  # _measure found no P2P all-reduce and fell back to dp
@@ -260,6 +260,21 @@ class LocalEngineProvider(Provider):
                              handoff=self.handoff)
         self.stage_plan[stage] = choice
         return int(choice["tp"]), bool(choice.get("handoff", False))
+
+    def _handoff_pays(self, prompts, reqs) -> bool:
+        """Disaggregated prefill for a TP=world stage when the cost model says it beats the TP forward:
+        always for many prompts (each rank prefills its share, no activation all-reduces); for ONE
+        prompt (the final reduce) it weighs one rank's whole prefill + the KV all-to-all against the TP
+        forward's 2 x n_layers RCCL all-reduces of the activations (parallel/plan.py)."""
+        if not self.handoff:
+            return False
+        if len(reqs) > 1:
+            return True
+        from ..parallel import plan
+        d = plan.ModelDims.of(self.model_config(), 1.0 if self._engine_options.get("weight_dtype") == "fp8" else 2.0)
+        hw = self.hw or plan.HWModel()
+        lens = [len(p) for p in prompts]
+        return plan.handoff_prefill_s(d, hw, lens, self.par.world) < plan.prefill_s(d, hw, sum(lens), self.par.world)
 
     def _handoff(self, prompts: Sequence[Sequence[int]], sp) -> Dict[int, Any]:
         """Disaggregated prefill for a TP stage: every rank prefills its LPT share of the prompts on

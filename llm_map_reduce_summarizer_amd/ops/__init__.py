@@ -187,8 +187,7 @@ class QKVParts:
 
 
 def _defer_ok(hip, defer, x, hq, hkv, d, page):
-    return defer and hip.FUSED_ROPE and d == 128 and page == 64 and hq % hkv == 0 and hq // hkv <= 16 \
-        and hip.DECODE_ATTN_IMPL == "mfma"
+    return defer and d == 128 and page == 64 and hq % hkv == 0 and hq // hkv <= 16
 
 
 def qkv_rope(x, wqkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page, defer=False):

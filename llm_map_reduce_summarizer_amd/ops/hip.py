@@ -31,15 +31,12 @@ _SIGS = {
     "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_attn_prefill_paged": [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp,
                                  _vp, _vp, _c_int, _vp, _vp, _vp],
-    "mrsum_attn_decode": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
-                          _c_int, _c_int, _c_int, _c_float, _vp, _vp],
     "mrsum_attn_decode_mfma": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int,
                                _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp],
     "mrsum_attn_decode_rope": [_vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int,
                                _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp],
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
-    "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int,
-                         _vp],
+    "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_stream_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_stream_gemm_swiglu_split": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _vp,
                                        _vp, _vp],
@@ -50,35 +47,18 @@ _SIGS = {
     "mrsum_sample_keys": [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
     "mrsum_sample_finish": [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "mrsum_gemm": [_vp, _c_int, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int,
-                   _c_int, _vp],
+                   _vp],
     "mrsum_sample": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp,
                      _c_int, _vp],
 }
 
 _fns = {}
-# stream GEMM weight loads with the nontemporal policy (1, default) or the default policy (0)
-STREAM_NT = os.environ.get("MRSUM_STREAM_NT", "1") == "1"
-# prefill attention softmax in packed fp32 (v_pk_fma_f32 / v_pk_add_f32) (1) or scalar (0, default: packed
-# measured 1-3 % slower, profiles/r1_prefill_packed_softmax_ab.jsonl -- the kernel is not VALU-issue bound)
-PREFILL_PK = os.environ.get("MRSUM_PREFILL_PK", "0") == "1"
-# decode attention KV page loads: 0 default policy, 1 nontemporal, 2 nontemporal for >= 64 groups (auto)
-ATTN_NT = int(os.environ.get("MRSUM_ATTN_NT", "2"))
 
 
 def _fn(name: str):
     f = _fns.get(name)
     if f is None:
         lib = kernels_lib()
-        if not _fns:  # first use of the library in this process: apply the launch-policy switches
-            lib.mrsum_stream_gemm_set_nt.argtypes = [_c_int]
-            lib.mrsum_stream_gemm_set_nt.restype = None
-            lib.mrsum_stream_gemm_set_nt(1 if STREAM_NT else 0)
-            lib.mrsum_attn_decode_set_nt.argtypes = [_c_int]
-            lib.mrsum_attn_decode_set_nt.restype = None
-            lib.mrsum_attn_decode_set_nt(ATTN_NT)
-            lib.mrsum_attn_prefill_set_pk.argtypes = [_c_int]
-            lib.mrsum_attn_prefill_set_pk.restype = None
-            lib.mrsum_attn_prefill_set_pk(1 if PREFILL_PK else 0)
         f = getattr(lib, name)
         f.argtypes = _SIGS[name]
         f.restype = ctypes.c_int
@@ -299,9 +279,7 @@ def decode_splits(batch: int, hkv: int, max_ctx: int, target_wgs: int = 1024, ma
     return s
 
 
-FUSED_COMBINE = os.environ.get("MRSUM_FUSED_COMBINE", "auto")
-ATTN_PAGES_PER_SPLIT = int(os.environ.get("MRSUM_ATTN_PPS", "2"))
-ATTN_FUSED_MAX_SPLITS = int(os.environ.get("MRSUM_ATTN_FUSED_MAX", "32"))
+ATTN_PAGES_PER_SPLIT = 2  # at least 2 pages per split (1 measured slower at B=1: r1_attn_splits_ab.jsonl)
 
 
 CTX_CLASSES = (6144, 12288, 32768, 1 << 30)  # decode context classes (tokens): graphs / split plans per class
@@ -315,7 +293,7 @@ def ctx_class(ctx: int) -> int:
     return len(CTX_CLASSES) - 1
 
 
-ATTN_SLOTS = int(os.environ.get("MRSUM_ATTN_SLOTS", "768"))
+ATTN_SLOTS = 768  # resident decode-attention workgroups (3 per CU, 162 VGPRs; 512 / 1024 measured equal or worse)
 
 
 def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
@@ -333,17 +311,18 @@ def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
     pages = max(1, -(-max_ctx // 64))
     groups = max(1, batch * hkv)
     splits = max(1, min(ATTN_SLOTS // groups, -(-pages // ATTN_PAGES_PER_SPLIT), 64))
-    if FUSED_COMBINE == "auto":
-        # measured at 4k context (tools/bench_attn_decode.py, profiles/r2_attn_decode_splits_fused_sweep.jsonl):
-        # B=1 fused 16 splits 16.1 us vs 32 unfused 19.0; B=10 fused 4 splits 37.5 us vs 9 unfused 40.1;
-        # B=39 unfused 2-4 splits 113 us vs fused 116-118
+    # measured (tools/bench_attn_decode.py; profiles/r2_attn_decode_splits_fused_sweep.jsonl at 4k,
+    # r2_attn_decode_splits_10k.jsonl): B=1 4k fused 16 splits 16.1 us vs 32 unfused 19.0, but B=1 10k
+    # 64 unfused 19.5 vs 16 fused 21.0 (a fused merge caps the splits, and long splits serialise);
+    # B=10 fused 4 splits 37.5 us vs 9 unfused 40.1 at 4k, equal at 10k; B=39 unfused 113 vs fused 116-118
+    if groups <= 16:
+        fused = -(-pages // 16) <= 4
+        if fused:
+            splits = min(splits, 16)
+    else:
         fused = groups <= 128
         if fused:
-            splits = min(splits, 16 if groups <= 16 else 4)
-    else:
-        fused = FUSED_COMBINE == "1"
-        if fused:
-            splits = min(splits, ATTN_FUSED_MAX_SPLITS)
+            splits = min(splits, 4)
     return splits, fused
 
 
@@ -363,8 +342,6 @@ class DecodeWorkspace:
                          if fused_combine else None)
 
 
-DECODE_ATTN_IMPL = os.environ.get("MRSUM_DECODE_ATTN", "mfma")
-FUSED_ROPE = os.environ.get("MRSUM_FUSED_ROPE", "1") == "1"
 
 
 def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
@@ -405,13 +382,13 @@ def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.T
 def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, block_tables: torch.Tensor,
                 positions: torch.Tensor, hq: int, hkv: int, d: int, page: int, scale: float,
                 out: Optional[torch.Tensor] = None, num_splits: Optional[int] = None,
-                workspace: Optional[DecodeWorkspace] = None, impl: Optional[str] = None) -> torch.Tensor:
-    """Paged decode attention.  impl "mfma" (page 64, G <= 16: K/V pages staged through LDS, QK^T and PV
-    on MFMA) or "valu" (any page % 16, G in 1/2/4/8: lane-sliced dot products)."""
+                workspace: Optional[DecodeWorkspace] = None) -> torch.Tensor:
+    """Paged decode attention on MFMA (page 64, G = hq / hkv <= 16): K/V pages staged through LDS,
+    QK^T and PV on MFMA, split-K over the context with a fused or separate split merge."""
     _bf16_cuda(q, kcache, vcache)
     _rows_ok(q)
     B = q.shape[0]
-    _req(d == 128 and hq % hkv == 0 and (hq // hkv) in (1, 2, 4, 8, 16) and page % 16 == 0, "attn_decode: bad config")
+    _req(d == 128 and hq % hkv == 0 and hq // hkv <= 16 and page == 64, "attn_decode: bad config")
     _req(tuple(kcache.shape[1:]) == (hkv, page, d) and kcache.is_contiguous() and vcache.is_contiguous(),
          "attn_decode: cache must be [pages, Hkv, P, D]")
     _i32(block_tables, positions)
@@ -424,18 +401,11 @@ def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, blo
     if out is None:
         out = torch.empty(B, hq * d, dtype=q.dtype, device=q.device)
     _rows_ok(out)
-    impl = impl or DECODE_ATTN_IMPL
-    if impl == "mfma" and page == 64 and hq // hkv <= 16:
-        _check(_fn("mrsum_attn_decode_mfma")(_p(q), q.stride(0), _p(kcache), _p(vcache), _p(block_tables),
-                                             block_tables.stride(0), _p(positions), _p(workspace.part_o),
-                                             _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
-                                             workspace.splits, scale, _p(workspace.counters), _stream()),
-               "attn_decode_mfma")
-        return out
-    _check(_fn("mrsum_attn_decode")(_p(q), q.stride(0), _p(kcache), _p(vcache), _p(block_tables),
-                                    block_tables.stride(0), _p(positions), _p(workspace.part_o),
-                                    _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
-                                    workspace.splits, scale, _p(workspace.counters), _stream()), "attn_decode")
+    _check(_fn("mrsum_attn_decode_mfma")(_p(q), q.stride(0), _p(kcache), _p(vcache), _p(block_tables),
+                                         block_tables.stride(0), _p(positions), _p(workspace.part_o),
+                                         _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
+                                         workspace.splits, scale, _p(workspace.counters), _stream()),
+           "attn_decode_mfma")
     return out
 
 
@@ -471,21 +441,19 @@ def sample_tp(logits: torch.Tensor, st, tok_offset: int, max_reduce) -> None:
 
 
 # ------------------------------------------------------------------ large-M GEMM (prefill, M > 64)
-GEMM_STAGGER = int(os.environ.get("MRSUM_GEMM_STAGGER", "1"))
-GEMM_GROUP_M = int(os.environ.get("MRSUM_GEMM_GROUP_M", "4"))
+GEMM_GROUP_M = 4  # tile rows per raster group (4 x 8 tiles per XCD at a time; 8 measured equal)
 GEMM_EPI_BF16, GEMM_EPI_SWIGLU = 0, 1
 
 
-def _gemm(xp, ldx, wp, ldw, out, M, N, K, fp8, epi, sx, sw, stagger, group_m):
+def _gemm(xp, ldx, wp, ldw, out, M, N, K, fp8, epi, sx, sw, group_m):
     _req(out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 8 == 0, "gemm: bad out layout")
     _check(_fn("mrsum_gemm")(xp, ldx, wp, ldw, _p(out), out.stride(0), M, N, K, fp8, epi, sx, sw,
-                             GEMM_STAGGER if stagger is None else stagger,
                              GEMM_GROUP_M if group_m is None else group_m, _stream()), "gemm")
     return out
 
 
 def gemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, swiglu: bool = False,
-         stagger: Optional[int] = None, group_m: Optional[int] = None) -> torch.Tensor:
+         group_m: Optional[int] = None) -> torch.Tensor:
     """x [M, K] @ w [N, K]^T in bf16 on the 256 x 256-tile MFMA kernel (csrc/kernels/gemm.hip), any M.
     ``swiglu``: w is the [8 gate | 8 up]-interleaved gate_up weight and the result is silu(gate) * up
     [M, N / 2]."""
@@ -504,11 +472,11 @@ def gemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, s
     if M == 0:
         return out
     return _gemm(_p(x), x.stride(0), _p(w), w.stride(0), out, M, N, K, 0,
-                 GEMM_EPI_SWIGLU if swiglu else GEMM_EPI_BF16, None, None, stagger, group_m)
+                 GEMM_EPI_SWIGLU if swiglu else GEMM_EPI_BF16, None, None, group_m)
 
 
 def gemm_fp8(xq: torch.Tensor, xs: torch.Tensor, w, out: Optional[torch.Tensor] = None, swiglu: bool = False,
-             stagger: Optional[int] = None, group_m: Optional[int] = None) -> torch.Tensor:
+             group_m: Optional[int] = None) -> torch.Tensor:
     """(xs[:, None] * xq) @ (w.scale[:, None] * w.q)^T on the fp8 MFMA path of the same kernel
     (v_mfma_scale_f32_16x16x128_f8f6f4, OCP e4m3fn operands), bf16 out."""
     _req(xq.is_cuda and xq.dtype == torch.float8_e4m3fn and xq.dim() == 2 and xq.stride(1) == 1
@@ -529,7 +497,7 @@ def gemm_fp8(xq: torch.Tensor, xs: torch.Tensor, w, out: Optional[torch.Tensor] 
     if M == 0:
         return out
     return _gemm(_p(xq), xq.stride(0), _p(q), K, out, M, N, K, 1, GEMM_EPI_SWIGLU if swiglu else GEMM_EPI_BF16,
-                 _p(xs), _p(sc), stagger, group_m)
+                 _p(xs), _p(sc), group_m)
 
 
 # ------------------------------------------------------------------ decode GEMMs (M <= 64)
@@ -564,12 +532,8 @@ def _skinny(x, w, out, epi, nt, splits, ldo):
     return out
 
 
-LDS_DEPTH = int(os.environ.get("MRSUM_LDS_DEPTH", "2"))
-
-
-def _skinny_lds(x, w, out, epi, splits, ldo, depth=None, wpb=4):
-    """Medium-M (x staged in LDS) variant; same contract as _skinny, 16*wpb-row tiles (wpb waves).
-    depth = W prefetch distance in 128-wide k blocks (1 or 2)."""
+def _skinny_lds(x, w, out, epi, splits, ldo, wpb=4):
+    """Medium-M (x staged in LDS) variant; same contract as _skinny, 16*wpb-row tiles (wpb waves)."""
     _bf16_cuda(x, w)
     _rows_ok(x)
     M, K = x.shape
@@ -577,8 +541,7 @@ def _skinny_lds(x, w, out, epi, splits, ldo, depth=None, wpb=4):
     _req(w.is_contiguous() and w.shape[1] == K, "skinny_lds: weight must be [N, K] contiguous")
     _req(1 <= M <= SKINNY_MAX_M and K % 128 == 0 and 4 <= wpb <= 8 and N % (16 * wpb) == 0
          and (K // 128) % splits == 0, "skinny_lds: unsupported shape M=%d N=%d K=%d S=%d wpb=%d" % (M, N, K, splits, wpb))
-    _check(_fn("mrsum_skinny_lds")(_p(x), x.stride(0), _p(w), N, K, M, _p(out), ldo, epi, splits,
-                                   LDS_DEPTH if depth is None else depth, wpb, _stream()),
+    _check(_fn("mrsum_skinny_lds")(_p(x), x.stride(0), _p(w), N, K, M, _p(out), ldo, epi, splits, wpb, _stream()),
            "skinny_lds")
     return out
 
@@ -610,7 +573,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
     if out is None:
         out = torch.empty(M, N, dtype=x.dtype, device=x.device)
     _req(out.is_contiguous() and out.shape == (M, N), "linear: bad out")
-    cfg = stream_config(N, K, splits=1) if STREAM_GEMM else None
+    cfg = stream_config(N, K, splits=1)
     if cfg is not None:
         return _stream_gemm(x, w, out, EPI_BF16, 1, N, cfg[0])
     nt = 2 if N % 32 == 0 and N >= 16384 else 1
@@ -750,10 +713,10 @@ def stream_config(N: int, K: int, swiglu: bool = False, splits: Optional[int] = 
 def plan(role: str, M: int, N: int, K: int, splits: Optional[int] = None, stream: bool = True):
     if M > SKINNY_MAX_M or K % 128:
         return ("gemm",)
-    cfg = stream_config(N, K, swiglu=(role == "gate_up"), splits=splits) if stream and STREAM_GEMM else None
+    cfg = stream_config(N, K, swiglu=(role == "gate_up"), splits=splits) if stream else None
     if cfg is not None:
         return ("stream",) + cfg
-    if role == "gate_up" and stream and STREAM_GEMM and SWIGLU_SPLIT and (K // 128) % 4 == 0:
+    if role == "gate_up" and stream and (K // 128) % 4 == 0:
         # narrow gate_up (TP shards) that the one-tile-per-CU stream kernel cannot fill: split-K over the
         # column tiles, SwiGLU by the last split to arrive -- where it beats the register-streaming kernel
         # (tools/bench_tp_shard.py with write-through partials, us: TP=4 N=7168 M=10 15.7 vs 17.0, M=39
@@ -789,8 +752,6 @@ def plan(role: str, M: int, N: int, K: int, splits: Optional[int] = None, stream
     return ("gemm",)
 
 
-STREAM_GEMM = os.environ.get("MRSUM_STREAM_GEMM", "1") == "1"
-SWIGLU_SPLIT = os.environ.get("MRSUM_SWIGLU_SPLIT", "1") == "1"
 
 
 # ------------------------------------------------------------------ FP8 (e4m3fn) weights
@@ -821,9 +782,6 @@ def _skinny_fp8(x, w, out, epi, nt, splits, ldo):
     return out
 
 
-STREAM_FP8 = os.environ.get("MRSUM_STREAM_FP8", "1") == "1"
-
-
 def stream_config_fp8(N: int, K: int, swiglu: bool = False, splits: Optional[int] = None, M: int = 1):
     """(wpb, S) for the fp8 stream GEMM (256-wide k slots), or None (register-streaming skinny_fp8).
 
@@ -831,7 +789,7 @@ def stream_config_fp8(N: int, K: int, swiglu: bool = False, splits: Optional[int
     wins (gate_up 103 vs 92, down 66 vs 51, qkv 24 vs 20) -- at M=16/40 the stream kernel does (gate_up
     110 / 138 vs 158 / 312, down 67 / 88 vs 66 / 161); TP=8 shards (< 64 M weights) the stream kernel at
     every M (o 12.9 vs 22.7, qkv 13.4 vs 18.1, down 13.7 vs 15.3 at M=1)."""
-    if not STREAM_FP8 or K % 256 or (M <= 8 and N * K >= (64 << 20)):
+    if K % 256 or (M <= 8 and N * K >= (64 << 20)):
         return None
     return stream_config(N, K // 2, swiglu=swiglu, splits=splits)  # K/256 slots == (K/2)/128 blocks
 

@@ -45,9 +45,6 @@ _SIGS = {
 }
 
 
-# 1 (default): write-through publish in the all-reduce kernels (no release fences), 0: fenced (A/B)
-AR_WT = os.environ.get("MRSUM_AR_WT", "1") == "1"
-
 
 def _lib():
     from ..ops._lib import kernels_lib
@@ -56,9 +53,6 @@ def _lib():
         f = getattr(lib, name)
         f.argtypes = args
         f.restype = res
-    lib.mrsum_ar_set_wt.argtypes = [ctypes.c_int]
-    lib.mrsum_ar_set_wt.restype = None
-    lib.mrsum_ar_set_wt(1 if AR_WT else 0)
     return lib
 
 

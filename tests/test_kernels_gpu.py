@@ -152,11 +152,8 @@ def test_attn_prefill_spike():
 
 @pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (4, 4), (16, 1)])
 @pytest.mark.parametrize("splits", [1, 3, 16, 48])
-@pytest.mark.parametrize("impl", ["mfma", "mfma_fused", "valu", "valu_fused"])
-def test_attn_decode(hq, hkv, splits, impl):
-    if impl.startswith("valu") and hq // hkv == 16:
-        pytest.skip("valu kernel supports G <= 8")
-    fused = impl.endswith("_fused")
+@pytest.mark.parametrize("fused", [False, True])
+def test_attn_decode(hq, hkv, splits, fused):
     d, page = 128, 64
     ctxs = [1, 65, 700, 129, 64, 1000]
     B = len(ctxs)
@@ -178,7 +175,7 @@ def test_attn_decode(hq, hkv, splits, impl):
     ws = hip.DecodeWorkspace(B, hq, d, splits, DEV, hkv, fused_combine=fused)
     o2 = reference.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc)
     for _ in range(3):  # replays re-use (and must re-arm) the arrival counters
-        o1 = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws, impl=impl[:4])
+        o1 = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws)
         _close(o1, o2, 2e-2)
     if fused:
         assert int(ws.counters.abs().sum()) == 0
@@ -304,9 +301,8 @@ def test_rope_kv_parts(S):
 
 
 @pytest.mark.parametrize("M", [1, 17, 33, 48, 64])
-@pytest.mark.parametrize("depth,K", [(1, 1024), (2, 1024), (2, 640)])
-def test_skinny_lds_all_epilogues(M, depth, K, monkeypatch):
-    monkeypatch.setattr(hip, "LDS_DEPTH", depth)
+@pytest.mark.parametrize("K", [1024, 640])
+def test_skinny_lds_all_epilogues(M, K):
     x = _rand(M, K, seed=40)
     w = _rand(512, K, scale=0.05, seed=41)
     ref = x.float() @ w.float().t()
@@ -320,7 +316,7 @@ def test_skinny_lds_all_epilogues(M, depth, K, monkeypatch):
         ww = _rand(n, K, scale=0.05, seed=44)
         S = 2 if (K // 128) % 2 == 0 else 1
         oo = torch.empty(S, M, n, dtype=torch.float32, device=DEV)
-        _close(hip._skinny_lds(x, ww, oo, hip.EPI_F32_PARTIAL, S, n, depth, wpb).sum(0),
+        _close(hip._skinny_lds(x, ww, oo, hip.EPI_F32_PARTIAL, S, n, wpb).sum(0),
                x.float() @ ww.float().t(), 1e-3, 1e-3)
 
 

@@ -79,6 +79,19 @@ def main():
            "weights_gib": round(eng.model.weight_bytes() / 2 ** 30, 1), "init_s": round(init_s, 1),
            "hbm_peak_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1),
            "data": "synthetic summaries; random-init weights; generation pinned to max_new_tokens"}
+    # the planner's cost model for this pass on an 8-GPU node (TP=8): what a TP prefill forward (RCCL
+    # all-reduces of the activations) and a one-rank prefill + KV hand-off would take, and the stage
+    from llm_map_reduce_summarizer_amd.parallel import plan
+    d = plan.ModelDims.of(prov.model_config(), 1.0 if a.dtype == "fp8" else 2.0)
+    hw = plan.HWModel()
+    pl, mn = [res.prompt_tokens], [a.max_new_tokens]
+    ch = plan.choose(d, hw, pl, mn, 8, handoff=True)
+    out["cost_model_tp8"] = {"tp_prefill_s": round(plan.prefill_s(d, hw, pl[0], 8), 3),
+                             "handoff_prefill_s": round(plan.handoff_prefill_s(d, hw, pl, 8), 3),
+                             "decode_ms_per_step": round(1e3 * plan.decode_step_s(d, hw, 1, pl[0] + mn[0] / 2, 8), 3),
+                             "stage_s": ch["estimates_s"], "choice": {k: v for k, v in ch.items() if k != "estimates_s"},
+                             "hw": {"hbm_bw": hw.hbm_bw, "ar_lat_s": hw.ar_lat_s, "ar_bw": hw.ar_bw,
+                                    "prefill_flops": hw.prefill_flops}}
     if rank == 0:
         print(json.dumps(out), flush=True)
     pdist.shutdown()

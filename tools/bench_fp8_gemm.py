@@ -41,10 +41,9 @@ def main():
             def nxt():
                 it[0] += 1
                 return ws[it[0] % ncopy]
-            hip.STREAM_FP8 = False
-            t_sk = timeit(lambda: hip.fp8_linear_swiglu(x, nxt()) if sw else
+            osw = torch.empty(M, N // 2, dtype=torch.bfloat16, device=dev)
+            t_sk = timeit(lambda: hip._skinny_fp8(x, nxt(), osw, hip.EPI_SWIGLU, 1, 1, N // 2) if sw else
                           hip.fp8_linear_parts(x, nxt(), *(_skinny_cfg(hip, name, M, N, K))))
-            hip.STREAM_FP8 = True
             cfg = hip.stream_config(N, K // 2, swiglu=sw)  # the stream kernel's config, whatever the plan says
             t_st = None
             if cfg is not None:

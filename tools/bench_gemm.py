@@ -41,7 +41,7 @@ def main():
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--ms", default="4096,8192,16384,24576,49152")
     ap.add_argument("--roles", default="qkv,o,gate_up,down")
-    ap.add_argument("--variants", default="s1g4,s0g4,s1g8,blas")
+    ap.add_argument("--variants", default="g4,g8,blas", help="gN = our kernel, group_m N; blas = hipBLASLt")
     ap.add_argument("--fp8", action="store_true")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
@@ -65,11 +65,11 @@ def main():
                     else:
                         fns[v] = lambda: torch.nn.functional.linear(x, w)
                 else:
-                    st, gm = int(v[1]), int(v[3:])
+                    gm = int(v[1:])
                     if a.fp8:
-                        fns[v] = (lambda st=st, gm=gm: hip.gemm_fp8(xq, xs, wq, out=out, stagger=st, group_m=gm))
+                        fns[v] = (lambda gm=gm: hip.gemm_fp8(xq, xs, wq, out=out, group_m=gm))
                     else:
-                        fns[v] = (lambda st=st, gm=gm: hip.gemm(x, w, out=out, stagger=st, group_m=gm))
+                        fns[v] = (lambda gm=gm: hip.gemm(x, w, out=out, group_m=gm))
             times = {v: [] for v in fns}
             for f in fns.values():
                 f()

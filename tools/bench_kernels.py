@@ -72,15 +72,12 @@ def main():
         pos = torch.full((B,), ctx - 1, dtype=torch.int32, device=dev)
         q = torch.randn(B, (hq + 2 * hkv) * d, device=dev, dtype=torch.bfloat16)
         for splits in sorted({hip.decode_splits(B, hkv, ctx), 4, 8, 16, 32}):
-            for impl in ("mfma", "valu"):
-                fused = False
-                ws = hip.DecodeWorkspace(B, hq, d, splits, dev, hkv, fused_combine=fused)
-                t = timeit(lambda: hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, 1 / math.sqrt(d),
-                                                   workspace=ws, impl=impl))
-                gb = B * ctx * hkv * d * 2 * 2 / 1e9
-                res["attn_decode"].append({"B": B, "ctx": ctx, "S": splits, "impl": impl, "us": round(t * 1e6, 1),
-                                           "TBps": round(gb / t / 1e3, 2)})
-                print(json.dumps(res["attn_decode"][-1]), flush=True)
+            ws = hip.DecodeWorkspace(B, hq, d, splits, dev, hkv)
+            t = timeit(lambda: hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, 1 / math.sqrt(d), workspace=ws))
+            gb = B * ctx * hkv * d * 2 * 2 / 1e9
+            res["attn_decode"].append({"B": B, "ctx": ctx, "S": splits, "us": round(t * 1e6, 1),
+                                       "TBps": round(gb / t / 1e3, 2)})
+            print(json.dumps(res["attn_decode"][-1]), flush=True)
     # prefill attention
     for nseq, L in ((1, 4096), (8, 4096), (4, 8192), (1, 32768)):
         T = nseq * L
@@ -90,8 +87,7 @@ def main():
         t = timeit(lambda: hip.attn_prefill(qkv, cu, hq, hkv, d, 1 / math.sqrt(d), items=items, seqlens=[L] * nseq),
                    iters=20)
         fl = nseq * 4 * L * L / 2 * d * hq
-        res["attn_prefill"].append({"nseq": nseq, "L": L, "ms": round(t * 1e3, 3), "TFLOPs": round(fl / t / 1e12, 1),
-                                    "packed_softmax": hip.PREFILL_PK})
+        res["attn_prefill"].append({"nseq": nseq, "L": L, "ms": round(t * 1e3, 3), "TFLOPs": round(fl / t / 1e12, 1)})
         print(json.dumps(res["attn_prefill"][-1]), flush=True)
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/bench_kernels.json", "w") as f:
