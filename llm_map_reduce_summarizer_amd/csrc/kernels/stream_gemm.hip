@@ -22,12 +22,36 @@
 //     per x tile, A = W fragment (ds_read_b128), B = x fragment (ds_read_b128) -- the same
 //     swapped out^T product and epilogues as skinny_gemm.hip (bf16 | fp32 split-K slab | SwiGLU
 //     over [8 gate | 8 up] row blocks).
+//
+// Deferred RMSNorm (the decode layer's two add + RMSNorm passes folded into the GEMMs around them):
+//   * producer (o / down projection, EPI_RESID_SPLIT): split-K partial tiles are published
+//     write-through; the last split of a column tile to arrive sums them in split order onto the
+//     residual rows (h = bf16(residual + sum), exactly the add_rmsnorm_parts arithmetic), stores h
+//     back and writes the tile's per-row sums of squares of h to ssp[M][tiles];
+//   * consumer (qkv / gate_up / LM head, any epilogue, e.ssq != null): x = the residual rows h and
+//     the norm gain folded into W (W' = W diag(g), engine/model.py), so rmsnorm(h) W^T =
+//     rsqrt(mean(h^2) + eps) * (h W'^T): the row scale multiplies the accumulator in the epilogue,
+//     from the producer's per-tile sums reduced in a fixed order (deterministic).
+// Two kernels per layer fewer than GEMM -> add_rmsnorm_parts -> GEMM.
 #include "common.h"
 
 namespace {
-enum { EPI_BF16 = 0, EPI_F32_PARTIAL = 1, EPI_SWIGLU = 2, EPI_SWIGLU_SPLIT = 3 };
+enum { EPI_BF16 = 0, EPI_F32_PARTIAL = 1, EPI_SWIGLU = 2, EPI_SWIGLU_SPLIT = 3, EPI_RESID_SPLIT = 4 };
+constexpr int SS_PARTS = 8;  // consumer: the tiles' sums of squares of a row reduced as 8 fixed partials
 constexpr int KBLK = 128;
-constexpr int LDS_BUDGET = 160 * 1024 - 1024;  // one KiB scratch for the dummy x pieces
+// one KiB scratch for the dummy x pieces + 2 KiB for the consumer's row-norm partials [64][SS_PARTS]
+constexpr int LDS_XTRA = 3 * 1024;
+constexpr int LDS_BUDGET = 160 * 1024 - LDS_XTRA;
+
+// deferred-RMSNorm operands (see the header); all null / zero for a plain GEMM
+struct NormArgs {
+    const float* ssq;  // consumer: [M][ssq_tiles] row sums of squares of x per producer column tile
+    int ssq_tiles;     // multiple of 4 * SS_PARTS
+    float inv_k, eps;  // 1 / hidden, RMSNorm epsilon
+    bf16* resid;       // producer: residual rows [M][ldr] (in / out)
+    int ldr;
+    float* ssp;        // producer: [M][gridDim.x] row sums of squares of h per column tile
+};
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
@@ -53,6 +77,227 @@ __device__ __forceinline__ void glds16(const void* g, char* lds) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                      (__attribute__((address_space(3))) void*)lds, 16, 0, AUX);
 }
+
+// consumer: s_ss[8 m + p] = sum of partial p (ssq_tiles / 8 consecutive tiles, fixed order) of row m
+__device__ __forceinline__ void row_norm_partials(const NormArgs& e, int M, int tid, int nthr, float* s_ss) {
+    const int C = e.ssq_tiles / SS_PARTS;
+    for (int i = tid; i < SS_PARTS * M; i += nthr) {
+        const int m = i / SS_PARTS, p = i % SS_PARTS;
+        const float4* src = reinterpret_cast<const float4*>(e.ssq + (size_t)m * e.ssq_tiles + p * C);
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 8
+        for (int q = 0; q < C / 4; ++q) {
+            const float4 v = src[q];
+            a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+        }
+        s_ss[i] = (a.x + a.y) + (a.z + a.w);
+    }
+}
+
+__device__ __forceinline__ float row_scale(const NormArgs& e, const float* s_ss, int m) {
+    float t = 0.f;
+#pragma unroll
+    for (int p = 0; p < SS_PARTS; ++p) t += s_ss[SS_PARTS * m + p];
+    return rsqrtf(t * e.inv_k + e.eps);
+}
+
+// split-K arrival: every wave drained its write-through partial stores; returns true in the last of
+// the nsplit workgroups of column tile ``tile`` to arrive (after an agent-scope acquire), and re-arms
+// the ticket there.  The flag goes through the kernel's one LDS array (a second __shared__ object can
+// de-pipeline the ring: cdna_hip_programming.md "Projection GEMM at M = 256" item 4(a)).
+__device__ __forceinline__ bool last_arrival(int* counters, int tile, int nsplit, int tid, int* s_flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {  // partials are write-through stores, drained above: no release fence (buffer_wbl2)
+        const int prev = __hip_atomic_fetch_add(counters + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_flag = prev == nsplit - 1;
+    }
+    __syncthreads();
+    const bool last = *s_flag != 0;
+    if (last) {
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+    }
+    return last;
+}
+}  // namespace
+
+namespace {
+// Epilogue shared by the bf16 and fp8 stream kernels.  acc[m]: lane holds out^T[n = n0 + 16w + 4g + jj]
+// [m = 16 mt + r] (fp8: already times the weight row scales).  ``lds`` = the kernel's one LDS array
+// (the ring is drained by now), ``s_ss`` its 2 KiB row-norm partials region.
+template <int MT, int EPI, int WPB>
+__device__ __forceinline__ void stream_epilogue(f32x4 (&acc)[MT], char* lds, float* s_ss, const int n0, const int M,
+                                                void* __restrict__ out, const int ldo, float* __restrict__ parts,
+                                                int* __restrict__ counters, const NormArgs& e) {
+    constexpr int R = 16 * WPB;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 15, g = lane >> 4;
+    // deferred RMSNorm consumer: scale row m of the product by rsqrt(mean(h_m^2) + eps) (the ring is
+    // drained: the partial-sum loads cannot stall it)
+    if (e.ssq) {
+        row_norm_partials(e, M, tid, 64 * WPB, s_ss);
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < MT; ++m) {
+            const float sc = row_scale(e, s_ss, min(16 * m + r, M - 1));
+            acc[m][0] *= sc; acc[m][1] *= sc; acc[m][2] *= sc; acc[m][3] *= sc;
+        }
+    }
+
+    // C: lane holds out^T[n = n0 + 16w + 4g + jj][m = 16 mt + r]
+    const int nw = n0 + 16 * w;
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const int mm = 16 * m + r;
+        if constexpr (EPI == EPI_SWIGLU) {
+            f32x4 up;
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) up[jj] = __shfl_xor(acc[m][jj], 32, 64);
+            if (g < 2 && mm < M) {
+                float rr[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    const float gv = acc[m][jj];
+                    rr[jj] = gv / (1.f + __expf(-gv)) * up[jj];
+                }
+                uint2 o;
+                o.x = pack2(rr[0], rr[1]);
+                o.y = pack2(rr[2], rr[3]);
+                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + (nw >> 1) + 4 * g) = o;
+            }
+        } else if (mm < M) {
+            if constexpr (EPI == EPI_BF16) {
+                uint2 o;
+                o.x = pack2(acc[m][0], acc[m][1]);
+                o.y = pack2(acc[m][2], acc[m][3]);
+                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + nw + 4 * g) = o;
+            } else if constexpr (EPI == EPI_F32_PARTIAL) {
+                float* o = reinterpret_cast<float*>(out) + ((size_t)blockIdx.y * M + mm) * ldo + nw + 4 * g;
+                *reinterpret_cast<float4*>(o) = make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
+            } else {  // write-through (global_store sc1): read by another XCD's last arriver, no release fence
+                float* o = parts + ((size_t)blockIdx.y * M + mm) * (gridDim.x * R) + nw + 4 * g;
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj)
+                    __hip_atomic_store(o + jj, acc[m][jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+    if constexpr (EPI == EPI_SWIGLU_SPLIT || EPI == EPI_RESID_SPLIT) {
+        // the last of the gridDim.y split workgroups of this column tile to arrive sums the fp32 partial
+        // tiles (write-through publish / ticket / acquire, as attn_decode.hip combine_if_last<G, true>)
+        if (!last_arrival(counters, blockIdx.x, gridDim.y, tid, reinterpret_cast<int*>(lds))) return;
+        const int S = gridDim.y;
+        const size_t ncols = (size_t)gridDim.x * R;
+        // every thread handles at most IT items and keeps all their partial-tile loads (4 splits at a time)
+        // in flight together: the reduction is a few memory round trips, not one per item
+        constexpr int NT = 64 * WPB;
+        if constexpr (EPI == EPI_SWIGLU_SPLIT) {
+            // silu(gate) * up.  Lets a narrow gate_up projection (TP shards: N = 3584) fill the chip with
+            // split-K instead of streaming its weights through N / (16 WPB) CUs.
+            // item = (row, 16-row block, half): 4 features = gate rows n0 + 16 bl + 4 hf .. +4, up rows + 8
+            constexpr int IT = (64 * 2 * WPB + NT - 1) / NT;
+            const float* pg[IT];
+            float4 gs[IT], us[IT];
+#pragma unroll
+            for (int j = 0; j < IT; ++j) {
+                const int it = min(tid + j * NT, M * 2 * WPB - 1);
+                const int mm = it / (2 * WPB), q = it % (2 * WPB), bl = q >> 1, hf = q & 1;
+                pg[j] = parts + (size_t)mm * ncols + n0 + 16 * bl + 4 * hf;
+                gs[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                us[j] = gs[j];
+            }
+            for (int s0 = 0; s0 < S; s0 += 4) {
+                float4 ga[IT][4], ua[IT][4];
+#pragma unroll
+                for (int j = 0; j < IT; ++j)
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const float* p = pg[j] + (size_t)min(s0 + u, S - 1) * M * ncols;
+                        ga[j][u] = *reinterpret_cast<const float4*>(p);
+                        ua[j][u] = *reinterpret_cast<const float4*>(p + 8);
+                    }
+#pragma unroll
+                for (int j = 0; j < IT; ++j)
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (s0 + u < S) {
+                            gs[j].x += ga[j][u].x; gs[j].y += ga[j][u].y; gs[j].z += ga[j][u].z; gs[j].w += ga[j][u].w;
+                            us[j].x += ua[j][u].x; us[j].y += ua[j][u].y; us[j].z += ua[j][u].z; us[j].w += ua[j][u].w;
+                        }
+            }
+#pragma unroll
+            for (int j = 0; j < IT; ++j) {
+                const int it = tid + j * NT;
+                if (it >= M * 2 * WPB) break;
+                const int mm = it / (2 * WPB), q = it % (2 * WPB), bl = q >> 1, hf = q & 1;
+                const float4 g4 = gs[j], u4 = us[j];
+                uint2 o;
+                o.x = pack2(g4.x / (1.f + __expf(-g4.x)) * u4.x, g4.y / (1.f + __expf(-g4.y)) * u4.y);
+                o.y = pack2(g4.z / (1.f + __expf(-g4.z)) * u4.z, g4.w / (1.f + __expf(-g4.w)) * u4.w);
+                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + (n0 >> 1) + 8 * bl + 4 * hf) = o;
+            }
+        } else {
+            // h = bf16(residual + partial 0 + partial 1 + ...) (add_rmsnorm_parts order), stored back; the
+            // tile's per-row sum of h^2 (of the rounded values) to ssp[m][tile] in a fixed order.
+            constexpr int Q = R / 4;  // 4-column items per row
+            constexpr int IT = (64 * Q + NT - 1) / NT;
+            float* s_sq = reinterpret_cast<float*>(lds + 64);  // [M][Q]; the ring is drained
+            const float* pg[IT];
+            uint2* rp[IT];
+            uint2 rv[IT];
+#pragma unroll
+            for (int j = 0; j < IT; ++j) {
+                const int it = min(tid + j * NT, M * Q - 1);
+                const int mm = it / Q, c = n0 + 4 * (it % Q);
+                pg[j] = parts + (size_t)mm * ncols + c;
+                rp[j] = reinterpret_cast<uint2*>(e.resid + (size_t)mm * e.ldr + c);
+                rv[j] = *rp[j];
+            }
+            float h[IT][4];
+#pragma unroll
+            for (int j = 0; j < IT; ++j) {
+                h[j][0] = __uint_as_float(rv[j].x << 16); h[j][1] = __uint_as_float(rv[j].x & 0xffff0000u);
+                h[j][2] = __uint_as_float(rv[j].y << 16); h[j][3] = __uint_as_float(rv[j].y & 0xffff0000u);
+            }
+            for (int s0 = 0; s0 < S; s0 += 4) {
+                float4 a4[IT][4];
+#pragma unroll
+                for (int j = 0; j < IT; ++j)
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        a4[j][u] = *reinterpret_cast<const float4*>(pg[j] + (size_t)min(s0 + u, S - 1) * M * ncols);
+#pragma unroll
+                for (int j = 0; j < IT; ++j)
+#pragma unroll
+                    for (int u = 0; u < 4; ++u)
+                        if (s0 + u < S) {
+                            h[j][0] += a4[j][u].x; h[j][1] += a4[j][u].y; h[j][2] += a4[j][u].z; h[j][3] += a4[j][u].w;
+                        }
+            }
+#pragma unroll
+            for (int j = 0; j < IT; ++j) {
+                const int it = tid + j * NT;
+                if (it >= M * Q) break;
+                const uint2 hv = make_uint2(pack2(h[j][0], h[j][1]), pack2(h[j][2], h[j][3]));
+                *rp[j] = hv;
+                const float h0 = __uint_as_float(hv.x << 16), h1 = __uint_as_float(hv.x & 0xffff0000u);
+                const float h2 = __uint_as_float(hv.y << 16), h3 = __uint_as_float(hv.y & 0xffff0000u);
+                s_sq[it] = (h0 * h0 + h1 * h1) + (h2 * h2 + h3 * h3);
+            }
+            __syncthreads();
+            for (int mm = tid; mm < M; mm += 64 * WPB) {
+                float t = 0.f;
+                for (int q = 0; q < Q; ++q) t += s_sq[mm * Q + q];
+                e.ssp[(size_t)mm * gridDim.x + blockIdx.x] = t;
+            }
+        }
+    }
+}
 }  // namespace
 
 // NTW: weight pieces loaded with the nontemporal policy (aux = 2): decode weights are read once per
@@ -62,7 +307,8 @@ template <int MT, int EPI, int WPB, bool NTW>
 __global__ __launch_bounds__(64 * WPB, 1) void stream_gemm_kernel(const bf16* __restrict__ x, int ldx,
                                                                   const bf16* __restrict__ W, int K, int M,
                                                                   void* __restrict__ out, int ldo, int kper,
-                                                                  float* __restrict__ parts, int* __restrict__ counters) {
+                                                                  float* __restrict__ parts, int* __restrict__ counters,
+                                                                  const NormArgs e) {
     constexpr int R = 16 * WPB, BM = 16 * MT;
     constexpr int WBYTES = R * 256, SLOT = WBYTES + BM * 256;
     constexpr int D = (LDS_BUDGET / SLOT) < 6 ? (LDS_BUDGET / SLOT) : 6;
@@ -70,7 +316,8 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_gemm_kernel(const bf16* __
     constexpr int XP = 2 * BM / 8;               // x pieces per slot (= 4 MT)
     constexpr int XI = (XP + WPB - 1) / WPB;     // x pieces per wave (padded)
     constexpr int NI = 4 + XI;                   // DMA instructions per wave per slot (W: R/4 pieces / WPB = 4)
-    __shared__ __attribute__((aligned(1024))) char lds[D * SLOT + 1024];
+    __shared__ __attribute__((aligned(1024))) char lds[D * SLOT + LDS_XTRA];
+    float* const s_ss = reinterpret_cast<float*>(lds + D * SLOT + 1024);  // consumer row-norm partials
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int n0 = blockIdx.x * R;
@@ -134,107 +381,42 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_gemm_kernel(const bf16* __
     }
 #undef ISSUE
 
-    // C: lane holds out^T[n = n0 + 16w + 4g + jj][m = 16 mt + r]
-    const int nw = n0 + 16 * w;
-#pragma unroll
-    for (int m = 0; m < MT; ++m) {
-        const int mm = 16 * m + r;
-        if constexpr (EPI == EPI_SWIGLU) {
-            f32x4 up;
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) up[jj] = __shfl_xor(acc[m][jj], 32, 64);
-            if (g < 2 && mm < M) {
-                float rr[4];
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const float gv = acc[m][jj];
-                    rr[jj] = gv / (1.f + __expf(-gv)) * up[jj];
-                }
-                uint2 o;
-                o.x = pack2(rr[0], rr[1]);
-                o.y = pack2(rr[2], rr[3]);
-                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + (nw >> 1) + 4 * g) = o;
-            }
-        } else if (mm < M) {
-            if constexpr (EPI == EPI_BF16) {
-                uint2 o;
-                o.x = pack2(acc[m][0], acc[m][1]);
-                o.y = pack2(acc[m][2], acc[m][3]);
-                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + nw + 4 * g) = o;
-            } else if constexpr (EPI == EPI_F32_PARTIAL) {
-                float* o = reinterpret_cast<float*>(out) + ((size_t)blockIdx.y * M + mm) * ldo + nw + 4 * g;
-                *reinterpret_cast<float4*>(o) = make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
-            } else {  // write-through (global_store sc1): read by another XCD's last arriver, no release fence
-                float* o = parts + ((size_t)blockIdx.y * M + mm) * (gridDim.x * R) + nw + 4 * g;
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj)
-                    __hip_atomic_store(o + jj, acc[m][jj], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-    }
-    if constexpr (EPI == EPI_SWIGLU_SPLIT) {
-        // split-K SwiGLU: the last of the gridDim.y split workgroups of this column tile to arrive sums
-        // the fp32 partial tiles and applies silu(gate) * up (write-through publish / ticket / acquire, as
-        // attn_decode.hip combine_if_last<G, true>; the ticket is re-armed for the next launch / replay).
-        // Lets a narrow gate_up projection (TP shards: N = 3584) fill the chip with split-K instead of
-        // streaming its weights through N / (16 WPB) CUs.
-        __shared__ int s_last;
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) {  // partials are write-through stores, drained above: no release fence (buffer_wbl2)
-            const int prev = __hip_atomic_fetch_add(counters + blockIdx.x, 1, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-            s_last = prev == (int)gridDim.y - 1;
-        }
-        __syncthreads();
-        if (!s_last) return;
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        const int S = gridDim.y;
-        const size_t ncols = (size_t)gridDim.x * R;
-        // item = (row, 16-row block, half): 4 features = gate rows n0 + 16 bl + 4 hf .. +4, up rows + 8
-        for (int it = tid; it < M * 2 * WPB; it += 64 * WPB) {
-            const int mm = it / (2 * WPB), q = it % (2 * WPB), bl = q >> 1, hf = q & 1;
-            const float* pg = parts + (size_t)mm * ncols + n0 + 16 * bl + 4 * hf;
-            float4 gs = make_float4(0.f, 0.f, 0.f, 0.f), us = gs;
-#pragma unroll 4
-            for (int sp = 0; sp < S; ++sp) {
-                const float4 a = *reinterpret_cast<const float4*>(pg + (size_t)sp * M * ncols);
-                const float4 u = *reinterpret_cast<const float4*>(pg + (size_t)sp * M * ncols + 8);
-                gs.x += a.x; gs.y += a.y; gs.z += a.z; gs.w += a.w;
-                us.x += u.x; us.y += u.y; us.z += u.z; us.w += u.w;
-            }
-            uint2 o;
-            o.x = pack2(gs.x / (1.f + __expf(-gs.x)) * us.x, gs.y / (1.f + __expf(-gs.y)) * us.y);
-            o.y = pack2(gs.z / (1.f + __expf(-gs.z)) * us.z, gs.w / (1.f + __expf(-gs.w)) * us.w);
-            *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + (n0 >> 1) + 8 * bl + 4 * hf) = o;
-        }
-        if (tid == 0) __hip_atomic_store(counters + blockIdx.x, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    stream_epilogue<MT, EPI, WPB>(acc, lds, s_ss, n0, M, out, ldo, parts, counters, e);
 }
 
-// out: bf16 [M, ldo] (EPI_BF16), fp32 slabs [splits, M, ldo] (EPI_F32_PARTIAL) or bf16 [M, ldo] of
-// N/2 SwiGLU features (EPI_SWIGLU, splits = 1).  N % (16 wpb) == 0, wpb in {4, 5, 6, 7, 8}.
-// decode weights are streamed with nontemporal loads (each weight row read once per step by one CU:
-// MI355X_MICROARCH.md "nt-weights"; profiles/r1_decode_nt_ab.jsonl)
-
-static int launch_stream_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
-                              int epi, int splits, int wpb, float* parts, int* counters, hipStream_t s) {
+// out: bf16 [M, ldo] (EPI_BF16), fp32 slabs [splits, M, ldo] (EPI_F32_PARTIAL), bf16 [M, ldo] of N/2
+// SwiGLU features (EPI_SWIGLU, splits = 1; EPI_SWIGLU_SPLIT with ``parts`` fp32 [splits, M, N] scratch),
+// or the residual update of EPI_RESID_SPLIT (``out`` unused; resid [M, ldr] bf16 += the product, ssp
+// fp32 [M, N / (16 wpb)] row sums of squares per column tile; ``parts`` scratch as SwiGLU_SPLIT).
+// Split-K last-arriver epilogues take ``counters`` >= N / (16 wpb) ints, zero on the first call (every
+// launch leaves them zero again).  ssq (any epilogue): deferred-RMSNorm input, [M, ssq_tiles] fp32 row
+// sums of squares of x (x = the un-normalised residual rows), ssq_tiles % 32 == 0; the product rows are
+// scaled by rsqrt(sum / K + eps).  N % (16 wpb) == 0, wpb in {4, 5, 6, 7, 8}, M <= 64.
+// Decode weights are streamed with nontemporal loads (each weight row read once per step by one CU:
+// MI355X_MICROARCH.md "nt-weights"; profiles/r1_decode_nt_ab.jsonl).
+MRSUM_API int mrsum_stream_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
+                                int epi, int splits, int wpb, void* parts, int* counters, const float* ssq,
+                                int ssq_tiles, float eps, void* resid, int ldr, float* ssp, hipStream_t s) {
     if (M <= 0) return 0;
-    if (wpb < 4 || wpb > 8 || M > 64 || K % KBLK || N % (16 * wpb) || splits < 1 || (K / KBLK) % splits)
+    if (wpb < 4 || wpb > 8 || M > 64 || K % KBLK || N % (16 * wpb) || splits < 1 || (K / KBLK) % splits ||
+        epi < EPI_BF16 || epi > EPI_RESID_SPLIT)
         return (int)hipErrorInvalidValue;
-    if (epi != EPI_F32_PARTIAL && epi != EPI_SWIGLU_SPLIT && splits != 1) return (int)hipErrorInvalidValue;
-    if (epi == EPI_SWIGLU_SPLIT && (!parts || !counters)) return (int)hipErrorInvalidValue;
+    const bool split_epi = epi == EPI_SWIGLU_SPLIT || epi == EPI_RESID_SPLIT;
+    if (epi != EPI_F32_PARTIAL && !split_epi && splits != 1) return (int)hipErrorInvalidValue;
+    if (split_epi && (!parts || !counters)) return (int)hipErrorInvalidValue;
+    if (epi == EPI_RESID_SPLIT && (!resid || !ssp || ldr % 4)) return (int)hipErrorInvalidValue;
+    if (ssq && (ssq_tiles <= 0 || ssq_tiles % (4 * SS_PARTS))) return (int)hipErrorInvalidValue;
+    NormArgs e;
+    e.ssq = ssq; e.ssq_tiles = ssq_tiles; e.inv_k = 1.f / (float)K; e.eps = eps;
+    e.resid = (bf16*)resid; e.ldr = ldr; e.ssp = ssp;
     const int kper = K / splits;
     const int mt = (M + 15) / 16;
     dim3 grid(N / (16 * wpb), splits), block(64 * wpb);
     auto X = (const bf16*)x;
     auto Wp = (const bf16*)W;
+    auto P = (float*)parts;
 #define L(MT_, EPI_, WPB_)                                                                                   \
-    stream_gemm_kernel<MT_, EPI_, WPB_, true><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, parts, counters)
+    stream_gemm_kernel<MT_, EPI_, WPB_, true><<<grid, block, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, P, counters, e)
 #define BY_WPB(MT_, EPI_)                          \
     switch (wpb) {                                 \
         case 4: L(MT_, EPI_, 4); break;            \
@@ -247,7 +429,8 @@ static int launch_stream_gemm(const void* x, int ldx, const void* W, int N, int 
     if (epi == EPI_BF16) { BY_WPB(MT_, EPI_BF16) }                            \
     else if (epi == EPI_F32_PARTIAL) { BY_WPB(MT_, EPI_F32_PARTIAL) }         \
     else if (epi == EPI_SWIGLU) { BY_WPB(MT_, EPI_SWIGLU) }                   \
-    else { BY_WPB(MT_, EPI_SWIGLU_SPLIT) }
+    else if (epi == EPI_SWIGLU_SPLIT) { BY_WPB(MT_, EPI_SWIGLU_SPLIT) }       \
+    else { BY_WPB(MT_, EPI_RESID_SPLIT) }
     switch (mt) {
         case 1: BY_EPI(1); break;
         case 2: BY_EPI(2); break;
@@ -258,22 +441,6 @@ static int launch_stream_gemm(const void* x, int ldx, const void* W, int N, int 
 #undef BY_WPB
 #undef L
     return (int)hipGetLastError();
-}
-
-MRSUM_API int mrsum_stream_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
-                                int epi, int splits, int wpb, hipStream_t s) {
-    if (epi == EPI_SWIGLU_SPLIT) return (int)hipErrorInvalidValue;
-    return launch_stream_gemm(x, ldx, W, N, K, M, out, ldo, epi, splits, wpb, nullptr, nullptr, s);
-}
-
-// out [M, ldo] bf16 = SwiGLU of the blocked gate_up product, split-K over ``splits`` workgroups per
-// column tile: ``parts`` fp32 [splits, M, N] scratch, ``counters`` >= N / (16 wpb) ints, zero on the
-// first call (every launch leaves them zero again).
-MRSUM_API int mrsum_stream_gemm_swiglu_split(const void* x, int ldx, const void* W, int N, int K, int M, void* out,
-                                             int ldo, int splits, int wpb, void* parts, int* counters,
-                                             hipStream_t s) {
-    return launch_stream_gemm(x, ldx, W, N, K, M, out, ldo, EPI_SWIGLU_SPLIT, splits, wpb, (float*)parts, counters,
-                              s);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -301,7 +468,9 @@ template <int MT, int EPI, int WPB>
 __global__ __launch_bounds__(64 * WPB, 1) void stream_fp8_kernel(const bf16* __restrict__ x, int ldx,
                                                                  const unsigned char* __restrict__ W,
                                                                  const float* __restrict__ wscale, int K, int M,
-                                                                 void* __restrict__ out, int ldo, int kper) {
+                                                                 void* __restrict__ out, int ldo, int kper,
+                                                                 float* __restrict__ parts, int* __restrict__ counters,
+                                                                 const NormArgs e) {
     constexpr int R = 16 * WPB, BM = 16 * MT;
     constexpr int WBYTES = R * 256, XBYTES = BM * 256, SLOT = WBYTES + 2 * XBYTES;
     constexpr int D = (LDS_BUDGET / SLOT) < 6 ? (LDS_BUDGET / SLOT) : 6;
@@ -309,7 +478,7 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_fp8_kernel(const bf16* __r
     constexpr int XP = 2 * (2 * BM / 8);         // x pieces per slot: two 128-k images
     constexpr int XI = (XP + WPB - 1) / WPB;
     constexpr int NI = 4 + XI;
-    __shared__ __attribute__((aligned(1024))) char lds[D * SLOT + 1024];
+    __shared__ __attribute__((aligned(1024))) char lds[D * SLOT + LDS_XTRA];
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int n0 = blockIdx.x * R;
@@ -371,62 +540,40 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_fp8_kernel(const bf16* __r
     }
 #undef ISSUE8
 
-    // C: lane holds out^T[n = n0 + 16w + 4g + jj][m = 16 mt + r]; scale rows first
-    const int nw = n0 + 16 * w;
-    const float4 sc = *reinterpret_cast<const float4*>(wscale + nw + 4 * g);
+    // weight row scales first (n = n0 + 16w + 4g + jj), then the shared epilogue
+    const float4 sc = *reinterpret_cast<const float4*>(wscale + n0 + 16 * w + 4 * g);
 #pragma unroll
     for (int m = 0; m < MT; ++m) {
-        acc[m][0] *= sc.x;
-        acc[m][1] *= sc.y;
-        acc[m][2] *= sc.z;
-        acc[m][3] *= sc.w;
-        const int mm = 16 * m + r;
-        if constexpr (EPI == EPI_SWIGLU) {
-            f32x4 up;
-#pragma unroll
-            for (int jj = 0; jj < 4; ++jj) up[jj] = __shfl_xor(acc[m][jj], 32, 64);
-            if (g < 2 && mm < M) {
-                float rr[4];
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {
-                    const float gv = acc[m][jj];
-                    rr[jj] = gv / (1.f + __expf(-gv)) * up[jj];
-                }
-                uint2 o;
-                o.x = pack2(rr[0], rr[1]);
-                o.y = pack2(rr[2], rr[3]);
-                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + (nw >> 1) + 4 * g) = o;
-            }
-        } else if (mm < M) {
-            if constexpr (EPI == EPI_BF16) {
-                uint2 o;
-                o.x = pack2(acc[m][0], acc[m][1]);
-                o.y = pack2(acc[m][2], acc[m][3]);
-                *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + nw + 4 * g) = o;
-            } else {
-                float* o = reinterpret_cast<float*>(out) + ((size_t)blockIdx.y * M + mm) * ldo + nw + 4 * g;
-                *reinterpret_cast<float4*>(o) = make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
-            }
-        }
+        acc[m][0] *= sc.x; acc[m][1] *= sc.y; acc[m][2] *= sc.z; acc[m][3] *= sc.w;
     }
+    stream_epilogue<MT, EPI, WPB>(acc, lds, reinterpret_cast<float*>(lds + D * SLOT + 1024), n0, M, out, ldo, parts,
+                                  counters, e);
 }
 
-// out: bf16 [M, ldo] (EPI_BF16), fp32 slabs [splits, M, ldo] (EPI_F32_PARTIAL) or bf16 [M, ldo] SwiGLU of the
-// blocked gate/up rows (EPI_SWIGLU, splits = 1).  W e4m3fn [N, K] row-major, wscale fp32 [N];
-// K % 256 == 0, (K / 256) % splits == 0, N % (16 wpb) == 0, wpb in 4..8, M <= 64.
+// Same contract as mrsum_stream_gemm (epilogues BF16 / F32_PARTIAL / SWIGLU / RESID_SPLIT, deferred
+// RMSNorm operands) with W e4m3fn [N, K] row-major and wscale fp32 [N]; K % 256 == 0, (K / 256) % splits == 0.
 MRSUM_API int mrsum_stream_fp8(const void* x, int ldx, const void* W, const float* wscale, int N, int K, int M,
-                               void* out, int ldo, int epi, int splits, int wpb, hipStream_t s) {
+                               void* out, int ldo, int epi, int splits, int wpb, void* parts, int* counters,
+                               const float* ssq, int ssq_tiles, float eps, void* resid, int ldr, float* ssp,
+                               hipStream_t s) {
     if (M <= 0) return 0;
     if (wpb < 4 || wpb > 8 || M > 64 || K % KB8 || N % (16 * wpb) || splits < 1 || (K / KB8) % splits ||
-        epi < EPI_BF16 || epi > EPI_SWIGLU)
+        epi < EPI_BF16 || epi > EPI_RESID_SPLIT || epi == EPI_SWIGLU_SPLIT)
         return (int)hipErrorInvalidValue;
-    if (epi != EPI_F32_PARTIAL && splits != 1) return (int)hipErrorInvalidValue;
+    if (epi != EPI_F32_PARTIAL && epi != EPI_RESID_SPLIT && splits != 1) return (int)hipErrorInvalidValue;
+    if (epi == EPI_RESID_SPLIT && (!parts || !counters || !resid || !ssp || ldr % 4)) return (int)hipErrorInvalidValue;
+    if (ssq && (ssq_tiles <= 0 || ssq_tiles % (4 * SS_PARTS))) return (int)hipErrorInvalidValue;
+    NormArgs e;
+    e.ssq = ssq; e.ssq_tiles = ssq_tiles; e.inv_k = 1.f / (float)K; e.eps = eps;
+    e.resid = (bf16*)resid; e.ldr = ldr; e.ssp = ssp;
     const int kper = K / splits;
     const int mt = (M + 15) / 16;
     dim3 grid(N / (16 * wpb), splits), block(64 * wpb);
     auto X = (const bf16*)x;
     auto Wp = (const unsigned char*)W;
-#define L8(MT_, EPI_, WPB_) stream_fp8_kernel<MT_, EPI_, WPB_><<<grid, block, 0, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper)
+    auto P = (float*)parts;
+#define L8(MT_, EPI_, WPB_) \
+    stream_fp8_kernel<MT_, EPI_, WPB_><<<grid, block, 0, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper, P, counters, e)
 #define BY_WPB8(MT_, EPI_)                          \
     switch (wpb) {                                  \
         case 4: L8(MT_, EPI_, 4); break;            \
@@ -438,7 +585,8 @@ MRSUM_API int mrsum_stream_fp8(const void* x, int ldx, const void* W, const floa
 #define BY_EPI8(MT_)                                                      \
     if (epi == EPI_BF16) { BY_WPB8(MT_, EPI_BF16) }                       \
     else if (epi == EPI_F32_PARTIAL) { BY_WPB8(MT_, EPI_F32_PARTIAL) }    \
-    else { BY_WPB8(MT_, EPI_SWIGLU) }
+    else if (epi == EPI_SWIGLU) { BY_WPB8(MT_, EPI_SWIGLU) }              \
+    else { BY_WPB8(MT_, EPI_RESID_SPLIT) }
     switch (mt) {
         case 1: BY_EPI8(1); break;
         case 2: BY_EPI8(2); break;

@@ -19,7 +19,14 @@ One residual block (both phases)::
     o   = a @ wo^T  (+ TP all-reduce over RCCL)
     x   = add_rmsnorm(o, residual)   HIP (residual += o, fused)
     gu  = x @ wgu^T ; act = swiglu(gu) (HIP) ; dn = act @ wdown^T (+ all-reduce)
-    x   = add_rmsnorm(dn, residual, next norm weight)   HIP
+    x   = add_rmsnorm(dn, residual)  HIP
+
+RMSNorm gains are folded into the projection that consumes the normalised rows (``wqkv`` <- ln1,
+``wgu`` <- ln2, ``lm_head`` <- the final norm: W' = W diag(g), at load time, before any fp8
+quantisation), so every norm in the forward pass is unit-gain -- which lets decode defer the norm
+into the consumer GEMM's epilogue (ops.NormRows): on one GPU the o / down projections update the
+residual themselves and no separate add + RMSNorm kernel runs.  ``ln1`` / ``ln2`` / ``final_norm``
+keep the checkpoint's gains for export (engine/weights.save_hf un-folds them).
 """
 
 from __future__ import annotations
@@ -88,8 +95,8 @@ class LlamaModel:
         engine.weights.load_hf instead of the seeded random init.
 
         ``weight_dtype="fp8"``: the four projection matrices of every layer are stored as OCP e4m3fn
-        with per-output-row fp32 scales (ops.Fp8Weight) -- W8A16 MFMA kernels at decode sizes,
-        hipBLASLt fp8 (dynamic per-token activation scales) at prefill sizes.  Embedding, norms and
+        with per-output-row fp32 scales (ops.Fp8Weight) -- W8A16 MFMA kernels at decode sizes, the
+        fp8 MFMA GEMM (dynamic per-token activation scales) at prefill sizes.  Embedding, norms and
         the LM head stay bf16."""
         if weight_dtype not in ("bf16", "fp8"):
             raise ValueError("weight_dtype must be bf16 or fp8")
@@ -145,7 +152,7 @@ class LlamaModel:
             if self.weight_dtype == "fp8":
                 wqkv, wo, wgu, wd = (Fp8Weight.quantize(t) for t in (wqkv, wo, wgu, wd))
             self.layers.append(LayerWeights(ones(), wqkv, wo, ones(), wgu, wd))
-        self.final_norm = ones()
+        self.final_norm = ones()  # unit gains: nothing to fold into the consumers
         lm = _randn((c.vocab_size, c.hidden), std, seed, "lm_head", dev, dt)
         v = self.vocab_local
         self.lm_head = lm[r * v:(r + 1) * v].contiguous()
@@ -188,27 +195,26 @@ class LlamaModel:
     def run_layers(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor,
                    block_tables: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
                    attention: Callable[[int, torch.Tensor], torch.Tensor], decode: bool = False) -> torch.Tensor:
-        """Embedding -> all layers -> final norm; returns normed hidden [T, hidden].
+        """Embedding -> all layers -> final (unit-gain) norm; returns the normed hidden rows [T, hidden]
+        -- a tensor, or on the GPU decode path an ops.NormRows (the deferred norm of the last residual).
 
         Projections go through the fused blocks of ``ops`` (qkv_rope, proj_add_rmsnorm,
         gate_up_swiglu): at decode row counts they run on the MFMA weight-streaming kernels
-        with fused epilogues (split-K fp32 slabs reduced inside rope_kv_parts /
-        add_rmsnorm_parts, SwiGLU inside the gate_up GEMM), at prefill sizes on hipBLASLt.
+        with fused epilogues (split-K residual update + deferred RMSNorm, SwiGLU inside the gate_up
+        GEMM, RoPE + KV write inside decode attention), at prefill sizes on the 256 x 256 MFMA GEMM.
         """
         c = self.cfg
         residual = ops.embed(ids, self.embed)
-        x = ops.rmsnorm(residual, self.layers[0].ln1, c.rms_eps)
+        x = ops.rmsnorm(residual, None, c.rms_eps)  # gains folded into the consumer weights
         page = kcache.shape[3]
-        n = len(self.layers)
         ar = _TPReduce(self) if self.tp_size > 1 else None
         for i, lw in enumerate(self.layers):
-            nxt = self.layers[i + 1].ln1 if i + 1 < n else self.final_norm
             qkv = ops.qkv_rope(x, lw.wqkv, positions, seq_idx, block_tables, kcache[i], vcache[i], self.cos_sin,
                                self.hq, self.hkv, self.hd, page, defer=decode)
             a = attention(i, qkv)
-            x = ops.proj_add_rmsnorm(a, lw.wo, residual, lw.ln2, c.rms_eps, "o", ar)
+            x = ops.proj_add_rmsnorm(a, lw.wo, residual, None, c.rms_eps, "o", ar)
             act = ops.gate_up_swiglu(x, lw.wgu)
-            x = ops.proj_add_rmsnorm(act, lw.wdown, residual, nxt, c.rms_eps, "down", ar)
+            x = ops.proj_add_rmsnorm(act, lw.wdown, residual, None, c.rms_eps, "down", ar)
         return x
 
     def logits(self, x: torch.Tensor, gather: bool = True) -> torch.Tensor:
@@ -236,7 +242,7 @@ class LlamaModel:
         x = self.run_layers(ids, positions, seq_idx, block_tables, kcache, vcache, attention)
         if not logits:
             return None
-        return self.logits(x.index_select(0, last_rows), gather)
+        return self.logits(ops.rows(x).index_select(0, last_rows), gather)
 
     def decode(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, block_tables: torch.Tensor,
                kcache: torch.Tensor, vcache: torch.Tensor, workspace=None, gather: bool = True) -> torch.Tensor:

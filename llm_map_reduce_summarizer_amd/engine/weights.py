@@ -9,8 +9,9 @@ the reference needs real models, so the engine loads the standard Hugging Face L
 
 HF checkpoints already use the rotate-half RoPE pairing our kernels implement.  Tensors are read
 with ``safetensors`` (no pickle), sliced for this rank's tensor-parallel shard, fused into the
-engine layouts (QKV rows, [8 gate | 8 up] blocks) and optionally quantised to fp8.  ``save_hf``
-writes the inverse (used by tests and to export random-init models).
+engine layouts (QKV rows, [8 gate | 8 up] blocks), the RMSNorm gains folded into the projections
+that consume the normed rows (fold_gain; engine/model.py) and optionally quantised to fp8.
+``save_hf`` writes the inverse (used by tests and to export random-init models).
 """
 
 from __future__ import annotations
@@ -60,22 +61,39 @@ def load_hf(model, path: str) -> None:
     model.embed = put(get("model.embed_tokens.weight"))
     lm = get("lm_head.weight") if "lm_head.weight" in index else get("model.embed_tokens.weight")
     v = model.vocab_local
-    model.lm_head = put(lm[r * v:(r + 1) * v])
     model.final_norm = put(get("model.norm.weight"))
+    model.lm_head = put(fold_gain(lm[r * v:(r + 1) * v], model.final_norm))
     for i, lw in enumerate(model.layers):
         p = "model.layers.%d." % i
+        lw.ln1 = put(get(p + "input_layernorm.weight"))
+        lw.ln2 = put(get(p + "post_attention_layernorm.weight"))
         wq, wk, wv = (get(p + "self_attn.%s_proj.weight" % n) for n in ("q", "k", "v"))
         wqkv = torch.cat([wq[r * qs:(r + 1) * qs], wk[r * ks:(r + 1) * ks], wv[r * ks:(r + 1) * ks]])
         wo = get(p + "self_attn.o_proj.weight")[:, r * qs:(r + 1) * qs]
         wg, wu = get(p + "mlp.gate_proj.weight"), get(p + "mlp.up_proj.weight")
         wgu = interleave_gate_up(wg[r * f:(r + 1) * f], wu[r * f:(r + 1) * f])
         wd = get(p + "mlp.down_proj.weight")[:, r * f:(r + 1) * f]
-        mats = [put(t) for t in (wqkv, wo, wgu, wd)]
+        # norm gains folded into the consumer projections (engine/model.py), before fp8 quantisation
+        mats = [put(t) for t in (fold_gain(wqkv, lw.ln1), wo, fold_gain(wgu, lw.ln2), wd)]
         if model.weight_dtype == "fp8":
             mats = [Fp8Weight.quantize(t) for t in mats]
         lw.wqkv, lw.wo, lw.wgu, lw.wdown = mats
-        lw.ln1 = put(get(p + "input_layernorm.weight"))
-        lw.ln2 = put(get(p + "post_attention_layernorm.weight"))
+
+
+def fold_gain(w: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    """W diag(g) in fp32, one rounding to the weight dtype (identity for an all-ones gain)."""
+    g = g.to(w.device)
+    if bool((g == 1).all()):
+        return w
+    return (w.float() * g.float()).to(w.dtype)
+
+
+def unfold_gain(w: torch.Tensor, g: torch.Tensor) -> torch.Tensor:
+    """Inverse of fold_gain for export (exact for unit gains, else within one bf16 rounding)."""
+    g = g.to(w.device)
+    if bool((g == 1).all()):
+        return w
+    return (w.float() / g.float()).to(w.dtype)
 
 
 def _dense(t) -> torch.Tensor:
@@ -93,16 +111,16 @@ def save_hf(model, path: str) -> None:
     out: Dict[str, torch.Tensor] = {
         "model.embed_tokens.weight": model.embed,
         "model.norm.weight": model.final_norm,
-        "lm_head.weight": model.lm_head,
+        "lm_head.weight": unfold_gain(model.lm_head, model.final_norm),
     }
     for i, lw in enumerate(model.layers):
         p = "model.layers.%d." % i
-        wqkv = _dense(lw.wqkv)
+        wqkv = unfold_gain(_dense(lw.wqkv), lw.ln1)
         out[p + "self_attn.q_proj.weight"] = wqkv[:qs]
         out[p + "self_attn.k_proj.weight"] = wqkv[qs:qs + ks]
         out[p + "self_attn.v_proj.weight"] = wqkv[qs + ks:]
         out[p + "self_attn.o_proj.weight"] = _dense(lw.wo)
-        g, u = split_gate_up(_dense(lw.wgu).t())
+        g, u = split_gate_up(unfold_gain(_dense(lw.wgu), lw.ln2).t())
         out[p + "mlp.gate_proj.weight"] = g.t()
         out[p + "mlp.up_proj.weight"] = u.t()
         out[p + "mlp.down_proj.weight"] = _dense(lw.wdown)

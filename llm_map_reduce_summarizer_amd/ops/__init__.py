@@ -36,8 +36,53 @@ def _impl(t):
     return reference
 
 
+_UNIT = {}
+
+
+def unit_gain(hidden, device):
+    """A cached all-ones RMSNorm gain: the model folds its norm gains into the consumer projections
+    (engine/model.py), so every norm the forward pass runs is unit-gain."""
+    key = (hidden, str(device))
+    t = _UNIT.get(key)
+    if t is None:
+        t = _UNIT[key] = torch.ones(hidden, dtype=torch.bfloat16, device=device)
+    return t
+
+
 def rmsnorm(x, w, eps, out=None):
+    """``w`` None: unit gain."""
+    if w is None:
+        w = unit_gain(x.shape[-1], x.device)
     return _impl(x).rmsnorm(x, w, eps, out)
+
+
+class NormRows:
+    """Deferred RMSNorm of decode rows (GPU): ``h`` = the residual rows (bf16 [M, hidden], not normalised)
+    and ``ssq`` = fp32 [M, tiles] per-column-tile sums of squares of h written by the producing GEMM
+    (ops.hip.stream_resid).  A consumer GEMM on the stream kernel takes h as its input and scales its
+    product rows by rsqrt(mean(h^2) + eps) in the epilogue -- exact because the norm gains are folded
+    into the consumer weights (engine/model.py).  ``materialize`` runs the unit-gain RMSNorm instead
+    (consumers on other kernels).  Valid until the next producer updates the residual in place."""
+
+    def __init__(self, h, ssq, eps):
+        self.h, self.ssq, self.eps = h, ssq, eps
+
+    @property
+    def shape(self):
+        return self.h.shape
+
+    @property
+    def norm(self):
+        return (self.ssq, self.eps)
+
+    def materialize(self):
+        from . import hip
+        return hip.rmsnorm(self.h, unit_gain(self.h.shape[1], self.h.device), self.eps)
+
+
+def rows(x):
+    """Plain normalised rows of ``x`` (a tensor or a NormRows)."""
+    return x.materialize() if isinstance(x, NormRows) else x
 
 
 def add_rmsnorm(x, residual, w, eps, out=None):
@@ -61,7 +106,17 @@ def swiglu(gu, out=None):
 
 def linear(x, w):
     """x @ w^T (bf16).  GPU: MFMA weight-streaming kernels for decode shapes, the 256 x 256 MFMA GEMM
-    otherwise; ``w`` may be an Fp8Weight (W8A16 decode kernel / fp8 MFMA GEMM at prefill sizes)."""
+    otherwise; ``w`` may be an Fp8Weight (W8A16 decode kernel / fp8 MFMA GEMM at prefill sizes).
+    ``x`` may be a NormRows (the LM head after the last layer)."""
+    if isinstance(x, NormRows):
+        from . import hip
+        M, K = x.shape
+        if isinstance(w, Fp8Weight):
+            if hip.fp8_stream_cfg(M, w.shape[0], K, splits=1) is not None:
+                return hip.fp8_linear(x.h, w, norm=x.norm)
+        elif hip.linear_takes_norm(M, w.shape[0], K):
+            return hip.linear(x.h, w, norm=x.norm)
+        x = x.materialize()
     if isinstance(w, Fp8Weight):
         if _use_hip(x):
             from . import hip
@@ -150,7 +205,10 @@ def sample_tp(logits, st, tok_offset, max_reduce):
 
 def _plan_parts(hip, p, x, w, splits):
     if p[0] == "stream":
+        if isinstance(x, NormRows):
+            return hip.linear_parts(x.h, w, p[2], nt=p[1], kernel="stream", norm=x.norm)
         return hip.linear_parts(x, w, p[2], nt=p[1], kernel="stream")
+    x = rows(x)
     if p[0] == "lds":
         return hip.linear_parts(x, w, splits or p[1], kernel="lds")
     return hip.linear_parts(x, w, splits or p[2], nt=p[1])
@@ -161,7 +219,10 @@ def _fp8_parts(hip, x, w, role, splits):
     it fills the chip, else the register-streaming kernel with the bf16 plan shapes."""
     cfg = hip.stream_config_fp8(w.shape[0], w.shape[1], splits=splits, M=x.shape[0])
     if cfg is not None:
+        if isinstance(x, NormRows):
+            return hip.fp8_linear_parts(x.h, w, cfg[1], stream_wpb=cfg[0], norm=x.norm)
         return hip.fp8_linear_parts(x, w, cfg[1], stream_wpb=cfg[0])
+    x = rows(x)
     p = hip.plan(role, x.shape[0], w.shape[0], w.shape[1], stream=False)
     nt = p[1] if p[0] == "skinny" else 1
     s = splits or (p[2] if p[0] == "skinny" else (p[1] if p[0] == "lds" else 1))
@@ -192,8 +253,10 @@ def _defer_ok(hip, defer, x, hq, hkv, d, page):
 
 def qkv_rope(x, wqkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page, defer=False):
     """qkv = x @ wqkv^T, RoPE on Q/K, K/V into the paged cache; returns bf16 qkv rows -- or, with
-    ``defer`` on the GPU decode path, a QKVParts for attn_decode's fused RoPE + KV write."""
-    if _use_hip(x) and isinstance(wqkv, Fp8Weight):
+    ``defer`` on the GPU decode path, a QKVParts for attn_decode's fused RoPE + KV write.  ``x`` may
+    be a NormRows (deferred RMSNorm of the previous layer's down projection)."""
+    xt = x.h if isinstance(x, NormRows) else x
+    if _use_hip(xt) and isinstance(wqkv, Fp8Weight):
         from . import hip
         if x.shape[0] <= hip.SKINNY_MAX_M:
             parts = _fp8_parts(hip, x, wqkv, "qkv", None)
@@ -201,10 +264,10 @@ def qkv_rope(x, wqkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin,
                 return QKVParts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page)
             return hip.rope_kv_parts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d,
                                      page)
-        qkv = hip.fp8_linear(x, wqkv)
+        qkv = hip.fp8_linear(rows(x), wqkv)
         hip.rope_kv(qkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page)
         return qkv
-    if _use_hip(x):
+    if _use_hip(xt):
         from . import hip
         p = hip.plan("qkv", x.shape[0], wqkv.shape[0], wqkv.shape[1])
         if p[0] != "gemm":
@@ -213,7 +276,7 @@ def qkv_rope(x, wqkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin,
                 return QKVParts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page)
             return hip.rope_kv_parts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv,
                                      d, page)
-        qkv = hip.gemm(x, wqkv)
+        qkv = hip.gemm(rows(x), wqkv)
         hip.rope_kv(qkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page)
         return qkv
     qkv = reference.linear(x, wqkv)
@@ -230,12 +293,46 @@ def _fused_ar(all_reduce, rows, hidden):
     return f
 
 
-def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
-    """residual += a @ w^T (TP-all-reduced when ``all_reduce``); returns rmsnorm(residual) * ln.
+# The deferred norm trades a separate add + RMSNorm launch for a split-K last-arriver tail in the
+# producer: measured on one box (tools/ab_decode_old_new.sh, profiles/r2_deferred_norm_ab.jsonl) decode
+# steps at B=1 -1.5 %, B=10 -0.5 %, B=39 +1 % -- so it runs up to 16 rows.
+DEFER_NORM_MAX_M = 16
 
-    ``all_reduce`` is a callable summing a tensor over the TP group in place; when it also offers
-    ``add_rmsnorm``/``fused_ok`` (the model's P2P all-reduce) the decode path runs the projection's
-    split-K slabs straight into one fused all-reduce + residual add + RMSNorm kernel."""
+
+def _resid_cfg(hip, a, w, role):
+    """(wpb, S) of the deferred-RMSNorm producer (stream kernel, split-K last-arriver residual update) for
+    this decode projection, or None."""
+    M = a.shape[0]
+    if M > DEFER_NORM_MAX_M:
+        return None
+    if isinstance(w, Fp8Weight):
+        cfg = hip.fp8_stream_cfg(M, w.shape[0], w.shape[1])
+    else:
+        p = hip.plan(role, M, w.shape[0], w.shape[1])
+        cfg = p[1:] if p[0] == "stream" else None
+    if cfg is None or (w.shape[0] // (16 * cfg[0])) % 32:
+        return None
+    return cfg
+
+
+def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
+    """residual += a @ w^T (TP-all-reduced when ``all_reduce``); returns rmsnorm(residual) * ln (``ln``
+    None: unit gain, the model's folded-gain form).
+
+    GPU decode rows with a unit gain and no TP: the projection itself updates the residual (split-K
+    last-arriver epilogue) and the result is a NormRows -- the RMSNorm is deferred into the consumer
+    GEMM, so no separate add + RMSNorm kernel runs.  ``all_reduce`` is a callable summing a tensor over
+    the TP group in place; when it also offers ``add_rmsnorm``/``fused_ok`` (the model's P2P
+    all-reduce) the decode path runs the projection's split-K slabs straight into one fused
+    all-reduce + residual add + RMSNorm kernel."""
+    if _use_hip(a):
+        from . import hip
+        if ln is None and all_reduce is None and a.shape[0] <= hip.SKINNY_MAX_M:
+            cfg = _resid_cfg(hip, a, w, role)
+            if cfg is not None:
+                return NormRows(residual, hip.stream_resid(a, w, residual, cfg[0], cfg[1]), eps)
+    if ln is None:
+        ln = unit_gain(residual.shape[1], residual.device)
     if _use_hip(a) and isinstance(w, Fp8Weight):
         from . import hip
         if a.shape[0] <= hip.SKINNY_MAX_M:
@@ -273,16 +370,22 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
 
 
 def gate_up_swiglu(x, wgu):
-    """silu(gate) * up of the fused, [8 gate | 8 up]-blocked gate_up projection."""
-    if _use_hip(x) and isinstance(wgu, Fp8Weight):
+    """silu(gate) * up of the fused, [8 gate | 8 up]-blocked gate_up projection; ``x`` may be a
+    NormRows (deferred RMSNorm)."""
+    xt = x.h if isinstance(x, NormRows) else x
+    if _use_hip(xt) and isinstance(wgu, Fp8Weight):
         from . import hip
-        return hip.fp8_linear_swiglu(x, wgu)
-    if _use_hip(x):
+        if isinstance(x, NormRows) and hip.fp8_stream_cfg(x.shape[0], wgu.shape[0], x.shape[1], swiglu=True):
+            return hip.fp8_linear_swiglu(x.h, wgu, norm=x.norm)
+        return hip.fp8_linear_swiglu(rows(x), wgu)
+    if _use_hip(xt):
         from . import hip
         p = hip.plan("gate_up", x.shape[0], wgu.shape[0], wgu.shape[1])
+        nr = isinstance(x, NormRows) and p[0] in ("stream", "stream_split")
+        xin, norm = (x.h, x.norm) if nr else (rows(x), None)
         if p[0] == "stream":
-            return hip.linear_swiglu(x, wgu, kernel="stream", wpb=p[1])
+            return hip.linear_swiglu(xin, wgu, kernel="stream", wpb=p[1], norm=norm)
         if p[0] == "stream_split":
-            return hip.linear_swiglu(x, wgu, kernel="stream_split", wpb=p[1], splits=p[2])
-        return hip.linear_swiglu(x, wgu, kernel=p[0])
+            return hip.linear_swiglu(xin, wgu, kernel="stream_split", wpb=p[1], splits=p[2], norm=norm)
+        return hip.linear_swiglu(xin, wgu, kernel=p[0])
     return reference.swiglu(reference.linear(x, wgu))

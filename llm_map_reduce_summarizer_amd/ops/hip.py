@@ -16,6 +16,7 @@ from typing import Optional
 import torch
 
 from ._lib import kernels_lib
+from .reference import Fp8Weight
 
 _c_int, _c_float, _vp = ctypes.c_int, ctypes.c_float, ctypes.c_void_p
 
@@ -37,10 +38,10 @@ _SIGS = {
                                _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp],
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
-    "mrsum_stream_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
-    "mrsum_stream_gemm_swiglu_split": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _vp,
-                                       _vp, _vp],
-    "mrsum_stream_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
+    "mrsum_stream_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp,
+                          _vp, _c_int, _c_float, _vp, _c_int, _vp, _vp],
+    "mrsum_stream_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp,
+                         _vp, _c_int, _c_float, _vp, _c_int, _vp, _vp],
     "mrsum_skinny_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_quant_fp8_rows": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
@@ -312,11 +313,12 @@ def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
     groups = max(1, batch * hkv)
     splits = max(1, min(ATTN_SLOTS // groups, -(-pages // ATTN_PAGES_PER_SPLIT), 64))
     # measured (tools/bench_attn_decode.py; profiles/r2_attn_decode_splits_fused_sweep.jsonl at 4k,
-    # r2_attn_decode_splits_10k.jsonl): B=1 4k fused 16 splits 16.1 us vs 32 unfused 19.0, but B=1 10k
-    # 64 unfused 19.5 vs 16 fused 21.0 (a fused merge caps the splits, and long splits serialise);
-    # B=10 fused 4 splits 37.5 us vs 9 unfused 40.1 at 4k, equal at 10k; B=39 unfused 113 vs fused 116-118
+    # r2_attn_decode_splits_10k.jsonl, r2_attn_decode_b1_class0.jsonl): B=1 4k fused 16 splits 16.1-18.0 us
+    # vs 32-48 unfused 19.0-21.4, 6k fused 16 17.0 vs 47 unfused 19.9, but B=1 10k 64 unfused 19.5 vs 16
+    # fused 21.0 (a fused merge caps the splits, and long splits serialise); B=10 fused 4 splits 37.5 us
+    # vs 9 unfused 40.1 at 4k, equal at 10k; B=39 unfused 113 vs fused 116-118
     if groups <= 16:
-        fused = -(-pages // 16) <= 4
+        fused = -(-pages // 16) <= 6  # the <= 6k context class
         if fused:
             splits = min(splits, 16)
     else:
@@ -502,7 +504,7 @@ def gemm_fp8(xq: torch.Tensor, xs: torch.Tensor, w, out: Optional[torch.Tensor] 
 
 # ------------------------------------------------------------------ decode GEMMs (M <= 64)
 SKINNY_MAX_M = 64
-EPI_BF16, EPI_F32_PARTIAL, EPI_SWIGLU = 0, 1, 2
+EPI_BF16, EPI_F32_PARTIAL, EPI_SWIGLU, EPI_SWIGLU_SPLIT, EPI_RESID_SPLIT = 0, 1, 2, 3, 4
 
 
 def choose_splits(N: int, K: int, nt: int, target_wgs: int = 512, max_splits: int = 8) -> int:
@@ -546,9 +548,31 @@ def _skinny_lds(x, w, out, epi, splits, ldo, wpb=4):
     return out
 
 
-def _stream_gemm(x, w, out, epi, splits, ldo, wpb):
+def _norm_args(x, norm):
+    """(ssq ptr, tiles, eps) of a deferred-RMSNorm input (``norm`` = (ssq [M, tiles] fp32, eps)) or nulls."""
+    if norm is None:
+        return None, 0, 0.0
+    ssq, eps = norm
+    _req(ssq.is_cuda and ssq.dtype == torch.float32 and ssq.is_contiguous() and ssq.dim() == 2
+         and ssq.shape[0] == x.shape[0] and ssq.shape[1] % 32 == 0, "deferred norm: ssq must be fp32 [M, 32k]")
+    return _p(ssq), ssq.shape[1], float(eps)
+
+
+def _resid_args(x, N, epi, resid, ssp):
+    if epi != EPI_RESID_SPLIT:
+        return None, 0, None
+    M = x.shape[0]
+    _bf16_cuda(resid)
+    _rows_ok(resid)
+    _req(resid.shape == (M, N) and ssp is not None and ssp.dtype == torch.float32 and ssp.is_contiguous()
+         and ssp.dim() == 2 and ssp.shape[0] == M, "resid split: residual [M, N] bf16 and ssp fp32 [M, tiles]")
+    return _p(resid), resid.stride(0), _p(ssp)
+
+
+def _stream_gemm(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, norm=None, resid=None, ssp=None):
     """LDS-DMA weight-ring decode GEMM (csrc/kernels/stream_gemm.hip); same contract as _skinny_lds,
-    one 16*wpb-row tile per workgroup, ~one workgroup per CU."""
+    one 16*wpb-row tile per workgroup, ~one workgroup per CU.  ``norm``: deferred-RMSNorm input
+    (ssq, eps); EPI_RESID_SPLIT: residual += x @ w^T with per-tile row sums of squares into ``ssp``."""
     _bf16_cuda(x, w)
     _rows_ok(x)
     M, K = x.shape
@@ -557,17 +581,31 @@ def _stream_gemm(x, w, out, epi, splits, ldo, wpb):
     _req(1 <= M <= SKINNY_MAX_M and K % 128 == 0 and 4 <= wpb <= 8 and N % (16 * wpb) == 0
          and (K // 128) % splits == 0, "stream_gemm: unsupported shape M=%d N=%d K=%d S=%d wpb=%d"
          % (M, N, K, splits, wpb))
-    _check(_fn("mrsum_stream_gemm")(_p(x), x.stride(0), _p(w), N, K, M, _p(out), ldo, epi, splits, wpb,
-                                    _stream()), "stream_gemm")
+    if epi in (EPI_SWIGLU_SPLIT, EPI_RESID_SPLIT):
+        _req(parts is not None and parts.shape == (splits, M, N) and parts.dtype == torch.float32
+             and counters is not None and counters.numel() >= N // (16 * wpb), "stream_gemm: split-K scratch")
+    if epi == EPI_RESID_SPLIT:
+        _req(ssp.shape[1] == N // (16 * wpb), "stream_gemm: ssp tiles")
+    sq, tiles, eps = _norm_args(x, norm)
+    rp, ldr, sp = _resid_args(x, N, epi, resid, ssp)
+    _check(_fn("mrsum_stream_gemm")(_p(x), x.stride(0), _p(w), N, K, M, _p(out), ldo, epi, splits, wpb, _p(parts),
+                                    _p(counters), sq, tiles, eps, rp, ldr, sp, _stream()), "stream_gemm")
     return out
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def linear_takes_norm(M: int, N: int, K: int) -> bool:
+    """Whether ``linear`` of this shape runs on the stream kernel (the one that takes a deferred norm)."""
+    return 1 <= M <= SKINNY_MAX_M and K % 128 == 0 and stream_config(N, K, splits=1) is not None
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, norm=None) -> torch.Tensor:
     """x @ w^T, bf16 out: the 256 x 256-tile MFMA GEMM for M > 64 (or shapes the decode kernels do not
     take), else the LDS-DMA weight-ring stream GEMM when it fills the chip (the LM head), else the
-    register-streaming skinny kernel."""
+    register-streaming skinny kernel.  ``norm`` (stream shapes only, see linear_takes_norm): x holds
+    un-normalised residual rows, scaled by their deferred RMSNorm factor in the epilogue."""
     M, K = x.shape
     N = w.shape[0]
+    _req(norm is None or linear_takes_norm(M, N, K), "linear: a deferred norm needs a stream-GEMM shape")
     if M > SKINNY_MAX_M or M == 0 or K % 128:
         return gemm(x, w, out=out)
     if out is None:
@@ -575,7 +613,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
     _req(out.is_contiguous() and out.shape == (M, N), "linear: bad out")
     cfg = stream_config(N, K, splits=1)
     if cfg is not None:
-        return _stream_gemm(x, w, out, EPI_BF16, 1, N, cfg[0])
+        return _stream_gemm(x, w, out, EPI_BF16, 1, N, cfg[0], norm=norm)
     nt = 2 if N % 32 == 0 and N >= 16384 else 1
     if N % (16 * nt):
         return gemm(x, w, out=out)
@@ -583,7 +621,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None)
 
 
 def linear_parts(x: torch.Tensor, w: torch.Tensor, splits: Optional[int] = None,
-                 out: Optional[torch.Tensor] = None, nt: int = 1, kernel: str = "skinny") -> torch.Tensor:
+                 out: Optional[torch.Tensor] = None, nt: int = 1, kernel: str = "skinny", norm=None) -> torch.Tensor:
     """fp32 split-K slabs [S, M, N] of x @ w^T (summed by add_rmsnorm_parts / rope_kv_parts).
     kernel "skinny" (waves split k, nt 16-row tiles), "lds" (x staged in LDS, 64-row tiles) or "stream"
     (LDS-DMA weight ring; nt = waves per workgroup, 16 * nt-row tiles)."""
@@ -595,7 +633,8 @@ def linear_parts(x: torch.Tensor, w: torch.Tensor, splits: Optional[int] = None,
         out = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
     _req(out.is_contiguous() and out.shape == (splits, M, N) and out.dtype == torch.float32, "linear_parts: bad out")
     if kernel == "stream":
-        return _stream_gemm(x, w, out, EPI_F32_PARTIAL, splits, N, nt)
+        return _stream_gemm(x, w, out, EPI_F32_PARTIAL, splits, N, nt, norm=norm)
+    _req(norm is None, "linear_parts: a deferred norm needs the stream kernel")
     if kernel == "lds":
         return _skinny_lds(x, w, out, EPI_F32_PARTIAL, splits, N)
     return _skinny(x, w, out, EPI_F32_PARTIAL, nt, splits, N)
@@ -618,38 +657,53 @@ def _tile_counters(device, n: int) -> torch.Tensor:
     return t
 
 
-def stream_swiglu_split(x: torch.Tensor, w_gu: torch.Tensor, out: torch.Tensor, wpb: int, splits: int) -> torch.Tensor:
+def stream_swiglu_split(x: torch.Tensor, w_gu: torch.Tensor, out: torch.Tensor, wpb: int, splits: int,
+                        norm=None) -> torch.Tensor:
     """SwiGLU of the gate_up GEMM split-K over ``splits`` workgroups per column tile; the last split
     of a tile to finish sums the fp32 partial tiles and applies silu(gate) * up (stream_gemm.hip)."""
-    _bf16_cuda(x, w_gu)
-    _rows_ok(x)
     M, K = x.shape
     N = w_gu.shape[0]
-    _req(w_gu.is_contiguous() and w_gu.shape[1] == K, "stream_swiglu_split: weight must be [N, K] contiguous")
-    _req(1 <= M <= SKINNY_MAX_M and K % 128 == 0 and 4 <= wpb <= 8 and N % (16 * wpb) == 0 and splits >= 1
-         and (K // 128) % splits == 0 and out.is_contiguous() and out.shape == (M, N // 2),
-         "stream_swiglu_split: unsupported shape M=%d N=%d K=%d S=%d wpb=%d" % (M, N, K, splits, wpb))
+    _req(out.is_contiguous() and out.shape == (M, N // 2), "stream_swiglu_split: bad out")
     parts = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
     cnt = _tile_counters(x.device, N // (16 * wpb))
-    _check(_fn("mrsum_stream_gemm_swiglu_split")(_p(x), x.stride(0), _p(w_gu), N, K, M, _p(out), out.stride(0),
-                                                 splits, wpb, _p(parts), _p(cnt), _stream()), "stream_swiglu_split")
-    return out
+    return _stream_gemm(x, w_gu, out, EPI_SWIGLU_SPLIT, splits, out.stride(0), wpb, parts=parts, counters=cnt,
+                        norm=norm)
+
+
+def stream_resid(x: torch.Tensor, w, residual: torch.Tensor, wpb: int, splits: int) -> torch.Tensor:
+    """Deferred-RMSNorm producer: residual += x @ w^T (bf16 or Fp8Weight ``w``), split-K over ``splits``
+    workgroups per column tile, summed by the last to arrive; returns the fp32 [M, N / (16 wpb)] per-tile
+    row sums of squares of the new residual (the consumers' ``norm`` input)."""
+    M = x.shape[0]
+    fp8 = isinstance(w, Fp8Weight)
+    N = (w.q if fp8 else w).shape[0]
+    tiles = N // (16 * wpb)
+    parts = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
+    ssp = torch.empty(M, tiles, dtype=torch.float32, device=x.device)
+    cnt = _tile_counters(x.device, tiles)
+    if fp8:
+        _stream_fp8(x, w, None, EPI_RESID_SPLIT, splits, 0, wpb, parts=parts, counters=cnt, resid=residual, ssp=ssp)
+    else:
+        _stream_gemm(x, w, None, EPI_RESID_SPLIT, splits, 0, wpb, parts=parts, counters=cnt, resid=residual, ssp=ssp)
+    return ssp
 
 
 def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tensor] = None,
-                  kernel: str = "skinny", wpb: int = 4, splits: int = 1) -> torch.Tensor:
-    """silu(gate) * up straight out of the gate_up GEMM (blocked [8 gate | 8 up] weight rows)."""
+                  kernel: str = "skinny", wpb: int = 4, splits: int = 1, norm=None) -> torch.Tensor:
+    """silu(gate) * up straight out of the gate_up GEMM (blocked [8 gate | 8 up] weight rows);
+    ``norm``: deferred-RMSNorm input (stream kernels only)."""
     M = x.shape[0]
     F2 = w_gu.shape[0]
+    _req(norm is None or kernel in ("stream", "stream_split"), "linear_swiglu: a deferred norm needs the stream kernel")
     if M > SKINNY_MAX_M or kernel == "gemm":
         return gemm(x, w_gu, out=out, swiglu=True)
     if out is None:
         out = torch.empty(M, F2 // 2, dtype=x.dtype, device=x.device)
     _req(out.is_contiguous() and out.shape == (M, F2 // 2), "linear_swiglu: bad out")
     if kernel == "stream":
-        return _stream_gemm(x, w_gu, out, EPI_SWIGLU, 1, F2 // 2, wpb)
+        return _stream_gemm(x, w_gu, out, EPI_SWIGLU, 1, F2 // 2, wpb, norm=norm)
     if kernel == "stream_split":
-        return stream_swiglu_split(x, w_gu, out, wpb, splits)
+        return stream_swiglu_split(x, w_gu, out, wpb, splits, norm=norm)
     if kernel == "lds":
         return _skinny_lds(x, w_gu, out, EPI_SWIGLU, 1, F2 // 2)
     return _skinny(x, w_gu, out, EPI_SWIGLU, 1, 1, F2 // 2)
@@ -794,8 +848,9 @@ def stream_config_fp8(N: int, K: int, swiglu: bool = False, splits: Optional[int
     return stream_config(N, K // 2, swiglu=swiglu, splits=splits)  # K/256 slots == (K/2)/128 blocks
 
 
-def _stream_fp8(x, w, out, epi, splits, ldo, wpb):
-    """fp8 (e4m3fn, per-row scale) LDS-DMA weight-ring decode GEMM (stream_gemm.hip stream_fp8_kernel)."""
+def _stream_fp8(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, norm=None, resid=None, ssp=None):
+    """fp8 (e4m3fn, per-row scale) LDS-DMA weight-ring decode GEMM (stream_gemm.hip stream_fp8_kernel);
+    the epilogues / deferred-RMSNorm operands of _stream_gemm."""
     _bf16_cuda(x)
     _rows_ok(x)
     M, K = x.shape
@@ -804,48 +859,66 @@ def _stream_fp8(x, w, out, epi, splits, ldo, wpb):
          "stream_fp8: weight must be e4m3fn [N, K] contiguous")
     _req(w.scale.dtype == torch.float32 and w.scale.numel() == N and w.scale.is_contiguous(), "stream_fp8: scale")
     _req(1 <= M <= SKINNY_MAX_M and K % 256 == 0 and 4 <= wpb <= 8 and N % (16 * wpb) == 0
-         and (K // 256) % splits == 0, "stream_fp8: unsupported shape M=%d N=%d K=%d S=%d wpb=%d"
-         % (M, N, K, splits, wpb))
+         and (K // 256) % splits == 0 and epi != EPI_SWIGLU_SPLIT, "stream_fp8: unsupported shape M=%d N=%d K=%d S=%d "
+         "wpb=%d" % (M, N, K, splits, wpb))
+    if epi == EPI_RESID_SPLIT:
+        _req(parts is not None and parts.shape == (splits, M, N) and parts.dtype == torch.float32
+             and counters is not None and counters.numel() >= N // (16 * wpb) and ssp.shape[1] == N // (16 * wpb),
+             "stream_fp8: split-K scratch")
+    sq, tiles, eps = _norm_args(x, norm)
+    rp, ldr, sp = _resid_args(x, N, epi, resid, ssp)
     _check(_fn("mrsum_stream_fp8")(_p(x), x.stride(0), _p(w.q), _p(w.scale), N, K, M, _p(out), ldo, epi, splits, wpb,
-                                   _stream()), "stream_fp8")
+                                   _p(parts), _p(counters), sq, tiles, eps, rp, ldr, sp, _stream()), "stream_fp8")
     return out
 
 
-def fp8_linear(x: torch.Tensor, w, swiglu: bool = False) -> torch.Tensor:
+def fp8_stream_cfg(M: int, N: int, K: int, swiglu: bool = False, splits: Optional[int] = None):
+    """(wpb, S) of the fp8 stream kernel for a decode shape, or None (register-streaming / fp8 GEMM)."""
+    if not 1 <= M <= SKINNY_MAX_M:
+        return None
+    return stream_config_fp8(N, K, swiglu=swiglu, splits=splits, M=M)
+
+
+def fp8_linear(x: torch.Tensor, w, swiglu: bool = False, norm=None) -> torch.Tensor:
     """x @ (scale * W8)^T for any M: MFMA W8A16 weight-streaming kernel at decode sizes; at prefill sizes
     row-wise e4m3fn activation quantisation + the fp8 MFMA GEMM (gemm.hip, per-row activation x
     per-row weight scales in the epilogue)."""
     M = x.shape[0]
     N = w.q.shape[0]
+    _req(norm is None or (not swiglu and fp8_stream_cfg(M, N, x.shape[1], splits=1) is not None),
+         "fp8_linear: a deferred norm needs the stream kernel")
     if M <= SKINNY_MAX_M:
         out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
         cfg = stream_config_fp8(N, x.shape[1], splits=1, M=M)
         if cfg is not None:
-            return _stream_fp8(x, w, out, EPI_BF16, 1, N, cfg[0])
+            return _stream_fp8(x, w, out, EPI_BF16, 1, N, cfg[0], norm=norm)
         nt = 2 if N % 32 == 0 and N >= 16384 else 1
         return _skinny_fp8(x, w, out, EPI_BF16, nt, 1, N)
     xq, xs = quant_fp8_rows(x)
     return gemm_fp8(xq, xs, w, swiglu=swiglu)
 
 
-def fp8_linear_parts(x: torch.Tensor, w, splits: int, nt: int = 1, stream_wpb: Optional[int] = None) -> torch.Tensor:
+def fp8_linear_parts(x: torch.Tensor, w, splits: int, nt: int = 1, stream_wpb: Optional[int] = None,
+                     norm=None) -> torch.Tensor:
     """fp32 split-K slabs [splits, M, N] of x @ (scale * W8)^T: the fp8 stream GEMM when ``stream_wpb`` is
-    given (its own split count), else the register-streaming kernel."""
+    given (its own split count; ``norm``: deferred-RMSNorm input), else the register-streaming kernel."""
     M, K = x.shape
     N = w.q.shape[0]
     out = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
     if stream_wpb is not None:
-        return _stream_fp8(x, w, out, EPI_F32_PARTIAL, splits, N, stream_wpb)
+        return _stream_fp8(x, w, out, EPI_F32_PARTIAL, splits, N, stream_wpb, norm=norm)
+    _req(norm is None, "fp8_linear_parts: a deferred norm needs the stream kernel")
     return _skinny_fp8(x, w, out, EPI_F32_PARTIAL, nt, splits, N)
 
 
-def fp8_linear_swiglu(x: torch.Tensor, w) -> torch.Tensor:
+def fp8_linear_swiglu(x: torch.Tensor, w, norm=None) -> torch.Tensor:
     M = x.shape[0]
     F2 = w.q.shape[0]
+    cfg = fp8_stream_cfg(M, F2, x.shape[1], swiglu=True)
+    _req(norm is None or cfg is not None, "fp8_linear_swiglu: a deferred norm needs the stream kernel")
     if M > SKINNY_MAX_M:
         return fp8_linear(x, w, swiglu=True)
     out = torch.empty(M, F2 // 2, dtype=torch.bfloat16, device=x.device)
-    cfg = stream_config_fp8(F2, x.shape[1], swiglu=True, M=M)
     if cfg is not None:
-        return _stream_fp8(x, w, out, EPI_SWIGLU, 1, F2 // 2, cfg[0])
+        return _stream_fp8(x, w, out, EPI_SWIGLU, 1, F2 // 2, cfg[0], norm=norm)
     return _skinny_fp8(x, w, out, EPI_SWIGLU, 1, 1, F2 // 2)

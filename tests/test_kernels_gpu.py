@@ -514,3 +514,117 @@ def test_tp_shard_decode_blocks(tp, M):
     d1 = ops.proj_add_rmsnorm(act2, wd, r1.copy_(x), ln, 1e-5, "down")
     d2 = reference.add_rmsnorm(reference.linear(act2, wd), r2.copy_(x), ln, 1e-5)
     _close(d1, d2, 5e-2, 5e-2)
+
+
+@pytest.mark.parametrize("M", [1, 39, 64])
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("N,K,wpb,S", [(4096, 4096, 4, 4), (4096, 14336, 4, 4), (2048, 1024, 8, 2), (4096, 2048, 4, 1)])
+def test_stream_resid_and_norm_consumer(M, fp8, N, K, wpb, S):
+    """The deferred-RMSNorm kernels at every decode M (ops uses them up to DEFER_NORM_MAX_M rows): the
+    split-K residual-update producer (bf16 / fp8 weights) vs fp32, its per-tile sums of squares, and a
+    stream consumer (fp32 slabs) scaling its rows by the deferred norm."""
+    from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight
+    if fp8 and K % 256:
+        pytest.skip("fp8 stream slots are 256 wide")
+    x = _rand(M, K, seed=100)
+    w = _rand(N, K, scale=0.02, seed=101)
+    wq = Fp8Weight.quantize(w) if fp8 else w
+    w32 = wq.dequant() if fp8 else w.float()
+    res0 = _rand(M, N, seed=102)
+    res = res0.clone()
+    ssp = hip.stream_resid(x, wq, res, wpb, S)
+    ref = (res0.float() + x.float() @ w32.t()).to(torch.bfloat16)
+    _close(res, ref, 2e-2, 2e-2)
+    tiles = N // (16 * wpb)
+    _close(ssp, res.float().pow(2).view(M, tiles, 16 * wpb).sum(-1), 1e-3, 1e-3)
+    if tiles % 32 == 0:  # consumer: rows of ``res`` normalised through the deferred norm
+        w2 = _rand(1024, N, scale=0.02, seed=103)
+        parts = torch.empty(2, M, 1024, dtype=torch.float32, device=DEV)
+        hip._stream_gemm(res, w2, parts, hip.EPI_F32_PARTIAL, 2, 1024, 4, norm=(ssp, 1e-5))
+        hf = res.float()
+        xn = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5)
+        _close(parts.sum(0), xn @ w2.float().t(), 2e-3, 2e-3)
+    assert all(int(t.abs().sum()) == 0 for t in hip._TILE_COUNTERS.values())
+
+
+@pytest.mark.parametrize("M", [1, 10, 16])
+@pytest.mark.parametrize("fp8", [False, True])
+def test_deferred_norm_decode_layer(M, fp8):
+    """Deferred RMSNorm through a Llama-3-8B decode layer (TP=1, unit gains as after folding): the o / down
+    projections update the residual in their split-K last-arriver epilogue and return an ops.NormRows
+    (per-tile sums of squares); qkv (+ fused RoPE attention), gate_up + SwiGLU and the LM head scale their
+    product rows by the deferred norm -- each against the fp32 reference of the plain composition
+    (add + RMSNorm, then the GEMM); a captured hipGraph replays it with re-armed tickets."""
+    from llm_map_reduce_summarizer_amd import ops
+    from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight
+    hid, hd, page, hq, hkv, ffn, eps = 4096, 128, 64, 32, 8, 14336, 1e-5
+    sc = 1.0 / math.sqrt(hd)
+    q8 = (lambda t: Fp8Weight.quantize(t)) if fp8 else (lambda t: t)
+    w32 = (lambda w: w.dequant()) if fp8 else (lambda w: w.float())  # exact fp8 x scale weights
+    x0 = _rand(M, hid, seed=90)
+    a = _rand(M, hq * hd, seed=91)
+    wo, wd = q8(_rand(hid, hq * hd, scale=0.02, seed=92)), q8(_rand(hid, ffn, scale=0.02, seed=93))
+    wgu, wqkv = q8(_rand(2 * ffn, hid, scale=0.02, seed=94)), q8(_rand((hq + 2 * hkv) * hd, hid, scale=0.02, seed=95))
+    head = _rand(16384, hid, scale=0.02, seed=96)
+    one = torch.ones(hid, dtype=torch.bfloat16, device=DEV)
+
+    def rms32(h):  # the consumer sees the un-rounded normalised rows: the fp32 oracle of the deferred norm
+        hf = h.float()
+        return hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + eps)
+
+    def swiglu32(gu):
+        gg, uu = reference.split_gate_up(gu)
+        return gg * torch.sigmoid(gg) * uu
+    # o projection -> NormRows; residual and the per-tile sums of squares
+    r1, r2 = x0.clone(), x0.clone()
+    nr = ops.proj_add_rmsnorm(a, wo, r1, None, eps, "o")
+    assert isinstance(nr, ops.NormRows) and nr.h is r1
+    h2 = reference.add_rmsnorm(reference.linear(a, wo), r2, one, eps)
+    _close(r1, r2, 2e-2, 2e-2)
+    tiles = nr.ssq.shape[1]
+    _close(nr.ssq, r1.float().pow(2).view(M, tiles, hid // tiles).sum(-1), 1e-3, 1e-3)
+    _close(nr.materialize(), h2, 3e-2, 3e-2)
+    # gate_up + SwiGLU consumes the deferred norm
+    # a consumer on the stream kernel takes the deferred norm (fp32 oracle); others get materialised bf16 rows
+    takes = hip.fp8_stream_cfg(M, 2 * ffn, hid, swiglu=True) is not None if fp8 else \
+        hip.plan("gate_up", M, 2 * ffn, hid)[0] in ("stream", "stream_split")
+    _close(ops.gate_up_swiglu(nr, wgu), swiglu32((rms32(r2) if takes else h2.float()) @ w32(wgu).t()),
+           3e-2, 5e-2)
+    act2 = reference.swiglu(reference.linear(h2, wgu))
+    # down -> NormRows -> next layer's qkv + fused RoPE attention, and the LM head
+    r1.copy_(x0)
+    r2.copy_(x0)
+    nr2 = ops.proj_add_rmsnorm(act2, wd, r1, None, eps, "down")
+    h3 = reference.add_rmsnorm(reference.linear(act2, wd), r2, one, eps)
+    _close(r1, r2, 2e-2, 2e-2)
+    g = torch.Generator().manual_seed(97)
+    k0 = torch.randn(M * 3 + 1, hkv, page, hd, generator=g).to(torch.bfloat16)
+    v0 = torch.randn(M * 3 + 1, hkv, page, hd, generator=g).to(torch.bfloat16)
+    bt = (1 + torch.arange(M * 3, dtype=torch.int32).view(M, 3)).to(DEV)
+    pos = torch.tensor([(41 * i) % 190 for i in range(M)], dtype=torch.int32, device=DEV)
+    sidx = torch.arange(M, dtype=torch.int32, device=DEV)
+    cs = reference.rope_cos_sin(4096, hd, 500000.0, DEV)
+    k1, v1, k2, v2 = k0.clone().to(DEV), v0.clone().to(DEV), k0.clone().to(DEV), v0.clone().to(DEV)
+    q1 = ops.qkv_rope(nr2, wqkv, pos, sidx, bt, k1, v1, cs, hq, hkv, hd, page, defer=True)
+    at1 = ops.attn_decode(q1, k1, v1, bt, pos, hq, hkv, hd, page, sc)
+    qkv2 = (rms32(r2) @ w32(wqkv).t()).to(torch.bfloat16)
+    reference.rope_kv(qkv2, pos, sidx, bt, k2, v2, cs, hq, hkv, hd, page)
+    _close(at1, reference.attn_decode(qkv2, k2, v2, bt, pos, hq, hkv, hd, page, sc), 3e-2, 5e-2)
+    _close(ops.linear(nr2, head), rms32(r2) @ head.float().t(), 3e-2, 5e-2)
+    _close(nr2.materialize(), h3, 3e-2, 3e-2)
+    # hipGraph: capture producer + consumer once, replay from the same residual -> same output
+    r1.copy_(x0)
+    out = {}
+    graph = torch.cuda.CUDAGraph()
+    ops.gate_up_swiglu(ops.proj_add_rmsnorm(a, wo, r1, None, eps, "o"), wgu)  # tickets / buffers before capture
+    with torch.cuda.graph(graph):
+        out["act"] = ops.gate_up_swiglu(ops.proj_add_rmsnorm(a, wo, r1, None, eps, "o"), wgu)
+    r2.copy_(x0)
+    reference.add_rmsnorm(reference.linear(a, wo), r2, one, eps)
+    ref = swiglu32((rms32(r2) if takes else rms32(r2).to(torch.bfloat16).float()) @ w32(wgu).t())
+    for _ in range(3):
+        r1.copy_(x0)
+        graph.replay()
+        torch.cuda.synchronize()
+        _close(out["act"], ref, 3e-2, 5e-2)
+    assert all(int(t.abs().sum()) == 0 for t in hip._TILE_COUNTERS.values())
