@@ -312,6 +312,11 @@ def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
     pages = max(1, -(-max_ctx // 64))
     groups = max(1, batch * hkv)
     splits = max(1, min(ATTN_SLOTS // groups, -(-pages // ATTN_PAGES_PER_SPLIT), 64))
+    if pages <= 96:
+        # the <= 6k context class (profiles/r2_attn_decode_split_sweep_4k.jsonl, B = 2..39 x splits 2..16; TP=4 / 8 shard head counts: r2_attn_decode_split_sweep_tp_shards_4k.jsonl):
+        # best at ~one workgroup per CU for small batches (B=5: 6 splits 22.6 us vs 4 25.0; B=10: 3 splits
+        # 33.4 vs 4 38.7) and 3 splits from 80 groups up (B=20 60.2 vs 65.3, B=39 111.9 vs 113.9)
+        splits = max(1, min(max(3, N_CU // groups), -(-pages // ATTN_PAGES_PER_SPLIT), 64))
     # measured (tools/bench_attn_decode.py; profiles/r2_attn_decode_splits_fused_sweep.jsonl at 4k,
     # r2_attn_decode_splits_10k.jsonl, r2_attn_decode_b1_class0.jsonl): B=1 4k fused 16 splits 16.1-18.0 us
     # vs 32-48 unfused 19.0-21.4, 6k fused 16 17.0 vs 47 unfused 19.9, but B=1 10k 64 unfused 19.5 vs 16
@@ -324,7 +329,7 @@ def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
     else:
         fused = groups <= 128
         if fused:
-            splits = min(splits, 4)
+            splits = min(splits, 8 if pages <= 96 else 4)  # B=5 at 4k: 6 splits fused 22.6 us, unfused 23.3
     return splits, fused
 
 

@@ -26,9 +26,11 @@ def main():
     ap.add_argument("--layers", type=int, default=8)
     ap.add_argument("--iters", type=int, default=32)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--hkv", type=int, default=8, help="kv heads (q heads = 4 x): 8 = TP=1, 2 / 1 = TP=4 / 8 shard")
     a = ap.parse_args()
     dev = "cuda:0"
-    hq, hkv, d, page = 32, 8, 128, 64
+    hkv, d, page = a.hkv, 128, 64
+    hq = 4 * hkv
     for B in (int(b) for b in a.batches.split(",")):
         ctx = a.ctx
         npg = -(-ctx // page)
@@ -66,7 +68,7 @@ def main():
         for (sp, s, fused), ts in res.items():
             ts.sort()
             us = ts[len(ts) // 2]
-            print(json.dumps({"B": B, "ctx": ctx, "splits": s, "plan": sp, "fused": fused, "us": round(us, 2),
+            print(json.dumps({"B": B, "hkv": hkv, "ctx": ctx, "splits": s, "plan": sp, "fused": fused, "us": round(us, 2),
                               "TBps": round(gb / us * 1e6 / 1e3, 2)}), flush=True)
         del caches
 
