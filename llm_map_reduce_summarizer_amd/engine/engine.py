@@ -26,6 +26,7 @@ import math
 import os
 import time
 from dataclasses import dataclass, field
+from types import SimpleNamespace
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -222,6 +223,7 @@ class LLMEngine:
             self._prefill_pass(seqs, [(0, len(s.prompt)) for s in seqs], paged=self.paged_prefill)
             return
         rounds = max(-(-len(s.prompt) // chunk) for s in seqs)
+        passes = []
         for r in range(rounds):
             k = rounds - 1 - r  # slices still to come after this one
             part, spans = [], []
@@ -231,12 +233,21 @@ class LLMEngine:
                 if end > 0:
                     part.append(s)
                     spans.append((max(0, end - chunk), end))
-            self._prefill_pass(part, spans, paged=True, final=(k == 0))
+            passes.append((part, spans))
             self.stats["prefill_slices"] = self.stats.get("prefill_slices", 0) + len(part)
+        if self.model.tp_size > 1:
+            # tensor parallel: all passes layer-major, each pass's all-reduces under the next one's GEMMs
+            inputs = [self._pass_inputs(part, spans, paged=True) for part, spans in passes]
+            logits = self.model.prefill_passes(inputs, self.state.block_tables, self.kv.k, self.kv.v,
+                                               gather=not self.model.tp_sampling)
+            self.stats["prefill_tokens"] += sum(int(x.ids.numel()) for x in inputs)
+            self._sample_first(passes[-1][0], logits)
+            return
+        for r, (part, spans) in enumerate(passes):
+            self._prefill_pass(part, spans, paged=True, final=(r == rounds - 1))
 
-    def _prefill_pass(self, seqs: List[_Seq], spans, paged: bool, final: bool = True) -> None:
-        """One packed forward over prompt slices ``spans`` [(start, end)] of ``seqs``; on the final pass,
-        sample each sequence's first token from its last row."""
+    def _pass_inputs(self, seqs: List[_Seq], spans, paged: bool):
+        """Device inputs of one packed forward over prompt slices ``spans`` [(start, end)] of ``seqs``."""
         st, dev = self.state, self.device
         ids, pos, sidx, cu, last, lens = [], [], [], [0], [], []
         for s, (b, e) in zip(seqs, spans):
@@ -246,10 +257,7 @@ class LLMEngine:
             cu.append(cu[-1] + e - b)
             last.append(cu[-1] - 1)
             lens.append(e - b)
-        T = len(ids)
         h = lambda x: torch.tensor(x, dtype=torch.int32).to(dev, non_blocking=True)  # noqa: E731
-        ids_t, pos_t, sidx_t, cu_t = h(ids), h(pos), h(sidx), h(cu)
-        last_t = torch.tensor(last, dtype=torch.long).to(dev, non_blocking=True)
         items = None
         if dev.type == "cuda":
             from ..ops.hip import prefill_items
@@ -259,17 +267,29 @@ class LLMEngine:
             slots = [s.slot for s in seqs]
             pre = [b for b, _ in spans]
             pp = ops.PagedPrefill(st.block_tables, h(slots), h(pre), slots, pre)
-        tp_s = self.model.tp_sampling
-        logits = self.model.prefill(ids_t, pos_t, sidx_t, cu_t, last_t, st.block_tables, self.kv.k, self.kv.v,
-                                    seqlens=lens, items=items, gather=not tp_s, paged=pp, logits=final)
-        self.stats["prefill_tokens"] += T
-        if not final:
-            return
-        first = seqs[0].slot
-        # sampling of the first generated token: position of the fed token = prompt_len - 1
-        v = st.view(first, len(seqs))
-        v.positions.copy_(h([len(s.prompt) - 1 for s in seqs]))
+        return SimpleNamespace(ids=h(ids), positions=h(pos), seq_idx=h(sidx), cu_seqlens=h(cu),
+                               last_rows=torch.tensor(last, dtype=torch.long).to(dev, non_blocking=True),
+                               seqlens=lens, items=items, paged=pp)
+
+    def _sample_first(self, seqs: List[_Seq], logits: torch.Tensor) -> None:
+        """Sample every sequence's first generated token from its prompt's last row (fed position
+        prompt_len - 1); ``seqs`` occupy consecutive slots."""
+        st = self.state
+        v = st.view(seqs[0].slot, len(seqs))
+        v.positions.copy_(torch.tensor([len(s.prompt) - 1 for s in seqs], dtype=torch.int32).to(
+            self.device, non_blocking=True))
         self._sample(logits, v)
+
+    def _prefill_pass(self, seqs: List[_Seq], spans, paged: bool, final: bool = True) -> None:
+        """One packed forward over prompt slices ``spans`` [(start, end)] of ``seqs``; on the final pass,
+        sample each sequence's first token from its last row."""
+        x = self._pass_inputs(seqs, spans, paged)
+        logits = self.model.prefill(x.ids, x.positions, x.seq_idx, x.cu_seqlens, x.last_rows, self.state.block_tables,
+                                    self.kv.k, self.kv.v, seqlens=x.seqlens, items=x.items,
+                                    gather=not self.model.tp_sampling, paged=x.paged, logits=final)
+        self.stats["prefill_tokens"] += int(x.ids.numel())
+        if final:
+            self._sample_first(seqs, logits)
 
     # ------------------------------------------------------------------ decode
     def _sample(self, logits: torch.Tensor, st_view) -> None:

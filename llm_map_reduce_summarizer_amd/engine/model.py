@@ -178,6 +178,17 @@ class LlamaModel:
                 torch.distributed.all_reduce(t, group=self.tp_group)
         return t
 
+    def _all_reduce_async(self, t: torch.Tensor):
+        """Start the TP sum of ``t``; returns a handle whose ``wait()`` orders later work on the current stream
+        after it (RCCL runs on its own stream, so compute issued before the wait overlaps it), or None when
+        the sum already happened (the P2P kernel for small messages, runs in stream order)."""
+        if self.tp_size == 1:
+            return None
+        if self.custom_ar is not None and self.custom_ar.fits(t):
+            self.custom_ar.all_reduce(t)
+            return None
+        return torch.distributed.all_reduce(t, group=self.tp_group, async_op=True)
+
     @property
     def tp_sampling(self) -> bool:
         """Sample from the local vocab shard + 8-byte key max instead of gathering the logits."""
@@ -243,6 +254,54 @@ class LlamaModel:
         if not logits:
             return None
         return self.logits(ops.rows(x).index_select(0, last_rows), gather)
+
+    def prefill_passes(self, passes, block_tables: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
+                       gather: bool = True) -> torch.Tensor:
+        """Chunked prefill of a tensor-parallel engine with the all-reduces under compute: the packed passes
+        (``passes``: objects with ids, positions, seq_idx, cu_seqlens, last_rows, seqlens, items, paged --
+        the slices of the same prompts, in order) run LAYER-MAJOR: at every layer each pass's attention
+        block is issued, its o-projection all-reduce started on the RCCL stream, and the next pass's
+        attention block issued before the first pass waits for its sum; the MLP half likewise.  Pass p+1's
+        attention reads pass p's K/V of the same layer, which its QKV stage wrote earlier in stream order.
+        All but the last pass's all-reduces overlap another pass's GEMMs (reference
+        result_aggregator.py:346-355 is the single long final-reduce call this serves).  Returns the logits
+        of the last pass's last rows."""
+        c = self.cfg
+        eps = c.rms_eps
+        page = kcache.shape[3]
+        st = []
+        for p in passes:
+            res = ops.embed(p.ids, self.embed)
+            st.append({"res": res, "x": ops.rmsnorm(res, None, eps)})
+
+        def wait(h):
+            if h is not None:
+                h.wait()
+
+        for i, lw in enumerate(self.layers):
+            for p, s in zip(passes, st):
+                if "w2" in s:  # previous layer's down-projection sum (overlapped with the other passes' MLPs)
+                    wait(s.pop("w2"))
+                    s["x"] = ops.add_rmsnorm(s.pop("d"), s["res"], None, eps)
+                qkv = ops.qkv_rope(s["x"], lw.wqkv, p.positions, p.seq_idx, block_tables, kcache[i], vcache[i],
+                                   self.cos_sin, self.hq, self.hkv, self.hd, page)
+                kw = {"seqlens": p.seqlens, "items": p.items} if qkv.is_cuda else {}
+                pp = p.paged.layer(kcache[i], vcache[i]) if p.paged is not None else None
+                a = ops.attn_prefill(qkv, p.cu_seqlens, self.hq, self.hkv, self.hd, self.scale, paged=pp, **kw)
+                s["o"] = ops.linear(a, lw.wo)
+                s["w1"] = self._all_reduce_async(s["o"])
+            for s in st:
+                wait(s.pop("w1"))
+                x = ops.add_rmsnorm(s.pop("o"), s["res"], None, eps)
+                act = ops.gate_up_swiglu(x, lw.wgu)
+                s["d"] = ops.linear(act, lw.wdown)
+                s["w2"] = self._all_reduce_async(s["d"])
+        last, s = passes[-1], st[-1]
+        for t in st[:-1]:
+            wait(t.pop("w2"))
+        wait(s.pop("w2"))
+        x = ops.add_rmsnorm(s.pop("d"), s["res"], None, eps)
+        return self.logits(x.index_select(0, last.last_rows), gather)
 
     def decode(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, block_tables: torch.Tensor,
                kcache: torch.Tensor, vcache: torch.Tensor, workspace=None, gather: bool = True) -> torch.Tensor:

@@ -274,7 +274,7 @@ class LocalEngineProvider(Provider):
         d = plan.ModelDims.of(self.model_config(), 1.0 if self._engine_options.get("weight_dtype") == "fp8" else 2.0)
         hw = self.hw or plan.HWModel()
         lens = [len(p) for p in prompts]
-        return plan.handoff_prefill_s(d, hw, lens, self.par.world) < plan.prefill_s(d, hw, sum(lens), self.par.world)
+        return plan.handoff_prefill_s(d, hw, lens, self.par.world) < plan.prefill_s(d, hw, sum(lens), self.par.world, max(lens))
 
     def _handoff(self, prompts: Sequence[Sequence[int]], sp) -> Dict[int, Any]:
         """Disaggregated prefill for a TP stage: every rank prefills its LPT share of the prompts on

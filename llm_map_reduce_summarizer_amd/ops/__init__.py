@@ -86,6 +86,9 @@ def rows(x):
 
 
 def add_rmsnorm(x, residual, w, eps, out=None):
+    """residual += x; returns rmsnorm(residual) * w (``w`` None: unit gain)."""
+    if w is None:
+        w = unit_gain(residual.shape[-1], residual.device)
     return _impl(x).add_rmsnorm(x, residual, w, eps, out)
 
 

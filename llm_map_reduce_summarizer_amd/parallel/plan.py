@@ -82,10 +82,22 @@ def decode_step_s(d: ModelDims, hw: HWModel, batch: int, ctx: float, tp: int) ->
     return stream + floor + comm
 
 
-def prefill_s(d: ModelDims, hw: HWModel, tokens: int, tp: int) -> float:
+PREFILL_CHUNK = 4096  # engine default slice length of chunked prefill (engine/engine.py)
+
+
+def prefill_s(d: ModelDims, hw: HWModel, tokens: int, tp: int, longest: int = 0,
+              chunk: int = PREFILL_CHUNK) -> float:
+    """TP=``tp`` prefill of ``tokens`` rows whose longest prompt has ``longest`` tokens (default: one
+    prompt).  The engine cuts prompts into end-aligned ``chunk``-token slices (n passes for the longest),
+    and a TP prefill of n > 1 passes runs layer-major with every pass's all-reduces under the next pass's
+    GEMMs (engine/model.py prefill_passes): the longer of compute and communication, plus the shorter
+    one's last-pass share."""
     compute = tokens * d.flops_per_token / tp / hw.prefill_flops
-    comm = 2 * d.n_layers * tokens * d.hidden * 2 / hw.ar_bw if tp > 1 else 0.0
-    return compute + comm
+    if tp == 1:
+        return compute
+    comm = 2 * d.n_layers * tokens * d.hidden * 2 / hw.ar_bw
+    n = max(1, -(-(longest or tokens) // chunk)) if chunk else 1
+    return max(compute, comm) + min(compute, comm) / n
 
 
 def _lpt(costs: Sequence[int], bins: int) -> List[List[int]]:
@@ -125,7 +137,7 @@ def stage_seconds(d: ModelDims, hw: HWModel, prompt_lens: Sequence[int], max_new
             continue
         pl = [prompt_lens[i] for i in idx]
         mn = [max_new[i] for i in idx]
-        t = prefill_s(d, hw, sum(pl), tp)
+        t = prefill_s(d, hw, sum(pl), tp, max(pl))
         if use_handoff:  # the cheaper of the TP forward and the disaggregated prefill
             t = min(t, handoff_prefill_s(d, hw, pl, tp))
         # sequences retire as they reach their max_new: walk the decode in segments of equal batch
@@ -155,7 +167,7 @@ def choose(d: ModelDims, hw: HWModel, prompt_lens: Sequence[int], max_new: Seque
         # disaggregated prefill only where it beats the TP forward: many prompts split over the ranks
         # win, one long prompt (the final reduce) prefills faster as one TP forward over all GPUs
         out["handoff"] = bool(handoff) and handoff_prefill_s(d, hw, prompt_lens, world) < \
-            prefill_s(d, hw, sum(prompt_lens), world)
+            prefill_s(d, hw, sum(prompt_lens), world, max(prompt_lens))
     return out
 
 

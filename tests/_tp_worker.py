@@ -1,6 +1,7 @@
 """Worker for tests/test_custom_ar_gpu.py::test_tp2_engine_one_gpu: a TP=2 engine whose two ranks
 share ONE GPU (gloo process group for the eager prefill all-reduces; the decode all-reduces and the
-vocab-parallel sampling key max run on the custom P2P kernel, inside the captured hipGraphs)."""
+vocab-parallel sampling key max run on the custom P2P kernel, inside the captured hipGraphs); the
+chunked TP prefill (layer-major passes, async all-reduces) against the one-pass prefill."""
 import os
 import sys
 
@@ -28,6 +29,12 @@ def main():
     assert tp.model.custom_ar.error() == 0
     tp_eager = LLMEngine(cfg, tp_rank=rank, tp_size=2, tp_group=None, use_graphs=False, **kw)
     assert [o.token_ids for o in tp_eager.generate(prompts, greedy)] == g2, "graph vs eager TP decode"
+    # chunked prefill of longer prompts: TP passes run layer-major with async all-reduces (model.prefill_passes)
+    longp = [[128000] + [(i * 53 + j * 7) % 120000 + 5 for j in range(150 + 40 * i)] for i in range(3)]
+    chunked = LLMEngine(cfg, tp_rank=rank, tp_size=2, tp_group=None, use_graphs=True, prefill_chunk=64, **kw)
+    gc = [o.token_ids for o in chunked.generate(longp, greedy)]
+    assert chunked.stats["prefill_slices"] > 3
+    assert gc == [o.token_ids for o in tp.generate(longp, greedy)], "layer-major chunked TP prefill vs one pass"
     # both ranks must have produced the same tokens
     allg = [None, None]
     dist.all_gather_object(allg, (g2, s2))

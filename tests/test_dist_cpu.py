@@ -88,18 +88,20 @@ TP_SCRIPT = textwrap.dedent("""
     from llm_map_reduce_summarizer_amd.engine.engine import LLMEngine, SamplingParams
     cfg = get_model_config("tiny-gqa4", init_std=0.05)
     eng = LLMEngine(cfg, device="cpu", max_model_len=512, max_num_seqs=4, kv_pages=64, sync_every=3,
-                    tp_rank=par.tp_rank, tp_size=par.tp, tp_group=par.tp_group)
-    prompts = [[128000] + [(i * 7 + j * 3) %% 9000 + 5 for j in range(20 + 9 * i)] for i in range(3)]
+                    tp_rank=par.tp_rank, tp_size=par.tp, tp_group=par.tp_group,
+                    prefill_chunk=int(os.environ.get("CHUNK", "0")))
+    n0 = int(os.environ.get("PLEN", "20"))
+    prompts = [[128000] + [(i * 7 + j * 3) %% 9000 + 5 for j in range(n0 + 9 * i)] for i in range(3)]
     outs = eng.generate(prompts, [SamplingParams(5, 0.0, i) for i in range(3)])
     print("RESULT " + json.dumps([o.token_ids for o in outs]), flush=True)
     pdist.shutdown()
 """)
 
 
-def _run_tp(world: int, tp: int):
+def _run_tp(world: int, tp: int, **extra):
     code = TP_SCRIPT % {"root": ROOT}
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
-               OMP_NUM_THREADS="2", TP=str(tp))
+               OMP_NUM_THREADS="2", TP=str(tp), **{k: str(v) for k, v in extra.items()})
     procs = [subprocess.Popen([sys.executable, "-c", code], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
     outs = []
@@ -117,6 +119,16 @@ def test_tp2_matches_tp1():
     assert tp[0] == tp[1]  # both TP ranks sample identically
     same = sum(a == b for a, b in zip(tp[0], ref))
     assert same >= 2, (tp[0], ref)  # greedy; a bf16 near-tie may flip one sequence
+
+
+@pytest.mark.slow
+def test_tp2_chunked_layer_major_prefill_matches_one_pass():
+    """TP=2 chunked prefill (prompts of 150-168 tokens in 64-token slices) runs layer-major with async
+    all-reduces (engine/model.py prefill_passes): same tokens as the one-pass TP=2 prefill."""
+    one = _run_tp(2, 2, PLEN=150)
+    chunked = _run_tp(2, 2, PLEN=150, CHUNK=64)
+    assert chunked[0] == chunked[1]
+    assert chunked[0] == one[0], (chunked[0], one[0])
 
 
 RTP_SCRIPT = SCRIPT.replace('engine_options={"kv_pages": 512, "max_num_seqs": 16})',
