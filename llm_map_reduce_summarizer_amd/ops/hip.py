@@ -49,8 +49,6 @@ _SIGS = {
     "mrsum_sample_finish": [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "mrsum_gemm": [_vp, _c_int, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int,
                    _vp],
-    "mrsum_decode_layer": [_vp, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int,
-                           _c_float, _vp],
     "mrsum_sample": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp,
                      _c_int, _vp],
 }
@@ -813,69 +811,6 @@ def plan(role: str, M: int, N: int, K: int, splits: Optional[int] = None, stream
     return ("gemm",)
 
 
-
-
-# ------------------------------------------------------------------ persistent post-attention decode layer
-_DL_SCRATCH = {}
-
-
-def decode_layer_supported(M: int, hidden: int, ffn: int, hq: int, hkv: int, d: int, device) -> bool:
-    """Shapes the persistent layer kernel (csrc/kernels/decode_layer.hip) is built for: Llama-3-8B on one
-    GPU of 256 CUs (one workgroup per CU, all co-resident), M <= 16 decode rows."""
-    if not (1 <= M <= 16 and (hidden, ffn, hq, hkv, d) == (4096, 14336, 32, 8, 128)):
-        return False
-    return torch.cuda.get_device_properties(torch.device(device)).multi_processor_count == 256
-
-
-def _dl_scratch(device, M: int):
-    key = (str(device), M)
-    sc = _DL_SCRATCH.get(key)
-    if sc is None:
-        # tickets / seam counters / error word must outlive every captured graph: never allocated inside a
-        # capture (the engine's eager warm-up step before each capture creates them)
-        _req(not torch.cuda.is_current_stream_capturing(), "decode_layer scratch first used inside a capture")
-        f32 = dict(dtype=torch.float32, device=device)
-        sc = _DL_SCRATCH[key] = {
-            "act": torch.empty(M, 14336, dtype=torch.bfloat16, device=device),
-            "parts": torch.empty(8, M, 4096, **f32),
-            "ssp_o": torch.empty(M, 32, **f32),
-            "ssp_d": torch.empty(M, 32, **f32),
-            "tickets": torch.zeros(64, dtype=torch.int32, device=device),
-            "sem": torch.zeros(16, dtype=torch.int32, device=device),
-            "err": torch.zeros(1, dtype=torch.int32, device=device),
-        }
-    return sc
-
-
-def decode_layer_error() -> int:
-    """Sticky error word of the persistent layer kernel (a bounded seam wait timed out: results invalid)."""
-    return max((int(sc["err"].item()) for sc in _DL_SCRATCH.values()), default=0)
-
-
-def decode_layer(a: torch.Tensor, wo: torch.Tensor, wgu: torch.Tensor, wd: torch.Tensor,
-                 wqkv: Optional[torch.Tensor], residual: torch.Tensor, eps: float):
-    """o projection + residual -> gate_up + SwiGLU -> down + residual -> (next layer's QKV) in ONE launch
-    (csrc/kernels/decode_layer.hip), RMSNorms deferred.  Returns (qkv slabs [4, M, 6144] fp32 or None,
-    ssp [M, 32]: per-tile row sums of squares of the final residual -- the deferred norm of the next
-    consumer)."""
-    _bf16_cuda(a, wo, wgu, wd, residual)
-    M = a.shape[0]
-    _req(a.dim() == 2 and a.shape[1] == 4096 and a.stride(1) == 1 and a.stride(0) % 8 == 0 and
-         residual.shape == (M, 4096) and residual.is_contiguous() and 1 <= M <= 16,
-         "decode_layer: rows / residual")
-    _req(wo.shape == (4096, 4096) and wgu.shape == (28672, 4096) and wd.shape == (4096, 14336) and
-         wo.is_contiguous() and wgu.is_contiguous() and wd.is_contiguous(), "decode_layer: weights")
-    out = None
-    if wqkv is not None:
-        _bf16_cuda(wqkv)
-        _req(wqkv.shape == (6144, 4096) and wqkv.is_contiguous(), "decode_layer: wqkv")
-        out = torch.empty(4, M, 6144, dtype=torch.float32, device=a.device)
-    sc = _dl_scratch(a.device, M)
-    _check(_fn("mrsum_decode_layer")(_p(a), a.stride(0), _p(wo), _p(wgu), _p(wd), _p(wqkv), _p(residual),
-                                     _p(sc["act"]), _p(sc["parts"]), _p(sc["ssp_o"]), _p(sc["ssp_d"]), _p(out),
-                                     _p(sc["tickets"]), _p(sc["sem"]), _p(sc["err"]), M, float(eps), _stream()),
-           "decode_layer")
-    return out, sc["ssp_d"]
 
 
 # ------------------------------------------------------------------ FP8 (e4m3fn) weights
