@@ -295,16 +295,19 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     const int st_row = tid >> 4, st_chunk = tid & 15;
     const size_t head_off = (size_t)kvh * PG * D + (size_t)st_row * D + st_chunk * 8;
     // staging registers are plain named arrays indexed only by unrolled constants (a lambda
-    // capturing them by reference put them in scratch), and the prefetch is unconditional
-    // (the last tile is re-read instead of branching) so hipcc keeps the loads in flight.
+    // capturing them by reference put them in scratch), and the prefetch is unconditional (no
+    // branch around the loads) so hipcc keeps them in flight.
     // (issued first by every split, the one holding the new token included: its new K/V row reaches
     // the tile through the LDS patch, so the page loads need not wait for the slab sums)
-    // TWO tiles in flight: register sets A (kreg/vreg) and B (kreg2/vreg2) alternate; loads past the
-    // last tile re-read it (clamped, unconditional).
+    // TWO tiles in flight: register sets A (kreg/vreg) and B (kreg2/vreg2) alternate; the (up to two)
+    // loads past the last tile stay unconditional but read the scratch page 0, which every workgroup's
+    // overshoot shares and so stays in L2 (re-reading the workgroup's own last tile cost ~9 % extra HBM
+    // traffic at B=39, PMC FETCH_SIZE).
     u32x4 kreg[4], vreg[4], kreg2[4], vreg2[4];
 #define KV_ISSUE(KR, VR, TILE)                                                          \
     {                                                                                   \
-        const size_t base_ = (size_t)bt[min((TILE), ntiles - 1)] * Hkv * PG * D + head_off; \
+        const int pg_ = bt[min((TILE), ntiles - 1)];                                    \
+        const size_t base_ = (size_t)((TILE) < ntiles ? pg_ : 0) * Hkv * PG * D + head_off; \
         _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                 \
             KR[i] = ld_kv<NT>(kc + base_ + (size_t)16 * i * D);                         \
             VR[i] = ld_kv<NT>(vc + base_ + (size_t)16 * i * D);                         \
