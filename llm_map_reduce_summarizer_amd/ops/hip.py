@@ -326,6 +326,10 @@ def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
         fused = -(-pages // 16) <= 6  # the <= 6k context class
         if fused:
             splits = min(splits, 16)
+        elif pages <= 192:
+            # the <= 12k class at B=1 (profiles/r2_attn_decode_b1_class1.jsonl, 7 rounds x 64 calls): 32 separate
+            # splits 18.6 / 17.5 us at 8k / 10k against 64 splits 18.9 / 18.8 and every fused variant >= 19.1
+            splits = min(splits, 32)
     else:
         fused = groups <= 128
         if fused:
