@@ -23,6 +23,8 @@ def main():
     ap.add_argument("--chunks", default="0,4096,8192")
     ap.add_argument("--paged", default="0,1")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--max-prefill-tokens", default=str(1 << 20),
+                    help="comma list: packed-prefill pass budgets to compare (engine max_prefill_tokens)")
     a = ap.parse_args()
     import torch
     from llm_map_reduce_summarizer_amd.engine.config import get_model_config
@@ -31,15 +33,16 @@ def main():
     lens = [int(x) for x in a.lens.split(",")]
     eng = LLMEngine(cfg, device="cuda:0", max_model_len=max(lens) + 64, max_num_seqs=max(64, a.nseq),
                     kv_fraction=0.3, weight_dtype=a.dtype, max_prefill_tokens=1 << 20)
+    budgets = [int(b) for b in a.max_prefill_tokens.split(",")]
     V = cfg.vocab_size
     for L in lens:
         prompts = [[1] + [(i * 7919 + j * 31) % (V - 20) + 10 for j in range(L - 1)] for i in range(a.nseq)]
         sp = [SamplingParams(1, 0.0, i) for i in range(a.nseq)]
-        for chunk in (int(c) for c in a.chunks.split(",")):
-            for paged in (int(p) for p in a.paged.split(",")):
+        for chunk, paged, budget in ((c, p, b) for c in (int(c) for c in a.chunks.split(","))
+                                     for p in (int(p) for p in a.paged.split(",")) for b in budgets):
                 if chunk and not paged:
                     continue  # chunked slices always read the paged cache
-                eng.prefill_chunk, eng.paged_prefill = chunk, bool(paged)
+                eng.prefill_chunk, eng.paged_prefill, eng.max_prefill_tokens = chunk, bool(paged), budget
                 eng.generate(prompts, sp)  # warm
                 ts = []
                 for _ in range(a.reps):
@@ -50,7 +53,8 @@ def main():
                     ts.append(time.perf_counter() - t0)
                 ts.sort()
                 print(json.dumps({"model": a.model, "dtype": a.dtype, "len": L, "nseq": a.nseq, "chunk": chunk,
-                                  "paged": paged, "s_med": round(ts[len(ts) // 2], 4), "s_min": round(ts[0], 4),
+                                  "paged": paged, "max_prefill_tokens": budget,
+                                  "s_med": round(ts[len(ts) // 2], 4), "s_min": round(ts[0], 4),
                                   "tok_s": round(L * a.nseq / ts[len(ts) // 2], 1)}), flush=True)
 
 
