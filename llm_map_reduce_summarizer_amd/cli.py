@@ -58,6 +58,8 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("--no-timestamps", action="store_true", help="merged text without inline [MM:SS] marks")
     g.add_argument("--reduce-levels", type=int, default=2,
                    help="max reduce depth incl. the final pass (0 = recursive until it fits)")
+    g.add_argument("--stream-reduce", action="store_true",
+                   help="start each level-1 reduce batch as soon as its chunks are summarised (no map barrier)")
     g.add_argument("--chunk-overlap", type=int, default=0, help="tokens of previous-chunk context to prepend")
     g.add_argument("--position-mode", choices=["transcript", "reference"], default="transcript")
     g.add_argument("--max-new-tokens", type=int, default=None, help="override $MAX_TOKENS")
@@ -159,7 +161,7 @@ async def async_main(args: argparse.Namespace) -> int:
         executor=executor, aggregator_executor=agg_executor,
         chunker_options={"position_mode": args.position_mode, "overlap_tokens": args.chunk_overlap,
                          "apply_overlap": args.chunk_overlap > 0},
-        aggregator_options={"max_levels": args.reduce_levels or None})
+        aggregator_options={"max_levels": args.reduce_levels or None}, stream_reduce=args.stream_reduce)
     from .utils.profiling import maybe_profile
     with maybe_profile(args.profile, int(os.environ.get("RANK", "0"))):
         result = await summarizer.summarize(

@@ -365,20 +365,27 @@ class LLMEngine:
     # ------------------------------------------------------------------ API
     def generate(self, prompts: Sequence[Sequence[int]], params: Sequence[SamplingParams],
                  ignore_eos: bool = False, imported: Optional[Dict[int, ImportedPrefill]] = None,
-                 on_prefill=None) -> List[GenOutput]:
+                 on_prefill=None, feeder=None) -> List[GenOutput]:
         """Generate for every prompt.  ``ignore_eos`` pins the work to max_new_tokens per request
         (benchmark mode, SURVEY §7.4: random weights emit EOS at random).
 
         ``imported``: request index -> ImportedPrefill; those requests skip the prefill (their KV pages
         are copied in and decoding starts from the imported first token).  ``on_prefill(seqs)`` is
-        called after every prefill forward with the just-prefilled sequences (pages still held)."""
+        called after every prefill forward with the just-prefilled sequences (pages still held).
+
+        ``feeder(done)``: streaming hook, called at every host sync point with the requests that
+        finished since the last call (``[(request index, GenOutput)]``); it returns new
+        ``(prompt, SamplingParams)`` requests, which join the running batch (continuous batching) and
+        take the next request indices.  The returned list covers every request, fed ones included.
+        (The map -> level-1 reduce pipeline uses it: a reduce batch starts as soon as its chunks are
+        summarised)"""
         if len(prompts) != len(params):
             raise ValueError("prompts and params differ in length")
         n_eos = self.state.n_eos
         if ignore_eos:
             self.state.n_eos = 0
         try:
-            out = self._generate(prompts, params, imported or {}, on_prefill)
+            out = self._generate(prompts, params, imported or {}, on_prefill, feeder)
         finally:
             self.state.n_eos = n_eos
         if self.model.custom_ar is not None and self.model.custom_ar.error():
@@ -386,36 +393,49 @@ class LLMEngine:
                                "results are invalid (set MRSUM_CUSTOM_AR=0 to use RCCL)")
         return out
 
+    def _new_seq(self, i: int, p: Sequence[int], sp: SamplingParams, imported=None) -> _Seq:
+        p = list(p)
+        if not p:
+            raise ValueError("empty prompt")
+        mn = max(1, min(sp.max_new_tokens, self.max_new_cap))
+        if len(p) + mn > self.max_model_len:
+            raise ValueError("prompt of %d tokens + %d new exceeds max_model_len %d"
+                             % (len(p), mn, self.max_model_len))
+        if max(p) >= self.cfg.vocab_size or min(p) < 0:
+            raise ValueError("token id out of range")
+        return _Seq(i, p, SamplingParams(mn, sp.temperature, sp.seed), imported=imported)
+
+    def _fit_ctx_class(self, seqs: Sequence[_Seq]) -> None:
+        """Decode attention split plan (graphs are keyed by it) for the longest sequence in flight."""
+        if seqs and self.device.type == "cuda":
+            from ..ops.hip import ctx_class
+            self._ctx_cls = max(self._ctx_cls, ctx_class(max(len(s.prompt) + s.params.max_new_tokens for s in seqs)))
+
     def _generate(self, prompts: Sequence[Sequence[int]], params: Sequence[SamplingParams],
-                  imported: Dict[int, ImportedPrefill], on_prefill) -> List[GenOutput]:
+                  imported: Dict[int, ImportedPrefill], on_prefill, feeder=None) -> List[GenOutput]:
         self.stats["generate_calls"] += 1
         self._on_prefill = on_prefill
         results: List[Optional[GenOutput]] = [None] * len(prompts)
+        finished: List[int] = []  # request indices done since the last feeder call
         waiting: List[_Seq] = []
         for i, (p, sp) in enumerate(zip(prompts, params)):
-            p = list(p)
-            if not p:
-                raise ValueError("empty prompt")
-            mn = max(1, min(sp.max_new_tokens, self.max_new_cap))
-            if len(p) + mn > self.max_model_len:
-                raise ValueError("prompt of %d tokens + %d new exceeds max_model_len %d"
-                                 % (len(p), mn, self.max_model_len))
-            if max(p) >= self.cfg.vocab_size or min(p) < 0:
-                raise ValueError("token id out of range")
-            s = _Seq(i, p, SamplingParams(mn, sp.temperature, sp.seed), imported=imported.get(i))
+            s = self._new_seq(i, p, sp, imported.get(i))
             if s.imported is not None:
                 tok = int(s.imported.first_token)
+                mn = s.params.max_new_tokens
                 if mn == 1 or tok in set(self.state.eos.tolist()[: self.state.n_eos]):
-                    results[i] = GenOutput([tok], len(p), "length" if mn == 1 else "stop")  # done at prefill
+                    results[i] = GenOutput([tok], len(s.prompt), "length" if mn == 1 else "stop")  # done at prefill
+                    finished.append(i)
                     continue
             waiting.append(s)
         # longest first: better packing and no late long straggler
         waiting.sort(key=lambda s: -(len(s.prompt) + s.params.max_new_tokens))
-        if waiting and self.device.type == "cuda":
-            from ..ops.hip import ctx_class
-            self._ctx_cls = ctx_class(len(waiting[0].prompt) + waiting[0].params.max_new_tokens)
+        self._ctx_cls = 0
+        self._fit_ctx_class(waiting)
         active: List[_Seq] = []
         st = self.state
+        if feeder is not None and finished:
+            self._feed(feeder, finished, results, waiting)
         while waiting or active:
             admitted = self._admit(waiting, active)
             if not active:
@@ -443,11 +463,28 @@ class LLMEngine:
                     ids = toks[i, :g].tolist()
                     reason = "length" if g >= s.params.max_new_tokens else "stop"
                     results[s.rid] = GenOutput(ids, len(s.prompt), reason)
+                    finished.append(s.rid)
                     self.stats["decode_tokens"] += g
                     self.kv.alloc.free(s.pages)
                 self._compact(active, set(fin))
+                if feeder is not None:
+                    self._feed(feeder, finished, results, waiting)
             del admitted
         return [r for r in results]  # type: ignore[return-value]
+
+    def _feed(self, feeder, finished: List[int], results: List[Optional[GenOutput]], waiting: List[_Seq]) -> None:
+        """Hand the just-finished requests to ``feeder`` and queue the requests it returns."""
+        done = [(i, results[i]) for i in finished]
+        finished.clear()
+        new = []
+        for p, sp in feeder(done) or ():
+            s = self._new_seq(len(results), p, sp)
+            results.append(None)
+            new.append(s)
+        if new:
+            self.stats["fed_requests"] = self.stats.get("fed_requests", 0) + len(new)
+            waiting.extend(sorted(new, key=lambda s: -(len(s.prompt) + s.params.max_new_tokens)))
+            self._fit_ctx_class(new)
 
     def _admit(self, waiting: List[_Seq], active: List[_Seq]) -> List[_Seq]:
         st = self.state

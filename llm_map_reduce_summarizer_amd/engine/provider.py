@@ -433,16 +433,93 @@ class LocalEngineProvider(Provider):
         else:
             merged = {r["i"]: r for r in local}
         self.timings["allgather_s"] += time.perf_counter() - t1
-        results = []
-        for i in range(len(reqs)):
-            r = merged.get(i)
-            if r is None:
-                results.append(GenResult("", error="request %d produced no result" % i))
-            elif "err" in r:
-                results.append(GenResult("", error=r["err"]))
-            else:
-                results.append(GenResult(r["text"], r["pt"], r["ct"], 0.0, extra={"finish_reason": r["fr"]}))
-        return results
+        return [_result(merged[i]) if i in merged else GenResult("", error="request %d produced no result" % i)
+                for i in range(len(reqs))]
+
+    async def generate_groups(self, reqs: Sequence[GenRequest], groups: Sequence[Sequence[int]], build):
+        """Streamed two-stage generate (map -> level-1 reduce): ``groups`` partitions
+        ``reqs``; as soon as every request of group g has finished, ``build(g, results)`` (results in
+        group order) returns group g's follow-up request (or None), which joins the SAME running
+        engine batch -- no stage barrier, no second prefill wave behind the slowest chunk.
+
+        Data-parallel: whole groups are LPT-assigned to the replicas, so a group's follow-up runs where
+        its inputs were produced and the only collective is ONE all-gather of both stages' results at
+        the end (every rank enters it, errors included).  Returns ``(first, second)`` result lists
+        (second[g] None when build returned None), or None when this job runs stages on a TP engine
+        (the caller then falls back to two barrier-separated generates)."""
+        from .engine import SamplingParams
+        if self.par.tp > 1 or (self.par.world > 1 and self.parallel != "dp"):
+            return None
+        t0 = time.perf_counter()
+        prompts = [self.encode_request(r) for r in reqs]
+        dp, dp_rank = self.par.dp, self.par.dp_rank
+        cost = [sum(len(prompts[i]) + 2 * reqs[i].max_tokens for i in g) for g in groups]
+        gowner = assign_balanced(cost, dp)
+        owner = [0] * len(reqs)
+        for g, members in enumerate(groups):
+            for i in members:
+                owner[i] = gowner[g]
+        self.owner_maps.setdefault(reqs[0].stage if reqs else "map", []).append(owner)
+        for st in ("map", "reduce_l1"):
+            self.stage_plan.setdefault(st, {"tp": 1, "handoff": False, "streamed": True})
+        mine_g = [g for g in range(len(groups)) if gowner[g] == dp_rank]
+        mine = [i for g in mine_g for i in groups[g]]
+        group_of = {i: g for g in mine_g for i in groups[g]}
+        left = {g: len(groups[g]) for g in mine_g}
+        first: Dict[int, Dict[str, Any]] = {}
+        second: Dict[int, Dict[str, Any]] = {}
+        fed: List[int] = []  # engine request index len(mine) + k -> group fed[k]
+
+        def rec(key, idx, o):
+            return {key: idx, "text": self.tokenizer.decode(o.token_ids), "pt": o.prompt_len, "ct": len(o.token_ids),
+                    "fr": o.finish_reason}
+
+        def feeder(done):
+            new = []
+            for rid, o in done:
+                if rid >= len(mine):
+                    g = fed[rid - len(mine)]
+                    second[g] = rec("g", g, o)
+                    continue
+                i = mine[rid]
+                first[i] = rec("i", i, o)
+                g = group_of[i]
+                left[g] -= 1
+                if left[g]:
+                    continue
+                r2 = build(g, [_result(first[j]) for j in groups[g]])
+                if r2 is None:
+                    continue
+                fed.append(g)
+                new.append((self.encode_request(r2),
+                            SamplingParams(r2.max_tokens, r2.temperature, _req_seed(self.seed, r2))))
+            return new
+
+        try:
+            if mine:
+                self._maybe_fault()
+                self.engine.generate([prompts[i] for i in mine],
+                                     [SamplingParams(reqs[i].max_tokens, reqs[i].temperature,
+                                                     _req_seed(self.seed, reqs[i])) for i in mine],
+                                     ignore_eos=self.ignore_eos, feeder=feeder)
+        except Exception as e:  # noqa: BLE001 -- never skip the all-gather below: the peers are in it
+            msg = "rank %d: %s: %s" % (self.par.rank, type(e).__name__, e)
+            log.error("engine failed on %d streamed requests: %s", len(mine), msg)
+            first = {i: {"i": i, "err": msg} for i in mine}
+            second = {g: {"g": g, "err": msg} for g in mine_g}
+        local = list(first.values()) + list(second.values())
+        t1 = time.perf_counter()
+        self.timings["generate_s"] += t1 - t0
+        if pdist.is_initialized():
+            parts = pdist.all_gather_json(local)
+            local = [r for part in parts for r in part]
+        self.timings["allgather_s"] += time.perf_counter() - t1
+        m1 = {r["i"]: r for r in local if "i" in r}
+        m2 = {r["g"]: r for r in local if "g" in r}
+        res1 = [_result(m1[i]) if i in m1 else GenResult("", error="request %d produced no result" % i)
+                for i in range(len(reqs))]
+        res2 = [_result(m2[g]) if g in m2 else None for g in range(len(groups))]
+        return res1, res2
 
     def stats(self) -> Dict[str, Any]:
         s: Dict[str, Any] = {"model": self.model, "dp": self.par.dp, "tp": self.par.tp, "parallel": self.parallel,
@@ -458,6 +535,13 @@ class LocalEngineProvider(Provider):
         if self._tp_engine is not None:
             s["tp_engine"] = self._tp_engine.engine_stats()
         return s
+
+
+def _result(r: Dict[str, Any]) -> GenResult:
+    """GenResult of an all-gathered result record ({"text", "pt", "ct", "fr"} or {"err"})."""
+    if "err" in r:
+        return GenResult("", error=r["err"])
+    return GenResult(r["text"], r["pt"], r["ct"], 0.0, extra={"finish_reason": r["fr"]})
 
 
 def _rccl_bandwidth(group, hidden: int, device, rows: int = 4096) -> float:

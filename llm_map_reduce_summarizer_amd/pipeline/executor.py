@@ -81,7 +81,19 @@ class LLMExecutor:
                     await asyncio.sleep(self.config.RETRY_DELAY)
         raise AssertionError("unreachable")
 
-    async def generate(self, reqs: Sequence[GenRequest], stage: str = "map") -> List[GenResult]:
+    def _account(self, results: Sequence[Optional[GenResult]]) -> None:
+        for r in results:
+            if r is None:
+                continue
+            self.total_requests += 1
+            if r.error:
+                self.failed_requests += 1
+            else:
+                self.total_tokens_used += r.tokens_used
+                self.total_cost += r.cost
+
+    async def generate(self, reqs: Sequence[GenRequest], stage: str = "map",
+                       attempts: Optional[int] = None) -> List[GenResult]:
         """Run requests through the provider with the executor's retry policy and accounting."""
         t0 = time.perf_counter()
         if not reqs:
@@ -89,7 +101,7 @@ class LLMExecutor:
         if self._provider.batched:
             results: List[Optional[GenResult]] = [None] * len(reqs)
             pending = list(range(len(reqs)))
-            attempts = max(1, self.config.RETRY_ATTEMPTS)
+            attempts = max(1, self.config.RETRY_ATTEMPTS if attempts is None else attempts)
             for attempt in range(1, attempts + 1):
                 try:
                     out = await self._provider.generate_batch([reqs[i] for i in pending])
@@ -111,23 +123,13 @@ class LLMExecutor:
         else:
             sem = asyncio.Semaphore(max(1, self.max_concurrent_requests))
             final = list(await asyncio.gather(*[self._one_with_retries(r, sem) for r in reqs]))
-        for r in final:
-            self.total_requests += 1
-            if r.error:
-                self.failed_requests += 1
-            else:
-                self.total_tokens_used += r.tokens_used
-                self.total_cost += r.cost
+        self._account(final)
         self.phase_seconds[stage] = self.phase_seconds.get(stage, 0.0) + time.perf_counter() - t0
         return final
 
-    async def process_chunks(self, chunks: List[Dict[str, Any]], prompt_template: str,
-                             summary_type: str = "summary", system_prompt: Optional[str] = None
-                             ) -> List[Dict[str, Any]]:
-        t0 = time.perf_counter()
-        log.info("map stage: %d chunks via %s", len(chunks), self.provider)
-        reqs = []
-        outs: List[Dict[str, Any]] = []
+    def _map_requests(self, chunks: List[Dict[str, Any]], prompt_template: str, summary_type: str,
+                      system_prompt: Optional[str]):
+        reqs, outs = [], []
         for idx, chunk in enumerate(chunks):
             res = dict(chunk)
             if system_prompt:
@@ -138,23 +140,110 @@ class LLMExecutor:
             reqs.append(GenRequest(user=prompt, system=system_prompt, max_tokens=self.config.MAX_TOKENS,
                                    temperature=self.config.TEMPERATURE, stage="map", tag=idx))
             outs.append(res)
+        return reqs, outs
+
+    @staticmethod
+    def _apply(res: Dict[str, Any], r: GenResult) -> Dict[str, Any]:
+        """Fill a chunk record from its map result (reference llm_executor.py:196-228 error text)."""
+        if r.error:
+            res["summary"] = "[Error processing chunk: %s]" % r.error
+            res["error"] = r.error
+            res["tokens_used"] = 0
+            res["cost"] = 0
+        else:
+            res["summary"] = r.text
+            res["tokens_used"] = r.tokens_used
+            res["cost"] = r.cost
+        return res
+
+    def _log_map(self, n: int, dt: float) -> None:
+        log.info("map stage done: %d chunks in %.2f s (%.2f chunks/s); tokens=%d failed=%d/%d", n, dt,
+                 n / dt if dt > 0 else 0.0, self.total_tokens_used, self.failed_requests, self.total_requests)
+
+    async def process_chunks(self, chunks: List[Dict[str, Any]], prompt_template: str,
+                             summary_type: str = "summary", system_prompt: Optional[str] = None
+                             ) -> List[Dict[str, Any]]:
+        t0 = time.perf_counter()
+        log.info("map stage: %d chunks via %s", len(chunks), self.provider)
+        reqs, outs = self._map_requests(chunks, prompt_template, summary_type, system_prompt)
         results = await self.generate(reqs, stage="map")
         for res, r in zip(outs, results):
-            if r.error:
-                res["summary"] = "[Error processing chunk: %s]" % r.error
-                res["error"] = r.error
-                res["tokens_used"] = 0
-                res["cost"] = 0
-            else:
-                res["summary"] = r.text
-                res["tokens_used"] = r.tokens_used
-                res["cost"] = r.cost
+            self._apply(res, r)
         outs.sort(key=lambda c: c["chunk_index"])
-        dt = time.perf_counter() - t0
-        log.info("map stage done: %d chunks in %.2f s (%.2f chunks/s); tokens=%d failed=%d/%d", len(chunks), dt,
-                 len(chunks) / dt if dt > 0 else 0.0, self.total_tokens_used, self.failed_requests,
-                 self.total_requests)
+        self._log_map(len(chunks), time.perf_counter() - t0)
         return outs
+
+    async def process_chunks_streamed(self, chunks: List[Dict[str, Any]], prompt_template: str,
+                                      groups: Sequence[Sequence[int]], build, summary_type: str = "summary",
+                                      system_prompt: Optional[str] = None):
+        """Map stage with a follow-up request per group of chunks, started as soon as the group's
+        chunks are summarised (the streamed map -> level-1 reduce of SURVEY §2.5; the reference waits for
+        every chunk, llm_executor.py:147).  ``groups`` holds positions in ``chunks``;
+        ``build(g, records)`` gets the group's chunk records (as process_chunks returns them) and returns
+        a GenRequest or None.
+
+        Returns ``(records, follow_ups)``: the chunk records sorted by chunk_index and one GenResult (or
+        None) per group.  A group with a chunk that failed in the streamed pass gets None -- its chunks
+        are retried like process_chunks' and the caller re-runs the group from the final records.
+
+        Transports: the local engine streams inside one continuous batch (``generate_groups``); a
+        per-request provider (hosted HTTP, mock) runs one asyncio task per group under the
+        ``max_concurrent_requests`` semaphore, so a group's follow-up is sent the moment its last chunk
+        returns; any other batched provider falls back to map, then follow-ups (a barrier)."""
+        t0 = time.perf_counter()
+        log.info("map stage (streamed into %d follow-ups): %d chunks via %s", len(groups), len(chunks), self.provider)
+        reqs, outs = self._map_requests(chunks, prompt_template, summary_type, system_prompt)
+        first: List[Optional[GenResult]] = [None] * len(reqs)
+        second: List[Optional[GenResult]] = [None] * len(groups)
+        records = lambda g, res: build(g, [self._apply(dict(outs[i]), r) for i, r in zip(groups[g], res)])
+        streamed = None
+        if self._provider.batched and hasattr(self._provider, "generate_groups"):
+            streamed = await self._provider.generate_groups(reqs, groups, records)
+        if streamed is not None:
+            first, second = list(streamed[0]), list(streamed[1])
+            self._account(first)
+            self._account(second)
+        elif not self._provider.batched:
+            sem = asyncio.Semaphore(max(1, self.max_concurrent_requests))
+
+            async def run_group(g: int) -> None:
+                res = await asyncio.gather(*[self._one_with_retries(reqs[i], sem) for i in groups[g]])
+                for i, r in zip(groups[g], res):
+                    first[i] = r
+                r2 = records(g, list(res))
+                if r2 is not None:
+                    second[g] = await self._one_with_retries(r2, sem)
+
+            await asyncio.gather(*[run_group(g) for g in range(len(groups))])
+            self._account(first)
+            self._account(second)
+        else:  # batched provider without a streaming path: map, then the follow-ups
+            first = await self.generate(reqs, stage="map")
+            follow = [(g, records(g, [first[i] for i in groups[g]])) for g in range(len(groups))]
+            follow = [(g, r) for g, r in follow if r is not None]
+            res2 = await self.generate([r for _, r in follow], stage=follow[0][1].stage if follow else "reduce_l1")
+            for (g, _), r in zip(follow, res2):
+                second[g] = r
+        self.phase_seconds["map+follow_ups"] = time.perf_counter() - t0
+        if streamed is not None:  # per-request transports retried inside the pass already
+            bad = [i for i, r in enumerate(first) if r.error]
+            if bad:
+                log.warning("%d/%d chunks failed in the streamed pass: retrying them", len(bad), len(reqs))
+                for g, members in enumerate(groups):
+                    if any(first[i].error for i in members):
+                        second[g] = None  # built from an error text: the caller re-runs it
+                retry = await self.generate([reqs[i] for i in bad], stage="map",
+                                            attempts=max(1, self.config.RETRY_ATTEMPTS - 1))
+                for i, r in zip(bad, retry):
+                    first[i] = r
+                # the failed pass's records were accounted above; keep failed_requests = final failures
+                self.failed_requests -= len(bad)
+                self.total_requests -= len(bad)
+        for res, r in zip(outs, first):
+            self._apply(res, r)
+        outs.sort(key=lambda c: c["chunk_index"])
+        self._log_map(len(chunks), time.perf_counter() - t0)
+        return outs, second
 
 
 async def process_chunks_parallel(chunks: List[Dict[str, Any]], prompt_template: str,

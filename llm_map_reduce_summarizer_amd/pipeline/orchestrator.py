@@ -13,6 +13,13 @@ stage), per-phase wall-clock timers and engine metrics under
 reset per run (Q17), and tokenizer injection so chunks are sized with the
 engine's vocabulary.
 
+``stream_reduce``: the level-1 reduce batches are planned before the map
+and each starts as soon as its own chunks are summarised (the
+reference's map ends with a full ``gather``, ``llm_executor.py:147``) --
+see ``ResultAggregator.stream_plan`` and ``LLMExecutor.process_chunks_streamed``.
+It needs the reduce on the map's executor; ``timings["map"]`` then covers
+the map and the streamed level 1.
+
 Under ``torch.distributed`` every rank runs this same code (SPMD): the
 CPU front-end is deterministic, the local provider scatters each generate
 batch over the data-parallel ranks and all-gathers the results, so every rank
@@ -63,7 +70,7 @@ class TranscriptSummarizer:
                  hierarchical_aggregation: bool = True, executor: Optional[LLMExecutor] = None,
                  chunker_options: Optional[Dict[str, Any]] = None, aggregator_options: Optional[Dict[str, Any]] = None,
                  provider_options: Optional[Dict[str, Any]] = None,
-                 aggregator_executor: Optional[LLMExecutor] = None):
+                 aggregator_executor: Optional[LLMExecutor] = None, stream_reduce: bool = False):
         """``aggregator_executor``: optional separate back-end for the reduce stage (e.g. the fp8
         Llama-3-70B aggregator of BASELINE config 5 while the map runs on Llama-3-8B); by default the
         reduce uses the map executor (the reference borrows its executor, result_aggregator.py:225)."""
@@ -79,6 +86,7 @@ class TranscriptSummarizer:
         self.aggregator_options = aggregator_options or {}
         self.provider_options = provider_options or {}
         self.aggregator_executor = aggregator_executor
+        self.stream_reduce = stream_reduce
 
     def _ensure_components(self) -> None:
         if self.executor is None:
@@ -141,8 +149,28 @@ class TranscriptSummarizer:
             prompt_template = self._get_prompt_template(prompt_file)
         sys_prompt = system_prompt or (self._get_system_prompt(system_prompt_file) if system_prompt_file else None)
 
+        agg_prompt = load_optional_prompt(aggregator_prompt_file, "aggregator prompt")
+        metadata = dict(metadata or {})
+        file_info = transcript_data.get("file_info") if hasattr(transcript_data, "get") else None
+        metadata.update({"File": file_info or "Unknown",
+                         "Total Duration": format_duration(chunks[-1]["end_time"] if chunks else 0)})
+
+        groups = None
+        if self.stream_reduce and not resume_chunks:
+            if self.aggregator_executor is not None:
+                log.warning("--stream-reduce needs the reduce on the map's back-end: running the stages apart")
+            else:
+                chunks = sorted(chunks, key=lambda c: c["chunk_index"])
+                groups = self.aggregator.stream_plan(chunks)
+        level1 = None
         t = time.perf_counter()
-        if resume_chunks:
+        if groups:
+            n = len(groups)
+            processed_chunks, l1 = await ex.process_chunks_streamed(
+                chunks, prompt_template, groups,
+                lambda g, recs: self.aggregator.level1_request(g, n, recs, metadata), system_prompt=sys_prompt)
+            level1 = (groups, l1)
+        elif resume_chunks:
             saved = {c["chunk_index"]: c for c in load_chunk_summaries(resume_chunks)}
             processed_chunks = []
             for c in chunks:
@@ -172,14 +200,9 @@ class TranscriptSummarizer:
             except OSError as e:
                 log.error("failed to save chunk summaries to %s: %s", save_intermediate_chunks, e)
 
-        agg_prompt = load_optional_prompt(aggregator_prompt_file, "aggregator prompt")
-        metadata = dict(metadata or {})
-        file_info = transcript_data.get("file_info") if hasattr(transcript_data, "get") else None
-        metadata.update({"File": file_info or "Unknown",
-                         "Total Duration": format_duration(chunks[-1]["end_time"] if chunks else 0)})
-
         t = time.perf_counter()
-        result = await self.aggregator.aggregate(processed_chunks, prompt_template=agg_prompt, metadata=metadata)
+        result = await self.aggregator.aggregate(processed_chunks, prompt_template=agg_prompt, metadata=metadata,
+                                                 level1=level1)
         timings["reduce"] = time.perf_counter() - t
 
         elapsed = time.perf_counter() - t_start

@@ -39,7 +39,8 @@ SCRIPT = textwrap.dedent("""
                                engine_options={"kv_pages": 512, "max_num_seqs": 16})
     ex = LLMExecutor(config=cfg, provider_obj=prov)
     summ = TranscriptSummarizer(executor=ex, max_tokens_per_chunk=1000,
-                                aggregator_options={"max_tokens_per_batch": 40})
+                                aggregator_options={"max_tokens_per_batch": 40},
+                                stream_reduce=os.environ.get("STREAM") == "1")
     rep = asyncio.run(summ.summarize(synthetic_transcript(0.5, seed=3)))
     out = {"rank": int(os.environ.get("RANK", 0)), "summary": rep["summary"], "chunks": rep["chunks"],
            "plan": rep["reduce_plan"], "engine_calls": prov.stats().get("generate_calls", 0)}
@@ -48,10 +49,10 @@ SCRIPT = textwrap.dedent("""
 """)
 
 
-def _run(world: int):
+def _run(world: int, **extra):
     code = SCRIPT % {"root": ROOT}
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE=str(world),
-               OMP_NUM_THREADS="2")
+               OMP_NUM_THREADS="2", **extra)
     procs = []
     for r in range(world):
         e = dict(env, RANK=str(r), LOCAL_RANK=str(r))
@@ -72,6 +73,19 @@ def test_dp2_equals_single_process():
     dp = _run(2)
     assert single["chunks"] > 2
     assert single["plan"]["levels"] >= 2  # exercises the hierarchical reduce
+    for r in dp:
+        assert r["summary"] == single["summary"]
+        assert {k: r["plan"][k] for k in ("levels", "calls")} == {k: single["plan"][k] for k in ("levels", "calls")}
+
+
+@pytest.mark.slow
+def test_dp2_streamed_reduce_equals_single_process():
+    """Streamed map -> level-1 reduce: whole level-1 batches are assigned to a replica, their reduce
+    joins that replica's running batch; world 2 ends with the world-1 summary and plan."""
+    single = _run(1, STREAM="1")[0]
+    dp = _run(2, STREAM="1")
+    assert single["plan"].get("level1_streamed") and single["plan"]["calls"][0] >= 2
+    assert single["engine_calls"] == 2  # map + level 1 in ONE engine generate, then the final pass
     for r in dp:
         assert r["summary"] == single["summary"]
         assert {k: r["plan"][k] for k in ("levels", "calls")} == {k: single["plan"][k] for k in ("levels", "calls")}

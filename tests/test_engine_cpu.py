@@ -237,3 +237,30 @@ def test_chunked_prefill_equals_one_pass(chunk):
         if c:
             assert eng.stats["prefill_slices"] > len(prompts)
     assert outs[0] == outs[chunk]
+
+
+def test_feeder_requests_join_the_running_batch(eng):
+    """Streaming hook: requests returned by ``feeder`` join the running batch (no second generate) and
+    produce exactly what a separate generate would (per-request seeds, batch-invariant engine)."""
+    ps = [SamplingParams(4 + 5 * i, 0.3, 20 + i) for i in range(3)]
+    extra = [SamplingParams(5, 0.3, 40 + i) for i in range(2)]
+    seen = []
+
+    def feeder(done):
+        new = []
+        for rid, o in done:
+            seen.append(rid)
+            if rid < 2:  # a follow-up for each of the first two requests, built from its output
+                new.append(([128000] + o.token_ids, extra[rid]))
+        return new
+
+    calls = eng.stats["generate_calls"]
+    outs = eng.generate(_prompts(3), ps, feeder=feeder)
+    assert eng.stats["generate_calls"] == calls + 1 and len(outs) == 5
+    assert sorted(seen) == [0, 1, 2, 3, 4] and seen.index(0) < seen.index(3)
+    solo = eng.generate(_prompts(3), ps)
+    assert [o.token_ids for o in outs[:3]] == [o.token_ids for o in solo]
+    for k in range(2):
+        ref = eng.generate([[128000] + solo[k].token_ids], [extra[k]])[0]
+        assert outs[3 + k].token_ids == ref.token_ids and outs[3 + k].prompt_len == 1 + len(solo[k].token_ids)
+    assert eng.kv.alloc.available() == eng.kv.num_pages - 1

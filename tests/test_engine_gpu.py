@@ -121,3 +121,23 @@ def test_fp8_engine_decode_matches_prefill():
         nxt = e.generate([p + o.token_ids[:-1]], [SamplingParams(1, 0.0, 0)])[0].token_ids[0]
         agree += nxt == o.token_ids[-1]
     assert agree >= len(prompts) - 1
+
+
+def test_feeder_follow_up_joins_running_batch_across_context_class():
+    """Streaming hook on the GPU engine: a fed follow-up whose context crosses into the 6k-12k class
+    joins the running batch (the decode graphs switch class mid-generate) and generates what a
+    separate generate does."""
+    e = LLMEngine(get_model_config("tiny-gqa4", init_std=0.05, max_position=16384), device="cuda:0",
+                  max_model_len=16384, max_num_seqs=8, kv_pages=1400, sync_every=4)
+    prompts = [[128000] + [(i * 41 + j * 3) % 120000 + 5 for j in range(n)] for i, n in enumerate((60, 300))]
+    sp = [SamplingParams(4, 0.0, 0), SamplingParams(24, 0.0, 0)]
+    long_p = [128000] + [(j * 17) % 120000 + 5 for j in range(6900)]
+
+    def feeder(done):
+        return [(long_p + o.token_ids, SamplingParams(6, 0.0, 0)) for rid, o in done if rid == 0]
+
+    outs = e.generate(prompts, sp, feeder=feeder)
+    assert len(outs) == 3 and e.stats.get("fed_requests") == 1 and e._ctx_cls == 1
+    ref = e.generate([long_p + outs[0].token_ids], [SamplingParams(6, 0.0, 0)])[0]
+    assert outs[2].token_ids == ref.token_ids
+    assert outs[1].token_ids == e.generate([prompts[1]], [sp[1]])[0].token_ids

@@ -148,3 +148,121 @@ def test_simple_aggregator_one_shot():
     assert r.system.strip().startswith("You are a professional transcript summarizer")
     ex2 = LLMExecutor(config=_cfg(RETRY_ATTEMPTS=1), provider_obj=MockProvider(fault_rate=1.0))
     assert aggregate_summaries(["x"], executor=ex2).startswith("Error generating summary: ")
+
+
+class TimedProvider(Provider):
+    """Per-request provider with a latency per chunk index; records (event, stage, tag, time)."""
+    name = "timed"
+
+    def __init__(self, fail_once=()):
+        super().__init__("timed")
+        self.events = []
+        self.fail_once = set(fail_once)
+        self.l1_users = []
+
+    async def generate(self, req):
+        import time as _t
+        self.events.append(("start", req.stage, req.tag, _t.perf_counter()))
+        if req.stage == "map":
+            await asyncio.sleep(0.004 * (1 + req.tag))
+            if req.tag in self.fail_once:
+                self.fail_once.discard(req.tag)
+                raise RuntimeError("flaky chunk %d" % req.tag)
+            text = " ".join(["c%dw%d" % (req.tag, i) for i in range(300)])
+        else:
+            if req.stage == "reduce_l1":
+                self.l1_users.append(req.user)
+            text = "reduced " + req.stage
+        self.events.append(("end", req.stage, req.tag, _t.perf_counter()))
+        return GenResult(text, 10, 300)
+
+
+def _stream_summarizer(prov, stream, **agg):
+    ex = LLMExecutor(config=_cfg(MAX_TOKENS=300), provider_obj=prov)
+    return TranscriptSummarizer(executor=ex, stream_reduce=stream, max_tokens_per_chunk=400,
+                                aggregator_options=dict({"max_tokens_per_batch": 1500}, **agg))
+
+
+def test_streamed_level1_starts_before_the_map_ends():
+    from llm_map_reduce_summarizer_amd.utils.synth import synthetic_transcript
+    prov = TimedProvider()
+    rep = asyncio.run(_stream_summarizer(prov, True).summarize(synthetic_transcript(1.0, seed=1)))
+    plan = rep["reduce_plan"]
+    assert plan.get("level1_streamed") and plan["levels"] == 2 and plan["calls"][0] >= 2
+    first_l1 = min(t for ev, st, _, t in prov.events if ev == "start" and st == "reduce_l1")
+    last_map = max(t for ev, st, _, t in prov.events if ev == "end" and st == "map")
+    assert first_l1 < last_map  # no map -> reduce barrier
+    assert rep["summary"] == "reduced reduce_final" and rep["failed_chunks"] == 0
+    # every chunk appears in exactly one level-1 request, batches in transcript order
+    for i in range(rep["chunks"]):
+        assert sum(1 for u in prov.l1_users if "c%dw0 " % i in u) == 1
+
+
+def test_streamed_level1_equals_barrier_with_the_same_batches():
+    """Same batches => same level-1 prompts and the same final prompt as the barrier reduce."""
+    from llm_map_reduce_summarizer_amd.utils.synth import synthetic_transcript
+    tr = synthetic_transcript(1.0, seed=2)
+    ps, pb = TimedProvider(), TimedProvider()
+    s_stream = _stream_summarizer(ps, True)
+    rs = asyncio.run(s_stream.summarize(tr))
+    bs = len(s_stream.aggregator.stream_plan([{"chunk_index": i} for i in range(rs["chunks"])])[0])
+    s_bar = _stream_summarizer(pb, False)
+    s_bar._ensure_components()
+    s_bar.aggregator._calculate_batch_size = lambda cur: bs
+    rb = asyncio.run(s_bar.summarize(tr))
+    assert rs["reduce_plan"]["calls"] == rb["reduce_plan"]["calls"]
+    assert sorted(ps.l1_users) == sorted(pb.l1_users)
+    fin = lambda p: [e for e in p.events if e[1] == "reduce_final"]
+    assert len(fin(ps)) == len(fin(pb)) == 2 and rs["summary"] == rb["summary"]
+
+
+def test_streamed_retries_a_failed_chunk_before_its_batch():
+    from llm_map_reduce_summarizer_amd.utils.synth import synthetic_transcript
+    prov = TimedProvider(fail_once={1})
+    rep = asyncio.run(_stream_summarizer(prov, True).summarize(synthetic_transcript(1.0, seed=1)))
+    assert rep["failed_chunks"] == 0
+    assert sum(1 for u in prov.l1_users if "c1w0 " in u) == 1 and not any("Error" in u for u in prov.l1_users)
+
+
+class BatchedGroupsProvider(Provider):
+    """Batched provider with a streaming path that reports one chunk as failed in the streamed pass."""
+    name = "bg"
+    batched = True
+
+    def __init__(self, bad=2):
+        super().__init__("bg")
+        self.bad = bad
+        self.batches = []
+
+    async def generate_batch(self, reqs):
+        self.batches.append([r.stage for r in reqs])
+        return [GenResult("ok %s %s" % (r.stage, r.tag), 5, 5) for r in reqs]
+
+    async def generate_groups(self, reqs, groups, build):
+        first = [GenResult("", error="boom") if i == self.bad else GenResult("s%d" % i, 5, 5)
+                 for i in range(len(reqs))]
+        second = []
+        for g, members in enumerate(groups):
+            r2 = build(g, [first[i] for i in members])
+            second.append(None if r2 is None else GenResult("l1 %d" % g, 5, 5))
+        self.batches.append(["streamed"])
+        return first, second
+
+
+def test_streamed_batched_failure_reruns_only_the_affected_batch():
+    prov = BatchedGroupsProvider(bad=2)
+    ex = LLMExecutor(config=_cfg(MAX_TOKENS=300), provider_obj=prov)
+    agg = ResultAggregator(executor=ex, max_tokens_per_batch=1500)
+    chunks = _chunks(9)
+    groups = agg.stream_plan(chunks)
+    assert groups and all(len(g) == len(groups[0]) for g in groups[:-1])
+    n = len(groups)
+    recs, l1 = asyncio.run(ex.process_chunks_streamed(chunks, "{transcript}", groups,
+                                                      lambda g, rs: agg.level1_request(g, n, rs)))
+    assert recs[2]["summary"] == "ok map 2" and "error" not in recs[2]  # retried through generate_batch
+    gbad = next(g for g, m in enumerate(groups) if 2 in m)
+    assert l1[gbad] is None and all(l1[g] is not None for g in range(n) if g != gbad)
+    assert ex.failed_requests == 0 and ex.total_requests == 9 + n
+    r = asyncio.run(agg.aggregate(recs, level1=(groups, l1)))
+    assert r["plan"]["calls"] == [n, 1] and r["plan"]["level1_streamed"]
+    assert prov.batches[-2] == ["reduce_l1"] and prov.batches[-1] == ["reduce_final"]
