@@ -67,6 +67,8 @@ def main() -> int:
                          "all-reduce latency and bandwidth measured on these GPUs at start-up")
     ap.add_argument("--no-hierarchical", action="store_true",
                     help="single-pass reduce over every summary (use a long-context model, e.g. llama3.1-8b)")
+    ap.add_argument("--stream-reduce", action="store_true",
+                    help="start each level-1 reduce batch as soon as its chunks are summarised (no map barrier)")
     ap.add_argument("--profile", default=None, metavar="DIR", help="torch.profiler trace of the timed steps")
     ap.add_argument("--log-level", default="WARNING")
     args = ap.parse_args()
@@ -95,7 +97,8 @@ def main() -> int:
                                    parallel=args.parallel)
     executor = LLMExecutor(config=cfg, provider_obj=provider)
     summarizer = TranscriptSummarizer(executor=executor, max_tokens_per_chunk=args.chunk_tokens,
-                                      hierarchical_aggregation=not args.no_hierarchical)
+                                      hierarchical_aggregation=not args.no_hierarchical,
+                                      stream_reduce=args.stream_reduce)
     transcript = synthetic_transcript(args.hours, seed=0)
     # weight init, KV allocation, planner measurements and the decode graphs of every batch bucket a
     # stage of this transcript can use: engine start-up, outside the timed region
@@ -133,8 +136,10 @@ def main() -> int:
     out = {
         "metric": "chunks/sec (whole node) + end-to-end wall-clock, 10h transcript, Llama-3-8B"
                   + ("" if args.model == "llama3-8b" and args.hours == 10.0 and not args.no_hierarchical
-                     else " [variant: %s, %gh%s]" % (args.model, args.hours,
-                                                     ", single-pass reduce" if args.no_hierarchical else "")),
+                     and not args.stream_reduce
+                     else " [variant: %s, %gh%s%s]" % (args.model, args.hours,
+                                                       ", single-pass reduce" if args.no_hierarchical else "",
+                                                       ", streamed level-1 reduce" if args.stream_reduce else "")),
         "value": round(value, 4),
         "unit": "chunks/s",
         "n_gpus": world,
