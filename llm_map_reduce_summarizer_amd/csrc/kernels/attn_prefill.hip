@@ -45,7 +45,6 @@ constexpr float RESCALE_LOG2 = 8.0f;  // deferred-rescale threshold (log2 units)
 
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
-typedef short v8s __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ int k_off(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
 __device__ __forceinline__ int v_off(int row, int chunk) { return row * 256 + ((chunk ^ ((row & 3) << 2)) << 4); }
@@ -104,77 +103,48 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
     // staging: thread loads rows tid/16 + 16i (i<4), chunk tid%16.  Named u32x4 registers and
     // UNCONDITIONAL loads (key clamped to the last row of the sequence; such rows are masked out of
     // the scores, and V rows stay finite) -- a conditional or lambda-captured prefetch made hipcc
-    // serialise the loop on vmcnt(0).  K runs one tile ahead of V (software pipeline, below).
+    // serialise the loop on vmcnt(0).
     const int st_chunk = tid & 15, st_row0 = tid >> 4;
     u32x4 kreg[4], vreg[4];
-#define LOAD_KV(tk, tv)                                                                           \
+#define LOAD_TILE(t)                                                                              \
     if constexpr (PAGED) {                                                                        \
-        const size_t pgk = (size_t)btab[tk] * Hkv * BN * D + head_pg + st_chunk * 8;              \
-        const size_t pgv = (size_t)btab[tv] * Hkv * BN * D + head_pg + st_chunk * 8;              \
+        const size_t pg = (size_t)btab[t] * Hkv * BN * D + head_pg + st_chunk * 8;                \
         _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                           \
-            kreg[i] = *reinterpret_cast<const u32x4*>(pk.kc + pgk + (size_t)(st_row0 + 16 * i) * D); \
-            vreg[i] = *reinterpret_cast<const u32x4*>(pk.vc + pgv + (size_t)(st_row0 + 16 * i) * D); \
+            kreg[i] = *reinterpret_cast<const u32x4*>(pk.kc + pg + (size_t)(st_row0 + 16 * i) * D); \
+            vreg[i] = *reinterpret_cast<const u32x4*>(pk.vc + pg + (size_t)(st_row0 + 16 * i) * D); \
         }                                                                                         \
     } else {                                                                                      \
         _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                           \
-            const int keyk = min((tk) * BN + st_row0 + 16 * i, len - 1);                         \
-            const int keyv = min((tv) * BN + st_row0 + 16 * i, len - 1);                         \
-            kreg[i] = *reinterpret_cast<const u32x4*>(base + (size_t)keyk * row_stride + st_chunk * 8 + kcol); \
-            vreg[i] = *reinterpret_cast<const u32x4*>(base + (size_t)keyv * row_stride + st_chunk * 8 + vcol); \
+            const int key = min((t) * BN + st_row0 + 16 * i, len - 1);                           \
+            const bf16* p = base + (size_t)key * row_stride + st_chunk * 8;                      \
+            kreg[i] = *reinterpret_cast<const u32x4*>(p + kcol);                                 \
+            vreg[i] = *reinterpret_cast<const u32x4*>(p + vcol);                                 \
         }                                                                                         \
     }
-#define STORE_K()                                                                                 \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                 \
-        *reinterpret_cast<u32x4*>(lds[0] + k_off(st_row0 + 16 * i, st_chunk)) = kreg[i];
-#define STORE_V()                                                                                 \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                 \
-        *reinterpret_cast<u32x4*>(lds[0] + BN * 256 + v_off(st_row0 + 16 * i, st_chunk)) = vreg[i];
+#define STORE_TILE(stage)                                                                         \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                               \
+        const int row = st_row0 + 16 * i;                                                         \
+        *reinterpret_cast<u32x4*>(lds[stage] + k_off(row, st_chunk)) = kreg[i];                  \
+        *reinterpret_cast<u32x4*>(lds[stage] + BN * 256 + v_off(row, st_chunk)) = vreg[i];       \
+    }
 
     f32x16 o[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
     float m = -INFINITY, l = 0.f;
 
+    LOAD_TILE(0);
+    STORE_TILE(0);
+    __syncthreads();
+
     const int wave_last_q = pre + qblock + 32 * w + 31;  // absolute position of the wave's last row
     const char* ldsK = lds[0];
     const char* ldsV = ldsK + BN * 256;
-    const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
-    // O^T[d][q] += V^T[d][key] P^T[key][q] for the tile in ldsV
-#define PV(pf_)                                                                                   \
-    _Pragma("unroll") for (int dt = 0; dt < 4; ++dt) {                                            \
-        const int col = dt * 32 + 16 * (g & 1) + 4 * p4; /* this lane's address column */         \
-        const int chunk = col >> 3, inoff = (col & 7) * 2;                                        \
-        _Pragma("unroll") for (int kt = 0; kt < 2; ++kt) {                                        \
-            _Pragma("unroll") for (int s = 0; s < 2; ++s) {                                       \
-                const int rowa = kt * 32 + 16 * s + 4 * (g >> 1) + q4;                            \
-                const int rowb = rowa + 8;                                                        \
-                const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(                           \
-                    (lds_v4s*)(ldsV + v_off(rowa, chunk) + inoff));                               \
-                const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(                           \
-                    (lds_v4s*)(ldsV + v_off(rowb, chunk) + inoff));                               \
-                const v8s a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};           \
-                o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),    \
-                                                                (pf_)[kt][s], o[dt], 0, 0, 0);    \
-            }                                                                                     \
-        }                                                                                         \
-    }
-
-    // Software pipeline (one tile of skew between the two products): iteration t holds K(t) and
-    // V(t-1) in LDS and issues S(t) = K(t).Q^T, then PV(t-1) = V(t-1).P(t-1), and only then the
-    // softmax of S(t) -- its VALU work runs while PV(t-1)'s MFMAs drain from the matrix pipe instead of
-    // serialising S -> softmax -> PV inside a tile.  The rare deferred rescale of o waits for PV(t-1)
-    // (o = (o + PV(t-1)) * alpha(t), as in the unpipelined order).
-    LOAD_KV(0, 0);
-    STORE_K();
-    __syncthreads();
-    bf16x8 pf[2][2];  // P(t-1) as the B operand of PV
-    bool prev = false;  // this wave computed tile t-1 (tiles wholly above its diagonal are skipped)
     for (int t = 0; t < ntiles; ++t) {
-        LOAD_KV(min(t + 1, ntiles - 1), t);
+        LOAD_TILE(min(t + 1, ntiles - 1));
         const int kv0 = t * BN;
-        const bool cur = kv0 <= wave_last_q;  // wave-uniform
-        f32x16 sacc[2];
-        if (cur) {
+        if (kv0 <= wave_last_q) {  // wave-uniform: tiles wholly above the diagonal are skipped
+            f32x16 sacc[2];
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt) {
                 sacc[kt] = f32x16{};
@@ -185,9 +155,6 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
                     sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kv), qf[ks], sacc[kt], 0, 0, 0);
                 }
             }
-        }
-        if (prev) PV(pf);
-        if (cur) {
             // mask + row max (key index of reg i: kt*32 + (i&3) + 8(i>>2) + 4half).  The causal/length
             // mask is only needed on tiles that reach past the wave's first query row or the sequence
             // end (wave-uniform test); scores stay unscaled until the exponent, which is one FMA:
@@ -224,6 +191,7 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
                 for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
             }
             float ls = 0.f;
+            bf16x8 pf[2][2];
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
@@ -234,18 +202,38 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
                 }
             }
             l += ls;
+            // O^T[d][q] += V^T[d][key] P^T[key][q]
+            const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const int col = dt * 32 + 16 * (g & 1) + 4 * p4;  // this lane's address column
+                const int chunk = col >> 3, inoff = (col & 7) * 2;
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const int rowa = kt * 32 + 16 * s + 4 * (g >> 1) + q4;
+                        const int rowb = rowa + 8;
+                        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (lds_v4s*)(ldsV + v_off(rowa, chunk) + inoff));
+                        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                            (lds_v4s*)(ldsV + v_off(rowb, chunk) + inoff));
+                        typedef short v8s __attribute__((ext_vector_type(8)));
+                        const v8s a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), pf[kt][s],
+                                                                        o[dt], 0, 0, 0);
+                    }
+                }
+            }
         }
-        prev = cur;
-        __syncthreads();  // every wave is done with K(t) and V(t-1)
-        STORE_K();        // K(t+1) (the last iteration rewrites K(t): never read again)
-        STORE_V();        // V(t)
         __syncthreads();
+        if (t + 1 < ntiles) {
+            STORE_TILE(0);
+            __syncthreads();
+        }
     }
-    if (prev) PV(pf);
-#undef LOAD_KV
-#undef STORE_K
-#undef STORE_V
-#undef PV
+#undef LOAD_TILE
+#undef STORE_TILE
 
     // normalise and store: reg i of tile dt holds d = dt*32 + (i&3) + 8(i>>2) + 4half for query qi
     const float lt = l + __shfl_xor(l, 32, 64);
