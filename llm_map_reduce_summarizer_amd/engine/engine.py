@@ -599,6 +599,124 @@ class LLMEngine:
                  torch.empty(0, dtype=self.dtype, device=self.device) for g in range(groups)]
         return firsts, packs
 
+    @staticmethod
+    def cp_slices(n: int, world: int) -> List[List[Tuple[int, int]]]:
+        """Zigzag context-parallel split of an ``n``-token prompt: 2 x world near-equal chunks, rank r
+        takes chunks r and 2 world - 1 - r, so every rank gets one early (cheap causal attention) and one
+        late (expensive) chunk -- balanced attention work; rank 0 holds the prompt's last token."""
+        b = [round(k * n / (2 * world)) for k in range(2 * world + 1)]
+        return [[(b[r], b[r + 1]), (b[2 * world - 1 - r], b[2 * world - r])] for r in range(world)]
+
+    def cp_preflight(self, prompt: Sequence[int], world: int) -> Optional[str]:
+        """Why prefill_export_cp cannot run here (None: it can) -- checked and agreed on by every rank
+        before the collective part starts."""
+        try:
+            self._new_seq(0, prompt, SamplingParams(1))
+        except ValueError as e:
+            return str(e)
+        if self.model.tp_size != 1 or self.model.hkv % world:
+            return "needs a TP=1 engine and Hkv divisible by %d" % world
+        if len(prompt) < 2 * world:
+            return "prompt of %d tokens is too short for %d ranks" % (len(prompt), world)
+        if self.kv.pages_for(len(prompt) + 1) > self.kv.alloc.available():
+            return "KV cache too small for %d tokens" % len(prompt)
+        return None
+
+    def prefill_export_cp(self, prompt: Sequence[int], params: SamplingParams, rank: int, world: int, group=None):
+        """Context-parallel prefill of ONE prompt over the ``world`` ranks of ``group`` (every rank calls
+        this with the same prompt on its full, TP=1 engine) for a TP=``world`` decode.
+
+        Each rank runs its zigzag slices (``cp_slices``) through all layers (model.prefill_cp); after each
+        layer's QKV stage the slices' K/V rows are all-gathered into every rank's paged cache, so the
+        slices' attention sees the whole prefix and, at the end, every rank holds the prompt's full KV.
+        Compute per rank is 1 / world of the prompt; the only traffic is each layer's K/V (128 KiB/token
+        over the whole Llama-3-8B stack, vs 2 x 32 x 8 KiB of activation all-reduces per token for a TP
+        forward), and no all-to-all is needed afterwards: each rank keeps the KV heads its TP shard owns.
+        Returns ``(first_token, kv)`` with kv [2, n_layers, pages, Hkv / world, page, head_dim] (this
+        rank's heads), the ImportedPrefill layout of the TP engine."""
+        import torch.distributed as dist
+        if self.model.tp_size != 1 or self.model.hkv % world:
+            raise ValueError("prefill_export_cp needs a TP=1 engine and Hkv divisible by %d" % world)
+        s = self._new_seq(0, prompt, SamplingParams(1, params.temperature, params.seed))
+        n = len(s.prompt)
+        if n < 2 * world:
+            raise ValueError("prompt of %d tokens is too short for context parallelism over %d ranks" % (n, world))
+        st, dev, P = self.state, self.device, self.page
+        need = self.kv.pages_for(n + 1)
+        if need > self.kv.alloc.available():
+            raise MemoryError("context-parallel prefill: KV cache too small for %d tokens" % n)
+        s.pages = self.kv.alloc.alloc(need)
+        s.slot = 0
+        try:
+            row = torch.zeros(self.max_pages, dtype=torch.int32)
+            row[:need] = torch.tensor(s.pages, dtype=torch.int32)
+            st.block_tables[0].copy_(row.to(dev, non_blocking=True))
+            st.max_new[0], st.gen_count[0], st.done[0], st.result[0] = 1, 0, 0, 0
+            st.temps[0], st.seeds[0] = float(params.temperature), int(params.seed)
+            slices = self.cp_slices(n, world)
+            mine = [(b, e) for b, e in slices[rank] if e > b]
+            passes = [self._pass_inputs([s], [span], paged=True) for span in mine]
+            # (page, row) of every position, per rank, for the K/V exchange
+            pg = torch.tensor(s.pages, dtype=torch.long)
+            idx = []
+            for q in range(world):
+                pos = torch.cat([torch.arange(b, e) for b, e in slices[q]])
+                idx.append((pg[pos // P].to(dev), (pos % P).to(dev), int(pos.numel())))
+            width = max(k for _, _, k in idx)
+            nccl = dist.get_backend(group) == "nccl"
+            kc, vc = self.kv.k, self.kv.v
+
+            def exchange(layer: int) -> None:
+                p0, r0, k0 = idx[rank]
+                mine_kv = torch.zeros(width, 2, self.model.hkv, self.cfg.head_dim, dtype=kc.dtype, device=dev)
+                mine_kv[:k0, 0] = kc[layer][p0, :, r0, :]
+                mine_kv[:k0, 1] = vc[layer][p0, :, r0, :]
+                if nccl:
+                    allkv = torch.empty((world,) + tuple(mine_kv.shape), dtype=kc.dtype, device=dev)
+                    dist.all_gather_into_tensor(allkv, mine_kv, group=group)
+                    parts = list(allkv.unbind(0))
+                else:
+                    parts = [torch.empty_like(mine_kv, device="cpu") for _ in range(world)]
+                    dist.all_gather(parts, mine_kv.cpu(), group=group)
+                for q in range(world):
+                    if q == rank:
+                        continue
+                    pq, rq, kq = idx[q]
+                    part = parts[q].to(dev)
+                    kc[layer][pq, :, rq, :] = part[:kq, 0]
+                    vc[layer][pq, :, rq, :] = part[:kq, 1]
+
+            t0 = time.perf_counter()
+            last = next((k for k, (b, e) in enumerate(mine) if e == n), None)
+            logits = self.model.prefill_cp(passes, st.block_tables, kc, vc, exchange, logits_pass=last)
+            self.stats["prefill_tokens"] += sum(e - b for b, e in mine)
+            self.stats["cp_prefills"] = self.stats.get("cp_prefills", 0) + 1
+            tok = 0
+            if logits is not None:
+                self._sample_first([s], logits)
+                tok = int(st.next_ids[0].item())
+            toks = [0] * world
+            if nccl:
+                t = torch.tensor([tok], dtype=torch.int64, device=dev)
+                out = [torch.empty_like(t) for _ in range(world)]
+                dist.all_gather(out, t, group=group)
+                toks = [int(x.item()) for x in out]
+            else:
+                dist.all_gather_object(toks, tok, group=group)
+            owner = next(q for q in range(world) if any(e == n for _, e in slices[q]))
+            first = toks[owner]
+            hl = self.model.hkv // world
+            npg = self.kv.pages_for(n)
+            pidx = torch.tensor(s.pages[:npg], dtype=torch.long, device=dev)
+            k = kc.index_select(1, pidx)[:, :, rank * hl:(rank + 1) * hl]
+            v = vc.index_select(1, pidx)[:, :, rank * hl:(rank + 1) * hl]
+            kv = torch.stack([k, v]).contiguous()
+            self._sync()
+            self.stats["prefill_s"] += time.perf_counter() - t0
+            return first, kv
+        finally:
+            self.kv.alloc.free(s.pages)
+
     def import_shape(self, prompt_len: int):
         """Shape of this engine's ImportedPrefill.kv for a prompt of ``prompt_len`` tokens."""
         return (2, self.cfg.n_layers, self.kv.pages_for(prompt_len), self.model.hkv, self.page, self.cfg.head_dim)

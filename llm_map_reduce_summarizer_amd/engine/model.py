@@ -303,6 +303,37 @@ class LlamaModel:
         x = ops.add_rmsnorm(s.pop("d"), s["res"], None, eps)
         return self.logits(x.index_select(0, last.last_rows), gather)
 
+    def prefill_cp(self, passes, block_tables: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
+                   exchange: Callable[[int], None], logits_pass: Optional[int] = None) -> Optional[torch.Tensor]:
+        """Context-parallel prefill (SURVEY §2.5 CP): ``passes`` are THIS rank's slices of one prompt (full
+        weights on every rank, no activation all-reduces), run layer-major.  After a layer's QKV stage has
+        written the slices' K/V rows into the local paged cache, ``exchange(layer)`` all-gathers every
+        rank's rows of that layer into every cache, so each slice's paged attention (causal offset = the
+        slice start) sees the whole prefix.  Returns the logits of ``passes[logits_pass]``'s last row (the
+        rank holding the prompt's end), else None."""
+        c = self.cfg
+        eps = c.rms_eps
+        page = kcache.shape[3]
+        st = []
+        for p in passes:
+            res = ops.embed(p.ids, self.embed)
+            st.append({"res": res, "x": ops.rmsnorm(res, None, eps)})
+        for i, lw in enumerate(self.layers):
+            qkvs = [ops.qkv_rope(s["x"], lw.wqkv, p.positions, p.seq_idx, block_tables, kcache[i], vcache[i],
+                                 self.cos_sin, self.hq, self.hkv, self.hd, page) for p, s in zip(passes, st)]
+            exchange(i)
+            for p, s, qkv in zip(passes, st, qkvs):
+                kw = {"seqlens": p.seqlens, "items": p.items} if qkv.is_cuda else {}
+                a = ops.attn_prefill(qkv, p.cu_seqlens, self.hq, self.hkv, self.hd, self.scale,
+                                     paged=p.paged.layer(kcache[i], vcache[i]), **kw)
+                x = ops.proj_add_rmsnorm(a, lw.wo, s["res"], None, eps, "o", None)
+                act = ops.gate_up_swiglu(x, lw.wgu)
+                s["x"] = ops.proj_add_rmsnorm(act, lw.wdown, s["res"], None, eps, "down", None)
+        if logits_pass is None:
+            return None
+        p, s = passes[logits_pass], st[logits_pass]
+        return self.logits(ops.rows(s["x"]).index_select(0, p.last_rows))
+
     def decode(self, ids: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, block_tables: torch.Tensor,
                kcache: torch.Tensor, vcache: torch.Tensor, workspace=None, gather: bool = True) -> torch.Tensor:
         """One token per sequence; context = positions + 1.  Returns logits [B, vocab] (or the local

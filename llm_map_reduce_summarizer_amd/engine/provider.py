@@ -288,6 +288,19 @@ class LocalEngineProvider(Provider):
         from .engine import ImportedPrefill
         t0 = time.perf_counter()
         world, rank = self.par.world, self.par.rank
+        if len(prompts) == 1 and len(prompts[0]) >= 2 * world:
+            # one prompt (the final reduce): context-parallel prefill over every rank instead of one rank
+            # prefilling it alone; every rank ends with its TP shard's KV heads, no all-to-all
+            # (rank-local faults were agreed on by the caller; the pre-flight check makes the ranks agree
+            # on their local resources BEFORE the per-layer all-gathers, which no rank may leave early)
+            pre = self.engine.cp_preflight(prompts[0], world)
+            errs = [x for x in pdist.all_gather_json(pre and "rank %d: %s" % (rank, pre)) if x]
+            if errs:
+                raise RuntimeError("context-parallel prefill: " + "; ".join(errs))
+            first, kv = self.engine.prefill_export_cp(prompts[0], sp[0], rank, world, group=pdist.tp_group_for(world))
+            self.timings["handoff_s"] = self.timings.get("handoff_s", 0.0) + time.perf_counter() - t0
+            self.timings["cp_prefills"] = self.timings.get("cp_prefills", 0) + 1
+            return {0: ImportedPrefill(first, kv)}
         owner = assign_balanced([len(p) for p in prompts], world)
         mine = [i for i in range(len(prompts)) if owner[i] == rank]
         tp_eng = self.tp_engine

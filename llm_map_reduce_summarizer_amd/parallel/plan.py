@@ -29,7 +29,8 @@ node, so the choice is a cost model whose hardware constants are *measured*:
 A TP stage may also prefill *disaggregated* (``handoff``): data-parallel on every rank's full
 TP=1 engine, then one all-to-all moves each prompt's KV heads to their TP owner -- the KV of a
 prompt is 128 KiB/token for Llama-3-8B, far less than the 2 x 32 activation all-reduces of
-8 KiB/token each that a TP prefill forward needs.
+8 KiB/token each that a TP prefill forward needs.  A single prompt is prefilled *context-parallel*
+instead (zigzag slices on every rank, per-layer K/V all-gather; every rank ends with the whole KV).
 
 The reference has a single form of parallelism, a semaphore-bounded fan-out of HTTPS calls
 (reference llm_executor.py:133-147); this module is the MI355X replacement for choosing how the
@@ -110,9 +111,20 @@ def _lpt(costs: Sequence[int], bins: int) -> List[List[int]]:
     return out
 
 
+def cp_prefill_s(d: ModelDims, hw: HWModel, tokens: int, world: int) -> float:
+    """Context-parallel prefill of ONE prompt over ``world`` ranks (engine.prefill_export_cp): each rank
+    runs 1 / world of the prompt (zigzag slices, balanced causal attention) through all layers and every
+    layer's K/V rows are all-gathered, so each rank receives (world - 1) / world of the prompt's KV."""
+    compute = prefill_s(d, hw, tokens, 1) / world
+    return compute + tokens * d.kv_bytes_per_token * (world - 1) / world / hw.ar_bw
+
+
 def handoff_prefill_s(d: ModelDims, hw: HWModel, prompt_lens: Sequence[int], world: int) -> float:
     """Disaggregated prefill of a TP=``world`` stage: the prompts are prefilled data-parallel on the
-    ranks' full (TP=1) engines, then every rank sends each TP peer its KV heads (one all-to-all)."""
+    ranks' full (TP=1) engines, then every rank sends each TP peer its KV heads (one all-to-all).  One
+    prompt (the final reduce) is prefilled context-parallel over all the ranks instead (cp_prefill_s)."""
+    if len(prompt_lens) == 1 and world > 1 and prompt_lens[0] >= 2 * world:
+        return cp_prefill_s(d, hw, prompt_lens[0], world)
     bins = _lpt(list(prompt_lens), world)
     compute = max(prefill_s(d, hw, sum(prompt_lens[i] for i in b), 1) for b in bins)
     kv = sum(prompt_lens) * d.kv_bytes_per_token
@@ -164,8 +176,9 @@ def choose(d: ModelDims, hw: HWModel, prompt_lens: Sequence[int], max_new: Seque
     best = min(cands, key=lambda tp: (est[tp], tp))
     out = {"tp": best, "estimates_s": {str(k): round(v, 3) for k, v in est.items()}}
     if best > 1 and best == world:
-        # disaggregated prefill only where it beats the TP forward: many prompts split over the ranks
-        # win, one long prompt (the final reduce) prefills faster as one TP forward over all GPUs
+        # disaggregated prefill only where it beats the TP forward: many prompts split over the ranks;
+        # one prompt (the final reduce) context-parallel, whose per-layer K/V all-gather moves a quarter
+        # of the TP forward's activation all-reduce bytes (Llama-3: 4 vs 16 KiB per token and layer)
         out["handoff"] = bool(handoff) and handoff_prefill_s(d, hw, prompt_lens, world) < \
             prefill_s(d, hw, sum(prompt_lens), world, max(prompt_lens))
     return out

@@ -45,6 +45,10 @@ PIPE = textwrap.dedent("""
     from llm_map_reduce_summarizer_amd.pipeline.orchestrator import TranscriptSummarizer
     from llm_map_reduce_summarizer_amd.utils.synth import synthetic_transcript
     opt = json.loads(os.environ["OPT"])
+    if opt.get("force_handoff"):
+        # the tiny preset's KV (128-dim heads) outweighs its 512-wide activations, so the cost model keeps
+        # its single-prompt stage on the TP forward; Llama-3 goes context-parallel (tests/test_plan.py)
+        LocalEngineProvider._handoff_pays = lambda self, prompts, reqs: self.handoff
     cfg = LLMConfig(MAX_TOKENS=6, RETRY_DELAY=0.05)
     prov = LocalEngineProvider(opt.get("model", "tiny-kv8"), cfg, device="cpu", max_model_len=4096,
                                engine_options={"kv_pages": 512, "max_num_seqs": 16},
@@ -66,7 +70,8 @@ PIPE = textwrap.dedent("""
            "plan": {k: rep["reduce_plan"][k] for k in ("levels", "calls")},
            "chunk_summaries": cap["s"],
            "failed": ex.failed_requests, "retried": ex.retried_requests, "owner_maps": prov.owner_maps, "stage_plan": st.get("stage_plan", {}),
-           "imported": st.get("tp_engine", {}).get("imported_prefills", 0), "seconds": time.time() - t0}
+           "imported": st.get("tp_engine", {}).get("imported_prefills", 0), "cp": st.get("cp_prefills", 0),
+           "seconds": time.time() - t0}
     print("RESULT " + json.dumps(out), flush=True)
     pdist.shutdown()
 """)
@@ -123,12 +128,14 @@ def test_dp_world_equals_single(single, world):
 
 
 def test_all_stages_tp8_with_handoff():
-    outs = _pipe(8, parallel="tp")
+    outs = _pipe(8, parallel="tp", force_handoff=True)
     assert all(o["summary"] == outs[0]["summary"] for o in outs)
     assert outs[0]["imported"] > 0  # TP stages prefilled data-parallel, KV moved by the 8-way all-to-all
     for stage, plan in outs[0]["stage_plan"].items():
         assert plan["tp"] == 8, (stage, plan)
     assert outs[0]["stage_plan"]["map"]["handoff"] is True
+    # the single-prompt final reduce prefilled context-parallel over the 8 ranks (no one-rank prefill)
+    assert outs[0]["stage_plan"]["reduce_final"]["handoff"] is True and all(o["cp"] >= 1 for o in outs)
 
 
 def test_reduce_tp4_map_dp4():
@@ -195,3 +202,47 @@ def test_persistent_fault_on_one_rank_is_consistent(world):
     assert all(o["retried"] == ref["retried"] for o in outs)
     assert all("injected engine fault on rank 1" in s for s in errs)
     _check_owner_maps(outs)
+
+
+CP_ENGINE = textwrap.dedent("""
+    import json, os, sys
+    sys.path.insert(0, %(root)r)
+    import torch
+    from llm_map_reduce_summarizer_amd.parallel import dist as pdist
+    pdist.init_distributed_from_env(backend="gloo", timeout_s=120)
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    from llm_map_reduce_summarizer_amd.engine.config import get_model_config
+    from llm_map_reduce_summarizer_amd.engine.engine import ImportedPrefill, LLMEngine, SamplingParams
+    cfg = get_model_config("tiny-kv8", init_std=0.05)
+    full = LLMEngine(cfg, device="cpu", max_model_len=1024, max_num_seqs=4, kv_pages=64, sync_every=3)
+    tp = LLMEngine(cfg, device="cpu", max_model_len=1024, max_num_seqs=4, kv_pages=64, sync_every=3,
+                   tp_rank=rank, tp_size=world, tp_group=pdist.tp_group_for(world))
+    prompt = [128000] + [(j * 37) %% 9000 + 5 for j in range(301)]
+    sp = SamplingParams(6, 0.0, 0)
+    first, kv = full.prefill_export_cp(prompt, sp, rank, world, group=pdist.tp_group_for(world))
+    # reference: the one-rank prefill_export of the same prompt (this rank's KV heads)
+    f1, packs = full.prefill_export([prompt], [sp], world)
+    ref = packs[rank].view(kv.shape)
+    err = float((kv.float() - ref.float()).abs().max())
+    cp_out = tp.generate([prompt], [sp], imported={0: ImportedPrefill(first, kv)})[0].token_ids
+    one = full.generate([prompt], [sp])[0].token_ids
+    print("RESULT " + json.dumps({"first": first, "f1": f1[0], "kv_err": err, "cp": cp_out, "one": one,
+                                  "free": full.kv.alloc.available(), "pages": full.kv.num_pages,
+                                  "cp_prefills": full.stats.get("cp_prefills", 0)}), flush=True)
+    pdist.shutdown()
+""")
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_context_parallel_prefill_matches_one_rank_prefill(world):
+    """Context-parallel prefill (zigzag slices per rank, per-layer K/V all-gather): every rank ends with
+    the same KV heads a one-rank prefill exports to it, the same first token, and the TP decode from it
+    generates what the TP=1 engine does (greedy; bf16 rounding of the slice order may flip a near-tie)."""
+    outs = _launch(CP_ENGINE % {"root": ROOT}, world, {})
+    for o in outs:
+        assert o["cp_prefills"] == 1 and o["free"] == o["pages"] - 1  # pages returned
+        assert o["kv_err"] < 0.05, o["kv_err"]
+        assert o["first"] == o["f1"] == outs[0]["first"]
+        assert o["cp"] == outs[0]["cp"]  # every TP rank samples the same tokens
+    same = sum(a == b for a, b in zip(outs[0]["cp"], outs[0]["one"]))
+    assert same >= len(outs[0]["one"]) - 1 or outs[0]["cp"][:3] == outs[0]["one"][:3], outs[0]

@@ -87,12 +87,18 @@ def test_per_row_all_reduce_cost_penalises_big_tp_batches():
     assert plan.decode_step_s(D8B, rowy, 48, 4000, 1) == plan.decode_step_s(D8B, base, 48, 4000, 1)
 
 
-def test_handoff_for_many_prompts_tp_forward_for_one():
+def test_handoff_for_many_prompts_context_parallel_for_one():
     hw = plan.with_measurements(plan.HWModel(), ar_lat_s=8e-6, ar_bw=150e9)
     many = plan.choose(D8B, hw, [3950] * 39, [1000] * 39, 8, handoff=True)
     one = plan.choose(D8B, hw, [23000], [1000], 8, handoff=True)
     assert many["tp"] == 8 and many["handoff"] is True
-    assert one["tp"] == 8 and one["handoff"] is False
+    # one prompt: context-parallel prefill (1/8 of the compute per rank + the K/V all-gather) beats both
+    # the TP forward (4x the bytes: activation all-reduces) and one rank prefilling alone
+    assert one["tp"] == 8 and one["handoff"] is True
+    cp = plan.cp_prefill_s(D8B, hw, 23000, 8)
+    assert cp == plan.handoff_prefill_s(D8B, hw, [23000], 8)
+    assert cp < plan.prefill_s(D8B, hw, 23000, 8) and cp < plan.prefill_s(D8B, hw, 23000, 1)
+    assert plan.cp_prefill_s(D8B, hw, 23000, 8) < plan.cp_prefill_s(D8B, hw, 23000, 2)
     # the handoff option never makes a TP stage look more expensive
     assert plan.stage_seconds(D8B, hw, [3950] * 39, [1000] * 39, 8, 8, True) <= \
         plan.stage_seconds(D8B, hw, [3950] * 39, [1000] * 39, 8, 8, False)
