@@ -716,6 +716,7 @@ class LLMEngine:
             return first, kv
         finally:
             self.kv.alloc.free(s.pages)
+            st.park_row(0)  # slot 0 was borrowed: idle again (stopped, pages -> scratch page 0)
 
     def import_shape(self, prompt_len: int):
         """Shape of this engine's ImportedPrefill.kv for a prompt of ``prompt_len`` tokens."""
