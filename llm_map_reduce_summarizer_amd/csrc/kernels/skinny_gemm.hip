@@ -430,16 +430,35 @@ __device__ __forceinline__ void mma_block8(f32x4 (&acc)[NT][MT], const A8Frag<NT
 }
 }  // namespace
 
-template <int NT, int MT, int EPI>
+// XL (M = 1): the x row slice [ks, ke) is staged in LDS once per workgroup and the B fragments are read
+// from there (a broadcast ds_read_b128 per k-step) -- otherwise every wave re-reads x from L2 for each
+// weight block, 4 KiB of VMEM requests per 2 KiB of fp8 weights, twice the weight traffic itself.
+template <int NT, int MT, int EPI, bool XL>
 __global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict__ x, int ldx,
                                                          const uint8_t* __restrict__ W,
                                                          const float* __restrict__ wscale, int K, int M,
                                                          void* __restrict__ out, int ldo, int kper) {
     constexpr int BN = 16 * NT, BM = 16 * MT;
+    static_assert(!XL || MT == 1, "the LDS x slice holds one row");
     __shared__ __attribute__((aligned(16))) float red[4][BM][BN + 4];
+    extern __shared__ __attribute__((aligned(16))) char xs[];  // XL: kper bf16 of x row 0
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int n0 = blockIdx.x * BN;
     const int ks = blockIdx.y * kper, ke = min(K, ks + kper);
+    if constexpr (XL) {
+        const uint4* src = reinterpret_cast<const uint4*>(x + ks);
+        for (int i = threadIdx.x; i < kper / 8; i += 256) reinterpret_cast<uint4*>(xs)[i] = src[i];
+        __syncthreads();
+    }
+    auto load_b = [&](BFrag<MT>& b, int kb) {
+        if constexpr (XL) {
+            const char* p = xs + (kb - ks + 16 * (lane >> 4)) * 2;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) b.v[0][i] = *reinterpret_cast<const uint4*>(p + (64 * (i >> 1) + 8 * (i & 1)) * 2);
+        } else {
+            load_b8<MT>(b, x, ldx, M, kb, lane);
+        }
+    };
 
     f32x4 acc[NT][MT];
 #pragma unroll
@@ -453,12 +472,12 @@ __global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict_
     if (kb < ke) load_a8<NT>(a0, W, K, n0, kb, lane);
     while (kb < ke) {
         const int kb1 = kb + 4 * KB;
-        load_b8<MT>(b, x, ldx, M, kb, lane);
+        load_b(b, kb);
         if (kb1 < ke) load_a8<NT>(a1, W, K, n0, kb1, lane);
         mma_block8<NT, MT>(acc, a0, b);
         if (kb1 >= ke) break;
         const int kb2 = kb1 + 4 * KB;
-        load_b8<MT>(b, x, ldx, M, kb1, lane);
+        load_b(b, kb1);
         if (kb2 < ke) load_a8<NT>(a0, W, K, n0, kb2, lane);
         mma_block8<NT, MT>(acc, a1, b);
         kb = kb2;
@@ -520,10 +539,14 @@ MRSUM_API int mrsum_skinny_fp8(const void* x, int ldx, const void* W, const floa
     const int mt = (M + 15) / 16;
     dim3 grid(N / (16 * nt), splits);
     auto X = (const bf16*)x; auto Wp = (const uint8_t*)W;
-#define L(NT_, MT_, EPI_) skinny_fp8_kernel<NT_, MT_, EPI_><<<grid, 256, 0, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper)
+    const bool xl = M == 1 && kper * 2 <= 56 * 1024;  // x slice in (default-limit) dynamic LDS
+#define L(NT_, MT_, EPI_) skinny_fp8_kernel<NT_, MT_, EPI_, false><<<grid, 256, 0, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper)
+#define L1(NT_, EPI_)                                                                                            \
+    if (xl) skinny_fp8_kernel<NT_, 1, EPI_, true><<<grid, 256, kper * 2, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper); \
+    else L(NT_, 1, EPI_)
 #define BY_MT(NT_, EPI_)                        \
     switch (mt) {                               \
-        case 1: L(NT_, 1, EPI_); break;         \
+        case 1: L1(NT_, EPI_); break;           \
         case 2: L(NT_, 2, EPI_); break;         \
         case 3: L(NT_, 3, EPI_); break;         \
         default: L(NT_, 4, EPI_); break;        \
@@ -537,6 +560,7 @@ MRSUM_API int mrsum_skinny_fp8(const void* x, int ldx, const void* W, const floa
         else { BY_MT(2, EPI_F32_PARTIAL) }
     }
 #undef BY_MT
+#undef L1
 #undef L
     return (int)hipGetLastError();
 }

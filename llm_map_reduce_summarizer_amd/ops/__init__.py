@@ -226,6 +226,15 @@ def _fp8_parts(hip, x, w, role, splits):
             return hip.fp8_linear_parts(x.h, w, cfg[1], stream_wpb=cfg[0], norm=x.norm)
         return hip.fp8_linear_parts(x, w, cfg[1], stream_wpb=cfg[0])
     x = rows(x)
+    if x.shape[0] == 1 and splits is None:
+        # one row: the x slice sits in LDS (skinny_fp8 XL), one 16-row tile per wave group and the
+        # largest split-K that keeps >= 2048 k per workgroup and <= 4096 workgroups -- measured best at
+        # Llama-3-70B shapes (profiles/r2_fp8_decode_x_in_lds_sweep.jsonl: qkv S=4, o S=4, down S=8;
+        # TP=8 shards sit at the ~9 us launch floor whatever the split)
+        N, K = w.shape
+        s = next(s for s in (8, 4, 2, 1) if (K // 128) % s == 0 and (K // s >= 2048 or s == 1)
+                 and N // 16 * s <= 4096)
+        return hip.fp8_linear_parts(x, w, s, 1)
     p = hip.plan(role, x.shape[0], w.shape[0], w.shape[1], stream=False)
     nt = p[1] if p[0] == "skinny" else 1
     s = splits or (p[2] if p[0] == "skinny" else (p[1] if p[0] == "lds" else 1))

@@ -393,6 +393,29 @@ def test_fp8_linear(M, N, K):
         _close(parts.sum(0), ref[:min(M, 64)], 2e-3, 2e-3)
 
 
+@pytest.mark.parametrize("N,K,S", [(256, 8192, 1), (128, 28672, 1), (128, 28672, 4), (96, 32768, 1), (64, 1024, 2)])
+def test_skinny_fp8_m1_x_in_lds(N, K, S):
+    """Register-streaming fp8 kernel at M = 1 (x slice staged in LDS when it fits 56 KiB: K / S <= 28672,
+    else x from global): bf16 out, split-K fp32 slabs and SwiGLU vs fp32 of the dequantised weights."""
+    from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight, interleave_gate_up
+    x = _rand(1, K, seed=60)
+    w = Fp8Weight.quantize(_rand(N, K, scale=0.05, seed=61))
+    ref = x.float() @ w.dequant().t()
+    if S == 1:
+        out = torch.empty(1, N, dtype=torch.bfloat16, device=DEV)
+        _close(hip._skinny_fp8(x, w, out, hip.EPI_BF16, 1, 1, N), ref, 2e-2)
+    parts = torch.empty(S, 1, N, dtype=torch.float32, device=DEV)
+    _close(hip._skinny_fp8(x, w, parts, hip.EPI_F32_PARTIAL, 2 if N % 32 == 0 else 1, S, N).sum(0), ref, 2e-3, 2e-3)
+    if S == 1:
+        wg = Fp8Weight.quantize(_rand(N, K, scale=0.05, seed=62))
+        wu = Fp8Weight.quantize(_rand(N, K, scale=0.05, seed=63))
+        g, u = x.float() @ wg.dequant().t(), x.float() @ wu.dequant().t()
+        wgu = Fp8Weight(interleave_gate_up(wg.q.view(torch.uint8), wu.q.view(torch.uint8)).view(torch.float8_e4m3fn)
+                        .contiguous(), interleave_gate_up(wg.scale[:, None], wu.scale[:, None])[:, 0].contiguous())
+        act = torch.empty(1, N, dtype=torch.bfloat16, device=DEV)
+        _close(hip._skinny_fp8(x, wgu, act, hip.EPI_SWIGLU, 1, 1, N), g * torch.sigmoid(g) * u, 3e-2)
+
+
 @pytest.mark.parametrize("M", [1, 9, 17, 40, 64])
 @pytest.mark.parametrize("N,K,wpb,S", [(640, 1024, 5, 1), (512, 2048, 4, 2), (896, 768, 7, 3), (1024, 512, 8, 2)])
 def test_stream_fp8(M, N, K, wpb, S):

@@ -34,9 +34,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ms", default="1")
     ap.add_argument("--ops", default="qkv,o,gate_up,down")
+    ap.add_argument("--tp", type=int, default=1, help="one rank's shard of a TP=tp engine")
     a = ap.parse_args()
     dev = "cuda:0"
-    shapes = {"qkv": (10240, 8192), "o": (8192, 8192), "gate_up": (57344, 8192), "down": (8192, 28672)}
+    t = a.tp
+    shapes = {"qkv": (10240 // t, 8192), "o": (8192, 8192 // t), "gate_up": (57344 // t, 8192),
+              "down": (8192, 28672 // t)}
     for name in a.ops.split(","):
         N, K = shapes[name]
         ncopy = max(2, int(1.2e9 // (N * K)))
@@ -79,7 +82,7 @@ def main():
                         cands.append(("stream", (wpb, S), lambda o=o, wpb=wpb, S=S: hip._stream_fp8(x, nxt(), o, hip.EPI_F32_PARTIAL, S, N, wpb)))
             for kind, cfg, f in cands:
                 us = min(timeit(f) for _ in range(2))
-                print(json.dumps({"op": name, "M": M, "kind": kind, "cfg": cfg, "us": round(us, 1),
+                print(json.dumps({"op": name, "tp": t, "M": M, "kind": kind, "cfg": cfg, "us": round(us, 1),
                                   "TBps": round(N * K / us / 1e6, 2)}), flush=True)
         del ws
         torch.cuda.empty_cache()
