@@ -326,9 +326,10 @@ def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
         fused = -(-pages // 16) <= 6  # the <= 6k context class
         if fused:
             splits = min(splits, 16)
-        elif pages <= 192:
+        elif pages <= 512:
             # the <= 12k class at B=1 (profiles/r2_attn_decode_b1_class1.jsonl, 7 rounds x 64 calls): 32 separate
-            # splits 18.6 / 17.5 us at 8k / 10k against 64 splits 18.9 / 18.8 and every fused variant >= 19.1
+            # splits 18.6 / 17.5 us at 8k / 10k against 64 splits 18.9 / 18.8 and every fused variant >= 19.1;
+            # the <= 32k class likewise (r2_attn_decode_b1_class2.jsonl: 16k 22.1 vs 24.1 us, 32k 32.5 vs 33.9)
             splits = min(splits, 32)
     else:
         fused = groups <= 128
