@@ -102,9 +102,11 @@ __device__ __forceinline__ float row_scale(const NormArgs& e, const float* s_ss,
 }
 
 // split-K arrival: every wave drained its write-through partial stores; returns true in the last of
-// the nsplit workgroups of column tile ``tile`` to arrive (after an agent-scope acquire), and re-arms
-// the ticket there.  The flag goes through the kernel's one LDS array (a second __shared__ object can
-// de-pipeline the ring: cdna_hip_programming.md "Projection GEMM at M = 256" item 4(a)).
+// the nsplit workgroups of column tile ``tile`` to arrive (after an agent-scope acquire).  The caller's
+// last arriver re-arms the ticket when it is done (rearm), off the reduction's critical path -- the
+// next launch's arrivals are ordered after it by the kernel boundary.  The flag goes through the
+// kernel's one LDS array (a second __shared__ object can de-pipeline the ring: cdna_hip_programming.md
+// "Projection GEMM at M = 256" item 4(a)).
 __device__ __forceinline__ bool last_arrival(int* counters, int tile, int nsplit, int tid, int* s_flag) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -115,14 +117,14 @@ __device__ __forceinline__ bool last_arrival(int* counters, int tile, int nsplit
     __syncthreads();
     const bool last = *s_flag != 0;
     if (last) {
-        if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         __syncthreads();
     }
     return last;
+}
+
+__device__ __forceinline__ void rearm(int* counters, int tile, int tid) {
+    if (tid == 0) __hip_atomic_store(counters + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 }  // namespace
 
@@ -241,6 +243,7 @@ __device__ __forceinline__ void stream_epilogue(f32x4 (&acc)[MT], char* lds, flo
                 o.y = pack2(g4.z / (1.f + __expf(-g4.z)) * u4.z, g4.w / (1.f + __expf(-g4.w)) * u4.w);
                 *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + (n0 >> 1) + 8 * bl + 4 * hf) = o;
             }
+            rearm(counters, blockIdx.x, tid);
         } else {
             // h = bf16(residual + partial 0 + partial 1 + ...) (add_rmsnorm_parts order), stored back; the
             // tile's per-row sum of h^2 (of the rounded values) to ssp[m][tile] in a fixed order.
@@ -295,6 +298,7 @@ __device__ __forceinline__ void stream_epilogue(f32x4 (&acc)[MT], char* lds, flo
                 for (int q = 0; q < Q; ++q) t += s_sq[mm * Q + q];
                 e.ssp[(size_t)mm * gridDim.x + blockIdx.x] = t;
             }
+            rearm(counters, blockIdx.x, tid);
         }
     }
 }
