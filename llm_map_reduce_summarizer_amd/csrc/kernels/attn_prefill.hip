@@ -2,11 +2,13 @@
 //
 // Packed batch: qkv [T, row_stride] bf16 (Q heads, then K heads, then V
 // heads, D=128 each, already rotated by rope_kv), cu_seqlens [nseq+1].
-// Work item = (sequence, 128-row query block) x query head; items are listed
+// Work item = (sequence, 256-row query block) x query head; items are listed
 // by the host heaviest-first (causal blocks late in a sequence do the most
 // key tiles), blockIdx.y = query head.
 //
-// Workgroup: 4 waves, wave w owns query rows [32w, 32w+32) of the block.
+// Workgroup: 8 waves (one per CU, 2 per SIMD at 209 VGPRs), wave w owns query rows [32w, 32w+32) of
+// the block: every staged K/V tile serves 256 query rows (8 x 4000-token / 32k prompts: +4-6 % over two
+// 4-wave 128-row workgroups per CU; 8 x 4096: -2 %, profiles/r2_attn_prefill_8wave_256rows_ab.jsonl).
 // Per 64-key tile (K and V staged through LDS, next tile prefetched into
 // registers while the current one is consumed - issue early / write late):
 //
@@ -39,8 +41,12 @@
 
 namespace {
 constexpr int D = 128;
-constexpr int BM = 128;  // query rows per workgroup
+constexpr int NW = 8;            // waves per workgroup (32 query rows each)
+constexpr int BM = 32 * NW;      // query rows per workgroup
+constexpr int NTHR = 64 * NW;
+constexpr int SROWS = NTHR / 16;  // tile rows staged per load round (16 lanes x 16 B per 256-B row)
 constexpr int BN = 64;   // keys per tile
+constexpr int SIT = BN / SROWS;   // load rounds per 64-row tile
 constexpr float RESCALE_LOG2 = 8.0f;  // deferred-rescale threshold (log2 units), see the softmax
 
 typedef short v4s __attribute__((ext_vector_type(4)));
@@ -62,7 +68,7 @@ struct PagedKV {
 };
 
 template <bool PAGED>
-__global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __restrict__ qkv, int row_stride,
+__global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __restrict__ qkv, int row_stride,
                                                               const int* __restrict__ cu_seqlens,
                                                               const int2* __restrict__ items,
                                                               bf16* __restrict__ out, int out_stride, int Hq,
@@ -100,30 +106,30 @@ __global__ __launch_bounds__(256, 2) void attn_prefill_kernel(const bf16* __rest
     const int kend = pre + min(len, qblock + BM);
     const int ntiles = (kend + BN - 1) / BN;
 
-    // staging: thread loads rows tid/16 + 16i (i<4), chunk tid%16.  Named u32x4 registers and
+    // staging: thread loads rows tid/16 + SROWS i (i < SIT), chunk tid%16.  Named u32x4 registers and
     // UNCONDITIONAL loads (key clamped to the last row of the sequence; such rows are masked out of
     // the scores, and V rows stay finite) -- a conditional or lambda-captured prefetch made hipcc
     // serialise the loop on vmcnt(0).
     const int st_chunk = tid & 15, st_row0 = tid >> 4;
-    u32x4 kreg[4], vreg[4];
+    u32x4 kreg[SIT], vreg[SIT];
 #define LOAD_TILE(t)                                                                              \
     if constexpr (PAGED) {                                                                        \
         const size_t pg = (size_t)btab[t] * Hkv * BN * D + head_pg + st_chunk * 8;                \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                           \
-            kreg[i] = *reinterpret_cast<const u32x4*>(pk.kc + pg + (size_t)(st_row0 + 16 * i) * D); \
-            vreg[i] = *reinterpret_cast<const u32x4*>(pk.vc + pg + (size_t)(st_row0 + 16 * i) * D); \
+        _Pragma("unroll") for (int i = 0; i < SIT; ++i) {                                           \
+            kreg[i] = *reinterpret_cast<const u32x4*>(pk.kc + pg + (size_t)(st_row0 + SROWS * i) * D); \
+            vreg[i] = *reinterpret_cast<const u32x4*>(pk.vc + pg + (size_t)(st_row0 + SROWS * i) * D); \
         }                                                                                         \
     } else {                                                                                      \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                           \
-            const int key = min((t) * BN + st_row0 + 16 * i, len - 1);                           \
+        _Pragma("unroll") for (int i = 0; i < SIT; ++i) {                                           \
+            const int key = min((t) * BN + st_row0 + SROWS * i, len - 1);                           \
             const bf16* p = base + (size_t)key * row_stride + st_chunk * 8;                      \
             kreg[i] = *reinterpret_cast<const u32x4*>(p + kcol);                                 \
             vreg[i] = *reinterpret_cast<const u32x4*>(p + vcol);                                 \
         }                                                                                         \
     }
 #define STORE_TILE(stage)                                                                         \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                               \
-        const int row = st_row0 + 16 * i;                                                         \
+    _Pragma("unroll") for (int i = 0; i < SIT; ++i) {                                               \
+        const int row = st_row0 + SROWS * i;                                                         \
         *reinterpret_cast<u32x4*>(lds[stage] + k_off(row, st_chunk)) = kreg[i];                  \
         *reinterpret_cast<u32x4*>(lds[stage] + BN * 256 + v_off(row, st_chunk)) = vreg[i];       \
     }
@@ -259,7 +265,7 @@ static int launch_prefill(const void* qkv, int row_stride, const int* cu_seqlens
                           hipStream_t s) {
     if (n_items <= 0) return 0;
     if (Dh != D || Hq % Hkv) return (int)hipErrorInvalidValue;
-    dim3 grid(n_items, Hq), block(256);
+    dim3 grid(n_items, Hq), block(NTHR);
     const float sl = scale * 1.4426950408889634f;
     auto Q = (const bf16*)qkv;
     auto IT = (const int2*)items;

@@ -219,7 +219,10 @@ def embed(ids: torch.Tensor, table: torch.Tensor, out: Optional[torch.Tensor] = 
 
 
 # ------------------------------------------------------------------ attention
-def prefill_items(seqlens, block_m: int = 128) -> torch.Tensor:
+PREFILL_BLOCK_M = 256  # query rows per prefill-attention workgroup (attn_prefill.hip BM: 8 waves x 32 rows)
+
+
+def prefill_items(seqlens, block_m: int = PREFILL_BLOCK_M) -> torch.Tensor:
     """(sequence, query-block start) work list, heaviest (latest) blocks first."""
     items = []
     for s, n in enumerate(seqlens):
