@@ -141,3 +141,26 @@ def test_feeder_follow_up_joins_running_batch_across_context_class():
     ref = e.generate([long_p + outs[0].token_ids], [SamplingParams(6, 0.0, 0)])[0]
     assert outs[2].token_ids == ref.token_ids
     assert outs[1].token_ids == e.generate([prompts[1]], [sp[1]])[0].token_ids
+
+
+def test_streamed_map_reduce_pipeline_on_gpu():
+    """The streamed map -> level-1 reduce (engine feeder, decode graphs across batch buckets) end to end on
+    the GPU engine: level 1 runs inside the map's generate call and the run completes with a summary."""
+    import asyncio
+
+    from llm_map_reduce_summarizer_amd.config import LLMConfig
+    from llm_map_reduce_summarizer_amd.engine.provider import LocalEngineProvider
+    from llm_map_reduce_summarizer_amd.pipeline.executor import LLMExecutor
+    from llm_map_reduce_summarizer_amd.pipeline.orchestrator import TranscriptSummarizer
+    from llm_map_reduce_summarizer_amd.utils.synth import synthetic_transcript
+    cfg = LLMConfig(MAX_TOKENS=12)
+    prov = LocalEngineProvider("tiny-gqa4", cfg, device="cuda:0", max_model_len=4096, ignore_eos=True,
+                               engine_options={"kv_pages": 512, "max_num_seqs": 16})
+    ex = LLMExecutor(config=cfg, provider_obj=prov)
+    summ = TranscriptSummarizer(executor=ex, max_tokens_per_chunk=1000, stream_reduce=True,
+                                aggregator_options={"max_tokens_per_batch": 60})
+    rep = asyncio.run(summ.summarize(synthetic_transcript(0.5, seed=3)))
+    st = prov.stats()
+    assert rep["reduce_plan"].get("level1_streamed") and rep["reduce_plan"]["calls"][0] >= 2
+    assert st.get("fed_requests", 0) == rep["reduce_plan"]["calls"][0] and st["generate_calls"] == 2
+    assert rep["summary"] and rep["failed_chunks"] == 0
