@@ -433,14 +433,19 @@ __device__ __forceinline__ void mma_block8(f32x4 (&acc)[NT][MT], const A8Frag<NT
 // XL (M = 1): the x row slice [ks, ke) is staged in LDS once per workgroup and the B fragments are read
 // from there (a broadcast ds_read_b128 per k-step) -- otherwise every wave re-reads x from L2 for each
 // weight block, 4 KiB of VMEM requests per 2 KiB of fp8 weights, twice the weight traffic itself.
+// XL also takes a deferred-RMSNorm input (stream_gemm.hip header): x = the un-normalised residual row,
+// ``ssq`` [1][ssq_tiles] its producer's per-tile sums of squares, reduced in the stream consumer's fixed
+// order (8 partials of ssq_tiles / 8 tiles, float4 steps) so both consumers scale by the same factor.
 template <int NT, int MT, int EPI, bool XL>
 __global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict__ x, int ldx,
                                                          const uint8_t* __restrict__ W,
                                                          const float* __restrict__ wscale, int K, int M,
-                                                         void* __restrict__ out, int ldo, int kper) {
+                                                         void* __restrict__ out, int ldo, int kper,
+                                                         const float* __restrict__ ssq, int ssq_tiles, float eps) {
     constexpr int BN = 16 * NT, BM = 16 * MT;
     static_assert(!XL || MT == 1, "the LDS x slice holds one row");
     __shared__ __attribute__((aligned(16))) float red[4][BM][BN + 4];
+    __shared__ float s_ss[8];
     extern __shared__ __attribute__((aligned(16))) char xs[];  // XL: kper bf16 of x row 0
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int n0 = blockIdx.x * BN;
@@ -448,6 +453,16 @@ __global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict_
     if constexpr (XL) {
         const uint4* src = reinterpret_cast<const uint4*>(x + ks);
         for (int i = threadIdx.x; i < kper / 8; i += 256) reinterpret_cast<uint4*>(xs)[i] = src[i];
+        if (ssq && threadIdx.x < 8) {
+            const int C = ssq_tiles / 8;
+            const float4* sp = reinterpret_cast<const float4*>(ssq + threadIdx.x * C);
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int q = 0; q < C / 4; ++q) {
+                const float4 v = sp[q];
+                a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+            }
+            s_ss[threadIdx.x] = (a.x + a.y) + (a.z + a.w);
+        }
         __syncthreads();
     }
     auto load_b = [&](BFrag<MT>& b, int kb) {
@@ -491,6 +506,13 @@ __global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict_
 #pragma unroll
             for (int j = 0; j < 4; ++j) red[w][16 * m + cm][16 * t + cn + j] = acc[t][m][j];
     __syncthreads();
+    float rs = 1.f;  // deferred-norm row scale (XL: one row)
+    if (XL && ssq) {
+        float t = 0.f;
+#pragma unroll
+        for (int p = 0; p < 8; ++p) t += s_ss[p];
+        rs = rsqrtf(t * (1.f / (float)K) + eps);
+    }
 
     constexpr int ITEMS = BM * (BN / 4);
     for (int it = threadIdx.x; it < ITEMS; it += 256) {
@@ -500,7 +522,7 @@ __global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict_
 #pragma unroll
         for (int j = 0; j < 4; ++j)
             v[j] = (red[0][m][n4 + j] + red[1][m][n4 + j] + red[2][m][n4 + j] + red[3][m][n4 + j]) *
-                   wscale[n0 + n4 + j];
+                   wscale[n0 + n4 + j] * rs;
         if constexpr (EPI == EPI_BF16) {
             uint2 o;
             o.x = pack2(v[0], v[1]);
@@ -516,7 +538,7 @@ __global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict_
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const float u = (red[0][m][n4 + H + j] + red[1][m][n4 + H + j] + red[2][m][n4 + H + j] +
-                                     red[3][m][n4 + H + j]) * wscale[n0 + n4 + H + j];
+                                     red[3][m][n4 + H + j]) * wscale[n0 + n4 + H + j] * rs;
                     rr[j] = v[j] / (1.f + __expf(-v[j])) * u;
                 }
                 uint2 o;
@@ -528,8 +550,11 @@ __global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict_
     }
 }
 
+// ssq (deferred-RMSNorm input, M = 1 with the x slice in LDS only): [1][ssq_tiles] fp32 row sums of squares
+// of x per producer tile, ssq_tiles % 32 == 0; the product is scaled by rsqrt(sum / K + eps).
 MRSUM_API int mrsum_skinny_fp8(const void* x, int ldx, const void* W, const float* wscale, int N, int K, int M,
-                               void* out, int ldo, int epi, int nt, int splits, hipStream_t s) {
+                               void* out, int ldo, int epi, int nt, int splits, const float* ssq, int ssq_tiles,
+                               float eps, hipStream_t s) {
     if (M <= 0) return 0;
     if (M > 64 || K % KB || splits < 1 || (K / KB) % splits || (nt != 1 && nt != 2) || N % (16 * nt))
         return (int)hipErrorInvalidValue;
@@ -540,9 +565,12 @@ MRSUM_API int mrsum_skinny_fp8(const void* x, int ldx, const void* W, const floa
     dim3 grid(N / (16 * nt), splits);
     auto X = (const bf16*)x; auto Wp = (const uint8_t*)W;
     const bool xl = M == 1 && kper * 2 <= 56 * 1024;  // x slice in (default-limit) dynamic LDS
-#define L(NT_, MT_, EPI_) skinny_fp8_kernel<NT_, MT_, EPI_, false><<<grid, 256, 0, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper)
+    if (ssq && (!xl || ssq_tiles <= 0 || ssq_tiles % 32)) return (int)hipErrorInvalidValue;
+#define L(NT_, MT_, EPI_)                                                                                        \
+    skinny_fp8_kernel<NT_, MT_, EPI_, false><<<grid, 256, 0, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper, nullptr, 0, 0.f)
 #define L1(NT_, EPI_)                                                                                            \
-    if (xl) skinny_fp8_kernel<NT_, 1, EPI_, true><<<grid, 256, kper * 2, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper); \
+    if (xl) skinny_fp8_kernel<NT_, 1, EPI_, true><<<grid, 256, kper * 2, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper, \
+                                                                             ssq, ssq_tiles, eps);             \
     else L(NT_, 1, EPI_)
 #define BY_MT(NT_, EPI_)                        \
     switch (mt) {                               \

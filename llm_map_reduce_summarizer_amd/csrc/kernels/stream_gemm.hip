@@ -468,7 +468,12 @@ __device__ __forceinline__ bf16x8 fp8x8_bf16(uint2 d) {
 }
 }  // namespace
 
-template <int MT, int EPI, int WPB>
+// XR (one x row, kper <= XR_MAX_K): the workgroup's whole x slice is DMA'd into LDS once, ahead of the
+// ring, and the ring carries weight pieces only -- at M = 1 the padded 16-row x images were a third of
+// every slot (15 copies of the clamped row), which left fewer weight bytes in flight per CU.
+constexpr int XR_MAX_K = 8192;
+
+template <int MT, int EPI, int WPB, bool XR>
 __global__ __launch_bounds__(64 * WPB, 1) void stream_fp8_kernel(const bf16* __restrict__ x, int ldx,
                                                                  const unsigned char* __restrict__ W,
                                                                  const float* __restrict__ wscale, int K, int M,
@@ -476,13 +481,18 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_fp8_kernel(const bf16* __r
                                                                  float* __restrict__ parts, int* __restrict__ counters,
                                                                  const NormArgs e) {
     constexpr int R = 16 * WPB, BM = 16 * MT;
-    constexpr int WBYTES = R * 256, XBYTES = BM * 256, SLOT = WBYTES + 2 * XBYTES;
-    constexpr int D = (LDS_BUDGET / SLOT) < 6 ? (LDS_BUDGET / SLOT) : 6;
+    constexpr int WBYTES = R * 256, XBYTES = BM * 256, SLOT = XR ? WBYTES : WBYTES + 2 * XBYTES;
+    constexpr int XRES = XR ? XR_MAX_K * 2 : 0;  // resident x row image (bf16)
+    constexpr int DCAP = XR ? 8 : 6;
+    constexpr int D = ((LDS_BUDGET - XRES) / SLOT) < DCAP ? ((LDS_BUDGET - XRES) / SLOT) : DCAP;
     static_assert(D >= 2, "ring too shallow");
-    constexpr int XP = 2 * (2 * BM / 8);         // x pieces per slot: two 128-k images
+    static_assert(!XR || MT == 1, "resident x: one row");
+    constexpr int XP = XR ? 0 : 2 * (2 * BM / 8);  // x pieces per slot: two 128-k images
     constexpr int XI = (XP + WPB - 1) / WPB;
     constexpr int NI = 4 + XI;
-    __shared__ __attribute__((aligned(1024))) char lds[D * SLOT + LDS_XTRA];
+    __shared__ __attribute__((aligned(1024))) char lds[D * SLOT + XRES + LDS_XTRA];
+    char* const xres = lds + D * SLOT;      // XR: x[0][ks .. ks + kper) as bf16
+    char* const xtra = lds + D * SLOT + XRES;  // dummy x pieces | row-norm partials
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int n0 = blockIdx.x * R;
@@ -498,8 +508,8 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_fp8_kernel(const bf16* __r
     }
     // x piece q: image q / (2 BM / 8) (k half of the 256-wide block), then the bf16 piece layout
     constexpr int XPI = 2 * BM / 8;  // pieces per image
-    const bf16* xsrc[XI];
-    int xdst[XI];
+    const bf16* xsrc[XI > 0 ? XI : 1];
+    int xdst[XI > 0 ? XI : 1];
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
         const int q = w + WPB * i;
@@ -514,11 +524,16 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_fp8_kernel(const bf16* __r
         char* base = lds + (slot) * SLOT;                                                            \
         _Pragma("unroll") for (int p = 0; p < 4; ++p) glds16<2>(wsrc[p] + (kb), base + (4 * w + p) * 1024); \
         _Pragma("unroll") for (int i = 0; i < XI; ++i)                                               \
-            glds16(xsrc[i] + (kb), xdst[i] >= 0 ? base + xdst[i] : lds + D * SLOT);                  \
+            glds16(xsrc[i] + (kb), xdst[i] >= 0 ? base + xdst[i] : xtra);                            \
     }
     f32x4 acc[MT];
 #pragma unroll
     for (int m = 0; m < MT; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (XR) {
+        // the x slice as contiguous 1 KiB pieces (512 bf16), issued before the ring prologue: the first
+        // counted ring wait (every op older than the newest D-2 slots) covers them
+        for (int p = w; p < kper / 512; p += WPB) glds16(x + ks + 512 * p + 8 * lane, xres + 1024 * p);
+    }
 #pragma unroll
     for (int s = 0; s < D - 1; ++s) ISSUE8(s, min(s, nkb - 1) * KB8);
 
@@ -534,11 +549,16 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_fp8_kernel(const bf16* __r
         for (int i = 0; i < 8; ++i) {  // 32-k MFMA steps: fp8 bytes 32 i + 8 g .. +8 of the row
             const uint2 araw = *reinterpret_cast<const uint2*>(wl + img_off(16 * w + r, 2 * i + (g >> 1)) + 8 * (g & 1));
             const bf16x8 av = fp8x8_bf16(araw);
+            if constexpr (XR) {  // every lane reads row 0 (broadcast); rows >= M are never stored
+                const u32x4 bv = *reinterpret_cast<const u32x4*>(xres + 2 * (KB8 * j + 32 * i + 8 * g));
+                acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, bv), acc[0], 0, 0, 0);
+            } else {
 #pragma unroll
-            for (int m = 0; m < MT; ++m) {
-                const u32x4 bv = *reinterpret_cast<const u32x4*>(xl + (i >> 2) * XBYTES +
-                                                                 img_off(16 * m + r, 4 * (i & 3) + g));
-                acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, bv), acc[m], 0, 0, 0);
+                for (int m = 0; m < MT; ++m) {
+                    const u32x4 bv = *reinterpret_cast<const u32x4*>(xl + (i >> 2) * XBYTES +
+                                                                     img_off(16 * m + r, 4 * (i & 3) + g));
+                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, bv), acc[m], 0, 0, 0);
+                }
             }
         }
     }
@@ -550,8 +570,7 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_fp8_kernel(const bf16* __r
     for (int m = 0; m < MT; ++m) {
         acc[m][0] *= sc.x; acc[m][1] *= sc.y; acc[m][2] *= sc.z; acc[m][3] *= sc.w;
     }
-    stream_epilogue<MT, EPI, WPB>(acc, lds, reinterpret_cast<float*>(lds + D * SLOT + 1024), n0, M, out, ldo, parts,
-                                  counters, e);
+    stream_epilogue<MT, EPI, WPB>(acc, lds, reinterpret_cast<float*>(xtra + 1024), n0, M, out, ldo, parts, counters, e);
 }
 
 // Same contract as mrsum_stream_gemm (epilogues BF16 / F32_PARTIAL / SWIGLU / RESID_SPLIT, deferred
@@ -576,8 +595,17 @@ MRSUM_API int mrsum_stream_fp8(const void* x, int ldx, const void* W, const floa
     auto X = (const bf16*)x;
     auto Wp = (const unsigned char*)W;
     auto P = (float*)parts;
-#define L8(MT_, EPI_, WPB_) \
-    stream_fp8_kernel<MT_, EPI_, WPB_><<<grid, block, 0, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper, P, counters, e)
+    // one row: x resident in LDS (weight-only ring)
+    const bool xr = M == 1 && kper <= XR_MAX_K && kper % 512 == 0;
+#define L8(MT_, EPI_, WPB_)                                                                                      \
+    do {                                                                                                         \
+        if (MT_ == 1 && xr)                                                                                      \
+            stream_fp8_kernel<1, EPI_, WPB_, true><<<grid, block, 0, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper, P, \
+                                                                          counters, e);                          \
+        else                                                                                                     \
+            stream_fp8_kernel<MT_, EPI_, WPB_, false><<<grid, block, 0, s>>>(X, ldx, Wp, wscale, K, M, out, ldo,  \
+                                                                             kper, P, counters, e);              \
+    } while (0)
 #define BY_WPB8(MT_, EPI_)                          \
     switch (wpb) {                                  \
         case 4: L8(MT_, EPI_, 4); break;            \

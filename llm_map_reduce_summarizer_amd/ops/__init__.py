@@ -225,16 +225,19 @@ def _fp8_parts(hip, x, w, role, splits):
         if isinstance(x, NormRows):
             return hip.fp8_linear_parts(x.h, w, cfg[1], stream_wpb=cfg[0], norm=x.norm)
         return hip.fp8_linear_parts(x, w, cfg[1], stream_wpb=cfg[0])
-    x = rows(x)
     if x.shape[0] == 1 and splits is None:
         # one row: the x slice sits in LDS (skinny_fp8 XL), one 16-row tile per wave group and the
         # largest split-K that keeps >= 2048 k per workgroup and <= 4096 workgroups -- measured best at
         # Llama-3-70B shapes (profiles/r2_fp8_decode_x_in_lds_sweep.jsonl: qkv S=4, o S=4, down S=8;
-        # TP=8 shards sit at the ~9 us launch floor whatever the split)
+        # TP=8 shards sit at the ~9 us launch floor whatever the split); a deferred norm is applied in
+        # its epilogue
         N, K = w.shape
         s = next(s for s in (8, 4, 2, 1) if (K // 128) % s == 0 and (K // s >= 2048 or s == 1)
                  and N // 16 * s <= 4096)
-        return hip.fp8_linear_parts(x, w, s, 1)
+        if isinstance(x, NormRows) and hip.skinny_fp8_takes_norm(1, K, s):
+            return hip.fp8_linear_parts(x.h, w, s, 1, norm=x.norm)
+        return hip.fp8_linear_parts(rows(x), w, s, 1)
+    x = rows(x)
     p = hip.plan(role, x.shape[0], w.shape[0], w.shape[1], stream=False)
     nt = p[1] if p[0] == "skinny" else 1
     s = splits or (p[2] if p[0] == "skinny" else (p[1] if p[0] == "lds" else 1))
@@ -318,7 +321,7 @@ def _resid_cfg(hip, a, w, role):
     if M > DEFER_NORM_MAX_M:
         return None
     if isinstance(w, Fp8Weight):
-        cfg = hip.fp8_stream_cfg(M, w.shape[0], w.shape[1])
+        cfg = hip.fp8_resid_cfg(M, w.shape[0], w.shape[1])
     else:
         p = hip.plan(role, M, w.shape[0], w.shape[1])
         cfg = p[1:] if p[0] == "stream" else None
@@ -387,7 +390,7 @@ def gate_up_swiglu(x, wgu):
     xt = x.h if isinstance(x, NormRows) else x
     if _use_hip(xt) and isinstance(wgu, Fp8Weight):
         from . import hip
-        if isinstance(x, NormRows) and hip.fp8_stream_cfg(x.shape[0], wgu.shape[0], x.shape[1], swiglu=True):
+        if isinstance(x, NormRows) and hip.fp8_swiglu_takes_norm(x.shape[0], wgu.shape[0], x.shape[1]):
             return hip.fp8_linear_swiglu(x.h, wgu, norm=x.norm)
         return hip.fp8_linear_swiglu(rows(x), wgu)
     if _use_hip(xt):

@@ -42,7 +42,8 @@ _SIGS = {
                           _vp, _c_int, _c_float, _vp, _c_int, _vp, _vp],
     "mrsum_stream_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp,
                          _vp, _c_int, _c_float, _vp, _c_int, _vp, _vp],
-    "mrsum_skinny_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
+    "mrsum_skinny_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp,
+                         _c_int, _c_float, _vp],
     "mrsum_quant_fp8_rows": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_sample_keys": [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
@@ -834,7 +835,12 @@ def quant_fp8_rows(x: torch.Tensor):
     return q, sc
 
 
-def _skinny_fp8(x, w, out, epi, nt, splits, ldo):
+def skinny_fp8_takes_norm(M: int, K: int, splits: int = 1) -> bool:
+    """Does the register-streaming fp8 kernel take a deferred-RMSNorm input (one row, x slice in LDS)?"""
+    return M == 1 and K % 128 == 0 and (K // 128) % splits == 0 and (K // splits) * 2 <= 56 * 1024
+
+
+def _skinny_fp8(x, w, out, epi, nt, splits, ldo, norm=None):
     _bf16_cuda(x)
     _rows_ok(x)
     M, K = x.shape
@@ -844,8 +850,10 @@ def _skinny_fp8(x, w, out, epi, nt, splits, ldo):
     _req(w.scale.dtype == torch.float32 and w.scale.numel() == N, "skinny_fp8: scale")
     _req(1 <= M <= SKINNY_MAX_M and K % 128 == 0 and N % (16 * nt) == 0 and (K // 128) % splits == 0,
          "skinny_fp8: unsupported shape M=%d N=%d K=%d nt=%d S=%d" % (M, N, K, nt, splits))
+    _req(norm is None or skinny_fp8_takes_norm(M, K, splits), "skinny_fp8: a deferred norm needs M = 1")
+    sq, tiles, eps = _norm_args(x, norm)
     _check(_fn("mrsum_skinny_fp8")(_p(x), x.stride(0), _p(w.q), _p(w.scale), N, K, M, _p(out), ldo, epi, nt, splits,
-                                   _stream()), "skinny_fp8")
+                                   sq, tiles, eps, _stream()), "skinny_fp8")
     return out
 
 
@@ -914,24 +922,49 @@ def fp8_linear(x: torch.Tensor, w, swiglu: bool = False, norm=None) -> torch.Ten
 def fp8_linear_parts(x: torch.Tensor, w, splits: int, nt: int = 1, stream_wpb: Optional[int] = None,
                      norm=None) -> torch.Tensor:
     """fp32 split-K slabs [splits, M, N] of x @ (scale * W8)^T: the fp8 stream GEMM when ``stream_wpb`` is
-    given (its own split count; ``norm``: deferred-RMSNorm input), else the register-streaming kernel."""
+    given (its own split count), else the register-streaming kernel; ``norm``: deferred-RMSNorm input (the
+    stream kernel at any M, the register-streaming one at M = 1)."""
     M, K = x.shape
     N = w.q.shape[0]
     out = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
     if stream_wpb is not None:
         return _stream_fp8(x, w, out, EPI_F32_PARTIAL, splits, N, stream_wpb, norm=norm)
-    _req(norm is None, "fp8_linear_parts: a deferred norm needs the stream kernel")
-    return _skinny_fp8(x, w, out, EPI_F32_PARTIAL, nt, splits, N)
+    return _skinny_fp8(x, w, out, EPI_F32_PARTIAL, nt, splits, N, norm=norm)
+
+
+def fp8_swiglu_takes_norm(M: int, F2: int, K: int) -> bool:
+    """Does the decode gate_up + SwiGLU of this shape consume a deferred RMSNorm (no materialised rows)?"""
+    return fp8_stream_cfg(M, F2, K, swiglu=True) is not None or skinny_fp8_takes_norm(M, K)
 
 
 def fp8_linear_swiglu(x: torch.Tensor, w, norm=None) -> torch.Tensor:
     M = x.shape[0]
     F2 = w.q.shape[0]
     cfg = fp8_stream_cfg(M, F2, x.shape[1], swiglu=True)
-    _req(norm is None or cfg is not None, "fp8_linear_swiglu: a deferred norm needs the stream kernel")
+    _req(norm is None or fp8_swiglu_takes_norm(M, F2, x.shape[1]),
+         "fp8_linear_swiglu: a deferred norm needs the stream kernel or one row")
     if M > SKINNY_MAX_M:
         return fp8_linear(x, w, swiglu=True)
     out = torch.empty(M, F2 // 2, dtype=torch.bfloat16, device=x.device)
     if cfg is not None:
         return _stream_fp8(x, w, out, EPI_SWIGLU, 1, F2 // 2, cfg[0], norm=norm)
-    return _skinny_fp8(x, w, out, EPI_SWIGLU, 1, 1, F2 // 2)
+    return _skinny_fp8(x, w, out, EPI_SWIGLU, 1, 1, F2 // 2, norm=norm)
+
+
+def fp8_resid_cfg(M: int, N: int, K: int):
+    """(wpb, S) of the fp8 deferred-RMSNorm producer (stream kernel, split-K residual update), or None.
+    Where the plan streams M <= 8 rows through the register-streaming kernel (large N K), one row still
+    goes through the stream kernel with the x row resident in LDS: measured at Llama-3-70B o / down
+    (profiles/r2_fp8_stream_xres_sweep.jsonl, us) wpb 8 S 4: o 16.7 vs 15.7 register-streaming, down 49.5
+    vs 50.5 -- and it removes the separate add + RMSNorm launch (6.9 us) behind each of them."""
+    cfg = fp8_stream_cfg(M, N, K)
+    if cfg is not None or M != 1 or K % 256:
+        return cfg
+    for wpb in (8, 4):
+        if N % (16 * wpb):
+            continue
+        tiles = N // (16 * wpb)
+        for S in range(1, 17):
+            if (K // 256) % S == 0 and tiles * S >= N_CU and K // S <= 8192 and (K // S) % 512 == 0:
+                return (wpb, S)
+    return None

@@ -541,7 +541,8 @@ def test_tp_shard_decode_blocks(tp, M):
 
 @pytest.mark.parametrize("M", [1, 39, 64])
 @pytest.mark.parametrize("fp8", [False, True])
-@pytest.mark.parametrize("N,K,wpb,S", [(4096, 4096, 4, 4), (4096, 14336, 4, 4), (2048, 1024, 8, 2), (4096, 2048, 4, 1)])
+@pytest.mark.parametrize("N,K,wpb,S", [(4096, 4096, 4, 4), (4096, 14336, 4, 4), (2048, 1024, 8, 2), (4096, 2048, 4, 1),
+                                       (8192, 8192, 8, 4), (8192, 28672, 8, 4)])
 def test_stream_resid_and_norm_consumer(M, fp8, N, K, wpb, S):
     """The deferred-RMSNorm kernels at every decode M (ops uses them up to DEFER_NORM_MAX_M rows): the
     split-K residual-update producer (bf16 / fp8 weights) vs fp32, its per-tile sums of squares, and a
@@ -609,7 +610,7 @@ def test_deferred_norm_decode_layer(M, fp8):
     _close(nr.materialize(), h2, 3e-2, 3e-2)
     # gate_up + SwiGLU consumes the deferred norm
     # a consumer on the stream kernel takes the deferred norm (fp32 oracle); others get materialised bf16 rows
-    takes = hip.fp8_stream_cfg(M, 2 * ffn, hid, swiglu=True) is not None if fp8 else \
+    takes = hip.fp8_swiglu_takes_norm(M, 2 * ffn, hid) if fp8 else \
         hip.plan("gate_up", M, 2 * ffn, hid)[0] in ("stream", "stream_split")
     _close(ops.gate_up_swiglu(nr, wgu), swiglu32((rms32(r2) if takes else h2.float()) @ w32(wgu).t()),
            3e-2, 5e-2)
@@ -651,3 +652,27 @@ def test_deferred_norm_decode_layer(M, fp8):
         torch.cuda.synchronize()
         _close(out["act"], ref, 3e-2, 5e-2)
     assert all(int(t.abs().sum()) == 0 for t in hip._TILE_COUNTERS.values())
+
+
+@pytest.mark.parametrize("N,K,S", [(10240, 8192, 4), (1024, 8192, 1), (512, 28672, 8), (256, 4096, 2)])
+def test_skinny_fp8_deferred_norm(N, K, S):
+    """One decode row through the register-streaming fp8 kernel with the x slice in LDS, consuming a deferred
+    RMSNorm (per-tile sums of squares of the un-normalised row): split-K slabs, bf16 and SwiGLU epilogues
+    against the fp32 oracle rmsnorm(h) @ W^T -- the Llama-3-70B M = 1 qkv / gate_up consumers."""
+    from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight
+    h = _rand(1, K, seed=110) * 3
+    tiles = 64
+    ssq = h.float().pow(2).view(1, tiles, K // tiles).sum(-1).contiguous()
+    hf = h.float()
+    xn = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5)
+    w = Fp8Weight.quantize(_rand(N, K, scale=0.02, seed=111))
+    ref = xn @ w.dequant().t()
+    assert hip.skinny_fp8_takes_norm(1, K, S)
+    parts = hip.fp8_linear_parts(h, w, S, 1, norm=(ssq, 1e-5))
+    _close(parts.sum(0), ref, 2e-3, 2e-3)
+    out = torch.empty(1, N, dtype=torch.bfloat16, device=DEV)
+    _close(hip._skinny_fp8(h, w, out, hip.EPI_BF16, 1, 1, N, norm=(ssq, 1e-5)), ref, 2e-2, 2e-2)
+    g, u = reference.split_gate_up(ref)
+    act = torch.empty(1, N // 2, dtype=torch.bfloat16, device=DEV)
+    _close(hip._skinny_fp8(h, w, act, hip.EPI_SWIGLU, 1, 1, N // 2, norm=(ssq, 1e-5)), g * torch.sigmoid(g) * u,
+           3e-2, 3e-2)
