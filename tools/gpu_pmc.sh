@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -s KILL 60 python3 tools/pmc_kernels.py > gpurun_out/pmc_plain.log 2>&1 || exit $?
+timeout -s KILL 180 python3 tools/pmc_kernels.py > gpurun_out/pmc_plain.log 2>&1 || exit $?
 i=0
 for CTRS in ${PASSES:-"FETCH_SIZE" "SQ_VALU_MFMA_BUSY_CYCLES"}; do
   i=$((i + 1))

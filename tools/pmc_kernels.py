@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """A lean, graph-free set of kernel launches for rocprofv3 --pmc passes (tools/gpu_pmc.sh): the
 Llama-3-8B decode GEMMs at M=1 and M=39 (our LDS-DMA stream kernel, fused epilogues), paged decode
-attention at B=1/39 x 4k context, and the prefill flash attention on 4 x 4k tokens.  Few dispatches,
+attention at B=1/39 x 4k context, the prefill flash attention on 4 x 4k tokens and the prefill GEMMs
+(bf16 at M = 16384, fp8 at a 70B shape).  Few dispatches,
 so the per-dispatch counter serialisation stays cheap."""
 import math
 import os
@@ -48,6 +49,16 @@ def main():
     items = hip.prefill_items(lens).to(dev)
     for _ in range(3):
         hip.attn_prefill(qkv, cu, 32, 8, hd, 1 / math.sqrt(hd), seqlens=lens, items=items)
+    # prefill GEMMs (gemm.hip, 256 x 256 tiles): bf16 qkv / gate_up + SwiGLU at M = 16384, fp8 gate_up at
+    # a Llama-3-70B shape (M = 8192)
+    xp = torch.randn(16384, hid, **bf)
+    for _ in range(2):
+        hip.gemm(xp, W["qkv"])
+        ops.linear_swiglu(xp, W["gate_up"])
+    w8 = reference.Fp8Weight.quantize(torch.randn(2 * 28672, 8192, **bf) * 0.02)
+    x8 = torch.randn(8192, 8192, **bf)
+    for _ in range(2):
+        hip.fp8_linear(x8, w8, swiglu=True)
     torch.cuda.synchronize()
     print("pmc kernels done", flush=True)
 

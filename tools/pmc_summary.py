@@ -32,8 +32,8 @@ def main(root):
         for c, v in cs.items():
             a[c] += v
     extra = sorted({c for a in agg.values() for c in a if c.startswith("SQ_WAIT") or c.startswith("SQ_ACTIVE")})
-    print("%-70s %6s %9s %9s %8s %8s %s" % ("kernel", "calls", "mean_us", "read_MB", "TB/s", "mfma%",
-                                             " ".join("%%%s" % c[3:] for c in extra)))
+    print("%-70s %6s %9s %9s %8s %8s %8s %s" % ("kernel", "calls", "mean_us", "read_MB", "TB/s", "mfma%", "ldsconf%",
+                                                 " ".join("%%%s" % c[3:] for c in extra)))
     for k, a in sorted(agg.items(), key=lambda kv: -kv[1]["us"])[:30]:
         n = a["n"]
         us = a["us"] / n
@@ -42,9 +42,12 @@ def main(root):
         mf = ""
         if "SQ_VALU_MFMA_BUSY_CYCLES" in a and us:
             mf = "%.1f" % (100.0 * a["SQ_VALU_MFMA_BUSY_CYCLES"] / n / (us * 2.4e3 * 1024))
+        lc = ""  # LDS bank-conflict cycles as a share of all LDS-array cycles
+        if a.get("SQ_LDS_IDX_ACTIVE"):
+            lc = "%.1f" % (100.0 * a.get("SQ_LDS_BANK_CONFLICT", 0.0) / a["SQ_LDS_IDX_ACTIVE"])
         wc = a.get("SQ_WAVE_CYCLES", 0.0)
         shares = " ".join("%5.1f" % (100.0 * a[c] / wc) if wc else "-" for c in extra)
-        print("%-70s %6d %9.1f %9.1f %8.2f %8s %s" % (k, n, us, rd / 1e6, tbps, mf, shares))
+        print("%-70s %6d %9.1f %9.1f %8.2f %8s %8s %s" % (k, n, us, rd / 1e6, tbps, mf, lc, shares))
 
 
 if __name__ == "__main__":
