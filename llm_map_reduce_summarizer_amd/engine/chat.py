@@ -13,7 +13,7 @@ engine tokenizer (special tokens at their Llama-3 ids)::
 
 from __future__ import annotations
 
-from typing import List, Optional
+from typing import Dict, List, Optional, Sequence
 
 from .tokenizer import LLAMA3_SPECIALS, BPETokenizer
 
@@ -32,5 +32,15 @@ def render_chat(tok: BPETokenizer, user: str, system: Optional[str] = None) -> L
     if system:
         ids += _header(tok, "system") + tok.encode_ordinary(system) + [EOT]
     ids += _header(tok, "user") + tok.encode_ordinary(user) + [EOT]
+    ids += _header(tok, "assistant")
+    return ids
+
+
+def render_messages(tok: BPETokenizer, messages: Sequence[Dict[str, str]]) -> List[int]:
+    """Any chat ([{"role", "content"}, ...]: system / user / assistant turns in order), rendered the same
+    way turn by turn, ending with the assistant header (the turn to generate)."""
+    ids = [BOT]
+    for m in messages:
+        ids += _header(tok, m["role"]) + tok.encode_ordinary(m["content"]) + [EOT]
     ids += _header(tok, "assistant")
     return ids

@@ -39,6 +39,7 @@ bandwidth measured on this job's GPUs at start-up).
 from __future__ import annotations
 
 import hashlib
+import json
 import logging
 import math
 import os
@@ -48,14 +49,17 @@ from typing import Any, Dict, List, Optional, Sequence
 from ..config import LLMConfig
 from ..parallel import dist as pdist
 from ..pipeline.providers import GenRequest, GenResult, Provider
-from .chat import render_chat
+from .chat import render_chat, render_messages
 from .tokenizer import get_tokenizer
 
 log = logging.getLogger("mrsum.local")
 
 
 def _req_seed(base: int, req: GenRequest) -> int:
-    h = hashlib.sha1(("%d|%s|%s" % (base, req.system or "", req.user)).encode("utf-8")).digest()
+    key = "%d|%s|%s" % (base, req.system or "", req.user)
+    if req.messages:
+        key += "|" + json.dumps(req.messages, sort_keys=True)
+    h = hashlib.sha1(key.encode("utf-8")).digest()
     return int.from_bytes(h[:8], "little") & ((1 << 62) - 1)
 
 
@@ -343,7 +347,8 @@ class LocalEngineProvider(Provider):
         return out
 
     def encode_request(self, req: GenRequest) -> List[int]:
-        ids = render_chat(self.tokenizer, req.user, req.system)
+        ids = (render_messages(self.tokenizer, req.messages) if req.messages
+               else render_chat(self.tokenizer, req.user, req.system))
         budget = self.max_model_len - max(1, req.max_tokens)
         if len(ids) > budget:
             log.warning("prompt of %d tokens truncated to %d (max_model_len %d)", len(ids), budget,

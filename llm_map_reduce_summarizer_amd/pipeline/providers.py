@@ -39,6 +39,9 @@ class GenRequest:
     temperature: float = 0.3
     stage: str = "map"
     tag: Any = None
+    # a whole chat ([{"role": "system" | "user" | "assistant", "content": str}, ...]) instead of the
+    # reference's [system?, user] pair -- the HTTP front-end (serve.py) passes multi-turn requests here
+    messages: Optional[List[Dict[str, str]]] = None
 
 
 @dataclass

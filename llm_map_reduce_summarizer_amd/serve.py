@@ -1,0 +1,345 @@
+"""OpenAI- and Anthropic-compatible HTTP front-end for the on-node engine.
+
+The reference's only process boundary is an HTTPS POST to a hosted model (``/root/reference/
+llm_executor.py:283-297`` ``/v1/chat/completions``, ``:376-382`` ``/v1/messages``).  This server puts the
+MI355X engine behind those two endpoints, so anything that speaks them -- the reference itself with
+``OPENAI_BASE_URL`` pointed here, this package's ``--provider openai|anthropic``, any OpenAI client --
+runs on the local GPUs unchanged:
+
+    python -m llm_map_reduce_summarizer_amd.serve --model llama3-8b --port 8000
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m llm_map_reduce_summarizer_amd.serve ...
+
+Endpoints: ``POST /v1/chat/completions``, ``POST /v1/messages``, ``GET /v1/models``, ``GET /health``,
+``GET /metrics`` (Prometheus text).  Non-streaming; ``stream: true`` gets the whole completion as one
+server-sent event followed by ``[DONE]``.  Stop sequences and n > 1 are not supported (400).
+
+Batching: HTTP handlers only enqueue.  One engine thread takes the first waiting request, keeps
+collecting for ``--batch-window-ms`` (or until ``--max-batch``), and runs the whole batch as one
+``LocalEngineProvider.generate_batch`` -- continuous batching, paged KV and the decode hipGraphs of the
+engine, and under torchrun the same DP / TP stage planner as the summarizer.  Multi-rank: rank 0 serves
+HTTP and broadcasts every batch (or an idle heartbeat, so peers never sit in a collective past its
+timeout) to the other ranks, which run the same SPMD ``generate_batch``.
+"""
+
+import argparse
+import asyncio
+import json
+import logging
+import os
+import queue
+import threading
+import time
+import uuid
+from dataclasses import asdict
+from typing import Any, Dict, List, Optional, Tuple
+
+from .config import LLMConfig
+from .parallel import dist as pdist
+from .pipeline.providers import GenRequest, GenResult
+
+log = logging.getLogger("mrsum.serve")
+
+HEARTBEAT_S = 1.0  # multi-rank: idle broadcast period
+
+
+class BadRequest(ValueError):
+    pass
+
+
+def _text(content: Any) -> str:
+    """OpenAI / Anthropic message content: a string or a list of parts ({"type": "text", "text": ...})."""
+    if isinstance(content, str):
+        return content
+    if isinstance(content, list):
+        out = []
+        for part in content:
+            if isinstance(part, dict) and part.get("type") == "text":
+                out.append(str(part.get("text", "")))
+            elif isinstance(part, str):
+                out.append(part)
+            else:
+                raise BadRequest("only text content parts are supported")
+        return "".join(out)
+    raise BadRequest("message content must be a string or a list of text parts")
+
+
+def _common(body: Dict[str, Any], default_temp: float) -> Tuple[int, float]:
+    if body.get("stop"):
+        raise BadRequest("stop sequences are not supported")
+    if int(body.get("n", 1) or 1) != 1:
+        raise BadRequest("n > 1 is not supported")
+    mt = body.get("max_completion_tokens", body.get("max_tokens"))
+    max_tokens = int(mt) if mt is not None else 1000
+    if max_tokens < 1:
+        raise BadRequest("max_tokens must be >= 1")
+    temp = body.get("temperature")
+    return max_tokens, float(default_temp if temp is None else temp)
+
+
+def openai_request(body: Dict[str, Any], default_temp: float = 1.0) -> GenRequest:
+    """GenRequest of an OpenAI ``/v1/chat/completions`` body.  A [system?, user] chat keeps the
+    reference's request shape (same prompt rendering and seed as the in-process provider)."""
+    msgs = body.get("messages")
+    if not isinstance(msgs, list) or not msgs:
+        raise BadRequest("messages must be a non-empty list")
+    turns = []
+    for m in msgs:
+        role = m.get("role") if isinstance(m, dict) else None
+        if role == "developer":
+            role = "system"
+        if role not in ("system", "user", "assistant"):
+            raise BadRequest("unsupported message role %r" % role)
+        turns.append({"role": role, "content": _text(m.get("content", ""))})
+    max_tokens, temp = _common(body, default_temp)
+    roles = [t["role"] for t in turns]
+    if roles in (["user"], ["system", "user"]):
+        return GenRequest(user=turns[-1]["content"], system=turns[0]["content"] if len(turns) == 2 else None,
+                          max_tokens=max_tokens, temperature=temp, stage="serve")
+    return GenRequest(user=turns[-1]["content"], max_tokens=max_tokens, temperature=temp, stage="serve",
+                      messages=turns)
+
+
+def anthropic_request(body: Dict[str, Any], default_temp: float = 1.0) -> GenRequest:
+    """GenRequest of an Anthropic ``/v1/messages`` body (top-level ``system``)."""
+    msgs = body.get("messages")
+    if not isinstance(msgs, list) or not msgs:
+        raise BadRequest("messages must be a non-empty list")
+    system = body.get("system")
+    system = _text(system) if system else None
+    turns = [{"role": "system", "content": system}] if system else []
+    for m in msgs:
+        role = m.get("role") if isinstance(m, dict) else None
+        if role not in ("user", "assistant"):
+            raise BadRequest("unsupported message role %r" % role)
+        turns.append({"role": role, "content": _text(m.get("content", ""))})
+    max_tokens, temp = _common(body, default_temp)
+    if [t["role"] for t in turns[-1:]] != ["user"]:
+        raise BadRequest("the last message must be from the user")
+    if len(msgs) == 1:
+        return GenRequest(user=turns[-1]["content"], system=system, max_tokens=max_tokens, temperature=temp,
+                          stage="serve")
+    return GenRequest(user=turns[-1]["content"], max_tokens=max_tokens, temperature=temp, stage="serve",
+                      messages=turns)
+
+
+def _finish(res: GenResult) -> str:
+    return "length" if (res.extra or {}).get("finish_reason") == "length" else "stop"
+
+
+def openai_response(res: GenResult, model: str) -> Dict[str, Any]:
+    return {"id": "chatcmpl-" + uuid.uuid4().hex[:24], "object": "chat.completion", "created": int(time.time()),
+            "model": model,
+            "choices": [{"index": 0, "message": {"role": "assistant", "content": res.text},
+                         "finish_reason": _finish(res)}],
+            "usage": {"prompt_tokens": res.prompt_tokens, "completion_tokens": res.completion_tokens,
+                      "total_tokens": res.prompt_tokens + res.completion_tokens}}
+
+
+def anthropic_response(res: GenResult, model: str) -> Dict[str, Any]:
+    return {"id": "msg_" + uuid.uuid4().hex[:24], "type": "message", "role": "assistant", "model": model,
+            "content": [{"type": "text", "text": res.text}],
+            "stop_reason": "max_tokens" if _finish(res) == "length" else "end_turn", "stop_sequence": None,
+            "usage": {"input_tokens": res.prompt_tokens, "output_tokens": res.completion_tokens}}
+
+
+class Batcher:
+    """Request queue -> batches -> ``provider.generate_batch`` on one engine thread (see module doc)."""
+
+    def __init__(self, provider, max_batch: int = 64, window_s: float = 0.005):
+        self.provider = provider
+        self.max_batch = max(1, int(max_batch))
+        self.window_s = max(0.0, float(window_s))
+        self.q: "queue.Queue[Tuple[GenRequest, asyncio.AbstractEventLoop, asyncio.Future]]" = queue.Queue()
+        self.stop = threading.Event()
+        self.stats = {"requests": 0, "batches": 0, "errors": 0, "prompt_tokens": 0, "completion_tokens": 0,
+                      "engine_s": 0.0, "max_batch_seen": 0}
+        self._thread: Optional[threading.Thread] = None
+
+    async def submit(self, req: GenRequest) -> GenResult:
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        self.q.put((req, loop, fut))
+        return await fut
+
+    def _collect(self, first_timeout: float):
+        try:
+            items = [self.q.get(timeout=first_timeout)]
+        except queue.Empty:
+            return []
+        deadline = time.perf_counter() + self.window_s
+        while len(items) < self.max_batch:
+            left = deadline - time.perf_counter()
+            try:
+                items.append(self.q.get(timeout=max(0.0, left)) if left > 0 else self.q.get_nowait())
+            except queue.Empty:
+                break
+        return items
+
+    def run_batch(self, reqs: List[GenRequest]) -> List[GenResult]:
+        t0 = time.perf_counter()
+        try:
+            res = asyncio.run(self.provider.generate_batch(reqs))
+        except Exception as e:  # noqa: BLE001 -- every waiting client gets the error, the server lives on
+            log.exception("batch of %d failed", len(reqs))
+            res = [GenResult("", error="%s: %s" % (type(e).__name__, e)) for _ in reqs]
+        self.stats["engine_s"] += time.perf_counter() - t0
+        return res
+
+    def loop(self) -> None:
+        """Rank 0's engine thread."""
+        multi = pdist.is_initialized() and self.provider.par.world > 1
+        while True:
+            items = [] if self.stop.is_set() else self._collect(HEARTBEAT_S if multi else 0.1)
+            if multi:  # every rank enters the same collectives, heartbeat or batch
+                pdist.broadcast_json({"stop": self.stop.is_set(), "reqs": [asdict(it[0]) for it in items]})
+            if self.stop.is_set() and not items:
+                break
+            if not items:
+                continue
+            reqs = [it[0] for it in items]
+            res = self.run_batch(reqs)
+            self.stats["batches"] += 1
+            self.stats["requests"] += len(reqs)
+            self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], len(reqs))
+            for (_, lp, fut), r in zip(items, res):
+                self.stats["errors"] += bool(r.error)
+                self.stats["prompt_tokens"] += r.prompt_tokens
+                self.stats["completion_tokens"] += r.completion_tokens
+                lp.call_soon_threadsafe(lambda f=fut, v=r: f.done() or f.set_result(v))
+
+    def start(self) -> None:
+        self._thread = threading.Thread(target=self.loop, name="mrsum-engine", daemon=True)
+        self._thread.start()
+
+    def shutdown(self, timeout: Optional[float] = None) -> None:
+        self.stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout)
+
+
+def follower_loop(provider) -> None:
+    """Ranks > 0: run every batch rank 0 broadcasts until it says stop."""
+    while True:
+        msg = pdist.broadcast_json(None)
+        reqs = [GenRequest(**r) for r in msg["reqs"]]
+        if reqs:
+            try:
+                asyncio.run(provider.generate_batch(reqs))
+            except Exception:  # noqa: BLE001 -- rank 0 reports; the collectives inside already matched
+                log.exception("follower batch failed")
+        if msg["stop"]:
+            return
+
+
+def build_app(batcher: Batcher, model_name: str, api_key: Optional[str] = None, default_temp: float = 1.0):
+    """The FastAPI app (handlers enqueue on ``batcher``; ``api_key``: required Bearer / x-api-key)."""
+    from fastapi import FastAPI, Request
+    from fastapi.responses import JSONResponse, PlainTextResponse, StreamingResponse
+
+    app = FastAPI(title="mrsum engine", version="1")
+    started = time.time()
+
+    def _err(status: int, msg: str, kind: str) -> JSONResponse:
+        return JSONResponse({"error": {"message": msg, "type": kind}}, status_code=status)
+
+    def _authorised(request: Request) -> bool:
+        if not api_key:
+            return True
+        auth = request.headers.get("authorization", "")
+        return auth == "Bearer " + api_key or request.headers.get("x-api-key") == api_key
+
+    async def _serve(request: Request, parse, render):
+        if not _authorised(request):
+            return _err(401, "invalid API key", "authentication_error")
+        try:
+            body = await request.json()
+            req = parse(body, default_temp)
+        except BadRequest as e:
+            return _err(400, str(e), "invalid_request_error")
+        except (ValueError, TypeError, AttributeError) as e:
+            return _err(400, "malformed request: %s" % e, "invalid_request_error")
+        res = await batcher.submit(req)
+        if res.error:
+            return _err(500, res.error, "engine_error")
+        out = render(res, body.get("model") or model_name)
+        if body.get("stream"):
+            async def events():
+                yield "data: %s\n\n" % json.dumps(out)
+                yield "data: [DONE]\n\n"
+            return StreamingResponse(events(), media_type="text/event-stream")
+        return JSONResponse(out)
+
+    @app.post("/v1/chat/completions")
+    async def chat_completions(request: Request):
+        return await _serve(request, openai_request, openai_response)
+
+    @app.post("/v1/messages")
+    async def messages(request: Request):
+        return await _serve(request, anthropic_request, anthropic_response)
+
+    @app.get("/v1/models")
+    async def models():
+        return {"object": "list", "data": [{"id": model_name, "object": "model", "created": int(started),
+                                            "owned_by": "mrsum"}]}
+
+    @app.get("/health")
+    async def health():
+        return {"status": "ok", "uptime_s": round(time.time() - started, 1), **batcher.stats}
+
+    @app.get("/metrics")
+    async def metrics():
+        lines = []
+        for k, v in batcher.stats.items():
+            kind = "gauge" if k == "max_batch_seen" else "counter"
+            lines += ["# TYPE mrsum_%s %s" % (k, kind), "mrsum_%s %s" % (k, v)]
+        return PlainTextResponse("\n".join(lines) + "\n", media_type="text/plain; version=0.0.4")
+
+    return app
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("--model", default="llama3-8b", help="engine preset (or hf with --weights)")
+    ap.add_argument("--served-model-name", default=None)
+    ap.add_argument("--weights", default=None, help="HF safetensors checkpoint directory")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--parallel", default="auto", choices=["auto", "dp", "reduce_tp", "tp"])
+    ap.add_argument("--max-model-len", type=int, default=None)
+    ap.add_argument("--host", default="127.0.0.1")
+    ap.add_argument("--port", type=int, default=8000)
+    ap.add_argument("--max-batch", type=int, default=64)
+    ap.add_argument("--batch-window-ms", type=float, default=5.0)
+    ap.add_argument("--api-key", default=os.environ.get("MRSUM_SERVE_API_KEY"))
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--log-level", default="INFO")
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=getattr(logging, a.log_level.upper()), format="%(asctime)s %(name)s %(message)s")
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # before any HIP call (dmabuf IPC for RCCL)
+    import torch
+    from .engine.provider import LocalEngineProvider
+
+    pdist.init_distributed_from_env()
+    if torch.cuda.is_available():
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
+    provider = LocalEngineProvider(a.model, LLMConfig(), tp=a.tp, dtype=a.dtype, weights=a.weights,
+                                   max_model_len=a.max_model_len, use_graphs=not a.no_graphs, parallel=a.parallel)
+    provider.warm()
+    batcher = Batcher(provider, a.max_batch, a.batch_window_ms / 1000.0)
+    if pdist.is_initialized() and provider.par.rank != 0:
+        follower_loop(provider)
+        pdist.shutdown()
+        return 0
+    import uvicorn
+    batcher.start()
+    app = build_app(batcher, a.served_model_name or a.model, a.api_key)
+    try:
+        uvicorn.run(app, host=a.host, port=a.port, log_level=a.log_level.lower())
+    finally:
+        batcher.shutdown()
+        pdist.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
