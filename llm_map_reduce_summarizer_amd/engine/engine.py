@@ -467,8 +467,8 @@ class LLMEngine:
                     self.stats["decode_tokens"] += g
                     self.kv.alloc.free(s.pages)
                 self._compact(active, set(fin))
-                if feeder is not None:
-                    self._feed(feeder, finished, results, waiting)
+            if feeder is not None:  # every sync point: new requests join without waiting for a finish
+                self._feed(feeder, finished, results, waiting)
             del admitted
         return [r for r in results]  # type: ignore[return-value]
 

@@ -13,12 +13,14 @@ Endpoints: ``POST /v1/chat/completions``, ``POST /v1/messages``, ``GET /v1/model
 ``GET /metrics`` (Prometheus text).  Non-streaming; ``stream: true`` gets the whole completion as one
 server-sent event followed by ``[DONE]``.  Stop sequences and n > 1 are not supported (400).
 
-Batching: HTTP handlers only enqueue.  One engine thread takes the first waiting request, keeps
-collecting for ``--batch-window-ms`` (or until ``--max-batch``), and runs the whole batch as one
-``LocalEngineProvider.generate_batch`` -- continuous batching, paged KV and the decode hipGraphs of the
-engine, and under torchrun the same DP / TP stage planner as the summarizer.  Multi-rank: rank 0 serves
-HTTP and broadcasts every batch (or an idle heartbeat, so peers never sit in a collective past its
-timeout) to the other ranks, which run the same SPMD ``generate_batch``.
+Batching: HTTP handlers only enqueue; one engine thread owns the engine.  Single process
+(``ContinuousBatcher``): the first requests start a generate and every request that arrives while it runs
+joins the running batch at the next host sync point (the engine's feeder hook) -- continuous batching
+with paged KV and the decode hipGraphs; each client is answered when its own sequence finishes.  Under
+torchrun (``Batcher``): rank 0 collects for ``--batch-window-ms`` (up to ``--max-batch``) and broadcasts
+every batch (or an idle heartbeat, so peers never sit in a collective past its timeout) to the other
+ranks, which all run the same SPMD ``generate_batch`` -- DP replicas or TP engines chosen by the
+summarizer's stage planner.
 """
 
 import argparse
@@ -217,6 +219,89 @@ class Batcher:
             self._thread.join(timeout)
 
 
+class ContinuousBatcher(Batcher):
+    """Single-process engine: requests that arrive while a generate runs JOIN it at the next host sync
+    point (the engine's feeder hook, every ``sync_every`` decode steps) instead of waiting for the whole
+    batch -- continuous batching across HTTP requests; each client is answered the moment its own
+    sequence finishes."""
+
+    def loop(self) -> None:
+        from .engine.engine import SamplingParams
+        from .engine.provider import _req_seed
+        prov = self.provider
+        while not self.stop.is_set():
+            items = self._collect(0.1)
+            if not items:
+                continue
+            pending: Dict[int, Any] = {}
+            nxt = [0]
+
+            def admit(its):
+                out = []
+                for req, lp, fut in its:
+                    try:
+                        if req.max_tokens >= prov.max_model_len:
+                            raise BadRequest("max_tokens must be below max_model_len (%d)" % prov.max_model_len)
+                        ids = prov.encode_request(req)
+                    except Exception as e:  # noqa: BLE001 -- this client only
+                        self._resolve(lp, fut, GenResult("", error="%s: %s" % (type(e).__name__, e)))
+                        continue
+                    pending[nxt[0]] = (req, lp, fut)
+                    nxt[0] += 1
+                    out.append((ids, SamplingParams(req.max_tokens, req.temperature, _req_seed(prov.seed, req))))
+                    self.stats["requests"] += 1
+                return out
+
+            def finish(done):
+                for rid, o in done:
+                    req, lp, fut = pending.pop(rid)
+                    self._resolve(lp, fut, GenResult(prov.tokenizer.decode(o.token_ids), o.prompt_len,
+                                                     len(o.token_ids), extra={"finish_reason": o.finish_reason}))
+
+            def feeder(done):
+                finish(done)
+                room = self.max_batch - len(pending)
+                more = []
+                while room > 0 and not self.stop.is_set():
+                    try:
+                        more.append(self.q.get_nowait())
+                    except queue.Empty:
+                        break
+                    room -= 1
+                return admit(more)
+
+            first = admit(items)
+            if not first:
+                continue
+            t0 = time.perf_counter()
+            self.stats["batches"] += 1
+            try:
+                outs = prov.engine.generate([ids for ids, _ in first], [sp for _, sp in first],
+                                            ignore_eos=prov.ignore_eos, feeder=feeder)
+                finish([(rid, o) for rid, o in enumerate(outs) if rid in pending and o is not None])
+            except Exception as e:  # noqa: BLE001 -- every in-flight client gets the error
+                log.exception("engine generate failed")
+                for rid in list(pending):
+                    req, lp, fut = pending.pop(rid)
+                    self._resolve(lp, fut, GenResult("", error="%s: %s" % (type(e).__name__, e)))
+            self.stats["engine_s"] += time.perf_counter() - t0
+            self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], nxt[0])
+
+    def _resolve(self, lp, fut, r: GenResult) -> None:
+        self.stats["errors"] += bool(r.error)
+        self.stats["prompt_tokens"] += r.prompt_tokens
+        self.stats["completion_tokens"] += r.completion_tokens
+        lp.call_soon_threadsafe(lambda f=fut, v=r: f.done() or f.set_result(v))
+
+
+def make_batcher(provider, max_batch: int = 64, window_s: float = 0.005) -> Batcher:
+    """Continuous (feeder) batching for a single-process engine, windowed batches broadcast to the ranks
+    otherwise (their SPMD generate needs every rank to see the same request set)."""
+    if provider.par.world == 1 and provider.tp == 1:
+        return ContinuousBatcher(provider, max_batch, window_s)
+    return Batcher(provider, max_batch, window_s)
+
+
 def follower_loop(provider) -> None:
     """Ranks > 0: run every batch rank 0 broadcasts until it says stop."""
     while True:
@@ -325,7 +410,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     provider = LocalEngineProvider(a.model, LLMConfig(), tp=a.tp, dtype=a.dtype, weights=a.weights,
                                    max_model_len=a.max_model_len, use_graphs=not a.no_graphs, parallel=a.parallel)
     provider.warm()
-    batcher = Batcher(provider, a.max_batch, a.batch_window_ms / 1000.0)
+    batcher = make_batcher(provider, a.max_batch, a.batch_window_ms / 1000.0)
     if pdist.is_initialized() and provider.par.rank != 0:
         follower_loop(provider)
         pdist.shutdown()

@@ -23,7 +23,8 @@ from llm_map_reduce_summarizer_amd.config import LLMConfig  # noqa: E402
 from llm_map_reduce_summarizer_amd.engine.provider import LocalEngineProvider  # noqa: E402
 from llm_map_reduce_summarizer_amd.pipeline.providers import (AnthropicProvider, GenRequest,  # noqa: E402
                                                               OpenAIProvider)
-from llm_map_reduce_summarizer_amd.serve import Batcher, anthropic_request, build_app, openai_request  # noqa: E402
+from llm_map_reduce_summarizer_amd.serve import (ContinuousBatcher, anthropic_request, build_app,  # noqa: E402
+                                                 make_batcher, openai_request)
 
 KEY = "sk-local-test"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -32,7 +33,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.fixture(scope="module")
 def server():
     provider = LocalEngineProvider("tiny-gqa4", LLMConfig(), device="cpu", use_graphs=False, max_model_len=2048)
-    batcher = Batcher(provider, max_batch=16, window_s=0.2)
+    batcher = make_batcher(provider, max_batch=16, window_s=0.2)
+    assert isinstance(batcher, ContinuousBatcher)
     batcher.start()
     app = build_app(batcher, "mrsum-tiny", api_key=KEY)
     with socket.socket() as s:
@@ -96,6 +98,27 @@ def test_concurrent_clients_share_batches(server):
         assert o["usage"]["completion_tokens"] == 4 and o["choices"][0]["finish_reason"] == "length"
     assert batcher.stats["requests"] - before["requests"] == 6
     assert batcher.stats["batches"] - before["batches"] < 6  # the window collected several per batch
+
+
+def test_late_request_joins_running_generate(server):
+    """Continuous batching across HTTP requests: a short request sent while a long one decodes joins the
+    running engine batch (feeder) and is answered before the long one finishes."""
+    provider, batcher, base = server
+    fed0 = provider.engine.stats.get("fed_requests", 0)
+    calls0 = batcher.stats["batches"]
+    done = {}
+
+    def send(name, n, delay):
+        time.sleep(delay)
+        st, out = _post(base + "/v1/chat/completions",
+                        {"messages": [{"role": "user", "content": name}], "max_tokens": n})
+        assert st == 200 and out["usage"]["completion_tokens"] == n
+        done[name] = time.perf_counter()
+    with ThreadPoolExecutor(2) as ex:
+        list(ex.map(lambda a: send(*a), [("long request", 96, 0.0), ("short request", 3, 0.6)]))
+    assert done["short request"] < done["long request"]
+    assert provider.engine.stats.get("fed_requests", 0) > fed0
+    assert batcher.stats["batches"] - calls0 == 1  # one engine generate served both
 
 
 def test_multi_turn_stream_models_health_metrics(server):
@@ -217,7 +240,7 @@ def test_server_on_gpu_engine():
     import torch
     assert torch.cuda.is_available()
     provider = LocalEngineProvider("tiny-gqa4", LLMConfig(), device="cuda:0", max_model_len=2048)
-    batcher = Batcher(provider, max_batch=8, window_s=0.05)
+    batcher = make_batcher(provider, max_batch=8, window_s=0.05)
     batcher.start()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
