@@ -365,7 +365,7 @@ class LLMEngine:
     # ------------------------------------------------------------------ API
     def generate(self, prompts: Sequence[Sequence[int]], params: Sequence[SamplingParams],
                  ignore_eos: bool = False, imported: Optional[Dict[int, ImportedPrefill]] = None,
-                 on_prefill=None, feeder=None) -> List[GenOutput]:
+                 on_prefill=None, feeder=None, on_sync=None) -> List[GenOutput]:
         """Generate for every prompt.  ``ignore_eos`` pins the work to max_new_tokens per request
         (benchmark mode, SURVEY §7.4: random weights emit EOS at random).
 
@@ -377,6 +377,9 @@ class LLMEngine:
         finished since the last call (``[(request index, GenOutput)]``); it returns new
         ``(prompt, SamplingParams)`` requests, which join the running batch (continuous batching) and
         take the next request indices.  The returned list covers every request, fed ones included.
+
+        ``on_sync({request index: token ids so far})``: streaming hook, called at every host sync point
+        with the tokens of every active sequence (one device -> host copy of the token buffer per sync)
         (The map -> level-1 reduce pipeline uses it: a reduce batch starts as soon as its chunks are
         summarised)"""
         if len(prompts) != len(params):
@@ -385,7 +388,7 @@ class LLMEngine:
         if ignore_eos:
             self.state.n_eos = 0
         try:
-            out = self._generate(prompts, params, imported or {}, on_prefill, feeder)
+            out = self._generate(prompts, params, imported or {}, on_prefill, feeder, on_sync)
         finally:
             self.state.n_eos = n_eos
         if self.model.custom_ar is not None and self.model.custom_ar.error():
@@ -412,7 +415,7 @@ class LLMEngine:
             self._ctx_cls = max(self._ctx_cls, ctx_class(max(len(s.prompt) + s.params.max_new_tokens for s in seqs)))
 
     def _generate(self, prompts: Sequence[Sequence[int]], params: Sequence[SamplingParams],
-                  imported: Dict[int, ImportedPrefill], on_prefill, feeder=None) -> List[GenOutput]:
+                  imported: Dict[int, ImportedPrefill], on_prefill, feeder=None, on_sync=None) -> List[GenOutput]:
         self.stats["generate_calls"] += 1
         self._on_prefill = on_prefill
         results: List[Optional[GenOutput]] = [None] * len(prompts)
@@ -454,6 +457,9 @@ class LLMEngine:
                 self.stats["decode_steps"] += steps
             done = st.done[:n].cpu()
             gen = st.gen_count[:n].cpu()
+            if on_sync is not None and steps:
+                toks_all = st.out_tokens[:n].cpu()
+                on_sync({active[i].rid: toks_all[i, :int(gen[i])].tolist() for i in range(n)})
             fin = [i for i in range(n) if int(done[i])]
             if fin:
                 toks = st.out_tokens[:n].cpu()

@@ -10,8 +10,10 @@ runs on the local GPUs unchanged:
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m llm_map_reduce_summarizer_amd.serve ...
 
 Endpoints: ``POST /v1/chat/completions``, ``POST /v1/messages``, ``GET /v1/models``, ``GET /health``,
-``GET /metrics`` (Prometheus text).  Non-streaming; ``stream: true`` gets the whole completion as one
-server-sent event followed by ``[DONE]``.  Stop sequences and n > 1 are not supported (400).
+``GET /metrics`` (Prometheus text).  ``stream: true`` on the chat endpoint streams
+``chat.completion.chunk`` events as the engine produces tokens (every host sync point, 16 decode steps)
+on a single-process engine, the whole completion as one event under torchrun; Anthropic streaming gets the
+message as one event.  Stop sequences and n > 1 are not supported (400).
 
 Batching: HTTP handlers only enqueue; one engine thread owns the engine.  Single process
 (``ContinuousBatcher``): the first requests start a generate and every request that arrives while it runs
@@ -163,6 +165,14 @@ class Batcher:
         self.q.put((req, loop, fut))
         return await fut
 
+    async def stream(self, req: GenRequest):
+        """Async iterator of ("delta", text) items, then ("done", GenResult).  Windowed batches (multi-rank)
+        deliver the whole completion as one delta; the continuous batcher streams at every sync point."""
+        res = await self.submit(req)
+        if not res.error and res.text:
+            yield "delta", res.text
+        yield "done", res
+
     def _collect(self, first_timeout: float):
         try:
             items = [self.q.get(timeout=first_timeout)]
@@ -225,6 +235,23 @@ class ContinuousBatcher(Batcher):
     batch -- continuous batching across HTTP requests; each client is answered the moment its own
     sequence finishes."""
 
+    async def stream(self, req: GenRequest):
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        sq: "asyncio.Queue[str]" = asyncio.Queue()
+        self.q.put((req, loop, fut, sq))
+        while True:
+            getter = asyncio.ensure_future(sq.get())
+            await asyncio.wait([getter, fut], return_when=asyncio.FIRST_COMPLETED)
+            if getter.done():
+                yield "delta", getter.result()
+                continue
+            getter.cancel()
+            while not sq.empty():
+                yield "delta", sq.get_nowait()
+            yield "done", fut.result()
+            return
+
     def loop(self) -> None:
         from .engine.engine import SamplingParams
         from .engine.provider import _req_seed
@@ -234,11 +261,13 @@ class ContinuousBatcher(Batcher):
             if not items:
                 continue
             pending: Dict[int, Any] = {}
+            sent: Dict[int, int] = {}  # streamed requests: characters already sent
             nxt = [0]
 
             def admit(its):
                 out = []
-                for req, lp, fut in its:
+                for it in its:
+                    req, lp, fut = it[:3]
                     try:
                         if req.max_tokens >= prov.max_model_len:
                             raise BadRequest("max_tokens must be below max_model_len (%d)" % prov.max_model_len)
@@ -246,17 +275,37 @@ class ContinuousBatcher(Batcher):
                     except Exception as e:  # noqa: BLE001 -- this client only
                         self._resolve(lp, fut, GenResult("", error="%s: %s" % (type(e).__name__, e)))
                         continue
-                    pending[nxt[0]] = (req, lp, fut)
+                    pending[nxt[0]] = it
+                    if len(it) > 3:
+                        sent[nxt[0]] = 0
                     nxt[0] += 1
                     out.append((ids, SamplingParams(req.max_tokens, req.temperature, _req_seed(prov.seed, req))))
                     self.stats["requests"] += 1
                 return out
 
+            def push(rid, text, final):
+                """Send the new characters of a streamed request (held back: a trailing incomplete
+                UTF-8 sequence, decoded as U+FFFD, until its bytes are complete)."""
+                it = pending[rid]
+                safe = text if final else text.rstrip("\ufffd")
+                if len(safe) > sent[rid]:
+                    delta, sent[rid] = safe[sent[rid]:], len(safe)
+                    it[1].call_soon_threadsafe(it[3].put_nowait, delta)
+
+            def on_sync(tok_map):
+                for rid, ids in tok_map.items():
+                    if rid in sent and rid in pending:
+                        push(rid, prov.tokenizer.decode(ids), False)
+
             def finish(done):
                 for rid, o in done:
-                    req, lp, fut = pending.pop(rid)
-                    self._resolve(lp, fut, GenResult(prov.tokenizer.decode(o.token_ids), o.prompt_len,
-                                                     len(o.token_ids), extra={"finish_reason": o.finish_reason}))
+                    text = prov.tokenizer.decode(o.token_ids)
+                    if rid in sent:
+                        push(rid, text, True)
+                        sent.pop(rid)
+                    req, lp, fut = pending.pop(rid)[:3]
+                    self._resolve(lp, fut, GenResult(text, o.prompt_len, len(o.token_ids),
+                                                     extra={"finish_reason": o.finish_reason}))
 
             def feeder(done):
                 finish(done)
@@ -277,12 +326,13 @@ class ContinuousBatcher(Batcher):
             self.stats["batches"] += 1
             try:
                 outs = prov.engine.generate([ids for ids, _ in first], [sp for _, sp in first],
-                                            ignore_eos=prov.ignore_eos, feeder=feeder)
+                                            ignore_eos=prov.ignore_eos, feeder=feeder,
+                                            on_sync=on_sync if sent else None)
                 finish([(rid, o) for rid, o in enumerate(outs) if rid in pending and o is not None])
             except Exception as e:  # noqa: BLE001 -- every in-flight client gets the error
                 log.exception("engine generate failed")
                 for rid in list(pending):
-                    req, lp, fut = pending.pop(rid)
+                    req, lp, fut = pending.pop(rid)[:3]
                     self._resolve(lp, fut, GenResult("", error="%s: %s" % (type(e).__name__, e)))
             self.stats["engine_s"] += time.perf_counter() - t0
             self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], nxt[0])
@@ -316,6 +366,30 @@ def follower_loop(provider) -> None:
             return
 
 
+async def _openai_events(items, model: str):
+    """Server-sent ``chat.completion.chunk`` events: the role, content deltas as the engine produces them
+    (every host sync point), then finish_reason + usage, then ``[DONE]``."""
+    cid, created = "chatcmpl-" + uuid.uuid4().hex[:24], int(time.time())
+
+    def chunk(delta, finish=None, usage=None):
+        c = {"id": cid, "object": "chat.completion.chunk", "created": created, "model": model,
+             "choices": [{"index": 0, "delta": delta, "finish_reason": finish}]}
+        if usage is not None:
+            c["usage"] = usage
+        return "data: %s\n\n" % json.dumps(c)
+    yield chunk({"role": "assistant", "content": ""})
+    async for kind, v in items:
+        if kind == "delta":
+            yield chunk({"content": v})
+            continue
+        if v.error:
+            yield "data: %s\n\n" % json.dumps({"error": {"message": v.error, "type": "engine_error"}})
+        else:
+            yield chunk({}, _finish(v), {"prompt_tokens": v.prompt_tokens, "completion_tokens": v.completion_tokens,
+                                         "total_tokens": v.prompt_tokens + v.completion_tokens})
+    yield "data: [DONE]\n\n"
+
+
 def build_app(batcher: Batcher, model_name: str, api_key: Optional[str] = None, default_temp: float = 1.0):
     """The FastAPI app (handlers enqueue on ``batcher``; ``api_key``: required Bearer / x-api-key)."""
     from fastapi import FastAPI, Request
@@ -343,11 +417,14 @@ def build_app(batcher: Batcher, model_name: str, api_key: Optional[str] = None, 
             return _err(400, str(e), "invalid_request_error")
         except (ValueError, TypeError, AttributeError) as e:
             return _err(400, "malformed request: %s" % e, "invalid_request_error")
+        model = body.get("model") or model_name
+        if body.get("stream") and render is openai_response:
+            return StreamingResponse(_openai_events(batcher.stream(req), model), media_type="text/event-stream")
         res = await batcher.submit(req)
         if res.error:
             return _err(500, res.error, "engine_error")
-        out = render(res, body.get("model") or model_name)
-        if body.get("stream"):
+        out = render(res, model)
+        if body.get("stream"):  # Anthropic: the whole message as one event
             async def events():
                 yield "data: %s\n\n" % json.dumps(out)
                 yield "data: [DONE]\n\n"

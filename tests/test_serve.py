@@ -128,11 +128,21 @@ def test_multi_turn_stream_models_health_metrics(server):
                              {"type": "text", "text": "and now?"}]}], "max_tokens": 3}
     st, out = _post(base + "/v1/chat/completions", body)
     assert st == 200 and out["usage"]["completion_tokens"] == 3
-    req = urllib.request.Request(base + "/v1/chat/completions", data=json.dumps(dict(body, stream=True)).encode(),
+    # streaming: content deltas at the engine's sync points; their concatenation is the completion
+    sbody = dict(body, max_tokens=40)
+    st, full = _post(base + "/v1/chat/completions", sbody)
+    req = urllib.request.Request(base + "/v1/chat/completions", data=json.dumps(dict(sbody, stream=True)).encode(),
                                  headers={"Authorization": "Bearer " + KEY, "Content-Type": "application/json"})
     with urllib.request.urlopen(req, timeout=120) as r:
         events = [ln for ln in r.read().decode().splitlines() if ln.startswith("data: ")]
-    assert events[-1] == "data: [DONE]" and json.loads(events[0][6:])["usage"]["completion_tokens"] == 3
+    assert events[-1] == "data: [DONE]"
+    chunks = [json.loads(e[6:]) for e in events[:-1]]
+    assert all(c["object"] == "chat.completion.chunk" for c in chunks)
+    assert chunks[0]["choices"][0]["delta"]["role"] == "assistant"
+    deltas = [c["choices"][0]["delta"].get("content", "") for c in chunks[1:-1]]
+    assert len([d for d in deltas if d]) >= 2  # 40 tokens = 3 sync points of 16 steps
+    assert "".join(deltas) == full["choices"][0]["message"]["content"]
+    assert chunks[-1]["choices"][0]["finish_reason"] == "length" and chunks[-1]["usage"]["completion_tokens"] == 40
     models = json.loads(urllib.request.urlopen(base + "/v1/models", timeout=30).read())
     assert models["data"][0]["id"] == "mrsum-tiny"
     health = json.loads(urllib.request.urlopen(base + "/health", timeout=30).read())
