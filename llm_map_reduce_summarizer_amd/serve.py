@@ -27,6 +27,7 @@ summarizer's stage planner.
 
 import argparse
 import asyncio
+import hmac
 import json
 import logging
 import os
@@ -405,7 +406,8 @@ def build_app(batcher: Batcher, model_name: str, api_key: Optional[str] = None, 
         if not api_key:
             return True
         auth = request.headers.get("authorization", "")
-        return auth == "Bearer " + api_key or request.headers.get("x-api-key") == api_key
+        token = auth[7:] if auth.startswith("Bearer ") else request.headers.get("x-api-key", "")
+        return hmac.compare_digest(token.encode(), api_key.encode())  # constant-time
 
     async def _serve(request: Request, parse, render):
         if not _authorised(request):
