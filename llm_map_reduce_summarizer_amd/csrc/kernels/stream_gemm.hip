@@ -51,6 +51,7 @@ struct NormArgs {
     bf16* resid;       // producer: residual rows [M][ldr] (in / out)
     int ldr;
     float* ssp;        // producer: [M][gridDim.x] row sums of squares of h per column tile
+    int slab_m;        // F32_PARTIAL: rows per slab (0: M) -- row chunks of decode batches above 64 rows
 };
 
 template <int N>
@@ -136,6 +137,8 @@ template <int MT, int EPI, int WPB>
 __device__ __forceinline__ void stream_epilogue(f32x4 (&acc)[MT], char* lds, float* s_ss, const int n0, const int M,
                                                 void* __restrict__ out, const int ldo, float* __restrict__ parts,
                                                 int* __restrict__ counters, const NormArgs& e) {
+    // F32_PARTIAL slab s starts slab_m rows after slab s-1 (slab_m > M: a row chunk of a taller slab set)
+    const int slab_m = e.slab_m > 0 ? e.slab_m : M;
     constexpr int R = 16 * WPB;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane & 15, g = lane >> 4;
@@ -179,7 +182,7 @@ __device__ __forceinline__ void stream_epilogue(f32x4 (&acc)[MT], char* lds, flo
                 o.y = pack2(acc[m][2], acc[m][3]);
                 *reinterpret_cast<uint2*>(reinterpret_cast<bf16*>(out) + (size_t)mm * ldo + nw + 4 * g) = o;
             } else if constexpr (EPI == EPI_F32_PARTIAL) {
-                float* o = reinterpret_cast<float*>(out) + ((size_t)blockIdx.y * M + mm) * ldo + nw + 4 * g;
+                float* o = reinterpret_cast<float*>(out) + ((size_t)blockIdx.y * slab_m + mm) * ldo + nw + 4 * g;
                 *reinterpret_cast<float4*>(o) = make_float4(acc[m][0], acc[m][1], acc[m][2], acc[m][3]);
             } else {  // write-through (global_store sc1): read by another XCD's last arriver, no release fence
                 float* o = parts + ((size_t)blockIdx.y * M + mm) * (gridDim.x * R) + nw + 4 * g;
@@ -388,7 +391,7 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_gemm_kernel(const bf16* __
     stream_epilogue<MT, EPI, WPB>(acc, lds, s_ss, n0, M, out, ldo, parts, counters, e);
 }
 
-// out: bf16 [M, ldo] (EPI_BF16), fp32 slabs [splits, M, ldo] (EPI_F32_PARTIAL), bf16 [M, ldo] of N/2
+// out: bf16 [M, ldo] (EPI_BF16), fp32 slabs [splits, slab_m (0: M), ldo] (EPI_F32_PARTIAL), bf16 [M, ldo] of N/2
 // SwiGLU features (EPI_SWIGLU, splits = 1; EPI_SWIGLU_SPLIT with ``parts`` fp32 [splits, M, N] scratch),
 // or the residual update of EPI_RESID_SPLIT (``out`` unused; resid [M, ldr] bf16 += the product, ssp
 // fp32 [M, N / (16 wpb)] row sums of squares per column tile; ``parts`` scratch as SwiGLU_SPLIT).
@@ -400,7 +403,8 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_gemm_kernel(const bf16* __
 // MI355X_MICROARCH.md "nt-weights"; profiles/r1_decode_nt_ab.jsonl).
 MRSUM_API int mrsum_stream_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
                                 int epi, int splits, int wpb, void* parts, int* counters, const float* ssq,
-                                int ssq_tiles, float eps, void* resid, int ldr, float* ssp, hipStream_t s) {
+                                int ssq_tiles, float eps, void* resid, int ldr, float* ssp, int slab_m,
+                                hipStream_t s) {
     if (M <= 0) return 0;
     if (wpb < 4 || wpb > 8 || M > 64 || K % KBLK || N % (16 * wpb) || splits < 1 || (K / KBLK) % splits ||
         epi < EPI_BF16 || epi > EPI_RESID_SPLIT)
@@ -410,9 +414,10 @@ MRSUM_API int mrsum_stream_gemm(const void* x, int ldx, const void* W, int N, in
     if (split_epi && (!parts || !counters)) return (int)hipErrorInvalidValue;
     if (epi == EPI_RESID_SPLIT && (!resid || !ssp || ldr % 4)) return (int)hipErrorInvalidValue;
     if (ssq && (ssq_tiles <= 0 || ssq_tiles % (4 * SS_PARTS))) return (int)hipErrorInvalidValue;
+    if (slab_m && (slab_m < M || epi != EPI_F32_PARTIAL)) return (int)hipErrorInvalidValue;
     NormArgs e;
     e.ssq = ssq; e.ssq_tiles = ssq_tiles; e.inv_k = 1.f / (float)K; e.eps = eps;
-    e.resid = (bf16*)resid; e.ldr = ldr; e.ssp = ssp;
+    e.resid = (bf16*)resid; e.ldr = ldr; e.ssp = ssp; e.slab_m = slab_m;
     const int kper = K / splits;
     const int mt = (M + 15) / 16;
     dim3 grid(N / (16 * wpb), splits), block(64 * wpb);
@@ -588,7 +593,7 @@ MRSUM_API int mrsum_stream_fp8(const void* x, int ldx, const void* W, const floa
     if (ssq && (ssq_tiles <= 0 || ssq_tiles % (4 * SS_PARTS))) return (int)hipErrorInvalidValue;
     NormArgs e;
     e.ssq = ssq; e.ssq_tiles = ssq_tiles; e.inv_k = 1.f / (float)K; e.eps = eps;
-    e.resid = (bf16*)resid; e.ldr = ldr; e.ssp = ssp;
+    e.resid = (bf16*)resid; e.ldr = ldr; e.ssp = ssp; e.slab_m = 0;
     const int kper = K / splits;
     const int mt = (M + 15) / 16;
     dim3 grid(N / (16 * wpb), splits), block(64 * wpb);

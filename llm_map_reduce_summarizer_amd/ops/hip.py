@@ -39,7 +39,7 @@ _SIGS = {
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_stream_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp,
-                          _vp, _c_int, _c_float, _vp, _c_int, _vp, _vp],
+                          _vp, _c_int, _c_float, _vp, _c_int, _vp, _c_int, _vp],
     "mrsum_stream_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp,
                          _vp, _c_int, _c_float, _vp, _c_int, _vp, _vp],
     "mrsum_skinny_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp,
@@ -518,6 +518,12 @@ def gemm_fp8(xq: torch.Tensor, xs: torch.Tensor, w, out: Optional[torch.Tensor] 
 
 # ------------------------------------------------------------------ decode GEMMs (M <= 64)
 SKINNY_MAX_M = 64
+# decode batches above 64 rows (e.g. the 92-chunk map of a 24 h transcript, bucket 96) run the stream GEMM
+# over 64-row chunks -- the weights are streamed once per chunk, still far cheaper than the 256 x 256-tile
+# GEMM, whose grid at M <= 256 is only N / 256 workgroups (16 for the 4096-wide o / down projections).
+# gate_up (+ SwiGLU, 112 tiles) switches back to the tile GEMM above 128 rows.
+STREAM_MAX_M = 256
+STREAM_MAX_M_SWIGLU = 128
 EPI_BF16, EPI_F32_PARTIAL, EPI_SWIGLU, EPI_SWIGLU_SPLIT, EPI_RESID_SPLIT = 0, 1, 2, 3, 4
 
 
@@ -591,6 +597,20 @@ def _stream_gemm(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, no
     _rows_ok(x)
     M, K = x.shape
     N = w.shape[0]
+    if M > SKINNY_MAX_M and epi in (EPI_BF16, EPI_F32_PARTIAL, EPI_SWIGLU) and norm is None:
+        # 64-row chunks: row slices of the bf16 output, or of every fp32 slab (slab row stride = M)
+        for r0 in range(0, M, SKINNY_MAX_M):
+            r1 = min(M, r0 + SKINNY_MAX_M)
+            o = out[:, r0:r1] if epi == EPI_F32_PARTIAL else out[r0:r1]
+            _stream_launch(x[r0:r1], w, o, epi, splits, ldo, wpb, None, None, None, None, None,
+                           M if epi == EPI_F32_PARTIAL else 0)
+        return out
+    return _stream_launch(x, w, out, epi, splits, ldo, wpb, parts, counters, norm, resid, ssp, 0)
+
+
+def _stream_launch(x, w, out, epi, splits, ldo, wpb, parts, counters, norm, resid, ssp, slab_m):
+    M, K = x.shape
+    N = w.shape[0]
     _req(w.is_contiguous() and w.shape[1] == K, "stream_gemm: weight must be [N, K] contiguous")
     _req(1 <= M <= SKINNY_MAX_M and K % 128 == 0 and 4 <= wpb <= 8 and N % (16 * wpb) == 0
          and (K // 128) % splits == 0, "stream_gemm: unsupported shape M=%d N=%d K=%d S=%d wpb=%d"
@@ -603,7 +623,7 @@ def _stream_gemm(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, no
     sq, tiles, eps = _norm_args(x, norm)
     rp, ldr, sp = _resid_args(x, N, epi, resid, ssp)
     _check(_fn("mrsum_stream_gemm")(_p(x), x.stride(0), _p(w), N, K, M, _p(out), ldo, epi, splits, wpb, _p(parts),
-                                    _p(counters), sq, tiles, eps, rp, ldr, sp, _stream()), "stream_gemm")
+                                    _p(counters), sq, tiles, eps, rp, ldr, sp, slab_m, _stream()), "stream_gemm")
     return out
 
 
@@ -709,7 +729,7 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tenso
     M = x.shape[0]
     F2 = w_gu.shape[0]
     _req(norm is None or kernel in ("stream", "stream_split"), "linear_swiglu: a deferred norm needs the stream kernel")
-    if M > SKINNY_MAX_M or kernel == "gemm":
+    if kernel == "gemm" or M > (STREAM_MAX_M_SWIGLU if kernel == "stream" else SKINNY_MAX_M):
         return gemm(x, w_gu, out=out, swiglu=True)
     if out is None:
         out = torch.empty(M, F2 // 2, dtype=x.dtype, device=x.device)
@@ -779,11 +799,13 @@ def stream_config(N: int, K: int, swiglu: bool = False, splits: Optional[int] = 
 
 
 def plan(role: str, M: int, N: int, K: int, splits: Optional[int] = None, stream: bool = True):
-    if M > SKINNY_MAX_M or K % 128:
+    if M > (STREAM_MAX_M_SWIGLU if role == "gate_up" else STREAM_MAX_M) or K % 128:
         return ("gemm",)
     cfg = stream_config(N, K, swiglu=(role == "gate_up"), splits=splits) if stream else None
     if cfg is not None:
         return ("stream",) + cfg
+    if M > SKINNY_MAX_M:
+        return ("gemm",)
     if role == "gate_up" and stream and (K // 128) % 4 == 0:
         # narrow gate_up (TP shards) that the one-tile-per-CU stream kernel cannot fill: split-K over the
         # column tiles, SwiGLU by the last split to arrive -- where it beats the register-streaming kernel

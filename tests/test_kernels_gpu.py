@@ -676,3 +676,28 @@ def test_skinny_fp8_deferred_norm(N, K, S):
     act = torch.empty(1, N // 2, dtype=torch.bfloat16, device=DEV)
     _close(hip._skinny_fp8(h, w, act, hip.EPI_SWIGLU, 1, 1, N // 2, norm=(ssq, 1e-5)), g * torch.sigmoid(g) * u,
            3e-2, 3e-2)
+
+
+@pytest.mark.parametrize("M", [65, 96, 128, 200, 256])
+@pytest.mark.parametrize("wpb,S", [(4, 4), (7, 1)])
+def test_stream_gemm_row_chunks(M, wpb, S):
+    """Decode batches above 64 rows (the 24 h map's bucket 96) run the stream GEMM over 64-row chunks: bf16
+    rows, fp32 split-K slabs written at their row offset of every [S, M, N] slab (slab row stride M) and
+    SwiGLU -- each against fp32; the ops-level plan takes the stream kernel up to 256 rows (gate_up 128)."""
+    K = 1024
+    x = _rand(M, K, seed=70)
+    n = 16 * wpb * 4
+    w = _rand(n, K, scale=0.05, seed=71)
+    ref = x.float() @ w.float().t()
+    o = torch.empty(M, n, dtype=torch.bfloat16, device=DEV)
+    _close(hip._stream_gemm(x, w, o, hip.EPI_BF16, 1, n, wpb), ref, 2e-2)
+    parts = torch.full((S, M, n), float("nan"), dtype=torch.float32, device=DEV)
+    _close(hip._stream_gemm(x, w, parts, hip.EPI_F32_PARTIAL, S, n, wpb).sum(0), ref, 1e-3, 1e-3)
+    f = 8 * wpb * 4
+    wg, wu = _rand(f, K, scale=0.05, seed=72), _rand(f, K, scale=0.05, seed=73)
+    g, u = x.float() @ wg.float().t(), x.float() @ wu.float().t()
+    act = torch.empty(M, f, dtype=torch.bfloat16, device=DEV)
+    _close(hip._stream_gemm(x, reference.interleave_gate_up(wg, wu).contiguous(), act, hip.EPI_SWIGLU, 1, f, wpb),
+           g * torch.sigmoid(g) * u, 2e-2)
+    assert hip.plan("o", M, 4096, 4096)[0] == "stream"
+    assert hip.plan("gate_up", M, 28672, 4096)[0] == ("stream" if M <= 128 else "gemm")
