@@ -930,6 +930,14 @@ def fp8_linear(x: torch.Tensor, w, swiglu: bool = False, norm=None) -> torch.Ten
     N = w.q.shape[0]
     _req(norm is None or (not swiglu and fp8_stream_cfg(M, N, x.shape[1], splits=1) is not None),
          "fp8_linear: a deferred norm needs the stream kernel")
+    if SKINNY_MAX_M < M <= (STREAM_MAX_M_SWIGLU if swiglu else STREAM_MAX_M) and norm is None:
+        # decode batches of 65-256 rows: the weight-streaming kernels over 64-row chunks (the fp8 tile
+        # GEMM's grid at M <= 256 is only N / 256 workgroups)
+        out = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=x.device)
+        for r0 in range(0, M, SKINNY_MAX_M):
+            r1 = min(M, r0 + SKINNY_MAX_M)
+            out[r0:r1] = fp8_linear_swiglu(x[r0:r1], w) if swiglu else fp8_linear(x[r0:r1], w)
+        return out
     if M <= SKINNY_MAX_M:
         out = torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
         cfg = stream_config_fp8(N, x.shape[1], splits=1, M=M)
@@ -966,7 +974,7 @@ def fp8_linear_swiglu(x: torch.Tensor, w, norm=None) -> torch.Tensor:
     _req(norm is None or fp8_swiglu_takes_norm(M, F2, x.shape[1]),
          "fp8_linear_swiglu: a deferred norm needs the stream kernel or one row")
     if M > SKINNY_MAX_M:
-        return fp8_linear(x, w, swiglu=True)
+        return fp8_linear(x, w, swiglu=True)  # 64-row chunks up to STREAM_MAX_M_SWIGLU, else the fp8 GEMM
     out = torch.empty(M, F2 // 2, dtype=torch.bfloat16, device=x.device)
     if cfg is not None:
         return _stream_fp8(x, w, out, EPI_SWIGLU, 1, F2 // 2, cfg[0], norm=norm)

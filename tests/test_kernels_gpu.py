@@ -701,3 +701,18 @@ def test_stream_gemm_row_chunks(M, wpb, S):
            g * torch.sigmoid(g) * u, 2e-2)
     assert hip.plan("o", M, 4096, 4096)[0] == "stream"
     assert hip.plan("gate_up", M, 28672, 4096)[0] == ("stream" if M <= 128 else "gemm")
+
+
+@pytest.mark.parametrize("M", [65, 96, 200])
+def test_fp8_linear_row_chunks(M):
+    """fp8 decode batches of 65-256 rows: the W8A16 streaming kernels over 64-row chunks (bf16 rows, SwiGLU
+    up to 128 rows) against the fp32 product of the dequantised weights."""
+    from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight
+    K, N = 1024, 768
+    x = _rand(M, K, seed=80)
+    w = Fp8Weight.quantize(_rand(N, K, scale=0.05, seed=81))
+    ref = x.float() @ w.dequant().t()
+    _close(hip.fp8_linear(x, w), ref, 3e-2, 3e-2)
+    if M <= hip.STREAM_MAX_M_SWIGLU:  # above: the W8A8 fp8 GEMM (activation quantisation, own tests)
+        g, u = reference.split_gate_up(ref)
+        _close(hip.fp8_linear_swiglu(x, w), g * torch.sigmoid(g) * u, 3e-2, 3e-2)
