@@ -790,7 +790,10 @@ def stream_config(N: int, K: int, swiglu: bool = False, splits: Optional[int] = 
                 continue
             grid = tiles * S
             eff = grid / (-(-grid // N_CU) * N_CU)
-            key = (round(eff, 3), -S, wpb)
+            # ties: wider tiles for grids of <= 2 rounds; narrower (finer-grained, better balanced rounds)
+            # for long multi-round grids -- the LM head (128256 rows): wpb 4 vs 8 at M = 1 / 10 / 39
+            # 179.8 / 179.6 / 202.3 vs 194.1 / 196.8 / 205.9 us (profiles/r2_lm_head_cfg_sweep.jsonl)
+            key = (round(eff, 3), -S, wpb if grid <= 2 * N_CU else -wpb)
             if best_key is None or key > best_key:
                 best, best_key = (wpb, S), key
     if best is None or best_key[0] < 0.7:
