@@ -328,7 +328,13 @@ def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
     # vs 9 unfused 40.1 at 4k, equal at 10k; B=39 unfused 113 vs fused 116-118
     if groups <= 16:
         fused = -(-pages // 16) <= 6  # the <= 6k context class
-        if fused:
+        if fused and batch == 1 and hkv >= 8 and pages > 32:
+            # one sequence x 8 kv heads: 32 splits with the separate merge beat 16 fused in situ (whole decode
+            # steps, 4k context: 3.47 vs 3.55 ms; profiles/r2_attn_plans_insitu_b1_b10.jsonl), as in the
+            # <= 12k class below -- the kernel microbench had ranked them the other way
+            fused = False
+            splits = min(splits, 32)
+        elif fused:
             splits = min(splits, 16)
         elif pages <= 512:
             # the <= 12k class at B=1 (profiles/r2_attn_decode_b1_class1.jsonl, 7 rounds x 64 calls): 32 separate
