@@ -18,6 +18,8 @@ def main():
     ap.add_argument("--new", type=int, default=256)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--variants", default="plan,fused16,fused8,sep64,sep16",
                     help="plan | fusedS | sepS (S splits, fused / separate merge)")
     a = ap.parse_args()
@@ -29,9 +31,9 @@ def main():
     variants = {}
     for v in a.variants.split(","):
         variants[v] = None if v == "plan" else ((int(v[5:]), True) if v.startswith("fused") else (int(v[3:]), False))
-    cfg = get_model_config("llama3-8b")
+    cfg = get_model_config(a.model)
     eng = LLMEngine(cfg, device="cuda:0", max_model_len=a.ctx + a.new + 64, max_num_seqs=max(8, a.batch),
-                    kv_fraction=0.5, sync_every=32)
+                    kv_fraction=0.5, sync_every=32, weight_dtype=a.dtype)
     V = cfg.vocab_size
     prompt = [[1] + [(i * 7919 + j * 31) % (V - 20) + 10 for j in range(a.ctx)] for i in range(a.batch)]
     for r in range(a.rounds):
@@ -47,8 +49,8 @@ def main():
             eng.generate(prompt, [SamplingParams(a.new, 0.3, i) for i in range(a.batch)], ignore_eos=True)
             st = eng.stats
             ms = 1000 * (st["decode_s"] - s0["decode_s"]) / max(1, st["decode_steps"] - s0["decode_steps"])
-            print(json.dumps({"round": r, "batch": a.batch, "variant": name,
-                              "splits_fused": base(eng._bucket(a.batch), 8, a.ctx + a.new) if v is None else v,
+            print(json.dumps({"round": r, "model": a.model, "batch": a.batch, "variant": name,
+                              "splits_fused": base(eng._bucket(a.batch), cfg.n_kv_heads, a.ctx + a.new) if v is None else v,
                               "ctx": a.ctx, "decode_ms_per_step": round(ms, 4)}), flush=True)
     hip.decode_attn_plan = base
 
