@@ -17,12 +17,17 @@ scaling is strong).  ms_per_step = end-to-end wall-clock of one summary.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N
+
+``python bench.py --gpus N`` (N > 1) without a torchrun environment launches the N ranks itself (a child
+``torch.distributed.run``), so both forms measure N ranks; the JSON reports the world size and backend
+the process group actually saw (``ranks_seen``, ``backend``) and a hash of the final summary.
 """
 
 from __future__ import annotations
 
 import argparse
 import asyncio
+import hashlib
 import json
 import logging
 import os
@@ -45,6 +50,28 @@ def _parallelism(provider, world: int) -> str:
     if world == 1 or not plan:
         return "dp%d" % world
     return ",".join("%s:%s" % (s, "tp%d" % world if int(c["tp"]) > 1 else "dp%d" % world) for s, c in plan.items())
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(n: int) -> int:
+    """``--gpus N > 1`` without a torchrun environment: start ``torch.distributed.run`` with N ranks as a
+    CHILD process (never an exec: nothing here has touched the GPU, and none of it may before the ranks
+    own it), let rank 0's JSON line through, and exit with the child's code.  So ``python bench.py
+    --gpus 8`` measures 8 ranks instead of silently timing one process N times."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ, MRSUM_BENCH_SELF_LAUNCHED="1")
+    print("bench: --gpus %d without WORLD_SIZE: launching %d ranks (%s)" % (n, n, " ".join(cmd[:8])),
+          file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=env)
 
 
 def main() -> int:
@@ -72,6 +99,11 @@ def main() -> int:
     ap.add_argument("--profile", default=None, metavar="DIR", help="torch.profiler trace of the timed steps")
     ap.add_argument("--log-level", default="WARNING")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _self_launch(args.gpus)
+    # a hung collective must end the job well inside the driver's slot (a rank waits for its peers at
+    # most one 1000-token generate of the slowest stage: seconds)
+    os.environ.setdefault("MRSUM_DIST_TIMEOUT", "240")
 
     logging.basicConfig(level=getattr(logging, args.log_level.upper()), stream=sys.stderr,
                         format="%(asctime)s %(name)s %(levelname)s %(message)s")
@@ -128,6 +160,12 @@ def main() -> int:
         torch.cuda.synchronize()
     elapsed = pdist.all_reduce_max(time.perf_counter() - t0)
 
+    # what the process group itself saw (not what the flags claim)
+    if pdist.is_initialized():
+        import torch.distributed as tdist
+        ranks_seen, backend = tdist.get_world_size(), tdist.get_backend()
+    else:
+        ranks_seen, backend = 1, "none"
     rep = reports[-1]
     ms = elapsed / max(1, args.steps) * 1000.0
     n_chunks = rep["chunks"]
@@ -156,6 +194,9 @@ def main() -> int:
                    "parallelism": _parallelism(provider, world),
                    "max_new_tokens": args.max_new_tokens,
                    "transcript_hours": args.hours},
+        "ranks_seen": ranks_seen,
+        "summary_sha16": hashlib.sha256(rep.get("summary", "").encode("utf-8")).hexdigest()[:16],
+        "backend": backend,
         "e2e_wall_s": round(ms / 1000.0, 3),
         "phases_s": {k: round(v, 3) for k, v in rep.get("timings", {}).items()},
         "map_chunks_per_s": round(rep["chunks_per_second"] or 0.0, 3),

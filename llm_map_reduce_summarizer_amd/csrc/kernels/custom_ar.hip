@@ -70,7 +70,7 @@ __device__ __forceinline__ void st_flag(unsigned* p, unsigned v, bool wt) {
 
 // Spin (relaxed system-scope loads, s_sleep between polls) until *f >= epoch, bounded in WALL time by
 // the 100 MHz s_memrealtime counter: ranks are launched by independent host threads and may lag each
-// other by host-side jitter (GC, logging, a first hipBLASLt call), so the bound is generous (4 s) but
+// other by host-side jitter (GC, logging, a first kernel-library load), so the bound is generous (4 s) but
 // finite -- a peer that is gone sets the sticky error word (checked by the host after every generate)
 // instead of hanging the GPU.  Once the error is set, later waits do not spin at all.
 constexpr unsigned long long WAIT_TICKS = 400000000ull;  // 4 s at 100 MHz

@@ -1,6 +1,6 @@
 // Row-wise dynamic FP8 (OCP e4m3fn) quantisation of bf16 activations for the fp8 prefill GEMMs
-// (hipBLASLt fp8 MFMA via torch._scaled_mm with per-row activation scales x per-column weight
-// scales), and the matching row-wise weight quantiser used at model load.
+// (gemm.hip's v_mfma_scale_f32_16x16x128_f8f6f4 path, per-row activation scales x per-output-row
+// weight scales applied in its epilogue), and the matching row-wise weight quantiser used at load.
 //
 //   scale[r] = max(|x[r, :]|, tiny) / 448;  q[r, k] = e4m3fn(x[r, k] / scale[r])
 //

@@ -41,6 +41,10 @@ log = logging.getLogger("mrsum.engine")
 BUCKETS = (1, 2, 4, 8, 16, 24, 32, 40, 48, 64, 80, 96, 128, 160, 192, 224, 256)
 
 
+def _always() -> bool:
+    return True
+
+
 @dataclass
 class SamplingParams:
     max_new_tokens: int = 1000
@@ -341,8 +345,8 @@ class LLMEngine:
         return n
 
     def _capture(self, B: int):
-        # snapshot state rows the warm-up step will advance, run it eagerly once (hipBLASLt
-        # heuristics, workspace allocation), restore, then capture.
+        # snapshot state rows the warm-up step will advance, run it eagerly once (lazy kernel-library
+        # load, workspace and split-K ticket allocation), restore, then capture.
         st = self.state
         snap = {f: getattr(st, f)[:B].clone() for f in DecodeState._ROW_FIELDS}
         s = torch.cuda.Stream(self.device)
@@ -379,7 +383,9 @@ class LLMEngine:
         take the next request indices.  The returned list covers every request, fed ones included.
 
         ``on_sync({request index: token ids so far})``: streaming hook, called at every host sync point
-        with the tokens of every active sequence (one device -> host copy of the token buffer per sync)
+        with the tokens of every active sequence (one device -> host copy of the token buffer per sync);
+        an ``on_sync.wanted()`` attribute, when present, is asked first at every sync point and a False
+        skips that copy (a server passes the hook always and wants it only while a client streams).
         (The map -> level-1 reduce pipeline uses it: a reduce batch starts as soon as its chunks are
         summarised)"""
         if len(prompts) != len(params):
@@ -457,7 +463,7 @@ class LLMEngine:
                 self.stats["decode_steps"] += steps
             done = st.done[:n].cpu()
             gen = st.gen_count[:n].cpu()
-            if on_sync is not None and steps:
+            if on_sync is not None and steps and getattr(on_sync, "wanted", _always)():
                 toks_all = st.out_tokens[:n].cpu()
                 on_sync({active[i].rid: toks_all[i, :int(gen[i])].tolist() for i in range(n)})
             fin = [i for i in range(n) if int(done[i])]

@@ -29,7 +29,10 @@ runs, from the token cap of a summary (``MAX_TOKENS`` + the ``[Time: ...]``
 prefix) instead of the measured average, so each batch's reduce can start as
 soon as its own chunks are summarised.  With capped (pinned-length) summaries
 the plan equals the reference's; with shorter ones it may use more, smaller
-batches than the reference would (never a batch over the token budget).
+batches than the reference would (never a batch over the token budget); and
+when the real summaries total no more than ``max_tokens_per_batch`` the
+streamed level-1 outputs are dropped and the reduce is the reference's single
+pass (the structure never gains a level the reference would not have).
 """
 
 from __future__ import annotations
@@ -153,10 +156,16 @@ class ResultAggregator:
         summaries = self._summaries(processed_chunks)
         log.info("aggregating %d summaries", len(summaries))
         self.level_seconds = []
+        single = not self.hierarchical or self._total_tokens(summaries) <= self.max_tokens_per_batch
+        if level1 is not None and single:
+            # the real summaries fit one reduce call (stream_plan sized its groups for summaries at the
+            # token cap): the reference does one pass here, so the streamed level-1 outputs are dropped
+            log.info("streamed level 1 not needed: %d summaries fit one reduce pass", len(summaries))
+            level1 = None
         if level1 is not None:
             final = await self._hierarchical_aggregation(summaries, prompt_template, metadata,
                                                          level1=(level1[0], level1[1], processed_chunks))
-        elif not self.hierarchical or self._total_tokens(summaries) <= self.max_tokens_per_batch:
+        elif single:
             self.last_plan = {"levels": 1, "calls": [1]}
             t1 = time.perf_counter()
             final = await self._single_aggregation(summaries, prompt_template, metadata)

@@ -202,7 +202,10 @@ class LLMExecutor:
         if streamed is not None:
             first, second = list(streamed[0]), list(streamed[1])
             self._account(first)
-            self._account(second)
+            # groups built from a failed chunk are dropped (below) and re-run by the aggregator, which
+            # accounts them then: count only the follow-ups that are kept
+            self._account([r for g, r in enumerate(second)
+                           if not any(first[i].error for i in groups[g])])
         elif not self._provider.batched:
             sem = asyncio.Semaphore(max(1, self.max_concurrent_requests))
 

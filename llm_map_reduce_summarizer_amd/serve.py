@@ -163,8 +163,21 @@ class Batcher:
     async def submit(self, req: GenRequest) -> GenResult:
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
+        if self.stop.is_set():
+            return GenResult("", error="server shutting down")
         self.q.put((req, loop, fut))
         return await fut
+
+    def _drain(self) -> None:
+        """Answer every request still queued when the engine thread stops (its client would otherwise
+        wait on its future until the process dies)."""
+        while True:
+            try:
+                it = self.q.get_nowait()
+            except queue.Empty:
+                return
+            lp, fut = it[1], it[2]
+            lp.call_soon_threadsafe(lambda f=fut: f.done() or f.set_result(GenResult("", error="server shutting down")))
 
     async def stream(self, req: GenRequest):
         """Async iterator of ("delta", text) items, then ("done", GenResult).  Windowed batches (multi-rank)
@@ -206,6 +219,7 @@ class Batcher:
             if multi:  # every rank enters the same collectives, heartbeat or batch
                 pdist.broadcast_json({"stop": self.stop.is_set(), "reqs": [asdict(it[0]) for it in items]})
             if self.stop.is_set() and not items:
+                self._drain()
                 break
             if not items:
                 continue
@@ -228,6 +242,7 @@ class Batcher:
         self.stop.set()
         if self._thread is not None:
             self._thread.join(timeout)
+        self._drain()
 
 
 class ContinuousBatcher(Batcher):
@@ -240,6 +255,9 @@ class ContinuousBatcher(Batcher):
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
         sq: "asyncio.Queue[str]" = asyncio.Queue()
+        if self.stop.is_set():
+            yield "done", GenResult("", error="server shutting down")
+            return
         self.q.put((req, loop, fut, sq))
         while True:
             getter = asyncio.ensure_future(sq.get())
@@ -298,6 +316,10 @@ class ContinuousBatcher(Batcher):
                     if rid in sent and rid in pending:
                         push(rid, prov.tokenizer.decode(ids), False)
 
+            # asked at every sync point: a streaming request that joins later through the feeder still
+            # gets its deltas, and batches with no streaming request skip the token-buffer copy
+            on_sync.wanted = lambda: bool(sent)
+
             def finish(done):
                 for rid, o in done:
                     text = prov.tokenizer.decode(o.token_ids)
@@ -327,8 +349,7 @@ class ContinuousBatcher(Batcher):
             self.stats["batches"] += 1
             try:
                 outs = prov.engine.generate([ids for ids, _ in first], [sp for _, sp in first],
-                                            ignore_eos=prov.ignore_eos, feeder=feeder,
-                                            on_sync=on_sync if sent else None)
+                                            ignore_eos=prov.ignore_eos, feeder=feeder, on_sync=on_sync)
                 finish([(rid, o) for rid, o in enumerate(outs) if rid in pending and o is not None])
             except Exception as e:  # noqa: BLE001 -- every in-flight client gets the error
                 log.exception("engine generate failed")
@@ -337,6 +358,7 @@ class ContinuousBatcher(Batcher):
                     self._resolve(lp, fut, GenResult("", error="%s: %s" % (type(e).__name__, e)))
             self.stats["engine_s"] += time.perf_counter() - t0
             self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], nxt[0])
+        self._drain()
 
     def _resolve(self, lp, fut, r: GenResult) -> None:
         self.stats["errors"] += bool(r.error)
@@ -483,7 +505,10 @@ def main(argv: Optional[List[str]] = None) -> int:
     import torch
     from .engine.provider import LocalEngineProvider
 
-    pdist.init_distributed_from_env()
+    # ranks with no share of a batch wait in the stage all-gather for as long as the longest generation
+    # runs (a 70B fp8 request near max_model_len, a big concurrent batch): give the collective watchdog
+    # a serving-scale bound instead of the pipeline's 600 s (MRSUM_DIST_TIMEOUT still overrides)
+    pdist.init_distributed_from_env(timeout_s=float(os.environ.get("MRSUM_DIST_TIMEOUT", "21600")))
     if torch.cuda.is_available():
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
     provider = LocalEngineProvider(a.model, LLMConfig(), tp=a.tp, dtype=a.dtype, weights=a.weights,

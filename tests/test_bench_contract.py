@@ -22,15 +22,17 @@ def _port() -> int:
         return s.getsockname()[1]
 
 
-def _run(world: int, *extra: str):
+def _run(world: int, *extra: str, self_launch: bool = False):
     args = ["--gpus", str(world), "--steps", "2", "--warmup", "1", "--model", "tiny-gqa4", "--hours", "0.2",
             "--max-new-tokens", "6", "--chunk-tokens", "400", "--no-graphs", *extra]
-    if world == 1:
+    if world == 1 or self_launch:
         cmd = [sys.executable, os.path.join(ROOT, "bench.py"), *args]
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
                "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), *args]
     env = dict(os.environ, MRSUM_OPS="torch", CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
     p = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -51,3 +53,15 @@ def test_bench_prints_one_json_line(world, extra):
     assert out["engine_rank0"]["dp"] * out["engine_rank0"]["tp"] == world or extra == ("--parallel", "tp")
     if extra == ("--parallel", "tp"):
         assert "tp2" in cfg["parallelism"]
+    assert out["ranks_seen"] == world
+    assert out["backend"] == ("gloo" if world > 1 else "none")
+
+
+def test_bench_self_launches_ranks():
+    """``python bench.py --gpus 2`` with no torchrun environment runs 2 ranks (not one process) and
+    produces the same summary as the torchrun launch."""
+    own = _run(2, "--parallel", "dp", self_launch=True)
+    ref = _run(2, "--parallel", "dp")
+    assert own["n_gpus"] == 2 and own["ranks_seen"] == 2 and own["backend"] == "gloo"
+    assert own["summary_sha16"] == ref["summary_sha16"]
+    assert own["config"]["global_batch"] == ref["config"]["global_batch"]

@@ -229,17 +229,18 @@ class BatchedGroupsProvider(Provider):
     name = "bg"
     batched = True
 
-    def __init__(self, bad=2):
+    def __init__(self, bad=2, words=300):
         super().__init__("bg")
         self.bad = bad
         self.batches = []
+        self.pad = " ".join("w%d" % i for i in range(words))  # summaries long enough for 2 levels
 
     async def generate_batch(self, reqs):
         self.batches.append([r.stage for r in reqs])
-        return [GenResult("ok %s %s" % (r.stage, r.tag), 5, 5) for r in reqs]
+        return [GenResult("ok %s %s %s" % (r.stage, r.tag, self.pad), 5, 5) for r in reqs]
 
     async def generate_groups(self, reqs, groups, build):
-        first = [GenResult("", error="boom") if i == self.bad else GenResult("s%d" % i, 5, 5)
+        first = [GenResult("", error="boom") if i == self.bad else GenResult("s%d %s" % (i, self.pad), 5, 5)
                  for i in range(len(reqs))]
         second = []
         for g, members in enumerate(groups):
@@ -259,10 +260,28 @@ def test_streamed_batched_failure_reruns_only_the_affected_batch():
     n = len(groups)
     recs, l1 = asyncio.run(ex.process_chunks_streamed(chunks, "{transcript}", groups,
                                                       lambda g, rs: agg.level1_request(g, n, rs)))
-    assert recs[2]["summary"] == "ok map 2" and "error" not in recs[2]  # retried through generate_batch
+    assert recs[2]["summary"].startswith("ok map 2") and "error" not in recs[2]  # retried via generate_batch
     gbad = next(g for g, m in enumerate(groups) if 2 in m)
     assert l1[gbad] is None and all(l1[g] is not None for g in range(n) if g != gbad)
-    assert ex.failed_requests == 0 and ex.total_requests == 9 + n
+    # the dropped follow-up of the failed group is not counted: the aggregator re-runs (and counts) it
+    assert ex.failed_requests == 0 and ex.total_requests == 9 + n - 1
     r = asyncio.run(agg.aggregate(recs, level1=(groups, l1)))
     assert r["plan"]["calls"] == [n, 1] and r["plan"]["level1_streamed"]
     assert prov.batches[-2] == ["reduce_l1"] and prov.batches[-1] == ["reduce_final"]
+    assert ex.total_requests == 9 + n + 1  # every request counted exactly once
+
+
+def test_streamed_level1_short_summaries_reduce_in_one_pass():
+    """Streamed groups are planned for summaries at the token cap; when the real ones fit one reduce
+    call, the reference's single pass runs (no extra level)."""
+    prov = BatchedGroupsProvider(bad=-1, words=3)
+    ex = LLMExecutor(config=_cfg(MAX_TOKENS=300), provider_obj=prov)
+    agg = ResultAggregator(executor=ex, max_tokens_per_batch=1500)
+    chunks = _chunks(9)
+    groups = agg.stream_plan(chunks)
+    n = len(groups)
+    recs, l1 = asyncio.run(ex.process_chunks_streamed(chunks, "{transcript}", groups,
+                                                      lambda g, rs: agg.level1_request(g, n, rs)))
+    r = asyncio.run(agg.aggregate(recs, level1=(groups, l1)))
+    assert r["plan"]["levels"] == 1 and r["plan"]["calls"] == [1] and "level1_streamed" not in r["plan"]
+    assert prov.batches[-1] == ["reduce_final"] or prov.batches[-1] == ["reduce"]

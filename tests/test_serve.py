@@ -121,6 +121,54 @@ def test_late_request_joins_running_generate(server):
     assert batcher.stats["batches"] - calls0 == 1  # one engine generate served both
 
 
+def test_streaming_request_joins_non_streaming_generate(server):
+    """A streaming client whose request joins (feeder) a generate that started with no streaming request
+    still gets deltas at the sync points, not one event at the end."""
+    provider, batcher, base = server
+    calls0 = batcher.stats["batches"]
+    out = {}
+
+    def long():
+        out["long"] = _post(base + "/v1/chat/completions",
+                            {"messages": [{"role": "user", "content": "long one"}], "max_tokens": 160})
+
+    def streamed():
+        time.sleep(0.6)
+        body = {"messages": [{"role": "user", "content": "streamed late"}], "max_tokens": 48, "stream": True}
+        req = urllib.request.Request(base + "/v1/chat/completions", data=json.dumps(body).encode(),
+                                     headers={"Authorization": "Bearer " + KEY, "Content-Type": "application/json"})
+        with urllib.request.urlopen(req, timeout=120) as r:
+            out["events"] = [ln for ln in r.read().decode().splitlines() if ln.startswith("data: ")]
+    with ThreadPoolExecutor(2) as ex:
+        list(ex.map(lambda f: f(), [long, streamed]))
+    assert out["long"][0] == 200
+    assert batcher.stats["batches"] - calls0 == 1  # the streaming request joined the running generate
+    chunks = [json.loads(e[6:]) for e in out["events"][:-1]]
+    deltas = [c["choices"][0]["delta"].get("content", "") for c in chunks[1:-1]]
+    assert len([d for d in deltas if d]) >= 2  # 48 tokens over 16-step sync windows
+
+
+def test_shutdown_answers_queued_requests():
+    """Requests still queued when the engine thread stops are answered with an error, and requests
+    submitted after shutdown are refused at once (no client waits forever)."""
+    class _Prov:
+        class par:
+            world = 1
+        tp = 1
+    b = ContinuousBatcher(_Prov(), max_batch=4)
+
+    async def run():
+        loop = asyncio.get_running_loop()
+        fut = loop.create_future()
+        b.q.put((GenRequest(user="queued"), loop, fut))
+        b.shutdown(1)  # never started: the queue still holds the request
+        r1 = await asyncio.wait_for(fut, 5)
+        r2 = await b.submit(GenRequest(user="late"))
+        return r1, r2
+    r1, r2 = asyncio.run(run())
+    assert r1.error == r2.error == "server shutting down"
+
+
 def test_multi_turn_stream_models_health_metrics(server):
     _, _, base = server
     body = {"messages": [{"role": "system", "content": "s"}, {"role": "user", "content": "hi"},
