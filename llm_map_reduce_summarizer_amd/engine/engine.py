@@ -67,6 +67,8 @@ class _Seq:
     pages: List[int] = field(default_factory=list)
     slot: int = -1
     imported: Optional["ImportedPrefill"] = None
+    spans: List[Tuple[int, int]] = field(default_factory=list)  # interleaved prefill: slices still to run
+    pf_slot: int = -1  # interleaved prefill: row of LLMEngine.pf_tables
 
 
 @dataclass
@@ -168,6 +170,10 @@ class LLMEngine:
         self.kv = PagedKVCache(cfg.n_layers, kv_pages, self.model.hkv, page_size, cfg.head_dim, dtype, self.device)
         self.max_pages = -(-self.max_model_len // page_size)
         self.state = DecodeState(self.max_num_seqs, self.max_pages, max_new_cap, self.device, eos_ids)
+        # block tables of requests whose prefill is interleaved with the running decode (they hold no
+        # decode slot until their last slice has run, so no decode step can touch their pages)
+        self.pf_tables = torch.zeros(self.max_num_seqs, self.max_pages, dtype=torch.int32, device=self.device)
+        self.interleave = os.environ.get("MRSUM_INTERLEAVE", "1") == "1"
         self.use_graphs = use_graphs and self.device.type == "cuda"
         if self.use_graphs and self.model.tp_size > 1 and self.model.custom_ar is None:
             # TP without the P2P all-reduce would put RCCL collectives inside the captured graphs;
@@ -250,16 +256,22 @@ class LLMEngine:
         for r, (part, spans) in enumerate(passes):
             self._prefill_pass(part, spans, paged=True, final=(r == rounds - 1))
 
-    def _pass_inputs(self, seqs: List[_Seq], spans, paged: bool):
-        """Device inputs of one packed forward over prompt slices ``spans`` [(start, end)] of ``seqs``."""
+    def _pass_inputs(self, seqs: List[_Seq], spans, paged: bool, tables: Optional[torch.Tensor] = None,
+                     slots: Optional[List[int]] = None, sample: Optional[List[bool]] = None):
+        """Device inputs of one packed forward over prompt slices ``spans`` [(start, end)] of ``seqs``
+        (block-table rows ``slots`` of ``tables``: default the decode slots of the decode state;
+        ``sample``: which sequences' last rows feed the LM head, default all)."""
         st, dev = self.state, self.device
+        tables = st.block_tables if tables is None else tables
+        slots = [s.slot for s in seqs] if slots is None else slots
         ids, pos, sidx, cu, last, lens = [], [], [], [0], [], []
-        for s, (b, e) in zip(seqs, spans):
+        for k, (s, (b, e)) in enumerate(zip(seqs, spans)):
             ids.extend(s.prompt[b:e])
             pos.extend(range(b, e))
-            sidx.extend([s.slot] * (e - b))
+            sidx.extend([slots[k]] * (e - b))
             cu.append(cu[-1] + e - b)
-            last.append(cu[-1] - 1)
+            if sample is None or sample[k]:
+                last.append(cu[-1] - 1)
             lens.append(e - b)
         h = lambda x: torch.tensor(x, dtype=torch.int32).to(dev, non_blocking=True)  # noqa: E731
         items = None
@@ -268,12 +280,11 @@ class LLMEngine:
             items = prefill_items(lens).to(dev, non_blocking=True)
         pp = None
         if paged:
-            slots = [s.slot for s in seqs]
             pre = [b for b, _ in spans]
-            pp = ops.PagedPrefill(st.block_tables, h(slots), h(pre), slots, pre)
+            pp = ops.PagedPrefill(tables, h(slots), h(pre), list(slots), pre)
         return SimpleNamespace(ids=h(ids), positions=h(pos), seq_idx=h(sidx), cu_seqlens=h(cu),
                                last_rows=torch.tensor(last, dtype=torch.long).to(dev, non_blocking=True),
-                               seqlens=lens, items=items, paged=pp)
+                               seqlens=lens, items=items, paged=pp, tables=tables)
 
     def _sample_first(self, seqs: List[_Seq], logits: torch.Tensor) -> None:
         """Sample every sequence's first generated token from its prompt's last row (fed position
@@ -445,9 +456,24 @@ class LLMEngine:
         st = self.state
         if feeder is not None and finished:
             self._feed(feeder, finished, results, waiting)
-        while waiting or active:
-            admitted = self._admit(waiting, active)
+        prefilling: List[_Seq] = []  # admitted while a batch decodes: prefilled slice by slice
+        t_window_end = None
+        while waiting or active or prefilling:
+            if active and self.interleave:
+                # requests joining a RUNNING batch: admit them into the prefill table and run ONE packed
+                # slice pass before each decode window, so the running sequences keep advancing (their
+                # longest inter-token gap is one slice's forward, not the joiners' whole prefill)
+                self._admit_interleaved(waiting, active, prefilling)
+                if prefilling:
+                    self._interleaved_pass(prefilling, active)
+                admitted = None
+            else:
+                while prefilling:  # nothing decodes: no one waits for the remaining slices
+                    self._interleaved_pass(prefilling, active)
+                admitted = self._admit(waiting, active)
             if not active:
+                if prefilling:
+                    continue
                 raise MemoryError("cannot admit any request: KV cache too small")
             n = len(active)
             self.stats["peak_active"] = max(self.stats["peak_active"], n)
@@ -457,9 +483,12 @@ class LLMEngine:
             steps = min(self.sync_every, max(0, remaining)) if not bool(done_now.all()) else 0
             if steps:
                 t0 = time.perf_counter()
+                if t_window_end is not None:  # host work + prefill between two windows of running rows
+                    self.stats["max_window_gap_s"] = max(self.stats.get("max_window_gap_s", 0.0), t0 - t_window_end)
                 self._decode_steps(B, steps)
                 self._sync()
-                self.stats["decode_s"] += time.perf_counter() - t0
+                t_window_end = time.perf_counter()
+                self.stats["decode_s"] += t_window_end - t0
                 self.stats["decode_steps"] += steps
             done = st.done[:n].cpu()
             gen = st.gen_count[:n].cpu()
@@ -479,6 +508,8 @@ class LLMEngine:
                     self.stats["decode_tokens"] += g
                     self.kv.alloc.free(s.pages)
                 self._compact(active, set(fin))
+                if not active:
+                    t_window_end = None
             if feeder is not None:  # every sync point: new requests join without waiting for a finish
                 self._feed(feeder, finished, results, waiting)
             del admitted
@@ -533,6 +564,93 @@ class LLMEngine:
         if batch:
             self._run_prefill(batch, active)
         return batch
+
+    def _slices(self, n: int) -> List[Tuple[int, int]]:
+        """Prefill slices of an ``n``-token prompt, aligned to its END exactly as ``_prefill`` cuts them
+        (so an interleaved prefill runs the same slices as a blocking one)."""
+        c = self.prefill_chunk
+        if not c or n <= c:
+            return [(0, n)]
+        r = -(-n // c)
+        return [(max(0, n - (k + 1) * c), n - k * c) for k in reversed(range(r))]
+
+    def _admit_interleaved(self, waiting: List[_Seq], active: List[_Seq], prefilling: List[_Seq]) -> None:
+        """Reserve pages (and a prefill-table row) for waiting requests while a batch decodes; their
+        forward passes run slice by slice in ``_interleaved_pass``.  Imported prefills need no forward:
+        they are installed into a decode slot at once."""
+        st = self.state
+        used = {s.pf_slot for s in prefilling}
+        while waiting and len(active) + len(prefilling) < self.max_num_seqs:
+            s = waiting[0]
+            need = self.kv.pages_for(len(s.prompt) + s.params.max_new_tokens)
+            if need > self.kv.alloc.available():
+                break
+            waiting.pop(0)
+            s.pages = self.kv.alloc.alloc(need)
+            row = torch.zeros(self.max_pages, dtype=torch.int32)
+            row[:need] = torch.tensor(s.pages, dtype=torch.int32)
+            if s.imported is not None:
+                s.slot = len(active)
+                self._setup_slot(s, row)
+                self._install(s)
+                active.append(s)
+                continue
+            s.pf_slot = next(i for i in range(self.max_num_seqs) if i not in used)
+            used.add(s.pf_slot)
+            self.pf_tables[s.pf_slot].copy_(row.to(self.device, non_blocking=True))
+            s.spans = self._slices(len(s.prompt))
+            prefilling.append(s)
+            self.stats["interleaved_prefills"] = self.stats.get("interleaved_prefills", 0) + 1
+
+    def _setup_slot(self, s: _Seq, row: torch.Tensor) -> None:
+        """Decode-state row of ``s`` at ``s.slot``: its pages, budget and sampling parameters."""
+        st = self.state
+        st.block_tables[s.slot].copy_(row.to(self.device, non_blocking=True))
+        st.max_new[s.slot] = s.params.max_new_tokens
+        st.gen_count[s.slot] = 0
+        st.done[s.slot] = 0
+        st.temps[s.slot] = float(s.params.temperature)
+        st.seeds[s.slot] = int(s.params.seed)
+        st.result[s.slot] = 0
+
+    def _interleaved_pass(self, prefilling: List[_Seq], active: List[_Seq]) -> None:
+        """One packed forward of the next slices of the prefilling requests (at most ``prefill_chunk``
+        tokens, or ``max_prefill_tokens`` without chunking; always at least one slice).  Requests whose
+        LAST slice ran take the next decode slots and sample their first token there."""
+        budget = self.prefill_chunk or self.max_prefill_tokens
+        part, spans, tokens = [], [], 0
+        for s in prefilling:
+            b, e = s.spans[0]
+            if part and tokens + (e - b) > budget:
+                break
+            part.append(s)
+            spans.append((b, e))
+            tokens += e - b
+        final = [len(s.spans) == 1 for s in part]
+        t0 = time.perf_counter()
+        x = self._pass_inputs(part, spans, paged=True, tables=self.pf_tables, slots=[s.pf_slot for s in part],
+                              sample=final)
+        logits = self.model.prefill(x.ids, x.positions, x.seq_idx, x.cu_seqlens, x.last_rows, self.pf_tables,
+                                    self.kv.k, self.kv.v, seqlens=x.seqlens, items=x.items,
+                                    gather=not self.model.tp_sampling, paged=x.paged, logits=any(final))
+        self.stats["prefill_tokens"] += tokens
+        self.stats["prefill_slices"] = self.stats.get("prefill_slices", 0) + len(part)
+        for s in part:
+            s.spans.pop(0)
+        done = [s for s, f in zip(part, final) if f]
+        if done:
+            for s in done:  # consecutive decode slots after the running rows
+                s.slot = len(active)
+                self._setup_slot(s, self.pf_tables[s.pf_slot])
+                active.append(s)
+                prefilling.remove(s)
+            self._sample_first(done, logits)
+            if self._on_prefill is not None:
+                self._on_prefill(done)
+        self._sync()
+        dt = time.perf_counter() - t0
+        self.stats["prefill_s"] += dt
+        self.stats["interleaved_pass_max_s"] = max(self.stats.get("interleaved_pass_max_s", 0.0), dt)
 
     def _install(self, s: _Seq) -> None:
         """Copy an imported prefill's KV into ``s``'s pages and set its slot as the sampler would have."""

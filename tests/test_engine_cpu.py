@@ -264,3 +264,37 @@ def test_feeder_requests_join_the_running_batch(eng):
         ref = eng.generate([[128000] + solo[k].token_ids], [extra[k]])[0]
         assert outs[3 + k].token_ids == ref.token_ids and outs[3 + k].prompt_len == 1 + len(solo[k].token_ids)
     assert eng.kv.alloc.available() == eng.kv.num_pages - 1
+
+
+def test_joining_prompt_prefills_between_decode_windows():
+    """A long prompt that joins a RUNNING batch (feeder) is prefilled one slice per decode window: the
+    running sequences keep producing tokens while it prefills (instead of stalling for its whole
+    prefill), and every request generates exactly what the blocking admission generates."""
+    cfg = get_model_config("tiny-gqa4", init_std=0.05)
+    running = [[128000] + [(i * 31 + j * 7) % 9000 + 5 for j in range(40 + 9 * i)] for i in range(3)]
+    joiner = [128000] + [(j * 13) % 9000 + 7 for j in range(600)]
+    sp = [SamplingParams(40, 0.3, 70 + i) for i in range(3)]
+    res = {}
+    for inter in (True, False):
+        eng = LLMEngine(cfg, device="cpu", dtype=torch.float32, max_model_len=1024, max_num_seqs=8, kv_pages=64,
+                        sync_every=2, prefill_chunk=64)
+        eng.interleave = inter
+        fed, syncs = [], []
+
+        def feeder(done, fed=fed):
+            if not fed:
+                fed.append(1)
+                return [(joiner, SamplingParams(12, 0.3, 99))]
+            return []
+
+        def on_sync(tok_map, syncs=syncs):
+            syncs.append(3 in tok_map)
+        outs = eng.generate(running, sp, feeder=feeder, on_sync=on_sync)
+        res[inter] = ([o.token_ids for o in outs], syncs, dict(eng.stats))
+    assert res[True][0] == res[False][0]  # identical tokens, running and joined requests alike
+    # windows the running rows decoded while the joiner was still prefilling: one per slice but its last
+    before_join = lambda syncs: syncs.index(True)  # noqa: E731
+    n_slices = -(-len(joiner) // 64)
+    assert before_join(res[True][1]) - before_join(res[False][1]) >= n_slices - 1
+    assert res[True][2]["interleaved_prefills"] == 1 and res[False][2].get("interleaved_prefills", 0) == 0
+    assert res[True][2]["prefill_slices"] >= n_slices
