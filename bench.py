@@ -44,12 +44,15 @@ BASELINE_VALUE = None  # the reference publishes no number
 
 
 def _parallelism(provider, world: int) -> str:
-    """e.g. "dp1", or per stage "map:tp8,reduce_l1:tp8,reduce_final:tp8" (tpK = one engine sharded over K
-    GPUs, dpK = K data-parallel replicas)."""
+    """e.g. "dp1", or per stage "map:tp2xdp4,reduce_l1:dp8,reduce_final:tp8" (tpK = one engine sharded
+    over K GPUs, dpK = K data-parallel replicas, tpKxdpD = D replicas of a TP=K engine)."""
     plan = getattr(provider, "stage_plan", {}) or {}
     if world == 1 or not plan:
         return "dp%d" % world
-    return ",".join("%s:%s" % (s, "tp%d" % world if int(c["tp"]) > 1 else "dp%d" % world) for s, c in plan.items())
+
+    def lay(k: int) -> str:
+        return "dp%d" % world if k <= 1 else ("tp%d" % k if k == world else "tp%dxdp%d" % (k, world // k))
+    return ",".join("%s:%s" % (s, lay(int(c["tp"]))) for s, c in plan.items())
 
 
 def _free_port() -> int:
@@ -86,12 +89,13 @@ def main() -> int:
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--stop-at-eos", action="store_true",
                     help="honour EOS (default: pin every generation to --max-new-tokens so the timed work is fixed)")
-    ap.add_argument("--parallel", choices=["auto", "dp", "reduce_tp", "tp"],
-                    default=os.environ.get("MRSUM_PARALLEL", "auto"),
+    ap.add_argument("--parallel", default=os.environ.get("MRSUM_PARALLEL", "auto"),
                     help="dp: every stage data-parallel over the ranks; reduce_tp: map data-parallel, reduce stages "
                          "tensor-parallel over all ranks; tp: every stage on one engine sharded over all ranks; "
-                         "auto: per stage, the cheaper of dp / tp under parallel/plan.py's cost model fed with the "
-                         "all-reduce latency and bandwidth measured on these GPUs at start-up")
+                         "tpK: TP=K x DP=N/K for every stage; a per-stage layout such as "
+                         "map:tp2,reduce_l1:tp4,reduce_final:tp8; auto: per stage, the cheapest TP degree (divisors "
+                         "of N) under parallel/plan.py's cost model fed with the all-reduce latency and bandwidth "
+                         "measured on these GPUs at start-up")
     ap.add_argument("--no-hierarchical", action="store_true",
                     help="single-pass reduce over every summary (use a long-context model, e.g. llama3.1-8b)")
     ap.add_argument("--stream-reduce", action="store_true",

@@ -90,10 +90,12 @@ def build_parser() -> argparse.ArgumentParser:
                         "several GPUs when the P2P all-reduce passes its self-test")
     e.add_argument("--no-reduce-tp", dest="reduce_tp", action="store_const", const=False,
                    help="keep every stage data-parallel")
-    e.add_argument("--parallel", choices=["auto", "dp", "reduce_tp", "tp"], default=None,
+    e.add_argument("--parallel", default=None,
                    help="multi-GPU policy per stage: dp replicas, one TP=world engine (tp), map dp + reduce tp "
-                        "(reduce_tp), or auto: the cheaper per stage under parallel/plan.py's cost model with the "
-                        "all-reduce latency/bandwidth measured at start-up (default; overrides --reduce-tp)")
+                        "(reduce_tp), TP=K x DP=N/K (tpK), an explicit per-stage layout (e.g. "
+                        "map:tp2,reduce_l1:tp4,reduce_final:tp8), or auto: the cheapest TP degree per stage under "
+                        "parallel/plan.py's cost model with the all-reduce latency/bandwidth measured at start-up "
+                        "(default; overrides --reduce-tp)")
     e.add_argument("--aggregator-model", default=None,
                    help="separate local model for the reduce stage (e.g. llama3-70b); default: the map model")
     e.add_argument("--aggregator-dtype", choices=["bf16", "fp8"], default=None,

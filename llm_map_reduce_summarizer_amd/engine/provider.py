@@ -27,13 +27,18 @@ vector before and after the sharded generate.  ``MRSUM_FAULT_INJECT=
 "rank:count"`` (or ``fault_inject=``) raises in the engine call of ``rank``
 for its first ``count`` calls (-1: every call) -- the test hook.
 
-With several GPUs a stage may instead run on ONE engine sharded over all of
-them (TP = world): decode is bound by streaming weights + KV from HBM, which
-DP replicas do not shorten and TP divides.  ``parallel`` selects the policy:
-``dp`` (every stage data-parallel), ``reduce_tp`` (map DP, reduce stages TP),
-``tp`` (every stage TP) or ``auto`` (per stage, the cheaper of the two under
-the cost model of ``parallel/plan.py``, fed with the all-reduce latency and
-bandwidth measured on this job's GPUs at start-up).
+With several GPUs a stage may instead run on engines sharded over groups of
+k consecutive GPUs (TP = k, world / k such replicas; k = world is one engine
+over the whole node): decode is bound by streaming weights + KV from HBM,
+which DP replicas do not shorten and TP divides.  ``parallel`` selects the
+policy: ``dp`` (every stage data-parallel), ``reduce_tp`` (map DP, reduce
+stages TP = world), ``tp`` (every stage TP = world), ``tpK`` (every stage
+TP = K x DP = world / K), an explicit per-stage layout such as
+``map:tp2,reduce_l1:tp4,reduce_final:tp8`` (``reduce`` matches every reduce
+stage, unnamed stages stay DP), or ``auto`` (per stage, the cheapest TP degree
+among the divisors of the world size under the cost model of
+``parallel/plan.py``, fed with the all-reduce latency and bandwidth measured
+on this job's GPUs at start-up).
 """
 
 from __future__ import annotations
@@ -61,6 +66,30 @@ def _req_seed(base: int, req: GenRequest) -> int:
         key += "|" + json.dumps(req.messages, sort_keys=True)
     h = hashlib.sha1(key.encode("utf-8")).digest()
     return int.from_bytes(h[:8], "little") & ((1 << 62) - 1)
+
+
+def parse_parallel(spec: str, world: int) -> Dict[str, int]:
+    """Stage -> TP degree of an explicit layout: ``tpK`` (every stage, key ``*``) or comma-separated
+    ``stage:tpK`` / ``stage:dp`` items (``reduce`` = every reduce stage).  Degrees must divide ``world``."""
+    out: Dict[str, int] = {}
+    items = [spec] if ":" not in spec else spec.split(",")
+    for it in items:
+        stage, _, lay = it.strip().rpartition(":")
+        lay = lay.strip().lower()
+        if lay == "dp":
+            k = 1
+        elif lay.startswith("tp") and lay[2:].isdigit():
+            k = int(lay[2:])
+        else:
+            raise ValueError("bad parallel layout %r (want dp, tpK or stage:tpK,...)" % it)
+        if k < 1 or world % k:
+            raise ValueError("TP degree %d does not divide the world size %d" % (k, world))
+        out[stage.strip() or "*"] = k
+    return out
+
+
+def divisors(n: int) -> List[int]:
+    return [k for k in range(1, n + 1) if n % k == 0]
 
 
 def assign_balanced(costs: Sequence[int], n_bins: int) -> List[int]:
@@ -121,15 +150,23 @@ class LocalEngineProvider(Provider):
         # parallel policy (module docstring); the legacy reduce_tp flag maps onto it
         if parallel is None:
             parallel = os.environ.get("MRSUM_PARALLEL") or {None: "auto", True: "reduce_tp", False: "dp"}[reduce_tp]
+        self.fixed_tp: Dict[str, int] = {}
         if parallel not in ("auto", "dp", "reduce_tp", "tp"):
-            raise ValueError("parallel must be auto, dp, reduce_tp or tp (got %r)" % parallel)
+            self.fixed_tp = parse_parallel(parallel, max(1, self.par.world))
+            bad = [k for k in self.fixed_tp.values() if k > 1 and not self._tp_ok(k)]
+            if bad:
+                raise ValueError("%s does not shard over TP=%d" % (self.model, bad[0]))
+            parallel = "fixed"
         import torch
-        multi = self.par.world > 1 and tp == 1 and self._tp_world_ok()
+        multi = self.par.world > 1 and tp == 1 and (self._tp_ok(self.par.world) or parallel == "fixed")
         if parallel == "auto" and not torch.cuda.is_available():
             parallel = "dp"  # the planner's constants are GPU measurements
+        if parallel == "fixed" and all(k == 1 for k in self.fixed_tp.values()):
+            parallel = "dp"
         self.parallel = parallel if multi else "dp"
-        self.use_tp_engine = self.parallel != "dp"  # a TP=world engine exists for some stage
-        self._tp_engine = None
+        self.use_tp_engine = self.parallel != "dp"  # a TP engine exists for some stage
+        self._tp_engines: Dict[int, Any] = {}  # TP degree -> this rank's engine of its k-rank group
+        self._tp_bad: set = set()  # degrees whose engine had no graph-safe all-reduce
         self._dp_needed = self.parallel != "tp"
         self.hw = None  # plan.HWModel with this job's measured all-reduce constants (auto mode)
         # TP stages prefill data-parallel on the TP=1 engines and move the KV with one all-to-all
@@ -141,15 +178,15 @@ class LocalEngineProvider(Provider):
         if self.use_tp_engine:
             self._engine_options.setdefault("kv_fraction", float(os.environ.get("MRSUM_DP_KV_FRACTION", "0.5")))
 
-    def _tp_world_ok(self) -> bool:
-        w = self.par.world
-        if w <= 1 or w > 8:
+    def _tp_ok(self, k: int) -> bool:
+        """The model shards over TP=k (heads, KV heads, FFN and vocab divisible; at most 8 GPUs)."""
+        if k <= 1 or k > 8 or self.par.world % k:
             return False
         try:
             c = self.model_config()
         except Exception:
             return False
-        return c.n_kv_heads % w == 0 and c.n_heads % w == 0 and c.ffn % w == 0 and c.vocab_size % w == 0
+        return c.n_kv_heads % k == 0 and c.n_heads % k == 0 and c.ffn % k == 0 and c.vocab_size % k == 0
 
     # ------------------------------------------------------------------ engine
     def model_config(self):
@@ -184,36 +221,59 @@ class LocalEngineProvider(Provider):
     @property
     def tp_engine(self):
         """TP=world engine of the same model/seed (the ``tp`` engine of the module docstring)."""
-        if self._tp_engine is None:
+        return self.tp_engine_for(self.par.world)
+
+    @property
+    def _tp_engine(self):
+        return self._tp_engines.get(self.par.world)
+
+    def tp_engine_for(self, k: int):
+        """This rank's engine of its TP=``k`` group (ranks [k * (rank // k), k * (rank // k + 1))), built
+        on first use -- collectively: every rank asks for the same degree at the same point of the
+        pipeline.  None when that degree had no graph-safe all-reduce (the stage then stays DP)."""
+        if k in self._tp_bad:
+            return None
+        eng = self._tp_engines.get(k)
+        if eng is None:
             import torch
             from .engine import LLMEngine
             world = self.par.world
             opts = dict(self._engine_options)
             frac = "0.6" if self.parallel == "tp" else "0.35"  # leave HBM for the DP engine
+            if k < world:
+                frac = "0.25"  # one more engine beside the DP / TP=world ones
             opts.update(max_model_len=self.max_model_len, max_num_seqs=self.config.ENGINE_MAX_NUM_SEQS,
                         kv_fraction=float(os.environ.get("MRSUM_REDUCE_KV_FRACTION", frac)),
                         eos_ids=self.tokenizer.eos_ids)
             if self._device is None:
                 self._device = ("cuda:%d" % (self.par.local_rank % max(1, torch.cuda.device_count()))
                                 if torch.cuda.is_available() else "cpu")
-            self._tp_engine = LLMEngine(self.model_config(), device=self._device, seed=self.seed,
-                                            tp_rank=self.par.rank, tp_size=world,
-                                            tp_group=pdist.tp_group_for(world), **opts)
-            log.info("TP engine up: %s TP=%d", self.model, world)
-            if self._tp_engine.model.custom_ar is None and torch.cuda.is_available() \
-                    and self.parallel in ("auto", "reduce_tp"):
+            eng = LLMEngine(self.model_config(), device=self._device, seed=self.seed,
+                            tp_rank=self.par.rank % k, tp_size=k, tp_group=pdist.tp_group_for(k), **opts)
+            log.info("TP engine up: %s TP=%d (x DP=%d)", self.model, k, world // k)
+            if eng.model.custom_ar is None and torch.cuda.is_available() \
+                    and self.parallel in ("auto", "reduce_tp", "fixed"):
                 # every rank built the same engine and got the same collective verdict: drop it (its
-                # decode could not run in hipGraphs) and keep every stage data-parallel
-                log.warning("no P2P all-reduce for the TP engine: every stage stays data-parallel")
-                self.parallel, self.use_tp_engine, self._dp_needed = "dp", False, True
-                self._tp_engine = None
+                # decode could not run in hipGraphs) and run the stages that wanted it data-parallel
+                log.warning("no P2P all-reduce for the TP=%d engine: its stages stay data-parallel", k)
+                self._tp_bad.add(k)
+                del eng
                 torch.cuda.empty_cache()
-        return self._tp_engine
+                if k == world and self.parallel in ("auto", "reduce_tp"):
+                    self.parallel, self.use_tp_engine, self._dp_needed = "dp", False, True
+                return None
+            self._tp_engines[k] = eng
+        return eng
 
     def warm(self, capture_batch: Optional[int] = None) -> None:
         """Build the engines (and measure the planner's constants) outside any timed region; with
         ``capture_batch``, also capture the decode graphs of every batch bucket up to it."""
-        if self.use_tp_engine:
+        if self.parallel == "fixed":
+            for k in sorted({k for k in self.fixed_tp.values() if k > 1}, reverse=True):
+                eng = self.tp_engine_for(k)
+                if capture_batch and eng is not None:
+                    eng.capture_graphs(-(-capture_batch // (self.par.world // k)))
+        elif self.use_tp_engine:
             _ = self.tp_engine
             if self.parallel == "auto":
                 self._measure()
@@ -221,7 +281,7 @@ class LocalEngineProvider(Provider):
                 self._tp_engine.capture_graphs(capture_batch)
         if self._dp_needed:
             _ = self.engine
-            if capture_batch and self.parallel in ("dp", "auto", "reduce_tp"):
+            if capture_batch and self.parallel in ("dp", "auto", "reduce_tp", "fixed"):
                 self._engine.capture_graphs(-(-capture_batch // self.par.dp))
 
     def _measure(self):
@@ -242,10 +302,24 @@ class LocalEngineProvider(Provider):
                      "RCCL all-reduce %.1f GB/s", lat * 1e6, per_row * 1e6, bw / 1e9)
         return self.hw
 
+    def _fixed_degree(self, stage: str) -> int:
+        f = self.fixed_tp
+        if stage in f:
+            return f[stage]
+        if stage.startswith("reduce") and "reduce" in f:
+            return f["reduce"]
+        return f.get("*", 1)
+
     def _stage_tp(self, stage: str, prompts: Sequence[Sequence[int]], reqs: Sequence[GenRequest]):
-        """(TP degree, disaggregated prefill?) for this stage's generate: TP 1 = DP replicas, world = one
-        sharded engine."""
+        """(TP degree k, disaggregated prefill?) for this stage's generate: 1 = DP replicas, k > 1 =
+        world / k replicas of a TP=k engine (world: one engine sharded over every GPU)."""
         world = self.par.world
+        if self.parallel == "fixed":
+            k = self._fixed_degree(stage) if reqs else 1
+            if k > 1 and self.tp_engine_for(k) is None:
+                k = 1
+            self.stage_plan[stage] = {"tp": k, "handoff": bool(k > 1 and self._handoff_pays(prompts, reqs, k))}
+            return k, self.stage_plan[stage]["handoff"]
         if self.parallel != "dp":
             _ = self.tp_engine  # may fall back to dp (no P2P all-reduce on this node)
         if self.parallel == "dp" or not reqs:
@@ -260,27 +334,34 @@ class LocalEngineProvider(Provider):
             return 1, False
         d = plan.ModelDims.of(self.model_config(),
                               1.0 if self._engine_options.get("weight_dtype") == "fp8" else 2.0)
+        cands = [k for k in divisors(world) if k == 1 or (self._tp_ok(k) and k not in self._tp_bad)]
         choice = plan.choose(d, hw, [len(p) for p in prompts], [r.max_tokens for r in reqs], world,
-                             handoff=self.handoff)
+                             candidates=cands, handoff=self.handoff)
+        k = int(choice["tp"])
+        if k > 1 and self.tp_engine_for(k) is None:  # that degree has no graph-safe all-reduce
+            k = 1
+            choice = dict(choice, tp=1)
         self.stage_plan[stage] = choice
-        return int(choice["tp"]), bool(choice.get("handoff", False))
+        return k, bool(choice.get("handoff", False))
 
-    def _handoff_pays(self, prompts, reqs) -> bool:
-        """Disaggregated prefill for a TP=world stage when the cost model says it beats the TP forward:
-        always for many prompts (each rank prefills its share, no activation all-reduces); for ONE
-        prompt (the final reduce) it weighs one rank's whole prefill + the KV all-to-all against the TP
-        forward's 2 x n_layers RCCL all-reduces of the activations (parallel/plan.py)."""
-        if not self.handoff:
+    def _handoff_pays(self, prompts, reqs, k: Optional[int] = None) -> bool:
+        """Disaggregated prefill for a TP=k stage (default k = world) when the cost model says it beats
+        the TP forward: always for many prompts (each rank of the group prefills its share, no activation
+        all-reduces); for ONE prompt (the final reduce) it weighs the context-parallel prefill over the
+        group against the TP forward's 2 x n_layers RCCL all-reduces of the activations
+        (parallel/plan.py)."""
+        if not self.handoff or not reqs:
             return False
         if len(reqs) > 1:
             return True
+        k = k or self.par.world
         from ..parallel import plan
         d = plan.ModelDims.of(self.model_config(), 1.0 if self._engine_options.get("weight_dtype") == "fp8" else 2.0)
         hw = self.hw or plan.HWModel()
         lens = [len(p) for p in prompts]
-        return plan.handoff_prefill_s(d, hw, lens, self.par.world) < plan.prefill_s(d, hw, sum(lens), self.par.world, max(lens))
+        return plan.handoff_prefill_s(d, hw, lens, k) < plan.prefill_s(d, hw, sum(lens), k, max(lens))
 
-    def _handoff(self, prompts: Sequence[Sequence[int]], sp) -> Dict[int, Any]:
+    def _handoff(self, prompts: Sequence[Sequence[int]], sp, k: Optional[int] = None) -> Dict[int, Any]:
         """Disaggregated prefill for a TP stage: every rank prefills its LPT share of the prompts on
         its full (TP=1) engine -- no activation all-reduces -- and ships each prompt's KV heads to the
         TP rank that owns them in ONE all-to-all (RCCL over xGMI: ~prompt tokens x 128 KiB x
@@ -291,23 +372,25 @@ class LocalEngineProvider(Provider):
 
         from .engine import ImportedPrefill
         t0 = time.perf_counter()
-        world, rank = self.par.world, self.par.rank
+        world = k or self.par.world  # the TP group: ranks [world * g, world * (g + 1))
+        rank = self.par.rank % world
+        group = pdist.tp_group_for(world)
         if len(prompts) == 1 and len(prompts[0]) >= 2 * world:
             # one prompt (the final reduce): context-parallel prefill over every rank instead of one rank
             # prefilling it alone; every rank ends with its TP shard's KV heads, no all-to-all
             # (rank-local faults were agreed on by the caller; the pre-flight check makes the ranks agree
             # on their local resources BEFORE the per-layer all-gathers, which no rank may leave early)
             pre = self.engine.cp_preflight(prompts[0], world)
-            errs = [x for x in pdist.all_gather_json(pre and "rank %d: %s" % (rank, pre)) if x]
+            errs = [x for x in pdist.all_gather_json(pre and "rank %d: %s" % (self.par.rank, pre), group) if x]
             if errs:
                 raise RuntimeError("context-parallel prefill: " + "; ".join(errs))
-            first, kv = self.engine.prefill_export_cp(prompts[0], sp[0], rank, world, group=pdist.tp_group_for(world))
+            first, kv = self.engine.prefill_export_cp(prompts[0], sp[0], rank, world, group=group)
             self.timings["handoff_s"] = self.timings.get("handoff_s", 0.0) + time.perf_counter() - t0
             self.timings["cp_prefills"] = self.timings.get("cp_prefills", 0) + 1
             return {0: ImportedPrefill(first, kv)}
         owner = assign_balanced([len(p) for p in prompts], world)
         mine = [i for i in range(len(prompts)) if owner[i] == rank]
-        tp_eng = self.tp_engine
+        tp_eng = self.tp_engine_for(world)
         shapes = [tp_eng.import_shape(len(p)) for p in prompts]
         numel = [math.prod(s) for s in shapes]
         recv_sizes = [sum(numel[i] for i in range(len(prompts)) if owner[i] == s) for s in range(world)]
@@ -320,7 +403,7 @@ class LocalEngineProvider(Provider):
             send = torch.cat(packs) if packs else torch.empty(0, dtype=torch.bfloat16)
             send_sizes = [p.numel() for p in packs]
         except Exception as e:  # noqa: BLE001 -- still enter the all-to-all with the sizes the peers expect
-            err = "rank %d prefill: %s: %s" % (rank, type(e).__name__, e)
+            err = "rank %d prefill: %s: %s" % (self.par.rank, type(e).__name__, e)
             log.error("%s", err)
             firsts = [0] * len(mine)
             send_sizes = [sum(numel[i] for i in mine)] * world
@@ -329,9 +412,10 @@ class LocalEngineProvider(Provider):
         dev = send.device if nccl else torch.device("cpu")
         send = send.to(dev)
         recv = torch.empty(sum(recv_sizes), dtype=send.dtype, device=dev)
-        dist.all_to_all_single(recv, send, recv_sizes, send_sizes)
+        dist.all_to_all_single(recv, send, recv_sizes, send_sizes, group=group)
         tok, errs = {}, []
-        for part in pdist.all_gather_json({"tok": {str(i): int(t) for i, t in zip(mine, firsts)}, "err": err}):
+        for part in pdist.all_gather_json({"tok": {str(i): int(t) for i, t in zip(mine, firsts)}, "err": err},
+                                          group):
             tok.update({int(k): v for k, v in part["tok"].items()})
             if part["err"]:
                 errs.append(part["err"])
@@ -367,17 +451,53 @@ class LocalEngineProvider(Provider):
     async def generate(self, req: GenRequest) -> GenResult:
         return (await self.generate_batch([req]))[0]
 
-    def _generate_tp(self, prompts, reqs, handoff: bool) -> List[GenResult]:
-        """One TP=world engine over every request; ranks agree on ok / error before and after, so a
-        rank-local error (raised before the sharded forward) fails the stage on every rank alike."""
+    def _generate_tp_groups(self, prompts, reqs, k: int, sp, stage: str) -> List[GenResult]:
+        """TP=k x DP=world/k: requests LPT-balanced over the world / k groups of k consecutive ranks, each
+        group runs its share on its TP=k engine (disaggregated / context-parallel prefill inside the group
+        when it pays), results all-gathered over the world (tp_rank 0 copies kept).  An engine error
+        fails the requests of that group only, identically on every rank."""
+        world, rank = self.par.world, self.par.rank
+        owner = assign_balanced([len(p) + r.max_tokens for p, r in zip(prompts, reqs)], world // k)
+        self.owner_maps.setdefault(stage, []).append(owner)
+        mine = [i for i in range(len(reqs)) if owner[i] == rank // k]
+        local: List[Dict[str, Any]] = []
+        if mine:
+            sub_p, sub_sp = [prompts[i] for i in mine], [sp[i] for i in mine]
+            try:
+                ho = self._handoff_pays(sub_p, [reqs[i] for i in mine], k)
+                imported = self._handoff(sub_p, sub_sp, k) if ho else None
+                outs = self.tp_engine_for(k).generate(sub_p, sub_sp, ignore_eos=self.ignore_eos, imported=imported)
+                for i, o in zip(mine, outs):
+                    local.append({"i": i, "text": self.tokenizer.decode(o.token_ids), "pt": o.prompt_len,
+                                  "ct": len(o.token_ids), "fr": o.finish_reason})
+            except Exception as e:  # noqa: BLE001 -- SPMD inside the group: its every rank raises alike
+                msg = "rank %d: %s: %s" % (rank, type(e).__name__, e)
+                log.error("TP=%d group %d failed on %d requests: %s", k, rank // k, len(mine), msg)
+                local = [{"i": i, "err": msg} for i in mine]
+        merged = {}
+        for r, part in enumerate(pdist.all_gather_json(local)):
+            if r % k == 0:
+                for rec in part:
+                    merged[rec["i"]] = rec
+        return [_result(merged[i]) if i in merged else GenResult("", error="request %d produced no result" % i)
+                for i in range(len(reqs))]
+
+    def _generate_tp(self, prompts, reqs, handoff: bool, k: Optional[int] = None,
+                     stage: str = "map") -> List[GenResult]:
+        """TP=k engines over every request (default k = world: one engine, every rank runs every request);
+        ranks agree on ok / error before and after, so a rank-local error (raised before the sharded
+        forward) fails the stage on every rank alike."""
         from .engine import SamplingParams
         sp = [SamplingParams(r.max_tokens, r.temperature, _req_seed(self.seed, r)) for r in reqs]
+        k = k or self.par.world
         err = None
         try:
             self._maybe_fault()  # (the TP engine itself was built by _stage_tp, collectively)
         except Exception as e:  # noqa: BLE001
             err = "rank %d: %s: %s" % (self.par.rank, type(e).__name__, e)
         errs = [x for x in pdist.all_gather_json(err) if x]
+        if not errs and k < self.par.world:
+            return self._generate_tp_groups(prompts, reqs, k, sp, stage)
         outs = None
         if not errs:
             try:
@@ -400,8 +520,8 @@ class LocalEngineProvider(Provider):
         tp, handoff = self._stage_tp(stage, prompts, reqs) if self.par.world > 1 and self.tp == 1 else (1, False)
         self.stage_plan.setdefault(stage, {"tp": tp, "handoff": handoff})
         if tp > 1:
-            # every rank runs every request on the TP engine; the TP ranks sample identically
-            res = self._generate_tp(prompts, reqs, handoff)
+            # TP=tp groups (tp = world: every rank runs every request); the TP ranks sample identically
+            res = self._generate_tp(prompts, reqs, handoff, tp, stage)
             self.timings["generate_s"] += time.perf_counter() - t0
             return res
         dp, dp_rank = self.par.dp, self.par.dp_rank
@@ -552,6 +672,9 @@ class LocalEngineProvider(Provider):
             s.update(self._engine.engine_stats())
         if self._tp_engine is not None:
             s["tp_engine"] = self._tp_engine.engine_stats()
+        others = {str(k): e.engine_stats() for k, e in self._tp_engines.items() if k != self.par.world}
+        if others:
+            s["tp_engines"] = others
         return s
 
 

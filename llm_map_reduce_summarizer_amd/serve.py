@@ -490,7 +490,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--weights", default=None, help="HF safetensors checkpoint directory")
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--tp", type=int, default=1)
-    ap.add_argument("--parallel", default="auto", choices=["auto", "dp", "reduce_tp", "tp"])
+    ap.add_argument("--parallel", default="auto",
+                    help="auto | dp | reduce_tp | tp | tpK | per-stage layout, e.g. map:tp2,reduce:tp8")
     ap.add_argument("--max-model-len", type=int, default=None)
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--port", type=int, default=8000)

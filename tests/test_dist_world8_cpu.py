@@ -48,7 +48,7 @@ PIPE = textwrap.dedent("""
     if opt.get("force_handoff"):
         # the tiny preset's KV (128-dim heads) outweighs its 512-wide activations, so the cost model keeps
         # its single-prompt stage on the TP forward; Llama-3 goes context-parallel (tests/test_plan.py)
-        LocalEngineProvider._handoff_pays = lambda self, prompts, reqs: self.handoff
+        LocalEngineProvider._handoff_pays = lambda self, prompts, reqs, k=None: self.handoff and bool(reqs)
     cfg = LLMConfig(MAX_TOKENS=6, RETRY_DELAY=0.05)
     prov = LocalEngineProvider(opt.get("model", "tiny-kv8"), cfg, device="cpu", max_model_len=4096,
                                engine_options={"kv_pages": 512, "max_num_seqs": 16},
@@ -66,7 +66,10 @@ PIPE = textwrap.dedent("""
     t0 = time.time()
     rep = asyncio.run(summ.summarize(synthetic_transcript(opt.get("hours", 0.5), seed=3)))
     st = prov.stats()
+    tpe = st.get("tp_engines", {})
     out = {"rank": int(os.environ.get("RANK", 0)), "summary": rep["summary"], "chunks": rep["chunks"],
+           "imported_groups": sum(e.get("imported_prefills", 0) for e in tpe.values()),
+           "cp_all": st.get("cp_prefills", 0),
            "plan": {k: rep["reduce_plan"][k] for k in ("levels", "calls")},
            "chunk_summaries": cap["s"],
            "failed": ex.failed_requests, "retried": ex.retried_requests, "owner_maps": prov.owner_maps, "stage_plan": st.get("stage_plan", {}),
@@ -136,6 +139,26 @@ def test_all_stages_tp8_with_handoff():
     assert outs[0]["stage_plan"]["map"]["handoff"] is True
     # the single-prompt final reduce prefilled context-parallel over the 8 ranks (no one-rank prefill)
     assert outs[0]["stage_plan"]["reduce_final"]["handoff"] is True and all(o["cp"] >= 1 for o in outs)
+
+
+def test_per_stage_layouts_tp2_tp4_tp8(single):
+    """One world-8 job with a different TP x DP layout per stage: map on 4 replicas of a TP=2 engine,
+    level-1 reduce on 2 replicas of a TP=4 engine, the final reduce on one TP=8 engine (each group
+    prefilling its share data-parallel / context-parallel and importing the KV).  Every rank ends with
+    the same summary; the chunk summaries match world 1 up to bf16 near-ties of the sharded sums."""
+    outs = _pipe(8, parallel="map:tp2,reduce_l1:tp4,reduce_final:tp8", force_handoff=True)
+    assert all(o["summary"] == outs[0]["summary"] for o in outs)
+    assert all(o["chunk_summaries"] == outs[0]["chunk_summaries"] for o in outs)
+    sp = outs[0]["stage_plan"]
+    assert sp["map"]["tp"] == 2 and sp["reduce_l1"]["tp"] == 4 and sp["reduce_final"]["tp"] == 8, sp
+    assert outs[0]["plan"] == single["plan"]
+    same = sum(a == b for a, b in zip(outs[0]["chunk_summaries"], single["chunk_summaries"]))
+    assert same >= len(single["chunk_summaries"]) // 2, (same, len(single["chunk_summaries"]))
+    assert outs[0]["imported_groups"] > 0 or outs[0]["imported"] > 0
+    maps = [o["owner_maps"] for o in outs]
+    assert all(m == maps[0] for m in maps), "ranks disagree on the request -> TP group assignment"
+    for owner in maps[0]["map"]:  # 4 TP=2 groups, each with work
+        assert set(owner) == {0, 1, 2, 3}, owner
 
 
 def test_reduce_tp4_map_dp4():
