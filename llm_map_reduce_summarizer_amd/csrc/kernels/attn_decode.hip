@@ -37,7 +37,9 @@ __device__ __forceinline__ void st_part(float* p, float v, bool wt) {
 // threads: the (max, sum) pairs are read in parallel into LDS and turned into per-split weights
 // once, then each output element sums S slabs with independent (unrolled) loads, so the merge
 // costs ~S/8 memory round trips instead of S dependent ones.
-template <int G>
+// SC1: the partials were published write-through in THIS launch and are read with L1-bypassing sc1
+// loads (common.h ld_sc1_*) instead of behind an agent-scope acquire.
+template <int G, bool SC1 = false>
 __device__ __forceinline__ void combine_group(const float* part_o, const float* part_ml, bf16* out, int out_stride,
                                               int b, int kvh, int Hq, int S, float* sw /* [G][S] LDS */,
                                               float* sden /* [G] */) {
@@ -48,6 +50,15 @@ __device__ __forceinline__ void combine_group(const float* part_o, const float* 
     constexpr int PRE = 16 / NR;                  // partial loads per thread issued up front
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const size_t bh0 = (size_t)b * Hq + (size_t)kvh * G;
+    // this group's partials: part_o [G][S][D] and part_ml [G][S][2] from one wave-uniform base each
+    const float* po0 = part_o + bh0 * S * D;
+    const float* pm0 = part_ml + bh0 * S * 2;
+    const __amdgpu_buffer_rsrc_t ro = sc1_rsrc(po0), rm = sc1_rsrc(pm0);  // (used by SC1 only)
+    auto ld_o = [&](int g, int sp, int d4) -> float4 {  // slab sp, float4 column d4 of head g
+        const int idx = (g * S + sp) * (D / 4) + d4;
+        if constexpr (SC1) return ld_sc1_f4(ro, idx * 16);
+        else return reinterpret_cast<const float4*>(po0)[idx];
+    };
     // 1. the first PRE partial slabs of every (item, subset) are loaded BEFORE the split weights are
     //    known, so the slab loads and the (max, sum) loads share one memory round trip
     float4 pre[NR][PRE];
@@ -55,20 +66,26 @@ __device__ __forceinline__ void combine_group(const float* part_o, const float* 
     for (int r = 0; r < NR; ++r) {
         const int t = r * 256 + tid, item = t % NV, h = t / NV;
         const int g = item / (D / 4), d4 = item % (D / 4);
-        const float4* po = reinterpret_cast<const float4*>(part_o + (bh0 + g) * S * D) + d4;
 #pragma unroll
         for (int j = 0; j < PRE; ++j) {
             const int sp = h + j * NH;
-            pre[r][j] = (h < NH && sp < S) ? po[(size_t)sp * (D / 4)] : make_float4(0.f, 0.f, 0.f, 0.f);
+            // unconditional load (clamped index; unused values weighted 0 below): no branch around it
+            const float4 v = ld_o(g, min(sp, S - 1), d4);
+            pre[r][j] = (h < NH && sp < S) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
     // 2. split weights: one wave per head, one lane per split (S <= MAX_SPLITS = 64)
     for (int g = wv; g < G; g += 4) {
         float ms = -INFINITY, ls = 0.f;
-        if (lane < S) {
-            const float2 v = *reinterpret_cast<const float2*>(part_ml + ((bh0 + g) * S + lane) * 2);
-            ms = v.x;
-            ls = v.y;
+        {
+            const int sl = min(lane, S - 1);
+            float2 v;
+            if constexpr (SC1) v = ld_sc1_f2(rm, (g * S + sl) * 8);
+            else v = reinterpret_cast<const float2*>(pm0)[g * S + sl];
+            if (lane < S) {
+                ms = v.x;
+                ls = v.y;
+            }
         }
         const float M = wave_max(ms);
         const float w = ms == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms - M);
@@ -95,9 +112,8 @@ __device__ __forceinline__ void combine_group(const float* part_o, const float* 
                 acc.z += ws * pre[r][j].z;
                 acc.w += ws * pre[r][j].w;
             }
-            const float4* po = reinterpret_cast<const float4*>(part_o + (bh0 + g) * S * D) + d4;
             for (int sp = h + PRE * NH; sp < S; sp += NH) {
-                const float4 v = po[(size_t)sp * (D / 4)];
+                const float4 v = ld_o(g, sp, d4);
                 const float ws = w[sp];
                 acc.x += ws * v.x;
                 acc.y += ws * v.y;
@@ -151,12 +167,19 @@ __device__ __forceinline__ void combine_if_last(const float* part_o, const float
     }
     __syncthreads();
     if (!*s_last) return;
-    if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (WT) {
+        // write-through partials, drained before every ticket add: the merge reads them with sc1 loads
+        // (L1 bypass), no acquire; the fence below only keeps the compiler from hoisting the loads
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        combine_group<G, true>(part_o, part_ml, out, out_stride, b, kvh, Hq, S, sw, sden);
+    } else {
+        if (tid == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        combine_group<G>(part_o, part_ml, out, out_stride, b, kvh, Hq, S, sw, sden);
     }
-    __syncthreads();
-    combine_group<G>(part_o, part_ml, out, out_stride, b, kvh, Hq, S, sw, sden);
     if (tid == 0) __hip_atomic_store(counters + b * Hkv + kvh, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -280,6 +303,10 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     const int ke = min(ctx, ks + chunk);
     const size_t ml_base = ((size_t)b * Hq + (size_t)kvh * G) * S + split;
     if (ks >= ke) {
+        // an empty split (the context ends before it) still publishes a zero slab: the merge weights it by
+        // 0, and 0 x a stale NaN / inf left in the (reused, uninitialised) workspace would be NaN
+        for (int i = tid; i < G * D; i += 256)
+            st_part(part_o + (ml_base + (size_t)(i / D) * S) * D + i % D, 0.f, counters != nullptr);
         if (tid < G) {
             st_part(part_ml + (ml_base + (size_t)tid * S) * 2 + 0, -INFINITY, counters != nullptr);
             st_part(part_ml + (ml_base + (size_t)tid * S) * 2 + 1, 0.f, counters != nullptr);

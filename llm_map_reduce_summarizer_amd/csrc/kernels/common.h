@@ -71,4 +71,23 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
     return t;
 }
 
+// Loads that bypass this CU's L1 (buffer_load ... sc1, aux 16): they read the XCD's L2 / memory copy, so
+// a split-K last arriver can read other workgroups' write-through (sc1) stores of THIS launch without an
+// agent-scope acquire (buffer_inv sc1 + wait, ~1.7 us) -- the hand-off form of MI355X_MICROARCH.md
+// "Valid forms" row 1 / cdna_hip_programming.md Guideline 16: every payload store sc1 and drained before
+// the ticket add, the last adder loads after its add returned, the other waves after a barrier, EVERY
+// load of the payload such a load.  ``base`` must be wave-uniform (one buffer resource), ``off`` bytes.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sc1_rsrc(const void* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ float4 ld_sc1_f4(__amdgpu_buffer_rsrc_t r, int off) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+    return make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]), __uint_as_float(v[2]), __uint_as_float(v[3]));
+}
+__device__ __forceinline__ float2 ld_sc1_f2(__amdgpu_buffer_rsrc_t r, int off) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 16);
+    return make_float2(__uint_as_float(v[0]), __uint_as_float(v[1]));
+}
+
 static inline int ceil_div(int a, int b) { return (a + b - 1) / b; }

@@ -103,11 +103,13 @@ __device__ __forceinline__ float row_scale(const NormArgs& e, const float* s_ss,
 }
 
 // split-K arrival: every wave drained its write-through partial stores; returns true in the last of
-// the nsplit workgroups of column tile ``tile`` to arrive (after an agent-scope acquire).  The caller's
-// last arriver re-arms the ticket when it is done (rearm), off the reduction's critical path -- the
-// next launch's arrivals are ordered after it by the kernel boundary.  The flag goes through the
-// kernel's one LDS array (a second __shared__ object can de-pipeline the ring: cdna_hip_programming.md
-// "Projection GEMM at M = 256" item 4(a)).
+// the nsplit workgroups of column tile ``tile`` to arrive.  No acquire: the last arriver reads the
+// partial tiles with L1-bypassing sc1 loads only (common.h ld_sc1_f4; the write-through publish +
+// drained ticket form of cdna_hip_programming.md Guideline 16), ~1.7 us of buffer_inv wait saved per
+// reduction.  The caller's last arriver re-arms the ticket when it is done (rearm), off the
+// reduction's critical path -- the next launch's arrivals are ordered after it by the kernel boundary.
+// The flag goes through the kernel's one LDS array (a second __shared__ object can de-pipeline the
+// ring: cdna_hip_programming.md "Projection GEMM at M = 256" item 4(a)).
 __device__ __forceinline__ bool last_arrival(int* counters, int tile, int nsplit, int tid, int* s_flag) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -117,10 +119,7 @@ __device__ __forceinline__ bool last_arrival(int* counters, int tile, int nsplit
     }
     __syncthreads();
     const bool last = *s_flag != 0;
-    if (last) {
-        if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        __syncthreads();
-    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: no load hoisted above the ticket
     return last;
 }
 
@@ -198,6 +197,7 @@ __device__ __forceinline__ void stream_epilogue(f32x4 (&acc)[MT], char* lds, flo
         if (!last_arrival(counters, blockIdx.x, gridDim.y, tid, reinterpret_cast<int*>(lds))) return;
         const int S = gridDim.y;
         const size_t ncols = (size_t)gridDim.x * R;
+        const __amdgpu_buffer_rsrc_t rp = sc1_rsrc(parts);  // partial tiles: sc1 loads only (last_arrival)
         // every thread handles at most IT items and keeps all their partial-tile loads (4 splits at a time)
         // in flight together: the reduction is a few memory round trips, not one per item
         constexpr int NT = 64 * WPB;
@@ -206,25 +206,26 @@ __device__ __forceinline__ void stream_epilogue(f32x4 (&acc)[MT], char* lds, flo
             // split-K instead of streaming its weights through N / (16 WPB) CUs.
             // item = (row, 16-row block, half): 4 features = gate rows n0 + 16 bl + 4 hf .. +4, up rows + 8
             constexpr int IT = (64 * 2 * WPB + NT - 1) / NT;
-            const float* pg[IT];
+            int pg[IT];  // element offset of the item in slab 0
             float4 gs[IT], us[IT];
 #pragma unroll
             for (int j = 0; j < IT; ++j) {
                 const int it = min(tid + j * NT, M * 2 * WPB - 1);
                 const int mm = it / (2 * WPB), q = it % (2 * WPB), bl = q >> 1, hf = q & 1;
-                pg[j] = parts + (size_t)mm * ncols + n0 + 16 * bl + 4 * hf;
+                pg[j] = mm * (int)ncols + n0 + 16 * bl + 4 * hf;
                 gs[j] = make_float4(0.f, 0.f, 0.f, 0.f);
                 us[j] = gs[j];
             }
+            const int slab = M * (int)ncols;
             for (int s0 = 0; s0 < S; s0 += 4) {
                 float4 ga[IT][4], ua[IT][4];
 #pragma unroll
                 for (int j = 0; j < IT; ++j)
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
-                        const float* p = pg[j] + (size_t)min(s0 + u, S - 1) * M * ncols;
-                        ga[j][u] = *reinterpret_cast<const float4*>(p);
-                        ua[j][u] = *reinterpret_cast<const float4*>(p + 8);
+                        const int p = pg[j] + min(s0 + u, S - 1) * slab;
+                        ga[j][u] = ld_sc1_f4(rp, 4 * p);
+                        ua[j][u] = ld_sc1_f4(rp, 4 * (p + 8));
                     }
 #pragma unroll
                 for (int j = 0; j < IT; ++j)
@@ -253,17 +254,18 @@ __device__ __forceinline__ void stream_epilogue(f32x4 (&acc)[MT], char* lds, flo
             constexpr int Q = R / 4;  // 4-column items per row
             constexpr int IT = (64 * Q + NT - 1) / NT;
             float* s_sq = reinterpret_cast<float*>(lds + 64);  // [M][Q]; the ring is drained
-            const float* pg[IT];
-            uint2* rp[IT];
+            int pg[IT];  // element offset of the item in slab 0
+            uint2* rsp[IT];
             uint2 rv[IT];
 #pragma unroll
             for (int j = 0; j < IT; ++j) {
                 const int it = min(tid + j * NT, M * Q - 1);
                 const int mm = it / Q, c = n0 + 4 * (it % Q);
-                pg[j] = parts + (size_t)mm * ncols + c;
-                rp[j] = reinterpret_cast<uint2*>(e.resid + (size_t)mm * e.ldr + c);
-                rv[j] = *rp[j];
+                pg[j] = mm * (int)ncols + c;
+                rsp[j] = reinterpret_cast<uint2*>(e.resid + (size_t)mm * e.ldr + c);
+                rv[j] = *rsp[j];  // residual: written by the previous kernels only (plain load)
             }
+            const int slab = M * (int)ncols;
             float h[IT][4];
 #pragma unroll
             for (int j = 0; j < IT; ++j) {
@@ -276,7 +278,7 @@ __device__ __forceinline__ void stream_epilogue(f32x4 (&acc)[MT], char* lds, flo
                 for (int j = 0; j < IT; ++j)
 #pragma unroll
                     for (int u = 0; u < 4; ++u)
-                        a4[j][u] = *reinterpret_cast<const float4*>(pg[j] + (size_t)min(s0 + u, S - 1) * M * ncols);
+                        a4[j][u] = ld_sc1_f4(rp, 4 * (pg[j] + min(s0 + u, S - 1) * slab));
 #pragma unroll
                 for (int j = 0; j < IT; ++j)
 #pragma unroll
@@ -290,7 +292,7 @@ __device__ __forceinline__ void stream_epilogue(f32x4 (&acc)[MT], char* lds, flo
                 const int it = tid + j * NT;
                 if (it >= M * Q) break;
                 const uint2 hv = make_uint2(pack2(h[j][0], h[j][1]), pack2(h[j][2], h[j][3]));
-                *rp[j] = hv;
+                *rsp[j] = hv;
                 const float h0 = __uint_as_float(hv.x << 16), h1 = __uint_as_float(hv.x & 0xffff0000u);
                 const float h2 = __uint_as_float(hv.y << 16), h3 = __uint_as_float(hv.y & 0xffff0000u);
                 s_sq[it] = (h0 * h0 + h1 * h1) + (h2 * h2 + h3 * h3);

@@ -77,6 +77,24 @@ class _TPReduce:
         return self.model.custom_ar.add_rmsnorm(parts, residual, ln, eps)
 
 
+class LocalReduce:
+    """Single-GPU stand-in for _TPReduce when measuring ONE rank's TP shard of the decode step
+    (tools/bench_decode.py --tp-shard K): the sum over ranks is the identity and the fused all-reduce +
+    residual add + RMSNorm kernel is replaced by the local add_rmsnorm_parts over this rank's split-K
+    slabs -- the same kernel sequence per layer as a real TP rank (the deferred norm of TP=1 is off),
+    minus the cross-GPU hop."""
+    fused = True
+
+    def __call__(self, t: torch.Tensor) -> torch.Tensor:
+        return t
+
+    def fused_ok(self, rows: int, hidden: int) -> bool:
+        return rows <= 64
+
+    def add_rmsnorm(self, parts, residual, ln, eps):
+        return ops.add_rmsnorm_parts(parts, residual, ln, eps)
+
+
 @dataclass
 class LayerWeights:
     ln1: torch.Tensor
@@ -118,6 +136,7 @@ class LlamaModel:
         self.cos_sin = rope_cos_sin(cfg.max_position, cfg.head_dim, cfg.rope_theta, self.device,
                                     scaling=cfg.rope_scaling)
         self.vocab_offset = tp_rank * self.vocab_local
+        self.emulate_tp_reduce = False  # LocalReduce in place of the TP all-reduce (shard measurements)
         # TP on GPUs: decode all-reduces (fp32 split-K slabs, <= 1 MiB) and the sampler's key max go
         # through the one-shot P2P kernel (parallel/custom_ar.py); larger messages through RCCL
         self.custom_ar = None
@@ -218,7 +237,7 @@ class LlamaModel:
         residual = ops.embed(ids, self.embed)
         x = ops.rmsnorm(residual, None, c.rms_eps)  # gains folded into the consumer weights
         page = kcache.shape[3]
-        ar = _TPReduce(self) if self.tp_size > 1 else None
+        ar = _TPReduce(self) if self.tp_size > 1 else (LocalReduce() if self.emulate_tp_reduce else None)
         for i, lw in enumerate(self.layers):
             qkv = ops.qkv_rope(x, lw.wqkv, positions, seq_idx, block_tables, kcache[i], vcache[i], self.cos_sin,
                                self.hq, self.hkv, self.hd, page, defer=decode)

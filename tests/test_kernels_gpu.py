@@ -173,6 +173,10 @@ def test_attn_decode(hq, hkv, splits, fused):
     q = _rand(B, (hq + 2 * hkv) * d, seed=14)
     sc = 1.0 / math.sqrt(d)
     ws = hip.DecodeWorkspace(B, hq, d, splits, DEV, hkv, fused_combine=fused)
+    # poisoned workspace (a reused allocation may hold NaN / inf): splits past a short context must not
+    # leave stale slabs for the merge to multiply by a zero weight (0 x NaN = NaN)
+    ws.part_o.fill_(float("nan"))
+    ws.part_ml.fill_(float("nan"))
     o2 = reference.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc)
     for _ in range(3):  # replays re-use (and must re-arm) the arrival counters
         o1 = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws)
@@ -483,6 +487,7 @@ def test_attn_decode_rope_fused(hq, hkv, S, fused_combine):
     o2 = reference.attn_decode(qkv, k2, v2, bt, pos, hq, hkv, d, page, sc)
     k1, v1 = kc0.clone().to(DEV), vc0.clone().to(DEV)
     ws = hip.DecodeWorkspace(B, hq, d, hip.decode_splits(B, hkv, 20 * page), DEV, hkv, fused_combine=fused_combine)
+    ws.part_o.fill_(float("nan"))  # poisoned workspace: empty splits must publish zero slabs
     for _ in range(3):  # idempotent: later calls rewrite the same K/V row (and re-armed merge tickets)
         o1 = hip.attn_decode_rope(parts, cs, k1, v1, bt, pos, hq, hkv, d, page, sc, workspace=ws)
         _close(o1, o2, 2e-2)

@@ -21,6 +21,9 @@ def main():
     ap.add_argument("--tp-shard", type=int, default=1,
                     help="run ONE rank's shard shapes of TP=K (heads, ffn and vocab / K) on this GPU with no "
                          "all-reduce: the compute + launch floor of a TP=K decode step")
+    ap.add_argument("--deferred-norm", action="store_true",
+                    help="with --tp-shard: keep the TP=1 deferred RMSNorm (default: the TP rank's kernel sequence, "
+                         "split-K slabs -> add_rmsnorm_parts standing in for the fused P2P all-reduce kernel)")
     a = ap.parse_args()
     import torch
     from llm_map_reduce_summarizer_amd.engine.config import get_model_config
@@ -32,6 +35,7 @@ def main():
                                ffn=cfg.ffn // k, vocab_size=cfg.vocab_size // k)
     eng = LLMEngine(cfg, device="cuda:0", max_model_len=a.ctx + a.new + 64,
                     max_num_seqs=64, kv_fraction=0.5, weight_dtype=a.dtype, sync_every=32)
+    eng.model.emulate_tp_reduce = a.tp_shard > 1 and not a.deferred_norm
     res = []
     for B in (int(b) for b in a.batches.split(",")):
         V = cfg.vocab_size
