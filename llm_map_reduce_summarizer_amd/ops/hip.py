@@ -328,6 +328,12 @@ def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
     # vs 9 unfused 40.1 at 4k, equal at 10k; B=39 unfused 113 vs fused 116-118
     if groups <= 16:
         fused = -(-pages // 16) <= 6  # the <= 6k context class
+        if fused and hkv <= 2:
+            # a TP shard's one or two kv heads: one workgroup per page (up to one per CU), separate merge --
+            # in situ after the sc1 merge loads (TP=8 shard at 4k, whole decode steps, profiles/
+            # r3_plans_insitu_sc1.jsonl): B=1 64 separate 1.370 ms vs 32 fused 1.39, 16 fused 1.451;
+            # B=10 25 separate 1.600 vs 24 fused 1.615, 16 fused 1.623
+            return max(1, min(N_CU // groups, pages, 64)), False
         if fused and batch == 1 and hkv >= 8 and pages > 32:
             # one sequence x 8 kv heads: 32 splits with the separate merge beat 16 fused in situ (whole decode
             # steps, 4k context: 3.47 vs 3.55 ms; profiles/r2_attn_plans_insitu_b1_b10.jsonl), as in the
@@ -810,6 +816,13 @@ def stream_config(N: int, K: int, swiglu: bool = False, splits: Optional[int] = 
 def plan(role: str, M: int, N: int, K: int, splits: Optional[int] = None, stream: bool = True):
     if M > (STREAM_MAX_M_SWIGLU if role == "gate_up" else STREAM_MAX_M) or K % 128:
         return ("gemm",)
+    if role in ("o", "down") and M <= 16 and K <= 2048 and stream:
+        # TP shard row-parallel projections (K = hidden / TP of the heads or the FFN): the register-
+        # streaming kernel, no split-K beyond 2 -- in situ, TP=8 shard B=1 (profiles/
+        # r3_plans_insitu_sc1.jsonl): down (K 1792) skinny S=2 1.394 ms vs stream (8, 7) 1.451; o (K 512)
+        # skinny S=1 1.43 vs stream (4, 4) 1.451
+        s = splits or (2 if (K // 128) % 2 == 0 and K >= 1024 else 1)
+        return ("skinny", 1, s)
     cfg = stream_config(N, K, swiglu=(role == "gate_up"), splits=splits) if stream else None
     if cfg is not None:
         return ("stream",) + cfg

@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""In-situ plan experiments as whole decode steps (one engine; the plan of one op swapped between runs,
+graphs / workspaces rebuilt; alternating rounds), for TP=1 or one rank's TP=K shard (the TP kernel
+sequence: split-K slabs -> add_rmsnorm_parts in place of the fused all-reduce, engine/model.py LocalReduce).
+
+Variants (comma separated, ``plan`` = unchanged):
+  attnfusedS / attnsepS        decode attention with S splits, fused / separate merge (the batch's bucket)
+  role:stream:WPB:S            stream GEMM for role (qkv | o | down | gate_up) with (wpb, S)
+  role:skinny:NT:S             register-streaming kernel
+  gate_up:stream_split:WPB:S   split-K gate_up with the SwiGLU in the last arriver
+
+    python tools/exp_plans_insitu.py --tp-shard 8 --batch 1 --variants plan,attnfused32,gate_up:stream_split:4:4
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=1)
+    ap.add_argument("--ctx", type=int, default=4000)
+    ap.add_argument("--new", type=int, default=256)
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--tp-shard", type=int, default=1)
+    ap.add_argument("--variants", default="plan")
+    a = ap.parse_args()
+    import torch
+    from llm_map_reduce_summarizer_amd.engine.config import get_model_config
+    from llm_map_reduce_summarizer_amd.engine.engine import LLMEngine, SamplingParams
+    from llm_map_reduce_summarizer_amd.ops import hip
+    base_attn, base_plan = hip.decode_attn_plan, hip.plan
+    cfg = get_model_config(a.model)
+    k = a.tp_shard
+    if k > 1:
+        cfg = get_model_config(a.model, n_heads=cfg.n_heads // k, n_kv_heads=cfg.n_kv_heads // k,
+                               ffn=cfg.ffn // k, vocab_size=cfg.vocab_size // k)
+    eng = LLMEngine(cfg, device="cuda:0", max_model_len=a.ctx + a.new + 64, max_num_seqs=max(8, a.batch),
+                    kv_fraction=0.5, sync_every=32)
+    eng.model.emulate_tp_reduce = k > 1
+    bucket = eng._bucket(a.batch)
+    V = cfg.vocab_size
+    prompt = [[1] + [(i * 7919 + j * 31) % (V - 20) + 10 for j in range(a.ctx)] for i in range(a.batch)]
+
+    def install(v):
+        hip.decode_attn_plan, hip.plan = base_attn, base_plan
+        if v == "plan":
+            return
+        if v.startswith("attn"):
+            fused = v.startswith("attnfused")
+            S = int(v[len("attnfused"):] if fused else v[len("attnsep"):])
+            hip.decode_attn_plan = lambda B, hkv, ctx: (S, fused) if B == bucket else base_attn(B, hkv, ctx)
+            return
+        role, kind, p1, p2 = v.split(":")
+        p = (kind, int(p1), int(p2))
+
+        def plan(r, M, N, K, splits=None, stream=True):
+            if r == role and M <= bucket and splits is None:
+                return p
+            return base_plan(r, M, N, K, splits=splits, stream=stream)
+        hip.plan = plan
+
+    variants = a.variants.split(",")
+    for r in range(a.rounds):
+        for v in variants:
+            install(v)
+            eng._workspaces.clear()
+            eng._graphs.clear()
+            eng.generate(prompt, [SamplingParams(8, 0.3, i) for i in range(a.batch)], ignore_eos=True)
+            s0 = dict(eng.stats)
+            torch.cuda.synchronize()
+            eng.generate(prompt, [SamplingParams(a.new, 0.3, i) for i in range(a.batch)], ignore_eos=True)
+            st = eng.stats
+            ms = 1000 * (st["decode_s"] - s0["decode_s"]) / max(1, st["decode_steps"] - s0["decode_steps"])
+            print(json.dumps({"round": r, "tp_shard": k, "batch": a.batch, "variant": v, "ctx": a.ctx,
+                              "decode_ms_per_step": round(ms, 4)}), flush=True)
+    hip.decode_attn_plan, hip.plan = base_attn, base_plan
+
+
+if __name__ == "__main__":
+    main()
