@@ -15,12 +15,12 @@ latency.  Prefill is compute-bound: DP divides it by N for free, TP adds RCCL al
 activations.  Which is faster depends on the batch, the context and the all-reduce latency of the
 node, so the choice is a cost model whose hardware constants are *measured*:
 
-* ``hbm_bw``, ``step_floor_s``, ``prefill_flops``: single-GPU decode/prefill measurements of the
-  engine (profiles/r1_decode_step_latency.log: B=1/5/10/39 at 4k context fit
-  t = (W + B ctx kv) / 5.4 TB/s + 0.96 ms to within 3 %; prefill 72k tok/s of Llama-3-8B);
-* ``tp_floor_s``, ``tp_row_s``: one rank's TP=2/4/8 shard of the decode graph run alone on one GPU
-  (profiles/r1_tp_shard_decode_steps.jsonl, B=1/10/39 at 4k context: the same bandwidth term + 0.96 ms
-  + (0.08 ms + 3 us per row) x log2(TP) within 4 %: few-kv-head attention is latency-bound);
+* ``hbm_bw``, ``step_floor_s``, ``tp_floor_s``, ``tp_row_s``: one least-squares fit over the round-3
+  decode steps of TP=1 and of one rank's TP=2/4/8 shard with the TP kernel sequence
+  (profiles/r3_decode_steps_tp_shards.jsonl, B=1/10/39 at 4k context):
+  t = (W + B ctx kv) / TP / 6.17 TB/s + 0.88 ms + [TP > 1] 0.17 ms + 3.3 us x B x log2(TP), every point
+  within 6 % (few-kv-head attention and the per-kernel latency of small shards are what stay);
+* ``prefill_flops``: the engine's prefill rate in the 10 h bench (~76k tok/s of Llama-3-8B);
 * ``ar_lat_s`` / ``ar_lat_row_s`` and ``ar_bw``: timed at start-up on the job's own GPUs (the fused
   all-reduce inside a replayed hipGraph at 1 and 64 rows -- a latency and a per-row link cost; one
   RCCL all-reduce of a prefill-sized activation), MAX-reduced over the ranks so every rank takes
@@ -46,10 +46,10 @@ from typing import Dict, List, Sequence
 
 @dataclass(frozen=True)
 class HWModel:
-    hbm_bw: float = 5.4e12          # bytes/s streamed by the decode GEMM + attention kernels
-    step_floor_s: float = 0.96e-3   # fixed per-step cost of the decode graph (kernel latencies), 32 layers
-    tp_floor_s: float = 0.08e-3     # extra fixed cost of a TP shard's decode graph per log2(TP) (32 layers) ...
-    tp_row_s: float = 3e-6          # ... plus this per decode row per log2(TP) (few-kv-head attention is latency-bound)
+    hbm_bw: float = 6.17e12         # bytes/s streamed by the decode GEMM + attention kernels
+    step_floor_s: float = 0.88e-3   # fixed per-step cost of the decode graph (kernel latencies), 32 layers
+    tp_floor_s: float = 0.17e-3     # extra fixed cost of a TP shard's decode graph (32 layers) ...
+    tp_row_s: float = 3.3e-6        # ... plus this per decode row per log2(TP) (few-kv-head attention is latency-bound)
     prefill_flops: float = 1.1e15   # effective prefill FLOP/s (MFMA GEMMs + flash attention)
     ar_lat_s: float = 20e-6         # one decode all-reduce (custom P2P kernel), measured at start-up ...
     ar_lat_row_s: float = 0.0       # ... plus this per decode row (the push sends every row to every peer)
@@ -78,7 +78,8 @@ def decode_step_s(d: ModelDims, hw: HWModel, batch: int, ctx: float, tp: int) ->
     if batch <= 0:
         return 0.0
     stream = (d.weight_bytes + batch * ctx * d.kv_bytes_per_token) / tp / hw.hbm_bw
-    floor = (hw.step_floor_s + (hw.tp_floor_s + hw.tp_row_s * batch) * math.log2(tp)) * d.n_layers / 32.0
+    floor = (hw.step_floor_s + (hw.tp_floor_s if tp > 1 else 0.0) + hw.tp_row_s * batch * math.log2(tp)) \
+        * d.n_layers / 32.0
     comm = (2 * d.n_layers + 1) * (hw.ar_lat_s + hw.ar_lat_row_s * batch) if tp > 1 else 0.0
     return stream + floor + comm
 

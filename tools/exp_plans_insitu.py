@@ -8,6 +8,7 @@ Variants (comma separated, ``plan`` = unchanged):
   role:stream:WPB:S            stream GEMM for role (qkv | o | down | gate_up) with (wpb, S)
   role:skinny:NT:S             register-streaming kernel
   gate_up:stream_split:WPB:S   split-K gate_up with the SwiGLU in the last arriver
+  deferM                       the TP=1 deferred RMSNorm up to M rows (ops.DEFER_NORM_MAX_M)
 
     python tools/exp_plans_insitu.py --tp-shard 8 --batch 1 --variants plan,attnfused32,gate_up:stream_split:4:4
 """
@@ -46,9 +47,16 @@ def main():
     V = cfg.vocab_size
     prompt = [[1] + [(i * 7919 + j * 31) % (V - 20) + 10 for j in range(a.ctx)] for i in range(a.batch)]
 
+    from llm_map_reduce_summarizer_amd import ops
+    base_defer = ops.DEFER_NORM_MAX_M
+
     def install(v):
         hip.decode_attn_plan, hip.plan = base_attn, base_plan
+        ops.DEFER_NORM_MAX_M = base_defer
         if v == "plan":
+            return
+        if v.startswith("defer"):  # deferFOO: the deferred RMSNorm up to FOO rows
+            ops.DEFER_NORM_MAX_M = int(v[5:])
             return
         if v.startswith("attn"):
             fused = v.startswith("attnfused")
