@@ -166,3 +166,34 @@ MRSUM_API int mrsum_rope_kv_parts(const void* parts, int S, void* qkv_out, int T
     return launch_rope<true>(nullptr, parts, S, qkv_out, T, row_stride, positions, seq_idx, block_tables, bt_stride,
                              kcache, vcache, cos_sin, Hq, Hkv, D, P, 1, s);
 }
+
+// ---------------------------------------------------------------------------------------------
+// K/V row scatter into the paged cache (context-parallel prefill, engine.prefill_export_cp): rows [n, 2, Hkv,
+// D] bf16 (K then V of every kv head of one token, as all-gathered from the other ranks) -> kc / vc [pages,
+// Hkv, P, D] at (page[i], slot[i]) for i < n; entries with page < 0 are skipped (all-gather padding).  One
+// 256-thread block per 4 tokens x ... : a work item is one 16-B vector (8 dims) of one head's K or V row.
+__global__ __launch_bounds__(256) void kv_scatter_kernel(const bf16* __restrict__ rows, int n, int Hkv, int D,
+                                                         const int* __restrict__ page, const int* __restrict__ slot,
+                                                         bf16* __restrict__ kc, bf16* __restrict__ vc, int P) {
+    const int vec_per_tok = 2 * Hkv * (D / 8);
+    const long total = (long)n * vec_per_tok;
+    for (long it = (long)blockIdx.x * 256 + threadIdx.x; it < total; it += (long)gridDim.x * 256) {
+        const int i = (int)(it / vec_per_tok), rem = (int)(it % vec_per_tok);
+        const int kv = rem / (Hkv * (D / 8)), h = (rem / (D / 8)) % Hkv, c = rem % (D / 8);
+        const int pg = page[i];
+        if (pg < 0) continue;
+        const uint4 v = *reinterpret_cast<const uint4*>(rows + (((size_t)i * 2 + kv) * Hkv + h) * D + 8 * c);
+        bf16* dst = (kv ? vc : kc) + (((size_t)pg * Hkv + h) * P + slot[i]) * D + 8 * c;
+        *reinterpret_cast<uint4*>(dst) = v;
+    }
+}
+
+MRSUM_API int mrsum_kv_scatter(const void* rows, int n, int Hkv, int D, const int* page, const int* slot, void* kc,
+                               void* vc, int P, hipStream_t s) {
+    if (n <= 0) return 0;
+    if (D % 8 || Hkv < 1 || P < 1) return (int)hipErrorInvalidValue;
+    const long vecs = (long)n * 2 * Hkv * (D / 8);
+    const int grid = (int)std::min<long>((vecs + 255) / 256, 4096);
+    kv_scatter_kernel<<<grid, 256, 0, s>>>((const bf16*)rows, n, Hkv, D, page, slot, (bf16*)kc, (bf16*)vc, P);
+    return (int)hipGetLastError();
+}

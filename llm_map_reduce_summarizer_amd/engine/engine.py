@@ -126,6 +126,63 @@ class DecodeState:
         self.gen_count[i] = 0
 
 
+class _CPExchange:
+    """Per-slice K/V all-gather of a context-parallel prefill (LLMEngine.prefill_export_cp /
+    LlamaModel.prefill_cp): slice k of every rank's zigzag split is exchanged on its own, asynchronously
+    (RCCL on its own stream; gloo async on CPU ranks), and the received rows land in the paged cache in ONE
+    kv_scatter kernel per slice (own and padding rows carry page -1)."""
+
+    def __init__(self, eng: "LLMEngine", pages: List[int], slices, rank: int, world: int, group):
+        import torch.distributed as dist
+        self.eng, self.rank, self.world, self.group = eng, rank, world, group
+        self.nccl = dist.get_backend(group) == "nccl"
+        dev, P = eng.device, eng.page
+        pg = torch.tensor(pages, dtype=torch.long)
+        self.mine, self.width, self.dst = [], [], []
+        for k in range(len(slices[rank])):
+            rows = [torch.arange(b, e) for b, e in (slices[q][k] for q in range(world))]
+            width = max(1, max(int(r.numel()) for r in rows))
+            b, e = slices[rank][k]
+            own = torch.arange(b, e)
+            self.mine.append(((pg[own // P]).to(dev), (own % P).to(dev), int(own.numel())))
+            # destination (page, slot) of every gathered row, rank-major with padding; own rows -> -1
+            page_d = torch.full((world, width), -1, dtype=torch.int32)
+            slot_d = torch.zeros((world, width), dtype=torch.int32)
+            for q, r in enumerate(rows):
+                if q != rank and r.numel():
+                    page_d[q, :r.numel()] = pg[r // P].to(torch.int32)
+                    slot_d[q, :r.numel()] = (r % P).to(torch.int32)
+            self.width.append(width)
+            self.dst.append((page_d.reshape(-1).to(dev), slot_d.reshape(-1).to(dev)))
+
+    def start(self, layer: int, k: int):
+        """Gather this rank's slice-k K/V rows of ``layer`` and start the all-gather (returns a handle)."""
+        import torch.distributed as dist
+        e = self.eng
+        kc, vc = e.kv.k[layer], e.kv.v[layer]
+        p0, r0, n0 = self.mine[k]
+        mine = torch.zeros(self.width[k], 2, e.model.hkv, e.cfg.head_dim, dtype=kc.dtype, device=e.device)
+        mine[:n0, 0] = kc[p0, :, r0, :]
+        mine[:n0, 1] = vc[p0, :, r0, :]
+        if self.nccl:
+            out = torch.empty((self.world,) + tuple(mine.shape), dtype=kc.dtype, device=e.device)
+            work = dist.all_gather_into_tensor(out, mine, group=self.group, async_op=True)
+        else:
+            out = [torch.empty_like(mine, device="cpu") for _ in range(self.world)]
+            work = dist.all_gather(out, mine.cpu(), group=self.group, async_op=True)
+        return (layer, k, work, out, mine)
+
+    def finish(self, h) -> None:
+        """Wait for a started exchange and scatter the other ranks' rows into the paged cache."""
+        layer, k, work, out, _mine = h
+        work.wait()
+        e = self.eng
+        rows = out if self.nccl else torch.stack(out).to(e.device)
+        page_d, slot_d = self.dst[k]
+        ops.kv_scatter(rows.reshape(-1, 2, e.model.hkv, e.cfg.head_dim).contiguous(), page_d, slot_d,
+                       e.kv.k[layer], e.kv.v[layer])
+
+
 class LLMEngine:
     def __init__(self, cfg: ModelConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0,
                  max_num_seqs: int = 256, max_model_len: int = 16384, max_new_cap: int = 2048,
@@ -785,40 +842,13 @@ class LLMEngine:
             st.temps[0], st.seeds[0] = float(params.temperature), int(params.seed)
             slices = self.cp_slices(n, world)
             mine = [(b, e) for b, e in slices[rank] if e > b]
+            if len(mine) != len(slices[rank]):  # n >= 2 world: every zigzag chunk holds a token
+                raise ValueError("context-parallel prefill: empty slice for %d tokens over %d ranks" % (n, world))
             passes = [self._pass_inputs([s], [span], paged=True) for span in mine]
-            # (page, row) of every position, per rank, for the K/V exchange
-            pg = torch.tensor(s.pages, dtype=torch.long)
-            idx = []
-            for q in range(world):
-                pos = torch.cat([torch.arange(b, e) for b, e in slices[q]])
-                idx.append((pg[pos // P].to(dev), (pos % P).to(dev), int(pos.numel())))
-            width = max(k for _, _, k in idx)
-            nccl = dist.get_backend(group) == "nccl"
-            kc, vc = self.kv.k, self.kv.v
-
-            def exchange(layer: int) -> None:
-                p0, r0, k0 = idx[rank]
-                mine_kv = torch.zeros(width, 2, self.model.hkv, self.cfg.head_dim, dtype=kc.dtype, device=dev)
-                mine_kv[:k0, 0] = kc[layer][p0, :, r0, :]
-                mine_kv[:k0, 1] = vc[layer][p0, :, r0, :]
-                if nccl:
-                    allkv = torch.empty((world,) + tuple(mine_kv.shape), dtype=kc.dtype, device=dev)
-                    dist.all_gather_into_tensor(allkv, mine_kv, group=group)
-                    parts = list(allkv.unbind(0))
-                else:
-                    parts = [torch.empty_like(mine_kv, device="cpu") for _ in range(world)]
-                    dist.all_gather(parts, mine_kv.cpu(), group=group)
-                for q in range(world):
-                    if q == rank:
-                        continue
-                    pq, rq, kq = idx[q]
-                    part = parts[q].to(dev)
-                    kc[layer][pq, :, rq, :] = part[:kq, 0]
-                    vc[layer][pq, :, rq, :] = part[:kq, 1]
-
+            exchange = _CPExchange(self, s.pages, slices, rank, world, group)
             t0 = time.perf_counter()
             last = next((k for k, (b, e) in enumerate(mine) if e == n), None)
-            logits = self.model.prefill_cp(passes, st.block_tables, kc, vc, exchange, logits_pass=last)
+            logits = self.model.prefill_cp(passes, st.block_tables, self.kv.k, self.kv.v, exchange, logits_pass=last)
             self.stats["prefill_tokens"] += sum(e - b for b, e in mine)
             self.stats["cp_prefills"] = self.stats.get("cp_prefills", 0) + 1
             tok = 0
@@ -826,7 +856,7 @@ class LLMEngine:
                 self._sample_first([s], logits)
                 tok = int(st.next_ids[0].item())
             toks = [0] * world
-            if nccl:
+            if exchange.nccl:
                 t = torch.tensor([tok], dtype=torch.int64, device=dev)
                 out = [torch.empty_like(t) for _ in range(world)]
                 dist.all_gather(out, t, group=group)
@@ -838,8 +868,8 @@ class LLMEngine:
             hl = self.model.hkv // world
             npg = self.kv.pages_for(n)
             pidx = torch.tensor(s.pages[:npg], dtype=torch.long, device=dev)
-            k = kc.index_select(1, pidx)[:, :, rank * hl:(rank + 1) * hl]
-            v = vc.index_select(1, pidx)[:, :, rank * hl:(rank + 1) * hl]
+            k = self.kv.k.index_select(1, pidx)[:, :, rank * hl:(rank + 1) * hl]
+            v = self.kv.v.index_select(1, pidx)[:, :, rank * hl:(rank + 1) * hl]
             kv = torch.stack([k, v]).contiguous()
             self._sync()
             self.stats["prefill_s"] += time.perf_counter() - t0

@@ -323,12 +323,15 @@ class LlamaModel:
         return self.logits(x.index_select(0, last.last_rows), gather)
 
     def prefill_cp(self, passes, block_tables: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
-                   exchange: Callable[[int], None], logits_pass: Optional[int] = None) -> Optional[torch.Tensor]:
+                   exchange, logits_pass: Optional[int] = None) -> Optional[torch.Tensor]:
         """Context-parallel prefill (SURVEY §2.5 CP): ``passes`` are THIS rank's slices of one prompt (full
-        weights on every rank, no activation all-reduces), run layer-major.  After a layer's QKV stage has
-        written the slices' K/V rows into the local paged cache, ``exchange(layer)`` all-gathers every
-        rank's rows of that layer into every cache, so each slice's paged attention (causal offset = the
-        slice start) sees the whole prefix.  Returns the logits of ``passes[logits_pass]``'s last row (the
+        weights on every rank, no activation all-reduces), run layer-major.  Slice k of every rank is
+        exchanged on its own: right after pass k's QKV stage has written its K/V rows into the local paged
+        cache, ``exchange.start(layer, k)`` starts the all-gather of every rank's slice-k rows (RCCL's
+        stream), and ``exchange.finish(handle)`` -- just before pass k's attention -- waits for it and
+        scatters the rows into the cache.  With the zigzag split (slice 0 early, slice 1 late) pass k's
+        causal prefix lies in slices <= k of the ranks, so exchange 0 overlaps pass 1's QKV and exchange 1
+        overlaps pass 0's attention + MLP.  Returns the logits of ``passes[logits_pass]``'s last row (the
         rank holding the prompt's end), else None."""
         c = self.cfg
         eps = c.rms_eps
@@ -338,10 +341,13 @@ class LlamaModel:
             res = ops.embed(p.ids, self.embed)
             st.append({"res": res, "x": ops.rmsnorm(res, None, eps)})
         for i, lw in enumerate(self.layers):
-            qkvs = [ops.qkv_rope(s["x"], lw.wqkv, p.positions, p.seq_idx, block_tables, kcache[i], vcache[i],
-                                 self.cos_sin, self.hq, self.hkv, self.hd, page) for p, s in zip(passes, st)]
-            exchange(i)
-            for p, s, qkv in zip(passes, st, qkvs):
+            qkvs, handles = [], []
+            for k, (p, s) in enumerate(zip(passes, st)):
+                qkvs.append(ops.qkv_rope(s["x"], lw.wqkv, p.positions, p.seq_idx, block_tables, kcache[i], vcache[i],
+                                         self.cos_sin, self.hq, self.hkv, self.hd, page))
+                handles.append(exchange.start(i, k))
+            for p, s, qkv, h in zip(passes, st, qkvs, handles):
+                exchange.finish(h)
                 kw = {"seqlens": p.seqlens, "items": p.items} if qkv.is_cuda else {}
                 a = ops.attn_prefill(qkv, p.cu_seqlens, self.hq, self.hkv, self.hd, self.scale,
                                      paged=p.paged.layer(kcache[i], vcache[i]), **kw)

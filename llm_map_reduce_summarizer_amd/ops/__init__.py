@@ -103,6 +103,11 @@ def rope_kv_parts(parts, positions, seq_idx, block_tables, kcache, vcache, cos_s
                                       page)
 
 
+def kv_scatter(rows, page, slot, kcache, vcache):
+    """Scatter all-gathered K/V rows [n, 2, hkv, d] into one layer's paged cache (see ops.hip.kv_scatter)."""
+    return _impl(rows).kv_scatter(rows, page, slot, kcache, vcache)
+
+
 def swiglu(gu, out=None):
     return _impl(gu).swiglu(gu, out)
 

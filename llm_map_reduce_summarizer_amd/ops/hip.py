@@ -28,6 +28,7 @@ _SIGS = {
     "mrsum_rope_kv_parts": [_vp, _c_int, _vp, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _c_int,
                             _c_int, _c_int, _c_int, _vp],
     "mrsum_swiglu": [_vp, _vp, _c_int, _c_int, _vp],
+    "mrsum_kv_scatter": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp],
     "mrsum_embed": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _vp],
     "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_attn_prefill_paged": [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp,
@@ -194,6 +195,21 @@ def rope_kv_parts(parts: torch.Tensor, positions: torch.Tensor, seq_idx: torch.T
     return out
 
 
+def kv_scatter(rows: torch.Tensor, page: torch.Tensor, slot: torch.Tensor, kcache: torch.Tensor,
+               vcache: torch.Tensor) -> None:
+    """kcache / vcache [pages, hkv, P, d] at (page[i], slot[i]) <- rows[i, 0] / rows[i, 1] ([n, 2, hkv, d] bf16;
+    page < 0: skipped).  The K/V rows a context-parallel prefill all-gathers from the other ranks."""
+    _bf16_cuda(rows, kcache, vcache)
+    _i32(page, slot)
+    n = rows.shape[0]
+    _req(rows.is_contiguous() and rows.dim() == 4 and rows.shape[1] == 2 and tuple(rows.shape[2:]) ==
+         (kcache.shape[1], kcache.shape[3]), "kv_scatter: rows must be [n, 2, hkv, d]")
+    _req(kcache.is_contiguous() and vcache.is_contiguous() and kcache.shape == vcache.shape, "kv_scatter: cache")
+    _req(page.numel() >= n and slot.numel() >= n, "kv_scatter: index")
+    _check(_fn("mrsum_kv_scatter")(_p(rows), n, kcache.shape[1], kcache.shape[3], _p(page), _p(slot), _p(kcache),
+                                   _p(vcache), kcache.shape[2], _stream()), "kv_scatter")
+
+
 # ------------------------------------------------------------------ activations
 def swiglu(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     _bf16_cuda(gu)
@@ -321,6 +337,10 @@ def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
         # best at ~one workgroup per CU for small batches (B=5: 6 splits 22.6 us vs 4 25.0; B=10: 3 splits
         # 33.4 vs 4 38.7) and 3 splits from 80 groups up (B=20 60.2 vs 65.3, B=39 111.9 vs 113.9)
         splits = max(1, min(max(3, N_CU // groups), -(-pages // ATTN_PAGES_PER_SPLIT), 64))
+        if groups >= 256:
+            # B = 39 x 8 kv heads in situ after the sc1 merge loads (profiles/r3_plans_insitu_b39_b10.jsonl):
+            # 4 separate splits 6.68 / 6.77 ms per step vs 3 6.86 / 6.86, 2 6.95 / 6.99, 6 6.96 / 6.88
+            splits = min(4, -(-pages // ATTN_PAGES_PER_SPLIT))
     # measured (tools/bench_attn_decode.py; profiles/r2_attn_decode_splits_fused_sweep.jsonl at 4k,
     # r2_attn_decode_splits_10k.jsonl, r2_attn_decode_b1_class0.jsonl): B=1 4k fused 16 splits 16.1-18.0 us
     # vs 32-48 unfused 19.0-21.4, 6k fused 16 17.0 vs 47 unfused 19.9, but B=1 10k 64 unfused 19.5 vs 16

@@ -102,6 +102,15 @@ def rope_kv_parts(parts: torch.Tensor, positions, seq_idx, block_tables, kcache,
     return qkv
 
 
+def kv_scatter(rows: torch.Tensor, page: torch.Tensor, slot: torch.Tensor, kcache: torch.Tensor,
+               vcache: torch.Tensor) -> None:
+    """Reference of ops.hip.kv_scatter: cache[page[i], :, slot[i], :] = rows[i, 0 | 1] (page < 0 skipped)."""
+    keep = page[: rows.shape[0]].long() >= 0
+    pg, sl, r = page[: rows.shape[0]].long()[keep], slot[: rows.shape[0]].long()[keep], rows[keep]
+    kcache[pg, :, sl, :] = r[:, 0].to(kcache.dtype)
+    vcache[pg, :, sl, :] = r[:, 1].to(vcache.dtype)
+
+
 def interleave_gate_up(wg: torch.Tensor, wu: torch.Tensor) -> torch.Tensor:
     """[F, H] gate + [F, H] up -> [2F, H] rows in blocks of 16 = [8 gate | 8 up]."""
     f, h = wg.shape

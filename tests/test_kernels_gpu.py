@@ -721,3 +721,23 @@ def test_fp8_linear_row_chunks(M):
     if M <= hip.STREAM_MAX_M_SWIGLU:  # above: the W8A8 fp8 GEMM (activation quantisation, own tests)
         g, u = reference.split_gate_up(ref)
         _close(hip.fp8_linear_swiglu(x, w), g * torch.sigmoid(g) * u, 3e-2, 3e-2)
+
+
+def test_kv_scatter_matches_reference():
+    """Context-parallel prefill: all-gathered K/V rows [n, 2, hkv, d] land in the paged cache at (page, slot);
+    page -1 rows (own rows, all-gather padding) are skipped."""
+    g = torch.Generator().manual_seed(31)
+    pages, hkv, P, d, n = 12, 2, 64, 128, 300
+    rows = torch.randn(n, 2, hkv, d, generator=g).to(torch.bfloat16)
+    perm = torch.randperm(pages * P, generator=g)[:n]
+    page = (perm // P).to(torch.int32)
+    slot = (perm % P).to(torch.int32)
+    page[::7] = -1
+    kc0 = torch.randn(pages, hkv, P, d, generator=g).to(torch.bfloat16)
+    vc0 = torch.randn(pages, hkv, P, d, generator=g).to(torch.bfloat16)
+    kr, vr = kc0.clone(), vc0.clone()
+    reference.kv_scatter(rows, page, slot, kr, vr)
+    kg, vg = kc0.to(DEV), vc0.to(DEV)
+    hip.kv_scatter(rows.to(DEV), page.to(DEV), slot.to(DEV), kg, vg)
+    assert torch.equal(kg.cpu(), kr) and torch.equal(vg.cpu(), vr)
+    assert not torch.equal(kr, kc0)  # something was written
