@@ -286,6 +286,15 @@ class LLMEngine:
         cache (ops.PagedPrefill, attn_prefill_paged); the K/V of every slice enter the cache before its
         attention, as in one-shot prefill."""
         chunk = self.prefill_chunk
+        if self.model.tp_size > 1 and self.model.sequence_parallel and self.model._sp_backend_ok() and \
+                (not chunk or max(len(s.prompt) for s in seqs) <= chunk):
+            # tensor parallel, one pass: the layer-major path (sequence-parallel norms, async reductions)
+            x = self._pass_inputs(seqs, [(0, len(s.prompt)) for s in seqs], paged=True)
+            logits = self.model.prefill_passes([x], self.state.block_tables, self.kv.k, self.kv.v,
+                                               gather=not self.model.tp_sampling)
+            self.stats["prefill_tokens"] += int(x.ids.numel())
+            self._sample_first(seqs, logits)
+            return
         if not chunk or max(len(s.prompt) for s in seqs) <= chunk:
             self._prefill_pass(seqs, [(0, len(s.prompt)) for s in seqs], paged=self.paged_prefill)
             return

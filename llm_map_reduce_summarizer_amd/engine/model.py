@@ -137,6 +137,8 @@ class LlamaModel:
                                     scaling=cfg.rope_scaling)
         self.vocab_offset = tp_rank * self.vocab_local
         self.emulate_tp_reduce = False  # LocalReduce in place of the TP all-reduce (shard measurements)
+        # TP prefill with sequence parallelism (prefill_passes; MRSUM_SP=0: all-reduces)
+        self.sequence_parallel = os.environ.get("MRSUM_SP", "1") == "1"
         # TP on GPUs: decode all-reduces (fp32 split-K slabs, <= 1 MiB) and the sampler's key max go
         # through the one-shot P2P kernel (parallel/custom_ar.py); larger messages through RCCL
         self.custom_ar = None
@@ -207,6 +209,48 @@ class LlamaModel:
             self.custom_ar.all_reduce(t)
             return None
         return torch.distributed.all_reduce(t, group=self.tp_group, async_op=True)
+
+    # ---- sequence parallelism (Megatron SP) of the TP prefill: the residual stream is split over the TP
+    # ranks by token rows; a projection's partial sums are REDUCE-SCATTERED to the row shards (instead of
+    # all-reduced), add + RMSNorm run on 1 / TP of the rows, and the normed rows are ALL-GATHERED for the
+    # next column-parallel GEMM -- the same bytes on the links as the all-reduce, 1 / TP of the norm work
+    # and residual memory.  Rows are padded to a multiple of TP.
+    def _sp_backend_ok(self) -> bool:
+        """Reduce-scatter of device tensors needs RCCL (gloo takes CPU tensors only: CPU ranks, or the
+        shared-GPU rehearsals, which then keep the all-reduces)."""
+        if self.device.type != "cuda":
+            return True
+        return torch.distributed.get_backend(self.tp_group) == "nccl"
+
+    def _sp_rows(self, T: int):
+        Tp = -(-T // self.tp_size) * self.tp_size
+        return Tp, Tp // self.tp_size
+
+    def _sp_shard(self, t: torch.Tensor) -> torch.Tensor:
+        """This rank's row shard of a replicated [T, H] tensor (padded rows are zero)."""
+        T = t.shape[0]
+        Tp, Ts = self._sp_rows(T)
+        out = torch.zeros(Ts, t.shape[1], dtype=t.dtype, device=t.device)
+        lo = self.tp_rank * Ts
+        n = max(0, min(T, lo + Ts) - lo)
+        if n:
+            out[:n] = t[lo:lo + n]
+        return out
+
+    def _sp_reduce_scatter_async(self, t: torch.Tensor):
+        """Start the TP sum of partial rows ``t`` [T, H], scattered by row shards: (shard, handle)."""
+        T = t.shape[0]
+        Tp, Ts = self._sp_rows(T)
+        if Tp != T:
+            t = torch.cat([t, torch.zeros(Tp - T, t.shape[1], dtype=t.dtype, device=t.device)])
+        out = torch.empty(Ts, t.shape[1], dtype=t.dtype, device=t.device)
+        h = torch.distributed.reduce_scatter_tensor(out, t.contiguous(), group=self.tp_group, async_op=True)
+        return out, h
+
+    def _sp_all_gather(self, shard: torch.Tensor, T: int) -> torch.Tensor:
+        out = torch.empty(shard.shape[0] * self.tp_size, shard.shape[1], dtype=shard.dtype, device=shard.device)
+        torch.distributed.all_gather_into_tensor(out, shard.contiguous(), group=self.tp_group)
+        return out[:T]
 
     @property
     def tp_sampling(self) -> bool:
@@ -288,38 +332,47 @@ class LlamaModel:
         c = self.cfg
         eps = c.rms_eps
         page = kcache.shape[3]
+        sp = self.sequence_parallel and self.tp_size > 1 and self._sp_backend_ok()
         st = []
         for p in passes:
             res = ops.embed(p.ids, self.embed)
-            st.append({"res": res, "x": ops.rmsnorm(res, None, eps)})
+            x = ops.rmsnorm(res, None, eps)
+            # SP: the residual is kept as this rank's row shard (see _sp_rows)
+            st.append({"res": self._sp_shard(res) if sp else res, "x": x, "T": int(res.shape[0])})
 
         def wait(h):
             if h is not None:
                 h.wait()
 
+        def reduce_async(s, t, key):  # the TP sum of a projection's partial rows
+            if sp:
+                s[key], s["w"] = self._sp_reduce_scatter_async(t)
+            else:
+                s[key], s["w"] = t, self._all_reduce_async(t)
+
+        def add_norm(s, key):  # residual += the summed projection; the normed rows for the next GEMM
+            wait(s.pop("w"))
+            x = ops.add_rmsnorm(s.pop(key), s["res"], None, eps)
+            return self._sp_all_gather(ops.rows(x), s["T"]) if sp else x
+
         for i, lw in enumerate(self.layers):
             for p, s in zip(passes, st):
-                if "w2" in s:  # previous layer's down-projection sum (overlapped with the other passes' MLPs)
-                    wait(s.pop("w2"))
-                    s["x"] = ops.add_rmsnorm(s.pop("d"), s["res"], None, eps)
+                if "d" in s:  # previous layer's down-projection sum (overlapped with the other passes' MLPs)
+                    s["x"] = add_norm(s, "d")
                 qkv = ops.qkv_rope(s["x"], lw.wqkv, p.positions, p.seq_idx, block_tables, kcache[i], vcache[i],
                                    self.cos_sin, self.hq, self.hkv, self.hd, page)
                 kw = {"seqlens": p.seqlens, "items": p.items} if qkv.is_cuda else {}
                 pp = p.paged.layer(kcache[i], vcache[i]) if p.paged is not None else None
                 a = ops.attn_prefill(qkv, p.cu_seqlens, self.hq, self.hkv, self.hd, self.scale, paged=pp, **kw)
-                s["o"] = ops.linear(a, lw.wo)
-                s["w1"] = self._all_reduce_async(s["o"])
+                reduce_async(s, ops.linear(a, lw.wo), "o")
             for s in st:
-                wait(s.pop("w1"))
-                x = ops.add_rmsnorm(s.pop("o"), s["res"], None, eps)
+                x = add_norm(s, "o")
                 act = ops.gate_up_swiglu(x, lw.wgu)
-                s["d"] = ops.linear(act, lw.wdown)
-                s["w2"] = self._all_reduce_async(s["d"])
+                reduce_async(s, ops.linear(act, lw.wdown), "d")
         last, s = passes[-1], st[-1]
         for t in st[:-1]:
-            wait(t.pop("w2"))
-        wait(s.pop("w2"))
-        x = ops.add_rmsnorm(s.pop("d"), s["res"], None, eps)
+            wait(t.pop("w"))
+        x = add_norm(s, "d")
         return self.logits(x.index_select(0, last.last_rows), gather)
 
     def prefill_cp(self, passes, block_tables: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,

@@ -145,6 +145,18 @@ def test_tp2_chunked_layer_major_prefill_matches_one_pass():
     assert chunked[0] == one[0], (chunked[0], one[0])
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("chunk", [0, 64])
+def test_tp2_sequence_parallel_prefill_matches_all_reduce(chunk):
+    """Sequence-parallel TP prefill (residual row shards: reduce-scatter -> add + RMSNorm on 1 / TP of the
+    rows -> all-gather; model.prefill_passes) generates what the all-reduce TP prefill generates."""
+    sp = _run_tp(2, 2, PLEN=150, CHUNK=chunk, MRSUM_SP=1)
+    ar = _run_tp(2, 2, PLEN=150, CHUNK=chunk, MRSUM_SP=0)
+    assert sp[0] == sp[1]
+    same = sum(a == b for a, b in zip(sp[0], ar[0]))
+    assert same >= 2, (sp[0], ar[0])  # greedy; the reduce order may flip a bf16 near-tie
+
+
 RTP_SCRIPT = SCRIPT.replace('engine_options={"kv_pages": 512, "max_num_seqs": 16})',
                             'engine_options={"kv_pages": 512, "max_num_seqs": 16}, reduce_tp=True)').replace(
     'LocalEngineProvider("tiny", cfg', 'LocalEngineProvider("tiny-gqa4", cfg').replace(

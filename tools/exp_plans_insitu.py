@@ -9,6 +9,7 @@ Variants (comma separated, ``plan`` = unchanged):
   role:skinny:NT:S             register-streaming kernel
   gate_up:stream_split:WPB:S   split-K gate_up with the SwiGLU in the last arriver
   deferM                       the TP=1 deferred RMSNorm up to M rows (ops.DEFER_NORM_MAX_M)
+  fp8resid:N:K:WPB:S           the fp8 deferred-norm producer (stream_fp8, residual epilogue) of one shape
 
     python tools/exp_plans_insitu.py --tp-shard 8 --batch 1 --variants plan,attnfused32,gate_up:stream_split:4:4
 """
@@ -28,6 +29,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--tp-shard", type=int, default=1)
+    ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--variants", default="plan")
     a = ap.parse_args()
     import torch
@@ -41,7 +43,7 @@ def main():
         cfg = get_model_config(a.model, n_heads=cfg.n_heads // k, n_kv_heads=cfg.n_kv_heads // k,
                                ffn=cfg.ffn // k, vocab_size=cfg.vocab_size // k)
     eng = LLMEngine(cfg, device="cuda:0", max_model_len=a.ctx + a.new + 64, max_num_seqs=max(8, a.batch),
-                    kv_fraction=0.5, sync_every=32)
+                    kv_fraction=0.5, sync_every=32, weight_dtype=a.dtype)
     eng.model.emulate_tp_reduce = k > 1
     bucket = eng._bucket(a.batch)
     V = cfg.vocab_size
@@ -49,11 +51,17 @@ def main():
 
     from llm_map_reduce_summarizer_amd import ops
     base_defer = ops.DEFER_NORM_MAX_M
+    base_fp8r = hip.fp8_resid_cfg
 
     def install(v):
         hip.decode_attn_plan, hip.plan = base_attn, base_plan
         ops.DEFER_NORM_MAX_M = base_defer
+        hip.fp8_resid_cfg = base_fp8r
         if v == "plan":
+            return
+        if v.startswith("fp8resid:"):  # fp8resid:N:K:wpb:S -- the fp8 deferred-norm producer of one shape
+            N0, K0, wpb, S = (int(t) for t in v.split(":")[1:])
+            hip.fp8_resid_cfg = lambda M, N, K: (wpb, S) if (N, K) == (N0, K0) else base_fp8r(M, N, K)
             return
         if v.startswith("defer"):  # deferFOO: the deferred RMSNorm up to FOO rows
             ops.DEFER_NORM_MAX_M = int(v[5:])

@@ -14,6 +14,9 @@ cat $OUT
 timeout -k 10 400 python tools/bench_decode.py --model llama3-70b --dtype fp8 --tp-shard 8 --batches 1,10 --ctx 32000 \
   --new 128 > gpurun_out/r3h/tp8_70b_fp8.log 2>&1 || exit 1
 grep "^{" gpurun_out/r3h/tp8_70b_fp8.log
+timeout -k 10 500 python tools/bench_decode.py --model llama3-70b --dtype fp8 --batches 1 --ctx 32000 \
+  --new 128 > gpurun_out/r3h/tp1_70b_fp8.log 2>&1 || exit 1
+grep "^{" gpurun_out/r3h/tp1_70b_fp8.log
 export MRSUM_DP_KV_FRACTION=0.05 MRSUM_REDUCE_KV_FRACTION=0.05 ENGINE_KV_FRACTION=0.05
 MRSUM_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
   --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 4 --hours 1 --steps 1 --warmup 1 --max-new-tokens 64 \
