@@ -17,77 +17,12 @@
 // Uncached memory keeps remote data and flags out of every L2 (no stale lines across GPUs); the
 // release store orders the slot stores before the flag (buffer_wbl2 + s_waitcnt before it).
 // A wait that exceeds its bound sets an error word (read by the host) instead of hanging the GPU.
-#include "common.h"
+#include "ar_common.h"
 
 #include <cstring>
 #include <new>
 
-namespace {
-constexpr int MAX_RANKS = 8;
-constexpr int MAX_BLOCKS = 64;
-constexpr size_t HDR = 64 * 1024;  // flags region, slot 0 starts here
-constexpr size_t CH = 16 * 1024;   // bytes per block (fixed: see ar_oneshot_kernel)
-// push-mode (ar_add_rmsnorm_kernel) flags: [MAX_ROWS][MAX_RANKS] u32 at PUSH_FLAGS inside HDR
-constexpr int MAX_ROWS = 256;
-constexpr size_t PUSH_FLAGS = 16 * 1024;
-static_assert(PUSH_FLAGS >= (size_t)MAX_BLOCKS * MAX_RANKS * 4, "flag regions overlap");
-static_assert(PUSH_FLAGS + (size_t)MAX_ROWS * MAX_RANKS * 4 <= HDR, "push flags exceed header");
-
-struct Peers {
-    char* base[MAX_RANKS];  // every rank's allocation (mine included)
-};
-
-struct ArHandle {
-    int rank, world;
-    size_t max_bytes;
-    char* mine;          // my uncached allocation
-    void* opened[MAX_RANKS];
-    Peers peers;
-    unsigned* epochs;    // [MAX_BLOCKS] local device counters (regular memory)
-    unsigned* error;     // [1] set on a timed-out wait
-    unsigned* push_epochs;  // [MAX_ROWS] per-row counters of the push-mode kernel
-};
-
-__device__ __forceinline__ void st_release_sys(unsigned* p, unsigned v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// Write-through publish (WT): payload stored with system-scope relaxed atomic stores (global_store
-// sc0 sc1: coherent at system scope once acknowledged), every store drained (s_waitcnt vmcnt(0)),
-// then a relaxed system-scope flag store.  The fenced form (release fence + release flag store)
-// emits two buffer_wbl2, each writing back EVERY dirty line of this XCD's L2 -- inside a decode graph
-// the preceding GEMM's split-K slabs -- for a payload that lives in uncached memory and never
-// touches L2.  (The same drained-payload-then-flag hand-off as attn_decode.hip's write-through merge;
-// cdna_hip_programming.md / MI355X_MICROARCH.md "handoff-flag".)
-__device__ __forceinline__ void st_wt8(void* p, unsigned long long v) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-__device__ __forceinline__ void st_flag(unsigned* p, unsigned v, bool wt) {
-    if (wt) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    else st_release_sys(p, v);
-}
-
-// Spin (relaxed system-scope loads, s_sleep between polls) until *f >= epoch, bounded in WALL time by
-// the 100 MHz s_memrealtime counter: ranks are launched by independent host threads and may lag each
-// other by host-side jitter (GC, logging, a first kernel-library load), so the bound is generous (4 s) but
-// finite -- a peer that is gone sets the sticky error word (checked by the host after every generate)
-// instead of hanging the GPU.  Once the error is set, later waits do not spin at all.
-constexpr unsigned long long WAIT_TICKS = 400000000ull;  // 4 s at 100 MHz
-
-__device__ __forceinline__ void wait_flag(const unsigned* f, unsigned epoch, unsigned* error) {
-    if (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= epoch) return;
-    if (__hip_atomic_load(error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < epoch) {
-        __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > WAIT_TICKS) {
-            atomicOr(error, 1u);
-            break;
-        }
-    }
-}
-}  // namespace
+using namespace mrsum_ar;
 
 enum { OP_SUM_F32 = 0, OP_MAX_U64 = 1 };
 
@@ -182,8 +117,6 @@ __global__ __launch_bounds__(256) void ar_oneshot_kernel(Peers peers, int rank, 
 // split-K sum folded in, so the producing GEMM keeps its split count under TP).  Slot reuse is safe
 // for the same reason as above, per row: a peer can only push call e+2 into my slot e & 1 after
 // passing call e+1's wait for row r, which needs my flag of call e+1, i.e. my call e is complete.
-constexpr size_t push_off(size_t slot_bytes) { return HDR + 2 * slot_bytes; }
-
 template <int VPT, bool WT>  // float4 vectors per thread: D <= 1024 * VPT
 __global__ __launch_bounds__(256) void ar_add_rmsnorm_kernel(Peers peers, int rank, int world, size_t slot_bytes,
                                                              const float* __restrict__ parts, int S, int T,
@@ -312,13 +245,12 @@ MRSUM_API void* mrsum_ar_create(int rank, int world, size_t max_bytes) {
     h->world = world;
     h->max_bytes = max_bytes;
     void* p = nullptr;
-    if (hipExtMallocWithFlags(&p, push_off(max_bytes) + 2 * (size_t)world * max_bytes, hipDeviceMallocUncached) !=
-        hipSuccess) {
+    if (hipExtMallocWithFlags(&p, alloc_bytes(max_bytes, world), hipDeviceMallocUncached) != hipSuccess) {
         delete h;
         return nullptr;
     }
     h->mine = (char*)p;
-    constexpr size_t n_ctr = MAX_BLOCKS + 16 + MAX_ROWS;  // epochs | error (+pad) | push epochs
+    constexpr size_t n_ctr = MAX_BLOCKS + 16 + MAX_ROWS + MAX_GRAN;  // epochs | error (+pad) | push | granule epochs
     if (hipMemset(p, 0, HDR) != hipSuccess || hipMalloc((void**)&h->epochs, n_ctr * sizeof(unsigned))) {
         (void)hipFree(p);
         delete h;
@@ -327,6 +259,7 @@ MRSUM_API void* mrsum_ar_create(int rank, int world, size_t max_bytes) {
     (void)hipMemset(h->epochs, 0, n_ctr * sizeof(unsigned));
     h->error = h->epochs + MAX_BLOCKS;
     h->push_epochs = h->epochs + MAX_BLOCKS + 16;
+    h->gran_epochs = h->push_epochs + MAX_ROWS;
     for (int r = 0; r < MAX_RANKS; ++r) {
         h->peers.base[r] = nullptr;
         h->opened[r] = nullptr;

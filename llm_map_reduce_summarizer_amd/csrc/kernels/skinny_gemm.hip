@@ -21,10 +21,44 @@
 //    out as [8 gate | 8 up] blocks so one workgroup tile holds gate and up of
 //    the same 8 features: act = silu(g) * u is written directly, the gate_up
 //    activation never exists in HBM).
-#include "common.h"
+//  * deferred-RMSNorm operands (stream_gemm.hip header), one 16-row tile per workgroup, no split-K:
+//    SWIGLU takes x = the un-normalised residual rows + the producer's per-tile sums of squares and
+//    scales gate and up rows by rsqrt(mean(h^2) + eps) (the stream consumer's reduction order, so every
+//    consumer of a row scales it by the same factor); RESID is a producer: residual += the tile (after
+//    the TP push all-reduce when ``tp.world`` > 0, ar_common.h), per-tile row sums of squares to ssp.
+//    A TP-shard row-parallel projection (K <= 2048) keeps this kernel's launch floor instead of the
+//    stream kernel's ring ramp.
+#include "ar_common.h"
 
 namespace {
-enum { EPI_BF16 = 0, EPI_F32_PARTIAL = 1, EPI_SWIGLU = 2 };
+enum { EPI_BF16 = 0, EPI_F32_PARTIAL = 1, EPI_SWIGLU = 2, EPI_RESID = 3 };
+
+struct SkinnyNorm {
+    const float* ssq;  // SWIGLU consumer: [M][ssq_tiles] row sums of squares of x per producer tile (or null)
+    int ssq_tiles;     // multiple of 32
+    float inv_k, eps;
+    bf16* resid;       // RESID producer: residual rows [M][ldr] (in / out)
+    int ldr;
+    float* ssp;        // RESID producer: [M][gridDim.x] row sums of squares of the new residual per tile
+    mrsum_ar::TPPush tp;
+};
+
+// rsqrt(mean(h_m^2) + eps) from the producer tiles' sums, in stream_gemm.hip's order (8 partials of
+// ssq_tiles / 8 consecutive tiles in float4 steps, then the partials in order)
+__device__ __forceinline__ float deferred_row_scale(const SkinnyNorm& e, int m) {
+    const int C = e.ssq_tiles / 8;
+    const float4* src = reinterpret_cast<const float4*>(e.ssq + (size_t)m * e.ssq_tiles);
+    float t = 0.f;
+    for (int p = 0; p < 8; ++p) {
+        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int q = 0; q < C / 4; ++q) {
+            const float4 v = src[p * (C / 4) + q];
+            a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+        }
+        t += (a.x + a.y) + (a.z + a.w);
+    }
+    return rsqrtf(t * e.inv_k + e.eps);
+}
 constexpr int KB = 128;  // k elements per wave round (4 MFMA k-steps of 32)
 
 template <int NT>
@@ -80,12 +114,16 @@ __device__ __forceinline__ void mma_block(f32x4 (&acc)[NT][MT], const AFrag<NT>&
 template <int NT, int MT, int EPI>
 __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16* __restrict__ x, int ldx,
                                                           const bf16* __restrict__ W, int K, int M,
-                                                          void* __restrict__ out, int ldo, int kper) {
+                                                          void* __restrict__ out, int ldo, int kper,
+                                                          const SkinnyNorm e) {
     constexpr int BN = 16 * NT, BM = 16 * MT;
+    static_assert(EPI != EPI_RESID || (NT == 1 && MT == 1), "RESID: one 16-row tile, M <= 16");
     __shared__ __attribute__((aligned(16))) float red[4][BM][BN + 4];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int n0 = blockIdx.x * BN;
     const int ks = blockIdx.y * kper, ke = min(K, ks + kper);
+    // TP push: this launch's epoch of the tile's granule, loaded long before it is needed
+    const unsigned tp_epoch = EPI == EPI_RESID && e.tp.world > 0 ? e.tp.epochs[n0 / mrsum_ar::GRAN] + 1 : 0;
 
     f32x4 acc[NT][MT];
 #pragma unroll
@@ -139,15 +177,33 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16* __restrict
         } else if constexpr (EPI == EPI_F32_PARTIAL) {
             float* o = reinterpret_cast<float*>(out) + ((size_t)blockIdx.y * M + m) * ldo + n0 + n4;
             *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        } else if constexpr (EPI == EPI_RESID) {
+            // h = bf16(residual + tile) (+ the TP group's tiles, rank order); the tile's row sum of h^2
+            // over its 4 items (lanes 4m .. 4m+3 of wave 0) to ssp[m][tile]
+            uint2* rp = reinterpret_cast<uint2*>(e.resid + (size_t)m * e.ldr + n0 + n4);
+            const uint2 rv = *rp;
+            float4 a = make_float4(v[0], v[1], v[2], v[3]);
+            if (e.tp.world > 0) {
+                const long long off = mrsum_ar::tp_item_off(m, gridDim.x * BN, n0 + n4);
+                mrsum_ar::tp_push_item(e.tp, off, tp_epoch, a);
+                a = mrsum_ar::tp_gather_item(e.tp, off, tp_epoch);
+            }
+            const uint2 hv = make_uint2(pack2(__uint_as_float(rv.x << 16) + a.x, __uint_as_float(rv.x & 0xffff0000u) + a.y),
+                                        pack2(__uint_as_float(rv.y << 16) + a.z, __uint_as_float(rv.y & 0xffff0000u) + a.w));
+            *rp = hv;
+            const float h0 = __uint_as_float(hv.x << 16), h1 = __uint_as_float(hv.x & 0xffff0000u);
+            const float h2 = __uint_as_float(hv.y << 16), h3 = __uint_as_float(hv.y & 0xffff0000u);
+            red[0][m][n4] = (h0 * h0 + h1 * h1) + (h2 * h2 + h3 * h3);  // own slot: every red read is done
         } else {  // SWIGLU: tile rows [0, BN/2) gate, [BN/2, BN) up of features [blockIdx.x*BN/2, +BN/2)
             constexpr int H = BN / 2;
             if (n4 < H) {
+                const float sc = e.ssq ? deferred_row_scale(e, m) : 1.f;
                 float r[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const float u = red[0][m][n4 + H + j] + red[1][m][n4 + H + j] + red[2][m][n4 + H + j] +
-                                    red[3][m][n4 + H + j];
-                    const float g = v[j];
+                    const float u = (red[0][m][n4 + H + j] + red[1][m][n4 + H + j] + red[2][m][n4 + H + j] +
+                                     red[3][m][n4 + H + j]) * sc;
+                    const float g = v[j] * sc;
                     r[j] = g / (1.f + __expf(-g)) * u;
                 }
                 uint2 o;
@@ -157,41 +213,69 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16* __restrict
             }
         }
     }
+    if constexpr (EPI == EPI_RESID) {
+        __syncthreads();
+        if (threadIdx.x < M) {
+            const float* q = red[0][threadIdx.x];
+            e.ssp[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = ((q[0] + q[4]) + (q[8] + q[12]));
+        }
+        if (e.tp.world > 0 && threadIdx.x == 0) e.tp.epochs[n0 / mrsum_ar::GRAN] = tp_epoch;
+    }
 }
 
 template <int NT, int EPI>
 static int launch_mt(int mt, dim3 grid, hipStream_t s, const bf16* x, int ldx, const bf16* W, int K, int M,
-                     void* out, int ldo, int kper) {
+                     void* out, int ldo, int kper, const SkinnyNorm& e) {
     switch (mt) {
-        case 1: skinny_gemm_kernel<NT, 1, EPI><<<grid, 256, 0, s>>>(x, ldx, W, K, M, out, ldo, kper); break;
-        case 2: skinny_gemm_kernel<NT, 2, EPI><<<grid, 256, 0, s>>>(x, ldx, W, K, M, out, ldo, kper); break;
-        case 3: skinny_gemm_kernel<NT, 3, EPI><<<grid, 256, 0, s>>>(x, ldx, W, K, M, out, ldo, kper); break;
-        case 4: skinny_gemm_kernel<NT, 4, EPI><<<grid, 256, 0, s>>>(x, ldx, W, K, M, out, ldo, kper); break;
+        case 1: skinny_gemm_kernel<NT, 1, EPI><<<grid, 256, 0, s>>>(x, ldx, W, K, M, out, ldo, kper, e); break;
+        case 2: skinny_gemm_kernel<NT, 2, EPI><<<grid, 256, 0, s>>>(x, ldx, W, K, M, out, ldo, kper, e); break;
+        case 3: skinny_gemm_kernel<NT, 3, EPI><<<grid, 256, 0, s>>>(x, ldx, W, K, M, out, ldo, kper, e); break;
+        case 4: skinny_gemm_kernel<NT, 4, EPI><<<grid, 256, 0, s>>>(x, ldx, W, K, M, out, ldo, kper, e); break;
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
 }
 
-// epi: 0 bf16 [M, ldo], 1 fp32 partial [S, M, ldo], 2 swiglu bf16 [M, ldo] (ldo >= N/2)
-// nt: 16-row W tiles per workgroup (1 or 2; swiglu needs 1); splits: S (K/S multiple of 128)
+// epi: 0 bf16 [M, ldo], 1 fp32 partial [S, M, ldo], 2 swiglu bf16 [M, ldo] (ldo >= N/2), 3 residual update
+// (resid [M, ldr] bf16 += x W^T, ssp fp32 [M, N / 16] per-tile row sums of squares of the new residual;
+// nt 1, splits 1, M <= 16; ``ar`` non-null: all-reduced over that custom all-reduce group first (TP push,
+// M * N * 4 <= its slot bytes)).  nt: 16-row W tiles per workgroup (1 or 2; swiglu needs 1); splits: S (K/S
+// multiple of 128).  ssq (swiglu only): deferred-RMSNorm input [M, ssq_tiles] fp32, ssq_tiles % 32 == 0.
 MRSUM_API int mrsum_skinny_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
-                                int epi, int nt, int splits, hipStream_t s) {
+                                int epi, int nt, int splits, const float* ssq, int ssq_tiles, float eps, void* resid,
+                                int ldr, float* ssp, void* ar, hipStream_t s) {
+    using namespace mrsum_ar;
     if (M <= 0) return 0;
-    if (M > 64 || K % KB || splits < 1 || (K / KB) % splits || (nt != 1 && nt != 2) || N % (16 * nt))
+    if (M > 64 || K % KB || splits < 1 || (K / KB) % splits || (nt != 1 && nt != 2) || N % (16 * nt) ||
+        epi < EPI_BF16 || epi > EPI_RESID)
         return (int)hipErrorInvalidValue;
     if (epi != EPI_F32_PARTIAL && splits != 1) return (int)hipErrorInvalidValue;
     if (epi == EPI_SWIGLU && nt != 1) return (int)hipErrorInvalidValue;  // weight blocks of [8 gate | 8 up]
+    if (ssq && (epi != EPI_SWIGLU || ssq_tiles <= 0 || ssq_tiles % 32)) return (int)hipErrorInvalidValue;
+    if (epi == EPI_RESID && (nt != 1 || M > 16 || !resid || !ssp || ldr % 4)) return (int)hipErrorInvalidValue;
+    if (ar) {
+        auto h = (const ArHandle*)ar;
+        if (epi != EPI_RESID || N / GRAN > MAX_GRAN || (size_t)M * N * 4 > h->max_bytes) return (int)hipErrorInvalidValue;
+        for (int r = 0; r < h->world; ++r)
+            if (!h->peers.base[r]) return (int)hipErrorInvalidValue;
+    }
+    SkinnyNorm e;
+    e.ssq = ssq; e.ssq_tiles = ssq_tiles; e.inv_k = 1.f / (float)K; e.eps = eps;
+    e.resid = (bf16*)resid; e.ldr = ldr; e.ssp = ssp;
+    e.tp = tp_push_of((const ArHandle*)ar);
     const int kper = K / splits;
     const int mt = (M + 15) / 16;
     dim3 grid(N / (16 * nt), splits);
     auto X = (const bf16*)x; auto Wp = (const bf16*)W;
     if (nt == 1) {
-        if (epi == EPI_BF16) return launch_mt<1, EPI_BF16>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper);
-        if (epi == EPI_F32_PARTIAL) return launch_mt<1, EPI_F32_PARTIAL>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper);
-        if (epi == EPI_SWIGLU) return launch_mt<1, EPI_SWIGLU>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper);
+        if (epi == EPI_BF16) return launch_mt<1, EPI_BF16>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper, e);
+        if (epi == EPI_F32_PARTIAL) return launch_mt<1, EPI_F32_PARTIAL>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper, e);
+        if (epi == EPI_SWIGLU) return launch_mt<1, EPI_SWIGLU>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper, e);
+        skinny_gemm_kernel<1, 1, EPI_RESID><<<grid, 256, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, e);
+        return (int)hipGetLastError();
     } else {
-        if (epi == EPI_BF16) return launch_mt<2, EPI_BF16>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper);
-        if (epi == EPI_F32_PARTIAL) return launch_mt<2, EPI_F32_PARTIAL>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper);
+        if (epi == EPI_BF16) return launch_mt<2, EPI_BF16>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper, e);
+        if (epi == EPI_F32_PARTIAL) return launch_mt<2, EPI_F32_PARTIAL>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper, e);
     }
     return (int)hipErrorInvalidValue;
 }

@@ -33,7 +33,27 @@
 //     rsqrt(mean(h^2) + eps) * (h W'^T): the row scale multiplies the accumulator in the epilogue,
 //     from the producer's per-tile sums reduced in a fixed order (deterministic).
 // Two kernels per layer fewer than GEMM -> add_rmsnorm_parts -> GEMM.
-#include "common.h"
+//
+// TP push (tensor-parallel decode, e.tp.world > 0): the producer's partial sum is this rank's share of a
+// row-parallel projection.  Its last arriver all-reduces the column tile across the TP group before the
+// residual update -- the custom all-reduce's push protocol (custom_ar.hip ar_add_rmsnorm_kernel) moved
+// into the GEMM epilogue, per 16-column granule instead of per row:
+//   1. bf16(tile partial sum) -> granule-push slot (epoch & 1, me) of EVERY rank over xGMI, as TAGGED
+//      8-byte words: 2 bf16 | the epoch (system-scope single-copy-atomic stores, fire and forget)
+//   2. poll my own slots until every rank's words carry this epoch -- the data is its own flag: no flag
+//      store, no drain before it, no acquire (the NCCL "LL" idea; 2 B of tag per 2 B of payload, nothing
+//      at M <= 16 rows)
+//   3. h = bf16(residual + sum_p slot[p] in rank order) -- every rank adds the same bf16 values in the
+//      same order, so the TP replicas of the residual stay bit-identical -- then the residual store and
+//      the per-tile sums of squares exactly as the local producer.
+// The epoch of a granule is a local counter advanced by the workgroup that owns the granule (every call
+// covers all granules of the hidden dimension, so all counters agree, whatever the tiling).  Payload
+// slot reuse two calls later is safe: a peer pushing call e+2 into parity e & 1 has passed call e+1's
+// wait, which needs my words of call e+1, pushed after my call e (stream order) read the slot.  Spinning
+// last arrivers hold at most one CU per column tile (< #CUs), so every rank completes all its tiles
+// whatever its peers do: no cross-rank deadlock.  One launch per projection fewer than GEMM ->
+// ar_add_rmsnorm, and the consumer takes the deferred norm as at TP = 1.
+#include "ar_common.h"
 
 namespace {
 enum { EPI_BF16 = 0, EPI_F32_PARTIAL = 1, EPI_SWIGLU = 2, EPI_SWIGLU_SPLIT = 3, EPI_RESID_SPLIT = 4 };
@@ -52,6 +72,7 @@ struct NormArgs {
     int ldr;
     float* ssp;        // producer: [M][gridDim.x] row sums of squares of h per column tile
     int slab_m;        // F32_PARTIAL: rows per slab (0: M) -- row chunks of decode batches above 64 rows
+    mrsum_ar::TPPush tp;  // RESID_SPLIT: all-reduce the tile over the TP group (tp.world == 0: off)
 };
 
 template <int N>
@@ -129,6 +150,27 @@ __device__ __forceinline__ void rearm(int* counters, int tile, int tid) {
 }  // namespace
 
 namespace {
+// TP push of one column tile (header "TP push"), M <= 16 rows: thread tid owns item tid < M * Q = (row mm,
+// 4 columns at c).  h[0] holds this rank's fp32 partial sums on entry and the rank-ordered all-reduced bf16
+// sums plus the residual rv[0] on exit (rounded exactly as ar_add_rmsnorm_kernel).  ``epoch``: this
+// launch's epoch of the tile's granules (read before the split-K ticket).
+template <int IT, int Q, int GT>
+__device__ __forceinline__ void tp_push_tile(const mrsum_ar::TPPush& tp, float (&h)[IT][4], const uint2 (&rv)[IT],
+                                             const int M, const int n0, const int ncols, const int tid,
+                                             const unsigned epoch) {
+    using namespace mrsum_ar;
+    if (tid < M * Q) {
+        const long long off = tp_item_off(tid / Q, ncols, n0 + 4 * (tid % Q));
+        tp_push_item(tp, off, epoch, make_float4(h[0][0], h[0][1], h[0][2], h[0][3]));
+        const float4 acc = tp_gather_item(tp, off, epoch);
+        h[0][0] = __uint_as_float(rv[0].x << 16) + acc.x;
+        h[0][1] = __uint_as_float(rv[0].x & 0xffff0000u) + acc.y;
+        h[0][2] = __uint_as_float(rv[0].y << 16) + acc.z;
+        h[0][3] = __uint_as_float(rv[0].y & 0xffff0000u) + acc.w;
+    }
+    if (tid < GT) tp.epochs[n0 / GRAN + tid] = epoch;
+}
+
 // Epilogue shared by the bf16 and fp8 stream kernels.  acc[m]: lane holds out^T[n = n0 + 16w + 4g + jj]
 // [m = 16 mt + r] (fp8: already times the weight row scales).  ``lds`` = the kernel's one LDS array
 // (the ring is drained by now), ``s_ss`` its 2 KiB row-norm partials region.
@@ -194,6 +236,8 @@ __device__ __forceinline__ void stream_epilogue(f32x4 (&acc)[MT], char* lds, flo
     if constexpr (EPI == EPI_SWIGLU_SPLIT || EPI == EPI_RESID_SPLIT) {
         // the last of the gridDim.y split workgroups of this column tile to arrive sums the fp32 partial
         // tiles (write-through publish / ticket / acquire, as attn_decode.hip combine_if_last<G, true>)
+        // TP push: this launch's epoch of the tile's granules, loaded ahead of the ticket's drain
+        const unsigned tp_epoch = EPI == EPI_RESID_SPLIT && e.tp.world > 0 ? e.tp.epochs[n0 / mrsum_ar::GRAN] + 1 : 0;
         if (!last_arrival(counters, blockIdx.x, gridDim.y, tid, reinterpret_cast<int*>(lds))) return;
         const int S = gridDim.y;
         const size_t ncols = (size_t)gridDim.x * R;
@@ -266,11 +310,14 @@ __device__ __forceinline__ void stream_epilogue(f32x4 (&acc)[MT], char* lds, flo
                 rv[j] = *rsp[j];  // residual: written by the previous kernels only (plain load)
             }
             const int slab = M * (int)ncols;
+            const bool tp = e.tp.world > 0;  // TP push: the partials first, the residual after the all-reduce
             float h[IT][4];
 #pragma unroll
             for (int j = 0; j < IT; ++j) {
-                h[j][0] = __uint_as_float(rv[j].x << 16); h[j][1] = __uint_as_float(rv[j].x & 0xffff0000u);
-                h[j][2] = __uint_as_float(rv[j].y << 16); h[j][3] = __uint_as_float(rv[j].y & 0xffff0000u);
+                h[j][0] = tp ? 0.f : __uint_as_float(rv[j].x << 16);
+                h[j][1] = tp ? 0.f : __uint_as_float(rv[j].x & 0xffff0000u);
+                h[j][2] = tp ? 0.f : __uint_as_float(rv[j].y << 16);
+                h[j][3] = tp ? 0.f : __uint_as_float(rv[j].y & 0xffff0000u);
             }
             for (int s0 = 0; s0 < S; s0 += 4) {
                 float4 a4[IT][4];
@@ -287,6 +334,7 @@ __device__ __forceinline__ void stream_epilogue(f32x4 (&acc)[MT], char* lds, flo
                             h[j][0] += a4[j][u].x; h[j][1] += a4[j][u].y; h[j][2] += a4[j][u].z; h[j][3] += a4[j][u].w;
                         }
             }
+            if (tp) tp_push_tile<IT, Q, WPB>(e.tp, h, rv, M, n0, (int)ncols, tid, tp_epoch);
 #pragma unroll
             for (int j = 0; j < IT; ++j) {
                 const int it = tid + j * NT;
@@ -393,6 +441,19 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_gemm_kernel(const bf16* __
     stream_epilogue<MT, EPI, WPB>(acc, lds, s_ss, n0, M, out, ldo, parts, counters, e);
 }
 
+// ar (RESID_SPLIT only, may be null): a custom all-reduce handle (custom_ar.hip) whose group the residual
+// update all-reduces over (header "TP push"); every peer mapped, M * N * 2 <= its slot bytes.
+static bool tp_push_ok(const void* ar, int epi, int M, int N) {
+    using namespace mrsum_ar;
+    if (!ar) return true;
+    auto h = (const ArHandle*)ar;
+    if (epi != EPI_RESID_SPLIT || M > 16 || N % GRAN || N / GRAN > MAX_GRAN || (size_t)M * N * 4 > h->max_bytes)
+        return false;
+    for (int r = 0; r < h->world; ++r)
+        if (!h->peers.base[r]) return false;
+    return true;
+}
+
 // out: bf16 [M, ldo] (EPI_BF16), fp32 slabs [splits, slab_m (0: M), ldo] (EPI_F32_PARTIAL), bf16 [M, ldo] of N/2
 // SwiGLU features (EPI_SWIGLU, splits = 1; EPI_SWIGLU_SPLIT with ``parts`` fp32 [splits, M, N] scratch),
 // or the residual update of EPI_RESID_SPLIT (``out`` unused; resid [M, ldr] bf16 += the product, ssp
@@ -405,7 +466,7 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_gemm_kernel(const bf16* __
 // MI355X_MICROARCH.md "nt-weights"; profiles/r1_decode_nt_ab.jsonl).
 MRSUM_API int mrsum_stream_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
                                 int epi, int splits, int wpb, void* parts, int* counters, const float* ssq,
-                                int ssq_tiles, float eps, void* resid, int ldr, float* ssp, int slab_m,
+                                int ssq_tiles, float eps, void* resid, int ldr, float* ssp, int slab_m, void* ar,
                                 hipStream_t s) {
     if (M <= 0) return 0;
     if (wpb < 4 || wpb > 8 || M > 64 || K % KBLK || N % (16 * wpb) || splits < 1 || (K / KBLK) % splits ||
@@ -417,9 +478,11 @@ MRSUM_API int mrsum_stream_gemm(const void* x, int ldx, const void* W, int N, in
     if (epi == EPI_RESID_SPLIT && (!resid || !ssp || ldr % 4)) return (int)hipErrorInvalidValue;
     if (ssq && (ssq_tiles <= 0 || ssq_tiles % (4 * SS_PARTS))) return (int)hipErrorInvalidValue;
     if (slab_m && (slab_m < M || epi != EPI_F32_PARTIAL)) return (int)hipErrorInvalidValue;
+    if (!tp_push_ok(ar, epi, M, N)) return (int)hipErrorInvalidValue;
     NormArgs e;
     e.ssq = ssq; e.ssq_tiles = ssq_tiles; e.inv_k = 1.f / (float)K; e.eps = eps;
     e.resid = (bf16*)resid; e.ldr = ldr; e.ssp = ssp; e.slab_m = slab_m;
+    e.tp = mrsum_ar::tp_push_of((const mrsum_ar::ArHandle*)ar);
     const int kper = K / splits;
     const int mt = (M + 15) / 16;
     dim3 grid(N / (16 * wpb), splits), block(64 * wpb);
@@ -585,7 +648,7 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_fp8_kernel(const bf16* __r
 MRSUM_API int mrsum_stream_fp8(const void* x, int ldx, const void* W, const float* wscale, int N, int K, int M,
                                void* out, int ldo, int epi, int splits, int wpb, void* parts, int* counters,
                                const float* ssq, int ssq_tiles, float eps, void* resid, int ldr, float* ssp,
-                               hipStream_t s) {
+                               void* ar, hipStream_t s) {
     if (M <= 0) return 0;
     if (wpb < 4 || wpb > 8 || M > 64 || K % KB8 || N % (16 * wpb) || splits < 1 || (K / KB8) % splits ||
         epi < EPI_BF16 || epi > EPI_RESID_SPLIT || epi == EPI_SWIGLU_SPLIT)
@@ -593,9 +656,11 @@ MRSUM_API int mrsum_stream_fp8(const void* x, int ldx, const void* W, const floa
     if (epi != EPI_F32_PARTIAL && epi != EPI_RESID_SPLIT && splits != 1) return (int)hipErrorInvalidValue;
     if (epi == EPI_RESID_SPLIT && (!parts || !counters || !resid || !ssp || ldr % 4)) return (int)hipErrorInvalidValue;
     if (ssq && (ssq_tiles <= 0 || ssq_tiles % (4 * SS_PARTS))) return (int)hipErrorInvalidValue;
+    if (!tp_push_ok(ar, epi, M, N)) return (int)hipErrorInvalidValue;
     NormArgs e;
     e.ssq = ssq; e.ssq_tiles = ssq_tiles; e.inv_k = 1.f / (float)K; e.eps = eps;
     e.resid = (bf16*)resid; e.ldr = ldr; e.ssp = ssp; e.slab_m = 0;
+    e.tp = mrsum_ar::tp_push_of((const mrsum_ar::ArHandle*)ar);
     const int kper = K / splits;
     const int mt = (M + 15) / 16;
     dim3 grid(N / (16 * wpb), splits), block(64 * wpb);

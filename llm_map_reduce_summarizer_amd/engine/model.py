@@ -76,14 +76,29 @@ class _TPReduce:
     def add_rmsnorm(self, parts, residual, ln, eps):
         return self.model.custom_ar.add_rmsnorm(parts, residual, ln, eps)
 
+    def push_ok(self, rows: int, hidden: int) -> bool:
+        """TP push (ops.proj_add_rmsnorm): the row-parallel GEMM all-reduces its own tiles."""
+        ar = self.model.custom_ar
+        return ar is not None and _tp_push_enabled() and ar.push_ok(rows, hidden)
+
+    def push_handle(self) -> int:
+        return self.model.custom_ar.push_handle()
+
+
+def _tp_push_enabled() -> bool:
+    return os.environ.get("MRSUM_TP_PUSH", "1") == "1"
+
 
 class LocalReduce:
     """Single-GPU stand-in for _TPReduce when measuring ONE rank's TP shard of the decode step
     (tools/bench_decode.py --tp-shard K): the sum over ranks is the identity and the fused all-reduce +
-    residual add + RMSNorm kernel is replaced by the local add_rmsnorm_parts over this rank's split-K
-    slabs -- the same kernel sequence per layer as a real TP rank (the deferred norm of TP=1 is off),
-    minus the cross-GPU hop."""
+    residual add + RMSNorm kernel and the TP push run over a group of one (parallel/custom_ar.py
+    LocalPush) -- the same kernels per layer as a real TP rank (the deferred norm of TP=1 is off), minus
+    the cross-GPU hop."""
     fused = True
+
+    def __init__(self, model: "LlamaModel"):
+        self.model = model
 
     def __call__(self, t: torch.Tensor) -> torch.Tensor:
         return t
@@ -92,7 +107,16 @@ class LocalReduce:
         return rows <= 64
 
     def add_rmsnorm(self, parts, residual, ln, eps):
+        lp = self.model.local_push()
+        if lp.fits_rows(parts):
+            return lp.add_rmsnorm(parts, residual, ln, eps)
         return ops.add_rmsnorm_parts(parts, residual, ln, eps)
+
+    def push_ok(self, rows: int, hidden: int) -> bool:
+        return _tp_push_enabled() and self.model.local_push().push_ok(rows, hidden)
+
+    def push_handle(self) -> int:
+        return self.model.local_push().push_handle()
 
 
 @dataclass
@@ -137,6 +161,7 @@ class LlamaModel:
                                     scaling=cfg.rope_scaling)
         self.vocab_offset = tp_rank * self.vocab_local
         self.emulate_tp_reduce = False  # LocalReduce in place of the TP all-reduce (shard measurements)
+        self._local_push = None
         # TP prefill with sequence parallelism (prefill_passes; MRSUM_SP=0: all-reduces)
         self.sequence_parallel = os.environ.get("MRSUM_SP", "1") == "1"
         # TP on GPUs: decode all-reduces (fp32 split-K slabs, <= 1 MiB) and the sampler's key max go
@@ -188,6 +213,14 @@ class LlamaModel:
         return n
 
     # ------------------------------------------------------------------ comm
+    def local_push(self):
+        """The one-rank TP-push handle of a TP-shard measurement (created on first use: outside a capture,
+        the engine's eager step before every capture gets here first)."""
+        if self._local_push is None:
+            from ..parallel.custom_ar import LocalPush
+            self._local_push = LocalPush()
+        return self._local_push
+
     def _all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.tp_size > 1:
             if self.custom_ar is not None and self.custom_ar.fits(t):
@@ -281,7 +314,7 @@ class LlamaModel:
         residual = ops.embed(ids, self.embed)
         x = ops.rmsnorm(residual, None, c.rms_eps)  # gains folded into the consumer weights
         page = kcache.shape[3]
-        ar = _TPReduce(self) if self.tp_size > 1 else (LocalReduce() if self.emulate_tp_reduce else None)
+        ar = _TPReduce(self) if self.tp_size > 1 else (LocalReduce(self) if self.emulate_tp_reduce else None)
         for i, lw in enumerate(self.layers):
             qkv = ops.qkv_rope(x, lw.wqkv, positions, seq_idx, block_tables, kcache[i], vcache[i], self.cos_sin,
                                self.hq, self.hkv, self.hd, page, defer=decode)

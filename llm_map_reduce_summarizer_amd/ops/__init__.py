@@ -319,38 +319,56 @@ def _fused_ar(all_reduce, rows, hidden):
 DEFER_NORM_MAX_M = 16
 
 
-def _resid_cfg(hip, a, w, role):
-    """(wpb, S) of the deferred-RMSNorm producer (stream kernel, split-K last-arriver residual update) for
-    this decode projection, or None."""
+def _resid_plan(hip, a, w, role, tp=False):
+    """The deferred-RMSNorm producer of this decode projection: ("stream", wpb, S) (stream kernel, split-K
+    last-arriver residual update), ("skinny",) (register-streaming kernel, one tile per workgroup, no
+    split-K) or None.  ``tp``: the TP-push producer of a row-parallel shard, which runs whatever the plan
+    for its bare GEMM (the all-reduce launch it saves outweighs the kernel choice): on the register-
+    streaming kernel where that is the plan (TP-shard o / down at K <= 2048), else the stream kernel
+    (MRSUM_TP_RESID_KERNEL=skinny|stream forces one, for measurements)."""
     M = a.shape[0]
     if M > DEFER_NORM_MAX_M:
         return None
+    N, K = w.shape
     if isinstance(w, Fp8Weight):
-        cfg = hip.fp8_resid_cfg(M, w.shape[0], w.shape[1])
+        cfg = hip.fp8_resid_cfg(M, N, K)
     else:
-        p = hip.plan(role, M, w.shape[0], w.shape[1])
+        p = hip.plan(role, M, N, K)
         cfg = p[1:] if p[0] == "stream" else None
-    if cfg is None or (w.shape[0] // (16 * cfg[0])) % 32:
+        if tp:
+            force = os.environ.get("MRSUM_TP_RESID_KERNEL", "auto")
+            if (force == "skinny" or (force == "auto" and p[0] == "skinny")) and N % 512 == 0:
+                return ("skinny",)
+            if cfg is None or force == "stream":
+                cfg = hip.tp_resid_config(N, K)
+    if cfg is None or (N // (16 * cfg[0])) % 32:
         return None
-    return cfg
+    return ("stream",) + tuple(cfg)
 
 
 def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
     """residual += a @ w^T (TP-all-reduced when ``all_reduce``); returns rmsnorm(residual) * ln (``ln``
     None: unit gain, the model's folded-gain form).
 
-    GPU decode rows with a unit gain and no TP: the projection itself updates the residual (split-K
-    last-arriver epilogue) and the result is a NormRows -- the RMSNorm is deferred into the consumer
-    GEMM, so no separate add + RMSNorm kernel runs.  ``all_reduce`` is a callable summing a tensor over
+    GPU decode rows with a unit gain: the projection itself updates the residual (split-K last-arriver
+    epilogue) and the result is a NormRows -- the RMSNorm is deferred into the consumer GEMM, so no
+    separate add + RMSNorm kernel runs; under TP (``all_reduce.push_ok``) that last arriver also
+    all-reduces its tile over the group first (TP push), so no all-reduce kernel runs either.  ``all_reduce`` is a callable summing a tensor over
     the TP group in place; when it also offers ``add_rmsnorm``/``fused_ok`` (the model's P2P
     all-reduce) the decode path runs the projection's split-K slabs straight into one fused
     all-reduce + residual add + RMSNorm kernel."""
     if _use_hip(a):
         from . import hip
-        if ln is None and all_reduce is None and a.shape[0] <= hip.SKINNY_MAX_M:
-            cfg = _resid_cfg(hip, a, w, role)
-            if cfg is not None:
-                return NormRows(residual, hip.stream_resid(a, w, residual, cfg[0], cfg[1]), eps)
+        if ln is None and a.shape[0] <= hip.SKINNY_MAX_M:
+            # TP: the producer all-reduces its own tiles (TP push) when the group's buffers take the rows
+            ok = getattr(all_reduce, "push_ok", None)
+            push = all_reduce.push_handle() if ok is not None and ok(a.shape[0], residual.shape[1]) else None
+            if all_reduce is None or push is not None:
+                rp = _resid_plan(hip, a, w, role, tp=push is not None)
+                if rp is not None and rp[0] == "skinny":
+                    return NormRows(residual, hip.skinny_resid(a, w, residual, tp=push), eps)
+                if rp is not None:
+                    return NormRows(residual, hip.stream_resid(a, w, residual, rp[1], rp[2], tp=push), eps)
     if ln is None:
         ln = unit_gain(residual.shape[1], residual.device)
     if _use_hip(a) and isinstance(w, Fp8Weight):
@@ -401,11 +419,11 @@ def gate_up_swiglu(x, wgu):
     if _use_hip(xt):
         from . import hip
         p = hip.plan("gate_up", x.shape[0], wgu.shape[0], wgu.shape[1])
-        nr = isinstance(x, NormRows) and p[0] in ("stream", "stream_split")
+        nr = isinstance(x, NormRows) and p[0] in ("stream", "stream_split", "skinny")
         xin, norm = (x.h, x.norm) if nr else (rows(x), None)
         if p[0] == "stream":
             return hip.linear_swiglu(xin, wgu, kernel="stream", wpb=p[1], norm=norm)
         if p[0] == "stream_split":
             return hip.linear_swiglu(xin, wgu, kernel="stream_split", wpb=p[1], splits=p[2], norm=norm)
-        return hip.linear_swiglu(xin, wgu, kernel=p[0])
+        return hip.linear_swiglu(xin, wgu, kernel=p[0], norm=norm)
     return reference.swiglu(reference.linear(x, wgu))

@@ -37,12 +37,13 @@ _SIGS = {
                                _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp],
     "mrsum_attn_decode_rope": [_vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int,
                                _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp],
-    "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
+    "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int,
+                          _c_float, _vp, _c_int, _vp, _vp, _vp],
     "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_stream_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp,
-                          _vp, _c_int, _c_float, _vp, _c_int, _vp, _c_int, _vp],
+                          _vp, _c_int, _c_float, _vp, _c_int, _vp, _c_int, _vp, _vp],
     "mrsum_stream_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp,
-                         _vp, _c_int, _c_float, _vp, _c_int, _vp, _vp],
+                         _vp, _c_int, _c_float, _vp, _c_int, _vp, _vp, _vp],
     "mrsum_skinny_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp,
                          _c_int, _c_float, _vp],
     "mrsum_quant_fp8_rows": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
@@ -557,6 +558,7 @@ SKINNY_MAX_M = 64
 STREAM_MAX_M = 256
 STREAM_MAX_M_SWIGLU = 128
 EPI_BF16, EPI_F32_PARTIAL, EPI_SWIGLU, EPI_SWIGLU_SPLIT, EPI_RESID_SPLIT = 0, 1, 2, 3, 4
+EPI_SKINNY_RESID = 3  # skinny_gemm.hip's residual-update epilogue
 
 
 def choose_splits(N: int, K: int, nt: int, target_wgs: int = 512, max_splits: int = 8) -> int:
@@ -573,7 +575,9 @@ def choose_splits(N: int, K: int, nt: int, target_wgs: int = 512, max_splits: in
     return best
 
 
-def _skinny(x, w, out, epi, nt, splits, ldo):
+def _skinny(x, w, out, epi, nt, splits, ldo, norm=None, resid=None, ssp=None, ar=None):
+    """Register-streaming decode GEMM (skinny_gemm.hip).  ``norm``: deferred-RMSNorm input of the SwiGLU
+    epilogue; EPI_SKINNY_RESID: residual += x @ w^T (TP push over ``ar`` when given), ``ssp`` [M, N / 16]."""
     _bf16_cuda(x, w)
     _rows_ok(x)
     M, K = x.shape
@@ -581,8 +585,17 @@ def _skinny(x, w, out, epi, nt, splits, ldo):
     _req(w.is_contiguous() and w.shape[1] == K, "skinny_gemm: weight must be [N, K] contiguous")
     _req(1 <= M <= SKINNY_MAX_M and K % 128 == 0 and N % (16 * nt) == 0 and (K // 128) % splits == 0,
          "skinny_gemm: unsupported shape M=%d N=%d K=%d nt=%d S=%d" % (M, N, K, nt, splits))
-    _check(_fn("mrsum_skinny_gemm")(_p(x), x.stride(0), _p(w), N, K, M, _p(out), ldo, epi, nt, splits, _stream()),
-           "skinny_gemm")
+    sq, tiles, eps = _norm_args(x, norm)
+    rp, ldr, sp = None, 0, None
+    if epi == EPI_SKINNY_RESID:
+        _req(nt == 1 and splits == 1 and M <= 16, "skinny resid: one 16-row tile per workgroup, M <= 16")
+        _bf16_cuda(resid)
+        _rows_ok(resid)
+        _req(resid.shape == (M, N) and ssp is not None and ssp.dtype == torch.float32 and ssp.is_contiguous()
+             and ssp.shape == (M, N // 16), "skinny resid: residual [M, N] bf16 and ssp fp32 [M, N / 16]")
+        rp, ldr, sp = _p(resid), resid.stride(0), _p(ssp)
+    _check(_fn("mrsum_skinny_gemm")(_p(x), x.stride(0), _p(w), N, K, M, _p(out), ldo, epi, nt, splits, sq, tiles, eps,
+                                    rp, ldr, sp, ar, _stream()), "skinny_gemm")
     return out
 
 
@@ -621,7 +634,8 @@ def _resid_args(x, N, epi, resid, ssp):
     return _p(resid), resid.stride(0), _p(ssp)
 
 
-def _stream_gemm(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, norm=None, resid=None, ssp=None):
+def _stream_gemm(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, norm=None, resid=None, ssp=None,
+                 ar=None):
     """LDS-DMA weight-ring decode GEMM (csrc/kernels/stream_gemm.hip); same contract as _skinny_lds,
     one 16*wpb-row tile per workgroup, ~one workgroup per CU.  ``norm``: deferred-RMSNorm input
     (ssq, eps); EPI_RESID_SPLIT: residual += x @ w^T with per-tile row sums of squares into ``ssp``."""
@@ -637,10 +651,10 @@ def _stream_gemm(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, no
             _stream_launch(x[r0:r1], w, o, epi, splits, ldo, wpb, None, None, None, None, None,
                            M if epi == EPI_F32_PARTIAL else 0)
         return out
-    return _stream_launch(x, w, out, epi, splits, ldo, wpb, parts, counters, norm, resid, ssp, 0)
+    return _stream_launch(x, w, out, epi, splits, ldo, wpb, parts, counters, norm, resid, ssp, 0, ar)
 
 
-def _stream_launch(x, w, out, epi, splits, ldo, wpb, parts, counters, norm, resid, ssp, slab_m):
+def _stream_launch(x, w, out, epi, splits, ldo, wpb, parts, counters, norm, resid, ssp, slab_m, ar=None):
     M, K = x.shape
     N = w.shape[0]
     _req(w.is_contiguous() and w.shape[1] == K, "stream_gemm: weight must be [N, K] contiguous")
@@ -655,7 +669,7 @@ def _stream_launch(x, w, out, epi, splits, ldo, wpb, parts, counters, norm, resi
     sq, tiles, eps = _norm_args(x, norm)
     rp, ldr, sp = _resid_args(x, N, epi, resid, ssp)
     _check(_fn("mrsum_stream_gemm")(_p(x), x.stride(0), _p(w), N, K, M, _p(out), ldo, epi, splits, wpb, _p(parts),
-                                    _p(counters), sq, tiles, eps, rp, ldr, sp, slab_m, _stream()), "stream_gemm")
+                                    _p(counters), sq, tiles, eps, rp, ldr, sp, slab_m, ar, _stream()), "stream_gemm")
     return out
 
 
@@ -736,21 +750,41 @@ def stream_swiglu_split(x: torch.Tensor, w_gu: torch.Tensor, out: torch.Tensor, 
                         norm=norm)
 
 
-def stream_resid(x: torch.Tensor, w, residual: torch.Tensor, wpb: int, splits: int) -> torch.Tensor:
+def stream_resid(x: torch.Tensor, w, residual: torch.Tensor, wpb: int, splits: int, tp=None) -> torch.Tensor:
     """Deferred-RMSNorm producer: residual += x @ w^T (bf16 or Fp8Weight ``w``), split-K over ``splits``
     workgroups per column tile, summed by the last to arrive; returns the fp32 [M, N / (16 wpb)] per-tile
-    row sums of squares of the new residual (the consumers' ``norm`` input)."""
+    row sums of squares of the new residual (the consumers' ``norm`` input).  ``tp``: a custom all-reduce
+    handle (parallel/custom_ar.py ``push_handle``): x @ w^T is this rank's share of a row-parallel
+    projection and the last arriver all-reduces its tile over the TP group before the residual update
+    (stream_gemm.hip "TP push") -- no separate all-reduce launch."""
     M = x.shape[0]
     fp8 = isinstance(w, Fp8Weight)
     N = (w.q if fp8 else w).shape[0]
     tiles = N // (16 * wpb)
+    if tp is not None:
+        STATS["tp_push"] += 1
     parts = torch.empty(splits, M, N, dtype=torch.float32, device=x.device)
     ssp = torch.empty(M, tiles, dtype=torch.float32, device=x.device)
     cnt = _tile_counters(x.device, tiles)
     if fp8:
-        _stream_fp8(x, w, None, EPI_RESID_SPLIT, splits, 0, wpb, parts=parts, counters=cnt, resid=residual, ssp=ssp)
+        _stream_fp8(x, w, None, EPI_RESID_SPLIT, splits, 0, wpb, parts=parts, counters=cnt, resid=residual, ssp=ssp,
+                    ar=tp)
     else:
-        _stream_gemm(x, w, None, EPI_RESID_SPLIT, splits, 0, wpb, parts=parts, counters=cnt, resid=residual, ssp=ssp)
+        _stream_gemm(x, w, None, EPI_RESID_SPLIT, splits, 0, wpb, parts=parts, counters=cnt, resid=residual, ssp=ssp,
+                     ar=tp)
+    return ssp
+
+
+def skinny_resid(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, tp=None) -> torch.Tensor:
+    """Deferred-RMSNorm producer on the register-streaming kernel (one 16-row tile per workgroup, no
+    split-K, M <= 16): residual += x @ w^T -- all-reduced over the custom all-reduce group ``tp`` first
+    (TP push) when given; returns the fp32 [M, N / 16] per-tile row sums of squares of the new residual."""
+    M = x.shape[0]
+    N = w.shape[0]
+    ssp = torch.empty(M, N // 16, dtype=torch.float32, device=x.device)
+    if tp is not None:
+        STATS["tp_push"] += 1
+    _skinny(x, w, None, EPI_SKINNY_RESID, 1, 1, 0, resid=residual, ssp=ssp, ar=tp)
     return ssp
 
 
@@ -760,7 +794,8 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tenso
     ``norm``: deferred-RMSNorm input (stream kernels only)."""
     M = x.shape[0]
     F2 = w_gu.shape[0]
-    _req(norm is None or kernel in ("stream", "stream_split"), "linear_swiglu: a deferred norm needs the stream kernel")
+    _req(norm is None or kernel in ("stream", "stream_split", "skinny"),
+         "linear_swiglu: a deferred norm needs the stream or register-streaming kernel")
     if kernel == "gemm" or M > (STREAM_MAX_M_SWIGLU if kernel == "stream" else SKINNY_MAX_M):
         return gemm(x, w_gu, out=out, swiglu=True)
     if out is None:
@@ -772,7 +807,7 @@ def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tenso
         return stream_swiglu_split(x, w_gu, out, wpb, splits, norm=norm)
     if kernel == "lds":
         return _skinny_lds(x, w_gu, out, EPI_SWIGLU, 1, F2 // 2)
-    return _skinny(x, w_gu, out, EPI_SWIGLU, 1, 1, F2 // 2)
+    return _skinny(x, w_gu, out, EPI_SWIGLU, 1, 1, F2 // 2, norm=norm)
 
 
 def add_rmsnorm_parts(parts: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
@@ -803,6 +838,7 @@ def add_rmsnorm_parts(parts: torch.Tensor, residual: torch.Tensor, w: torch.Tens
 # Streaming floor (probe): qkv 9.5, o 7.6, down 20.1, gate_up 39.1.
 # Plan = ("stream", wpb, S) | ("skinny", nt, S) | ("lds", S) | ("gemm",) (the 256 x 256-tile kernel)
 N_CU = 256
+STATS = {"tp_push": 0}  # host-side launch counts of selected paths (tests check which path ran)
 
 
 def stream_config(N: int, K: int, swiglu: bool = False, splits: Optional[int] = None, max_splits: int = 16):
@@ -831,6 +867,44 @@ def stream_config(N: int, K: int, swiglu: bool = False, splits: Optional[int] = 
     if best is None or best_key[0] < 0.7:
         return None
     return best
+
+
+def tp_resid_config(N: int, K: int):
+    """(wpb, S) of the TP-push residual producer (a row-parallel shard projection on the stream kernel)
+    where the bare-GEMM plan picks the register-streaming kernel: the best-filling stream grid, with
+    N / (16 wpb) a multiple of 32 (the consumers' deferred-norm tile count)."""
+    best, best_key = None, None
+    for wpb in (4, 8):
+        if N % (16 * wpb) or (N // (16 * wpb)) % 32:
+            continue
+        tiles = N // (16 * wpb)
+        for S in range(1, 17):
+            if (K // 128) % S:
+                continue
+            grid = tiles * S
+            eff = grid / (-(-grid // N_CU) * N_CU)
+            key = (round(eff, 3), -S, wpb)
+            if best_key is None or key > best_key:
+                best, best_key = (wpb, S), key
+    return best
+
+
+def swiglu_split_config(N: int, K: int):
+    """(wpb, S) of the split-K SwiGLU stream kernel that best fills the chip (a narrow gate_up shard taking
+    a deferred norm), or None."""
+    best, best_key = None, None
+    for wpb in (4, 7, 8):
+        if N % (16 * wpb):
+            continue
+        tiles = N // (16 * wpb)
+        for S in (1, 2, 4, 8, 16):
+            if (K // 128) % S or tiles * S > 2 * N_CU:
+                continue
+            grid = tiles * S
+            key = (round(grid / (-(-grid // N_CU) * N_CU), 3), -S, wpb)
+            if best_key is None or key > best_key:
+                best, best_key = (wpb, S), key
+    return best if best_key is not None and best_key[0] >= 0.7 else None
 
 
 def plan(role: str, M: int, N: int, K: int, splits: Optional[int] = None, stream: bool = True):
@@ -933,7 +1007,8 @@ def stream_config_fp8(N: int, K: int, swiglu: bool = False, splits: Optional[int
     return stream_config(N, K // 2, swiglu=swiglu, splits=splits)  # K/256 slots == (K/2)/128 blocks
 
 
-def _stream_fp8(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, norm=None, resid=None, ssp=None):
+def _stream_fp8(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, norm=None, resid=None, ssp=None,
+                ar=None):
     """fp8 (e4m3fn, per-row scale) LDS-DMA weight-ring decode GEMM (stream_gemm.hip stream_fp8_kernel);
     the epilogues / deferred-RMSNorm operands of _stream_gemm."""
     _bf16_cuda(x)
@@ -953,7 +1028,7 @@ def _stream_fp8(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, nor
     sq, tiles, eps = _norm_args(x, norm)
     rp, ldr, sp = _resid_args(x, N, epi, resid, ssp)
     _check(_fn("mrsum_stream_fp8")(_p(x), x.stride(0), _p(w.q), _p(w.scale), N, K, M, _p(out), ldo, epi, splits, wpb,
-                                   _p(parts), _p(counters), sq, tiles, eps, rp, ldr, sp, _stream()), "stream_fp8")
+                                   _p(parts), _p(counters), sq, tiles, eps, rp, ldr, sp, ar, _stream()), "stream_fp8")
     return out
 
 

@@ -13,6 +13,13 @@ split-K slabs, writes the row (bf16 payload) straight into every peer's buffer (
 fp32, adds the residual and applies the RMSNorm -- the all-reduce, the split-K reduction and the
 add_rmsnorm kernel of the TP=1 graph in one launch.
 
+The decode projections at up to 16 rows go one step further (``push_handle``, "TP push" in
+csrc/kernels/stream_gemm.hip): the row-parallel GEMM's split-K last arriver pushes its column tile to
+every peer itself and updates the residual after the rank-ordered sum, so neither a separate
+all-reduce nor an add + RMSNorm launch runs -- the consumer GEMM applies the norm (deferred norm).
+``LocalPush`` is the same handle over a group of one rank: a single-GPU TP-shard measurement runs the
+identical kernels.
+
 The reference has no collective of any kind (its only "communication" is HTTPS, reference
 llm_executor.py:290-297); this is the MI355X replacement for the TP reduce path it implies.
 """
@@ -136,6 +143,18 @@ class CustomAllReduce:
             raise RuntimeError("custom all-reduce (add_rmsnorm) launch failed (%d)" % rc)
         return out
 
+    # granule-push (GEMM epilogue) limits: csrc/kernels/ar_common.h MAX_GRAN x GRAN columns
+    PUSH_MAX_HIDDEN = 8192
+
+    def push_ok(self, rows: int, hidden: int) -> bool:
+        """Can a TP-push GEMM epilogue all-reduce ``rows`` x ``hidden`` over this group?"""
+        return (bool(self._h) and 1 <= rows <= 16 and hidden % 16 == 0 and hidden <= self.PUSH_MAX_HIDDEN
+                and rows * hidden * 4 <= self.max_bytes)
+
+    def push_handle(self) -> int:
+        """The native handle a TP-push GEMM epilogue takes (ops.hip.stream_resid ``tp``)."""
+        return self._h
+
     def max_u64_(self, t: torch.Tensor) -> torch.Tensor:
         """Element-wise max over the group, in place, of an int64 tensor holding unsigned 64-bit keys
         (the sampler's Gumbel-max keys; values are compared as unsigned)."""
@@ -182,6 +201,7 @@ class CustomAllReduce:
                 torch.cuda.synchronize(dev)
                 ok &= bool(torch.equal(x, ref))
             ok &= self._test_fused(dev, iters)
+            ok &= _test_push(self, dev, iters, group=self.group)
             ok &= self.error() == 0
         except Exception as e:  # keep the collective sequence aligned across ranks
             log.warning("custom all-reduce self-test raised: %s", e)
@@ -301,6 +321,96 @@ class CustomAllReduce:
             self.close()
         except Exception:  # interpreter teardown
             pass
+
+
+def _test_push(h, dev, iters: int, group=None, M: int = 3, N: int = 2048, K: int = 512, wpb: int = 4,
+               S: int = 4) -> bool:
+    """The TP-push residual producer (ops.hip.stream_resid with ``tp``) against the collective sum of every
+    rank's x @ w^T on the same residual, eager and graph-replayed (values change per call: a stale slot,
+    flag or epoch shows up); the residual must also be bit-identical across ranks.  ``group`` None with
+    a LocalPush ``h`` (one rank)."""
+    from ..ops import hip
+    ok = True
+    g = torch.Generator(device="cpu").manual_seed(4321)
+    res0 = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
+    res = res0.clone()
+    x = torch.empty(M, K, dtype=torch.bfloat16, device=dev)
+    w = torch.empty(N, K, dtype=torch.bfloat16, device=dev)
+    ssp = [None]
+    rank = h.rank
+
+    def fill(i):
+        gi = torch.Generator(device="cpu").manual_seed(1000 * i + 7 * rank)
+        x.copy_((torch.randn(M, K, generator=gi) * 0.5).to(torch.bfloat16))
+        w.copy_((torch.randn(N, K, generator=gi) * 0.05).to(torch.bfloat16))
+        res.copy_(res0)
+
+    def run():
+        ssp[0] = hip.stream_resid(x, w, res, wpb, S, tp=h.push_handle())
+
+    def check():
+        tot = x.float() @ w.float().t()
+        if h.world > 1:
+            dist.all_reduce(tot, group=group)
+        ref = (res0.float() + tot).to(torch.bfloat16).float()
+        good = bool(torch.allclose(res.float(), ref, atol=6e-2, rtol=2e-2))
+        ss = res.float().pow(2).reshape(M, N // (16 * wpb), 16 * wpb).sum(-1)
+        good &= bool(torch.allclose(ssp[0], ss, rtol=1e-3, atol=1e-2))
+        if h.world > 1:
+            mine = res.float().sum().reshape(1)
+            hi, lo = mine.clone(), mine.clone()
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+            good &= bool(torch.equal(hi, lo))
+        return good
+
+    for i in range(iters):
+        fill(i)
+        run()
+        torch.cuda.synchronize(dev)
+        ok &= check()
+    s = torch.cuda.Stream(device=dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        fill(90)
+        run()
+    torch.cuda.synchronize(dev)
+    ok &= check()
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr, stream=s):
+        run()
+    for i in range(iters):
+        fill(60 + i)
+        gr.replay()
+        torch.cuda.synchronize(dev)
+        ok &= check()
+    return ok and h.error() == 0
+
+
+class LocalPush:
+    """A custom all-reduce over a group of ONE rank (no IPC, no process group): the decode of a TP shard
+    measured on one GPU runs the same kernels as a rank of a real group -- the TP-push GEMM epilogue and
+    the fused push-mode all-reduce + add + RMSNorm (push to its own slot, wait, rank-ordered sum) --
+    without the xGMI latency of the remote stores."""
+
+    rank, world = 0, 1
+    PUSH_MAX_HIDDEN = CustomAllReduce.PUSH_MAX_HIDDEN
+
+    def __init__(self, max_bytes: int = 4 << 20):
+        self.max_bytes = int(max_bytes)
+        self._lib = _lib()
+        self._h = self._lib.mrsum_ar_create(0, 1, self.max_bytes)
+        if not self._h:
+            raise RuntimeError("LocalPush: allocation failed")
+
+    MAX_ROWS = CustomAllReduce.MAX_ROWS
+    push_ok = CustomAllReduce.push_ok
+    push_handle = CustomAllReduce.push_handle
+    fits_rows = CustomAllReduce.fits_rows
+    add_rmsnorm = CustomAllReduce.add_rmsnorm
+    error = CustomAllReduce.error
+    close = CustomAllReduce.close
+    __del__ = CustomAllReduce.__del__
 
 
 def maybe_custom_all_reduce(group=None, max_bytes: int = 4 << 20) -> Optional[CustomAllReduce]:

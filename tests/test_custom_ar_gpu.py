@@ -33,3 +33,16 @@ def test_tp2_engine_one_gpu():
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert r.stdout.count("tp worker ok") == 2, r.stdout[-2000:]
+
+
+@pytest.mark.gpu
+def test_tp2_push_decode_one_gpu():
+    """TP push (row-parallel decode GEMM all-reducing its own tiles) across 2 IPC-mapped ranks: exact on
+    integer operands, graph-replayed in the self-test, and a TP=2 Llama-3-8B-dims engine decoding through
+    it against the separate fused all-reduce kernel."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(_port()), os.path.join(ROOT, "tests", "_tp_push_worker.py")]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.count("tp push ok") == 2, r.stdout[-2000:]

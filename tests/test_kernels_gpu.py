@@ -741,3 +741,65 @@ def test_kv_scatter_matches_reference():
     hip.kv_scatter(rows.to(DEV), page.to(DEV), slot.to(DEV), kg, vg)
     assert torch.equal(kg.cpu(), kr) and torch.equal(vg.cpu(), vr)
     assert not torch.equal(kr, kc0)  # something was written
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+def test_stream_resid_tp_push_group_of_one(fp8):
+    """TP-push residual producer over a group of ONE rank (parallel/custom_ar.py LocalPush: the TP-shard
+    measurement path): push to its own slot, flag, wait, rank-ordered sum -- against the fp32 reference
+    residual update, eager and graph-replayed with changing inputs (the self-test), and against the local
+    (non-TP) producer on the same operands."""
+    from llm_map_reduce_summarizer_amd.parallel.custom_ar import LocalPush, _test_push
+    h = LocalPush(max_bytes=1 << 20)
+    try:
+        if not fp8:
+            assert _test_push(h, torch.device(DEV), 3)
+        M, N, K = 7, 4096, 1024
+        x = _rand(M, K, scale=0.5, seed=3)
+        wb = _rand(N, K, scale=0.05, seed=4)
+        w = reference.Fp8Weight.quantize(wb) if fp8 else wb
+        res0 = _rand(M, N, seed=5)
+        wpb, S = (8, 2) if fp8 else (4, 4)
+        r_tp, r_loc = res0.clone(), res0.clone()
+        ss_tp = hip.stream_resid(x, w, r_tp, wpb, S, tp=h.push_handle())
+        ss_loc = hip.stream_resid(x, w, r_loc, wpb, S)
+        ref = (res0.float() + reference.linear(x, w).float()).to(torch.bfloat16)
+        _close(r_tp, ref, 3e-2, 2e-2)
+        _close(r_tp, r_loc, 3e-2, 2e-2)
+        _close(ss_tp, ss_loc, 1.0, 1e-2)
+        assert h.error() == 0
+    finally:
+        h.close()
+
+
+@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("tp", [False, True])
+def test_skinny_resid_producer(M, tp):
+    """Register-streaming deferred-norm producer (skinny_gemm.hip EPI_RESID): residual += x @ w^T (through
+    the TP push over a group of one when ``tp``) and per-16-column-tile row sums of squares -- against the
+    fp32 reference; the SwiGLU consumer with that deferred norm against the materialised RMSNorm rows."""
+    from llm_map_reduce_summarizer_amd.parallel.custom_ar import LocalPush
+    h = LocalPush(max_bytes=1 << 20) if tp else None
+    try:
+        N, K, F = 4096, 1024, 3584
+        x = _rand(M, K, scale=0.5, seed=11)
+        w = _rand(N, K, scale=0.05, seed=12)
+        res0 = _rand(M, N, seed=13)
+        res = res0.clone()
+        for it in range(3):  # repeated calls: the TP push epochs / slot parities advance
+            res.copy_(res0)
+            ssp = hip.skinny_resid(x, w, res, tp=h.push_handle() if tp else None)
+        ref = (res0.float() + reference.linear(x, w).float()).to(torch.bfloat16)
+        _close(res, ref, 3e-2, 2e-2)
+        ss = res.float().pow(2).reshape(M, N // 16, 16).sum(-1)
+        _close(ssp, ss, 1e-2, 1e-3)
+        wgu = _rand(F, N, scale=0.02, seed=14)
+        eps = 1e-5
+        y = hip.linear_swiglu(res, wgu, kernel="skinny", norm=(ssp, eps))
+        xn = reference.rmsnorm(res, torch.ones(N, dtype=torch.bfloat16, device=DEV), eps)
+        _close(y, hip.linear_swiglu(xn, wgu, kernel="skinny"), 2e-2, 3e-2)
+        if tp:
+            assert h.error() == 0
+    finally:
+        if h is not None:
+            h.close()
