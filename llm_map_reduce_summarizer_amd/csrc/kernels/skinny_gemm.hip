@@ -43,20 +43,35 @@ struct SkinnyNorm {
     mrsum_ar::TPPush tp;
 };
 
-// rsqrt(mean(h_m^2) + eps) from the producer tiles' sums, in stream_gemm.hip's order (8 partials of
-// ssq_tiles / 8 consecutive tiles in float4 steps, then the partials in order)
-__device__ __forceinline__ float deferred_row_scale(const SkinnyNorm& e, int m) {
-    const int C = e.ssq_tiles / 8;
-    const float4* src = reinterpret_cast<const float4*>(e.ssq + (size_t)m * e.ssq_tiles);
-    float t = 0.f;
-    for (int p = 0; p < 8; ++p) {
-        float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int q = 0; q < C / 4; ++q) {
-            const float4 v = src[p * (C / 4) + q];
-            a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
-        }
-        t += (a.x + a.y) + (a.z + a.w);
+// Deferred norm of row m, in stream_gemm.hip's order: partial p (< 8) of ssq_tiles / 8 consecutive tiles
+// summed in float4 steps (thread 8 m + p; its loads issued in the kernel prologue, into registers, so they
+// overlap the weight stream and nothing waits for them before the epilogue), then rsqrt(sum of the
+// partials in order / K + eps).  ssq_tiles <= 32 * SS_C4.
+constexpr int SS_C4 = 16;
+struct SsLoads {
+    float4 v[SS_C4];
+};
+
+__device__ __forceinline__ void deferred_issue(const SkinnyNorm& e, int m, int p, SsLoads& l) {
+    const int C4 = e.ssq_tiles / 32;
+    const float4* src = reinterpret_cast<const float4*>(e.ssq + (size_t)m * e.ssq_tiles) + p * C4;
+#pragma unroll
+    for (int q = 0; q < SS_C4; ++q) l.v[q] = q < C4 ? src[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+
+__device__ __forceinline__ float deferred_partial(const SsLoads& l) {
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < SS_C4; ++q) {
+        a.x += l.v[q].x; a.y += l.v[q].y; a.z += l.v[q].z; a.w += l.v[q].w;
     }
+    return (a.x + a.y) + (a.z + a.w);
+}
+
+__device__ __forceinline__ float deferred_row_scale(const SkinnyNorm& e, const float* s_part, int m) {
+    float t = 0.f;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) t += s_part[8 * m + p];
     return rsqrtf(t * e.inv_k + e.eps);
 }
 constexpr int KB = 128;  // k elements per wave round (4 MFMA k-steps of 32)
@@ -119,11 +134,17 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16* __restrict
     constexpr int BN = 16 * NT, BM = 16 * MT;
     static_assert(EPI != EPI_RESID || (NT == 1 && MT == 1), "RESID: one 16-row tile, M <= 16");
     __shared__ __attribute__((aligned(16))) float red[4][BM][BN + 4];
+    __shared__ float s_part[EPI == EPI_SWIGLU ? 8 * BM : 1];  // deferred-norm partials [m][8]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int n0 = blockIdx.x * BN;
     const int ks = blockIdx.y * kper, ke = min(K, ks + kper);
     // TP push: this launch's epoch of the tile's granule, loaded long before it is needed
     const unsigned tp_epoch = EPI == EPI_RESID && e.tp.world > 0 ? e.tp.epochs[n0 / mrsum_ar::GRAN] + 1 : 0;
+    const bool ss_mine = EPI == EPI_SWIGLU && e.ssq && threadIdx.x < 8 * M;
+    SsLoads ssl;
+    if constexpr (EPI == EPI_SWIGLU) {
+        if (ss_mine) deferred_issue(e, threadIdx.x >> 3, threadIdx.x & 7, ssl);
+    }
 
     f32x4 acc[NT][MT];
 #pragma unroll
@@ -159,6 +180,9 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16* __restrict
         for (int m = 0; m < MT; ++m)
 #pragma unroll
             for (int j = 0; j < 4; ++j) red[w][16 * m + cm][16 * t + cn + j] = acc[t][m][j];
+    if constexpr (EPI == EPI_SWIGLU) {
+        if (ss_mine) s_part[threadIdx.x] = deferred_partial(ssl);
+    }
     __syncthreads();
 
     // each item = 4 consecutive n of one m
@@ -197,7 +221,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16* __restrict
         } else {  // SWIGLU: tile rows [0, BN/2) gate, [BN/2, BN) up of features [blockIdx.x*BN/2, +BN/2)
             constexpr int H = BN / 2;
             if (n4 < H) {
-                const float sc = e.ssq ? deferred_row_scale(e, m) : 1.f;
+                const float sc = e.ssq ? deferred_row_scale(e, s_part, m) : 1.f;
                 float r[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -251,7 +275,8 @@ MRSUM_API int mrsum_skinny_gemm(const void* x, int ldx, const void* W, int N, in
         return (int)hipErrorInvalidValue;
     if (epi != EPI_F32_PARTIAL && splits != 1) return (int)hipErrorInvalidValue;
     if (epi == EPI_SWIGLU && nt != 1) return (int)hipErrorInvalidValue;  // weight blocks of [8 gate | 8 up]
-    if (ssq && (epi != EPI_SWIGLU || ssq_tiles <= 0 || ssq_tiles % 32)) return (int)hipErrorInvalidValue;
+    if (ssq && (epi != EPI_SWIGLU || ssq_tiles <= 0 || ssq_tiles % 32 || ssq_tiles > 32 * SS_C4))
+        return (int)hipErrorInvalidValue;
     if (epi == EPI_RESID && (nt != 1 || M > 16 || !resid || !ssp || ldr % 4)) return (int)hipErrorInvalidValue;
     if (ar) {
         auto h = (const ArHandle*)ar;
