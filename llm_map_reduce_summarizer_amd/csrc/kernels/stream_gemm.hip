@@ -150,23 +150,33 @@ __device__ __forceinline__ void rearm(int* counters, int tile, int tid) {
 }  // namespace
 
 namespace {
-// TP push of one column tile (header "TP push"), M <= 16 rows: thread tid owns item tid < M * Q = (row mm,
-// 4 columns at c).  h[0] holds this rank's fp32 partial sums on entry and the rank-ordered all-reduced bf16
-// sums plus the residual rv[0] on exit (rounded exactly as ar_add_rmsnorm_kernel).  ``epoch``: this
-// launch's epoch of the tile's granules (read before the split-K ticket).
-template <int IT, int Q, int GT>
+// TP push of one column tile (header "TP push"): thread tid owns items it = tid + j NT < M * Q = (row mm,
+// 4 columns at c).  h[j] holds this rank's fp32 partial sums on entry and the rank-ordered all-reduced
+// bf16 sums plus the residual rv[j] on exit (rounded exactly as ar_add_rmsnorm_kernel).  Every item is
+// pushed before the first is gathered.  ``epoch``: this launch's epoch of the tile's granules (read
+// before the split-K ticket).
+template <int IT, int Q, int NT, int GT>
 __device__ __forceinline__ void tp_push_tile(const mrsum_ar::TPPush& tp, float (&h)[IT][4], const uint2 (&rv)[IT],
                                              const int M, const int n0, const int ncols, const int tid,
                                              const unsigned epoch) {
     using namespace mrsum_ar;
-    if (tid < M * Q) {
-        const long long off = tp_item_off(tid / Q, ncols, n0 + 4 * (tid % Q));
-        tp_push_item(tp, off, epoch, make_float4(h[0][0], h[0][1], h[0][2], h[0][3]));
-        const float4 acc = tp_gather_item(tp, off, epoch);
-        h[0][0] = __uint_as_float(rv[0].x << 16) + acc.x;
-        h[0][1] = __uint_as_float(rv[0].x & 0xffff0000u) + acc.y;
-        h[0][2] = __uint_as_float(rv[0].y << 16) + acc.z;
-        h[0][3] = __uint_as_float(rv[0].y & 0xffff0000u) + acc.w;
+#pragma unroll
+    for (int j = 0; j < IT; ++j) {
+        const int it = tid + j * NT;
+        if (it < M * Q)
+            tp_push_item(tp, tp_item_off(it / Q, ncols, n0 + 4 * (it % Q)), epoch,
+                         make_float4(h[j][0], h[j][1], h[j][2], h[j][3]));
+    }
+#pragma unroll
+    for (int j = 0; j < IT; ++j) {
+        const int it = tid + j * NT;
+        if (it < M * Q) {
+            const float4 acc = tp_gather_item(tp, tp_item_off(it / Q, ncols, n0 + 4 * (it % Q)), epoch);
+            h[j][0] = __uint_as_float(rv[j].x << 16) + acc.x;
+            h[j][1] = __uint_as_float(rv[j].x & 0xffff0000u) + acc.y;
+            h[j][2] = __uint_as_float(rv[j].y << 16) + acc.z;
+            h[j][3] = __uint_as_float(rv[j].y & 0xffff0000u) + acc.w;
+        }
     }
     if (tid < GT) tp.epochs[n0 / GRAN + tid] = epoch;
 }
@@ -334,7 +344,7 @@ __device__ __forceinline__ void stream_epilogue(f32x4 (&acc)[MT], char* lds, flo
                             h[j][0] += a4[j][u].x; h[j][1] += a4[j][u].y; h[j][2] += a4[j][u].z; h[j][3] += a4[j][u].w;
                         }
             }
-            if (tp) tp_push_tile<IT, Q, WPB>(e.tp, h, rv, M, n0, (int)ncols, tid, tp_epoch);
+            if (tp) tp_push_tile<IT, Q, NT, WPB>(e.tp, h, rv, M, n0, (int)ncols, tid, tp_epoch);
 #pragma unroll
             for (int j = 0; j < IT; ++j) {
                 const int it = tid + j * NT;
@@ -447,7 +457,7 @@ static bool tp_push_ok(const void* ar, int epi, int M, int N) {
     using namespace mrsum_ar;
     if (!ar) return true;
     auto h = (const ArHandle*)ar;
-    if (epi != EPI_RESID_SPLIT || M > 16 || N % GRAN || N / GRAN > MAX_GRAN || (size_t)M * N * 4 > h->max_bytes)
+    if (epi != EPI_RESID_SPLIT || N % GRAN || N / GRAN > MAX_GRAN || (size_t)M * N * 4 > h->max_bytes)
         return false;
     for (int r = 0; r < h->world; ++r)
         if (!h->peers.base[r]) return false;

@@ -317,6 +317,10 @@ def _fused_ar(all_reduce, rows, hidden):
 # producer: measured on one box (tools/ab_decode_old_new.sh, profiles/r2_deferred_norm_ab.jsonl) decode
 # steps at B=1 -1.5 %, B=10 -0.5 %, B=39 +1 % -- so it runs up to 16 rows.
 DEFER_NORM_MAX_M = 16
+# Under TP the producer's tail replaces the all-reduce + add + RMSNorm launch (7.8 us at B=1, 14 us at B=20
+# on a TP=8 shard: profiles/r3_tp8shard_b20_gaps.txt), so the TP push runs at every decode batch the
+# stream kernel takes.
+TP_PUSH_MAX_M = 64
 
 
 def _resid_plan(hip, a, w, role, tp=False):
@@ -327,14 +331,24 @@ def _resid_plan(hip, a, w, role, tp=False):
     streaming kernel where that is the plan (TP-shard o / down at K <= 2048), else the stream kernel
     (MRSUM_TP_RESID_KERNEL=skinny|stream forces one, for measurements)."""
     M = a.shape[0]
-    if M > DEFER_NORM_MAX_M:
+    if M > (TP_PUSH_MAX_M if tp else DEFER_NORM_MAX_M):
         return None
     N, K = w.shape
+    if tp and M > 16:  # the register-streaming producer takes one 16-row tile
+        cfg = (hip.fp8_resid_cfg(M, N, K) if isinstance(w, Fp8Weight) else
+               (hip.plan(role, M, N, K)[1:] if hip.plan(role, M, N, K)[0] == "stream" else hip.tp_resid_config(N, K)))
+        return None if cfg is None or (N // (16 * cfg[0])) % 32 else ("stream",) + tuple(cfg)
     if isinstance(w, Fp8Weight):
         cfg = hip.fp8_resid_cfg(M, N, K)
     else:
         p = hip.plan(role, M, N, K)
         cfg = p[1:] if p[0] == "stream" else None
+        env = os.environ.get("MRSUM_RESID_SKINNY_" + role.upper())  # measurement override (exp_plans_insitu.py)
+        if not tp and N % 512 == 0 and (env == "1" or (env is None and role == "o" and K <= 4096)):
+            # TP=1 o projection on the register-streaming producer (no split-K tail), in situ 4k context
+            # (profiles/r3_tp1_resid_skinny_insitu.jsonl): B=1 3.336 vs 3.380 ms per step, B=10 4.078 vs 4.087;
+            # down (K 14336) loses (3.50 / 4.32)
+            return ("skinny",)
         if tp:
             force = os.environ.get("MRSUM_TP_RESID_KERNEL", "auto")
             if (force == "skinny" or (force == "auto" and p[0] == "skinny")) and N % 512 == 0:

@@ -930,7 +930,9 @@ def plan(role: str, M: int, N: int, K: int, splits: Optional[int] = None, stream
         # 10.3: skinny)
         if N >= 7168 and N % 112 == 0 and M > 8:
             return ("stream_split", 7, 4)
-        if N % 64 == 0 and M > 32:
+        if N % 64 == 0 and M > 16:
+            # (> 32 rows measured as above; 17..32 rows fell through to the 256 x 256 prefill GEMM: 81 us per
+            # layer at a TP=8 shard, profiles/r3_tp8shard_b20_gaps.txt)
             return ("stream_split", 4, 4)
     blocks = K // 128
 

@@ -148,7 +148,7 @@ class CustomAllReduce:
 
     def push_ok(self, rows: int, hidden: int) -> bool:
         """Can a TP-push GEMM epilogue all-reduce ``rows`` x ``hidden`` over this group?"""
-        return (bool(self._h) and 1 <= rows <= 16 and hidden % 16 == 0 and hidden <= self.PUSH_MAX_HIDDEN
+        return (bool(self._h) and 1 <= rows <= 64 and hidden % 16 == 0 and hidden <= self.PUSH_MAX_HIDDEN
                 and rows * hidden * 4 <= self.max_bytes)
 
     def push_handle(self) -> int:
@@ -258,11 +258,14 @@ class CustomAllReduce:
         return ok
 
     def measure_latency(self, rows=(1, 64), hidden: int = 4096, calls: int = 64, reps: int = 3):
-        """(a, b): a fused all-reduce + add_rmsnorm call costs a + b * rows seconds MORE than the local
-        add_rmsnorm_parts it replaces in a TP=1 graph (least squares over ``rows``; both timed inside
-        replayed hipGraphs).  MAX over the ranks, so every rank plans with the same numbers."""
-        from ..ops import hip
+        """(a, b): a fused all-reduce + add_rmsnorm call over this group costs a + b * rows seconds MORE
+        than the same kernel over a group of one rank (LocalPush: the push to its own slot, the wait and
+        the rank-ordered sum, which a TP-shard decode step measured on one GPU already contains) -- the
+        cross-GPU part of a decode all-reduce, the TP push of the GEMM epilogues included (the same
+        remote stores and polls).  Least squares over ``rows``; both timed inside replayed hipGraphs.
+        MAX over the ranks, so every rank plans with the same numbers."""
         dev = torch.device("cuda", torch.cuda.current_device())
+        local = LocalPush(self.max_bytes)
         pts = []
         for r in rows:
             r = max(1, min(int(r), self.max_bytes // (hidden * 2), self.MAX_ROWS))
@@ -295,8 +298,9 @@ class CustomAllReduce:
                 return best
 
             t_ar = timed(lambda: self.add_rmsnorm(parts, res, w, 1e-5, out))
-            t_local = timed(lambda: hip.add_rmsnorm_parts(parts, res, w, 1e-5, out))
+            t_local = timed(lambda: local.add_rmsnorm(parts, res, w, 1e-5, out))
             pts.append((r, max(0.0, t_ar - t_local)))
+        local.close()
         n = len(pts)
         mx = sum(p[0] for p in pts) / n
         my = sum(p[1] for p in pts) / n

@@ -15,15 +15,17 @@ latency.  Prefill is compute-bound: DP divides it by N for free, TP adds RCCL al
 activations.  Which is faster depends on the batch, the context and the all-reduce latency of the
 node, so the choice is a cost model whose hardware constants are *measured*:
 
-* ``hbm_bw``, ``step_floor_s``, ``tp_floor_s``, ``tp_row_s``: one least-squares fit over the round-3
-  decode steps of TP=1 and of one rank's TP=2/4/8 shard with the TP kernel sequence
-  (profiles/r3_decode_steps_tp_shards.jsonl, B=1/10/39 at 4k context):
-  t = (W + B ctx kv) / TP / 6.17 TB/s + 0.88 ms + [TP > 1] 0.17 ms + 3.3 us x B x log2(TP), every point
-  within 6 % (few-kv-head attention and the per-kernel latency of small shards are what stay);
+* ``hbm_bw``, ``step_floor_s``, ``tp_floor_s``, ``tp_row_s``: one least-squares fit (tools/fit_hwmodel.py)
+  over the round-3 decode steps of TP=1 and of one rank's TP=2/4/8 shard with the TP kernel sequence over
+  a group of one rank (TP push in the row-parallel GEMM epilogues; profiles/r3_decode_steps_push.jsonl,
+  B=1/5/10/20/39 at 4k context):
+  t = (W + B ctx kv) / TP / 5.82 TB/s + 0.70 ms + [TP > 1] 0.25 ms + 6.9 us x B x log2(TP), every point
+  within 8.3 % (few-kv-head attention and the per-kernel latency of small shards are what stay);
 * ``prefill_flops``: the engine's prefill rate in the 10 h bench (~76k tok/s of Llama-3-8B);
 * ``ar_lat_s`` / ``ar_lat_row_s`` and ``ar_bw``: timed at start-up on the job's own GPUs (the fused
-  all-reduce inside a replayed hipGraph at 1 and 64 rows -- a latency and a per-row link cost; one
-  RCCL all-reduce of a prefill-sized activation), MAX-reduced over the ranks so every rank takes
+  all-reduce inside a replayed hipGraph at 1 and 64 rows against the same kernel over a group of one
+  rank -- the cross-GPU part the shard fit above does not contain: a latency and a per-row link cost;
+  one RCCL all-reduce of a prefill-sized activation), MAX-reduced over the ranks so every rank takes
   the same decision.
 
 A TP stage may also prefill *disaggregated* (``handoff``): data-parallel on every rank's full
@@ -46,10 +48,10 @@ from typing import Dict, List, Sequence
 
 @dataclass(frozen=True)
 class HWModel:
-    hbm_bw: float = 6.17e12         # bytes/s streamed by the decode GEMM + attention kernels
-    step_floor_s: float = 0.88e-3   # fixed per-step cost of the decode graph (kernel latencies), 32 layers
-    tp_floor_s: float = 0.17e-3     # extra fixed cost of a TP shard's decode graph (32 layers) ...
-    tp_row_s: float = 3.3e-6        # ... plus this per decode row per log2(TP) (few-kv-head attention is latency-bound)
+    hbm_bw: float = 5.82e12         # bytes/s streamed by the decode GEMM + attention kernels
+    step_floor_s: float = 0.70e-3   # fixed per-step cost of the decode graph (kernel latencies), 32 layers
+    tp_floor_s: float = 0.25e-3     # extra fixed cost of a TP shard's decode graph (32 layers) ...
+    tp_row_s: float = 6.9e-6        # ... plus this per decode row per log2(TP) (few-kv-head attention is latency-bound)
     prefill_flops: float = 1.1e15   # effective prefill FLOP/s (MFMA GEMMs + flash attention)
     ar_lat_s: float = 20e-6         # one decode all-reduce (custom P2P kernel), measured at start-up ...
     ar_lat_row_s: float = 0.0       # ... plus this per decode row (the push sends every row to every peer)

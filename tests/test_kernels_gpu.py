@@ -743,8 +743,9 @@ def test_kv_scatter_matches_reference():
     assert not torch.equal(kr, kc0)  # something was written
 
 
+@pytest.mark.parametrize("M", [7, 39])
 @pytest.mark.parametrize("fp8", [False, True])
-def test_stream_resid_tp_push_group_of_one(fp8):
+def test_stream_resid_tp_push_group_of_one(fp8, M):
     """TP-push residual producer over a group of ONE rank (parallel/custom_ar.py LocalPush: the TP-shard
     measurement path): push to its own slot, flag, wait, rank-ordered sum -- against the fp32 reference
     residual update, eager and graph-replayed with changing inputs (the self-test), and against the local
@@ -752,9 +753,9 @@ def test_stream_resid_tp_push_group_of_one(fp8):
     from llm_map_reduce_summarizer_amd.parallel.custom_ar import LocalPush, _test_push
     h = LocalPush(max_bytes=1 << 20)
     try:
-        if not fp8:
+        if not fp8 and M == 7:
             assert _test_push(h, torch.device(DEV), 3)
-        M, N, K = 7, 4096, 1024
+        N, K = 4096, 1024
         x = _rand(M, K, scale=0.5, seed=3)
         wb = _rand(N, K, scale=0.05, seed=4)
         w = reference.Fp8Weight.quantize(wb) if fp8 else wb

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 D8B = plan.ModelDims.of(get_model_config("llama3-8b"))
 
 
-STEPS = os.path.join(ROOT, "profiles", "r3_decode_steps_tp_shards.jsonl")
+STEPS = os.path.join(ROOT, "profiles", "r3_decode_steps_push.jsonl")
 
 
 def test_decode_model_matches_measured_single_gpu_steps():
@@ -37,13 +37,14 @@ def test_tp_divides_streams_and_adds_all_reduces():
 
 
 def test_tp_shard_model_matches_measured_steps():
-    """One rank's TP=2/4/8 shard decode steps measured on one MI355X (no all-reduce) within 7 %."""
+    """One rank's TP=2/4/8 shard decode steps measured on one MI355X (all-reduces over a group of one rank)
+    within 9 %."""
     rows = [json.loads(l) for l in open(STEPS) if l.startswith("{")]
     assert {r["tp_shard"] for r in rows} >= {2, 4, 8}
     hw = plan.HWModel(ar_lat_s=0.0)
     for r in rows:
         est = plan.decode_step_s(D8B, hw, r["B"], r["ctx"] + 128, r["tp_shard"]) * 1e3
-        assert abs(est - r["decode_ms_per_step"]) / r["decode_ms_per_step"] < 0.07, (r, est)
+        assert abs(est - r["decode_ms_per_step"]) / r["decode_ms_per_step"] < 0.09, (r, est)
 
 
 def test_choice_follows_all_reduce_latency():
@@ -107,14 +108,19 @@ def test_handoff_for_many_prompts_context_parallel_for_one():
 
 
 @pytest.mark.parametrize("ar_lat_us", [8.0, 15.0])
-def test_full_tp_beats_intermediate_layouts_for_10h_stages(ar_lat_us):
+def test_sharded_layouts_beat_dp_for_10h_stages(ar_lat_us):
     """A property of the COST MODEL (not a hardware measurement -- no 8-GPU run backs it yet): with every
-    TP layout allowed the same hand-off prefill inside its own group, the model ranks TP=8 ahead of
-    TP=2 x DP=4, TP=4 x DP=2 and DP=8 for the 10 h headline's three stages.  This is why ``auto``
-    weighs TP=1 against TP=N only; an 8-GPU measurement may overturn it."""
+    TP x DP layout allowed the same hand-off prefill inside its own group, the model ranks some sharded
+    layout ahead of DP=8 for each of the 10 h headline's three stages, the single-sequence final reduce
+    at full TP=8; ``choose`` over the divisors of the world size (what ``auto`` passes, engine/provider.py)
+    returns the cheapest."""
     hw = plan.with_measurements(plan.HWModel(), ar_lat_s=ar_lat_us * 1e-6, ar_bw=150e9, ar_lat_row_s=0.03e-6)
     for prompts in ([4000] * 39, [10500] * 10, [10500]):
         new = [1000] * len(prompts)
         est = {tp: plan.stage_seconds(D8B, hw, prompts, new, tp, 8, handoff=True) for tp in (1, 2, 4, 8)}
-        assert min(est, key=est.get) == 8, est
-        assert est[8] < est[4] < est[2] < est[1], est
+        best = min(est, key=est.get)
+        assert best > 1, est
+        if len(prompts) == 1:
+            assert best == 8, est
+        ch = plan.choose(D8B, hw, prompts, new, 8, candidates=(1, 2, 4, 8), handoff=True)
+        assert ch["tp"] == best, (ch, est)

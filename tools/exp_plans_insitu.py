@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """In-situ plan experiments as whole decode steps (one engine; the plan of one op swapped between runs,
 graphs / workspaces rebuilt; alternating rounds), for TP=1 or one rank's TP=K shard (the TP kernel
-sequence: split-K slabs -> add_rmsnorm_parts in place of the fused all-reduce, engine/model.py LocalReduce).
+sequence over a group of one rank, engine/model.py LocalReduce).
 
 Variants (comma separated, ``plan`` = unchanged):
   attnfusedS / attnsepS        decode attention with S splits, fused / separate merge (the batch's bucket)
@@ -10,6 +10,8 @@ Variants (comma separated, ``plan`` = unchanged):
   gate_up:stream_split:WPB:S   split-K gate_up with the SwiGLU in the last arriver
   deferM                       the TP=1 deferred RMSNorm up to M rows (ops.DEFER_NORM_MAX_M)
   fp8resid:N:K:WPB:S           the fp8 deferred-norm producer (stream_fp8, residual epilogue) of one shape
+  env:NAME=VALUE[+NAME=VALUE]  environment overrides read at call time (e.g. env:MRSUM_RESID_SKINNY_O=1,
+                               env:MRSUM_TP_PUSH=0)
 
     python tools/exp_plans_insitu.py --tp-shard 8 --batch 1 --variants plan,attnfused32,gate_up:stream_split:4:4
 """
@@ -53,11 +55,25 @@ def main():
     base_defer = ops.DEFER_NORM_MAX_M
     base_fp8r = hip.fp8_resid_cfg
 
+    env_set = []
+
     def install(v):
         hip.decode_attn_plan, hip.plan = base_attn, base_plan
         ops.DEFER_NORM_MAX_M = base_defer
         hip.fp8_resid_cfg = base_fp8r
+        for name, old in env_set:
+            if old is None:
+                os.environ.pop(name, None)
+            else:
+                os.environ[name] = old
+        env_set.clear()
         if v == "plan":
+            return
+        if v.startswith("env:"):
+            for kv in v[4:].split("+"):
+                name, val = kv.split("=", 1)
+                env_set.append((name, os.environ.get(name)))
+                os.environ[name] = val
             return
         if v.startswith("fp8resid:"):  # fp8resid:N:K:wpb:S -- the fp8 deferred-norm producer of one shape
             N0, K0, wpb, S = (int(t) for t in v.split(":")[1:])
