@@ -7,12 +7,17 @@
 // One 256-thread block per row; each lane holds VPT 16-byte vectors of the
 // row in registers, so the row is read once and written once (memory bound:
 // 2-3 x D x 2 bytes per row).  D % 8 == 0 and D <= 256*8*VPT.
+//
+// Q8 (the fp8 prefill GEMMs' input): the normalised row is quantised in the same pass -- row-wise
+// dynamic OCP e4m3fn as quant.hip (scale = max|y| / 448, from the fp32 values) -- so neither the bf16
+// normalised rows nor a separate quantisation pass over them exist.
 #include "common.h"
 
-template <int VPT, bool ADD>
+template <int VPT, bool ADD, bool Q8 = false>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16* __restrict__ x, bf16* __restrict__ residual,
                                                       const bf16* __restrict__ w, bf16* __restrict__ out,
-                                                      int D, int x_stride, int out_stride, float eps) {
+                                                      int D, int x_stride, int out_stride, float eps,
+                                                      float* __restrict__ qscale = nullptr) {
     __shared__ float red[16];
     const int row = blockIdx.x;
     const int nvec = D >> 3;
@@ -42,7 +47,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16* __restrict__ x
     }
     ss = block_sum(ss, red);
     const float inv = rsqrtf(ss / (float)D + eps);
-    uint4* orow = reinterpret_cast<uint4*>(out + (size_t)row * out_stride);
+    float amax = 0.f;
 #pragma unroll
     for (int i = 0; i < VPT; ++i) {
         const int c = threadIdx.x + i * 256;
@@ -51,24 +56,59 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16* __restrict__ x
             unpack8(wv[i], wf);
 #pragma unroll
             for (int j = 0; j < 8; ++j) v[i][j] = v[i][j] * inv * wf[j];
-            orow[c] = pack8(v[i]);
+            if constexpr (Q8) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(v[i][j]));
+            } else {
+                reinterpret_cast<uint4*>(out + (size_t)row * out_stride)[c] = pack8(v[i]);
+            }
+        }
+    }
+    if constexpr (Q8) {
+        amax = wave_max(amax);
+        __syncthreads();  // red[] of the sum above has been read by every wave
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = amax;
+        __syncthreads();
+        amax = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+        const float sc = fmaxf(amax, 1e-12f) / 448.f, qi = 1.f / sc;
+        if (threadIdx.x == 0) qscale[row] = sc;
+        uint2* qr = reinterpret_cast<uint2*>(reinterpret_cast<uint8_t*>(out) + (size_t)row * out_stride);
+#pragma unroll
+        for (int i = 0; i < VPT; ++i) {
+            const int c = threadIdx.x + i * 256;
+            if (c < nvec) {
+                int lo = 0, hi = 0;
+                lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][0] * qi, v[i][1] * qi, lo, false);
+                lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][2] * qi, v[i][3] * qi, lo, true);
+                hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][4] * qi, v[i][5] * qi, hi, false);
+                hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][6] * qi, v[i][7] * qi, hi, true);
+                qr[c] = make_uint2((unsigned)lo, (unsigned)hi);
+            }
         }
     }
 }
 
-template <bool ADD>
+// Q8: ``out`` is e4m3fn [T, out_stride bytes], ``qscale`` fp32 [T]
+template <bool ADD, bool Q8 = false>
 static int launch_rmsnorm(const void* x, void* residual, const void* w, void* out, int T, int D, int x_stride,
-                          int out_stride, float eps, hipStream_t s) {
+                          int out_stride, float eps, hipStream_t s, float* qscale = nullptr) {
     if (T <= 0) return 0;
-    if (D % 8 || D > 256 * 8 * 8) return (int)hipErrorInvalidValue;
+    if (D % 8 || D > 256 * 8 * 8 || (Q8 && !qscale)) return (int)hipErrorInvalidValue;
     const int vpt = ceil_div(D / 8, 256);
     dim3 g(T), b(256);
     auto X = (const bf16*)x; auto R = (bf16*)residual; auto W = (const bf16*)w; auto O = (bf16*)out;
-    if (vpt <= 1) rmsnorm_kernel<1, ADD><<<g, b, 0, s>>>(X, R, W, O, D, x_stride, out_stride, eps);
-    else if (vpt <= 2) rmsnorm_kernel<2, ADD><<<g, b, 0, s>>>(X, R, W, O, D, x_stride, out_stride, eps);
-    else if (vpt <= 4) rmsnorm_kernel<4, ADD><<<g, b, 0, s>>>(X, R, W, O, D, x_stride, out_stride, eps);
-    else rmsnorm_kernel<8, ADD><<<g, b, 0, s>>>(X, R, W, O, D, x_stride, out_stride, eps);
+    if (vpt <= 1) rmsnorm_kernel<1, ADD, Q8><<<g, b, 0, s>>>(X, R, W, O, D, x_stride, out_stride, eps, qscale);
+    else if (vpt <= 2) rmsnorm_kernel<2, ADD, Q8><<<g, b, 0, s>>>(X, R, W, O, D, x_stride, out_stride, eps, qscale);
+    else if (vpt <= 4) rmsnorm_kernel<4, ADD, Q8><<<g, b, 0, s>>>(X, R, W, O, D, x_stride, out_stride, eps, qscale);
+    else rmsnorm_kernel<8, ADD, Q8><<<g, b, 0, s>>>(X, R, W, O, D, x_stride, out_stride, eps, qscale);
     return (int)hipGetLastError();
+}
+
+// rmsnorm / residual-add + rmsnorm whose output rows are e4m3fn (q [T, ldq bytes]) with row scales [T]
+MRSUM_API int mrsum_rmsnorm_fp8(const void* x, void* residual, const void* w, void* q, float* qscale, int T, int D,
+                                int x_stride, int ldq, float eps, hipStream_t s) {
+    if (residual) return launch_rmsnorm<true, true>(x, residual, w, q, T, D, x_stride, ldq, eps, s, qscale);
+    return launch_rmsnorm<false, true>(x, nullptr, w, q, T, D, x_stride, ldq, eps, s, qscale);
 }
 
 MRSUM_API int mrsum_rmsnorm(const void* x, const void* w, void* out, int T, int D, int x_stride, int out_stride,

@@ -85,6 +85,9 @@ class _TPReduce:
         return self.model.custom_ar.push_handle()
 
 
+_QUANT_NORM = os.environ.get("MRSUM_QUANT_NORM", "1") == "1"
+
+
 def _tp_push_enabled() -> bool:
     return os.environ.get("MRSUM_TP_PUSH", "1") == "1"
 
@@ -312,16 +315,20 @@ class LlamaModel:
         """
         c = self.cfg
         residual = ops.embed(ids, self.embed)
-        x = ops.rmsnorm(residual, None, c.rms_eps)  # gains folded into the consumer weights
+        # fp8 prefill: the norms feeding the fp8 GEMMs quantise their rows in the same pass (ops.QuantRows)
+        q8 = not decode and self.weight_dtype == "fp8" and _QUANT_NORM
+        x = ops.rmsnorm(residual, None, c.rms_eps, quant=q8)  # gains folded into the consumer weights
         page = kcache.shape[3]
         ar = _TPReduce(self) if self.tp_size > 1 else (LocalReduce(self) if self.emulate_tp_reduce else None)
+        last = len(self.layers) - 1
         for i, lw in enumerate(self.layers):
             qkv = ops.qkv_rope(x, lw.wqkv, positions, seq_idx, block_tables, kcache[i], vcache[i], self.cos_sin,
                                self.hq, self.hkv, self.hd, page, defer=decode)
             a = attention(i, qkv)
-            x = ops.proj_add_rmsnorm(a, lw.wo, residual, None, c.rms_eps, "o", ar)
+            x = ops.proj_add_rmsnorm(a, lw.wo, residual, None, c.rms_eps, "o", ar, quant=q8)
             act = ops.gate_up_swiglu(x, lw.wgu)
-            x = ops.proj_add_rmsnorm(act, lw.wdown, residual, None, c.rms_eps, "down", ar)
+            x = ops.proj_add_rmsnorm(act, lw.wdown, residual, None, c.rms_eps, "down", ar,
+                                     quant=q8 and i < last)  # the last one feeds the bf16 LM head
         return x
 
     def logits(self, x: torch.Tensor, gather: bool = True) -> torch.Tensor:

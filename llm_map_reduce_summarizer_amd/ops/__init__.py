@@ -49,10 +49,14 @@ def unit_gain(hidden, device):
     return t
 
 
-def rmsnorm(x, w, eps, out=None):
-    """``w`` None: unit gain."""
+def rmsnorm(x, w, eps, out=None, quant=False):
+    """``w`` None: unit gain.  ``quant`` (the consumer is an fp8 GEMM): on the GPU at prefill sizes the
+    rows come back quantised (QuantRows)."""
     if w is None:
         w = unit_gain(x.shape[-1], x.device)
+    if quant and out is None and _quant_ok(x):
+        from . import hip
+        return QuantRows(*hip.rmsnorm_fp8(x, w, eps))
     return _impl(x).rmsnorm(x, w, eps, out)
 
 
@@ -80,9 +84,36 @@ class NormRows:
         return hip.rmsnorm(self.h, unit_gain(self.h.shape[1], self.h.device), self.eps)
 
 
+class QuantRows:
+    """Normalised prefill rows already quantised to row-wise e4m3fn by their producer (ops.hip.rmsnorm_fp8:
+    the norm and the quantisation in one pass) for an fp8-weight GEMM: ``q`` [T, K] float8_e4m3fn,
+    ``scale`` [T] fp32."""
+
+    def __init__(self, q, scale):
+        self.q, self.scale = q, scale
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+    @property
+    def pair(self):
+        return (self.q, self.scale)
+
+
 def rows(x):
     """Plain normalised rows of ``x`` (a tensor or a NormRows)."""
+    if isinstance(x, QuantRows):
+        raise TypeError("QuantRows feed fp8 GEMMs only")
     return x.materialize() if isinstance(x, NormRows) else x
+
+
+def _quant_ok(x) -> bool:
+    """Prefill rows that every fp8 consumer sends to the fp8 MFMA GEMM (above the stream kernels' rows)."""
+    if not _use_hip(x):
+        return False
+    from . import hip
+    return x.shape[0] > max(hip.STREAM_MAX_M, hip.STREAM_MAX_M_SWIGLU) and x.shape[1] % 16 == 0
 
 
 def add_rmsnorm(x, residual, w, eps, out=None):
@@ -275,6 +306,11 @@ def qkv_rope(x, wqkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin,
     """qkv = x @ wqkv^T, RoPE on Q/K, K/V into the paged cache; returns bf16 qkv rows -- or, with
     ``defer`` on the GPU decode path, a QKVParts for attn_decode's fused RoPE + KV write.  ``x`` may
     be a NormRows (deferred RMSNorm of the previous layer's down projection)."""
+    if isinstance(x, QuantRows):
+        from . import hip
+        qkv = hip.fp8_linear(x.pair, wqkv)
+        hip.rope_kv(qkv, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page)
+        return qkv
     xt = x.h if isinstance(x, NormRows) else x
     if _use_hip(xt) and isinstance(wqkv, Fp8Weight):
         from . import hip
@@ -360,7 +396,7 @@ def _resid_plan(hip, a, w, role, tp=False):
     return ("stream",) + tuple(cfg)
 
 
-def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
+def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None, quant=False):
     """residual += a @ w^T (TP-all-reduced when ``all_reduce``); returns rmsnorm(residual) * ln (``ln``
     None: unit gain, the model's folded-gain form).
 
@@ -398,6 +434,8 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
         o = hip.fp8_linear(a, w)
         if all_reduce:
             all_reduce(o)
+        if quant and _quant_ok(o):
+            return QuantRows(*hip.rmsnorm_fp8(o, ln, eps, residual=residual))
         return hip.add_rmsnorm(o, residual, ln, eps)
     if _use_hip(a):
         from . import hip
@@ -414,6 +452,8 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
         o = hip.gemm(a, w)
         if all_reduce:
             all_reduce(o)
+        if quant and _quant_ok(o):
+            return QuantRows(*hip.rmsnorm_fp8(o, ln, eps, residual=residual))
         return hip.add_rmsnorm(o, residual, ln, eps)
     o = reference.linear(a, w)
     if all_reduce:
@@ -423,7 +463,10 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None):
 
 def gate_up_swiglu(x, wgu):
     """silu(gate) * up of the fused, [8 gate | 8 up]-blocked gate_up projection; ``x`` may be a
-    NormRows (deferred RMSNorm)."""
+    NormRows (deferred RMSNorm) or QuantRows (fp8 prefill rows quantised by the norm)."""
+    if isinstance(x, QuantRows):
+        from . import hip
+        return hip.fp8_linear_swiglu(x.pair, wgu)
     xt = x.h if isinstance(x, NormRows) else x
     if _use_hip(xt) and isinstance(wgu, Fp8Weight):
         from . import hip

@@ -23,6 +23,7 @@ _c_int, _c_float, _vp = ctypes.c_int, ctypes.c_float, ctypes.c_void_p
 _SIGS = {
     "mrsum_rmsnorm": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_add_rmsnorm": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
+    "mrsum_rmsnorm_fp8": [_vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_rope_kv": [_vp, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
                       _c_int, _vp],
     "mrsum_rope_kv_parts": [_vp, _c_int, _vp, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _c_int,
@@ -141,6 +142,23 @@ def add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: f
     _check(_fn("mrsum_add_rmsnorm")(_p(x), _p(residual), _p(w), _p(out), T, D, x.stride(0), out.stride(0), eps,
                                     _stream()), "add_rmsnorm")
     return out
+
+
+def rmsnorm_fp8(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None):
+    """rmsnorm(x) * w -- or residual += x; rmsnorm(residual) * w -- quantised in the same pass to row-wise
+    e4m3fn (the fp8 prefill GEMM's input, as quant_fp8_rows): returns (q [T, D] float8_e4m3fn, scale [T])."""
+    _bf16_cuda(x, w)
+    _rows_ok(x)
+    T, D = x.shape
+    _req(w.numel() == D and w.is_contiguous() and D % 16 == 0 and D <= 16384, "rmsnorm_fp8: bad weight / D")
+    if residual is not None:
+        _bf16_cuda(residual)
+        _req(residual.shape == (T, D) and residual.is_contiguous(), "rmsnorm_fp8: residual must be [T, D] contiguous")
+    q = torch.empty(T, D, dtype=torch.float8_e4m3fn, device=x.device)
+    sc = torch.empty(T, dtype=torch.float32, device=x.device)
+    _check(_fn("mrsum_rmsnorm_fp8")(_p(x), _p(residual), _p(w), _p(q), _p(sc), T, D, x.stride(0), D, eps,
+                                    _stream()), "rmsnorm_fp8")
+    return q, sc
 
 
 # ------------------------------------------------------------------ rope + kv
@@ -1045,10 +1063,14 @@ def fp8_linear(x: torch.Tensor, w, swiglu: bool = False, norm=None) -> torch.Ten
     """x @ (scale * W8)^T for any M: MFMA W8A16 weight-streaming kernel at decode sizes; at prefill sizes
     row-wise e4m3fn activation quantisation + the fp8 MFMA GEMM (gemm.hip, per-row activation x
     per-row weight scales in the epilogue)."""
-    M = x.shape[0]
+    M = x[0].shape[0] if isinstance(x, tuple) else x.shape[0]
     N = w.q.shape[0]
     _req(norm is None or (not swiglu and fp8_stream_cfg(M, N, x.shape[1], splits=1) is not None),
          "fp8_linear: a deferred norm needs the stream kernel")
+    if isinstance(x, tuple):  # (q, scale): prefill rows quantised by their producer (rmsnorm_fp8)
+        _req(norm is None and M > max(STREAM_MAX_M, STREAM_MAX_M_SWIGLU), "fp8_linear: pre-quantised rows are "
+             "prefill rows")
+        return gemm_fp8(x[0], x[1], w, swiglu=swiglu)
     if SKINNY_MAX_M < M <= (STREAM_MAX_M_SWIGLU if swiglu else STREAM_MAX_M) and norm is None:
         # decode batches of 65-256 rows: the weight-streaming kernels over 64-row chunks (the fp8 tile
         # GEMM's grid at M <= 256 is only N / 256 workgroups)
@@ -1087,6 +1109,8 @@ def fp8_swiglu_takes_norm(M: int, F2: int, K: int) -> bool:
 
 
 def fp8_linear_swiglu(x: torch.Tensor, w, norm=None) -> torch.Tensor:
+    if isinstance(x, tuple):
+        return fp8_linear(x, w, swiglu=True)
     M = x.shape[0]
     F2 = w.q.shape[0]
     cfg = fp8_stream_cfg(M, F2, x.shape[1], swiglu=True)

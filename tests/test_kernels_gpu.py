@@ -804,3 +804,29 @@ def test_skinny_resid_producer(M, tp):
     finally:
         if h is not None:
             h.close()
+
+
+@pytest.mark.parametrize("add", [False, True])
+@pytest.mark.parametrize("D", [4096, 8192])
+def test_rmsnorm_fp8_matches_norm_then_quant(add, D):
+    """Fused norm + row-wise e4m3fn quantisation (norm.hip Q8) against rmsnorm / add_rmsnorm followed by
+    quant_fp8_rows: the same residual update, dequantised rows within one e4m3 step of the two-pass result
+    (the fused pass quantises the fp32 values, not their bf16 rounding)."""
+    T = 300
+    x = _rand(T, D, seed=21)
+    res0 = _rand(T, D, seed=22)
+    w = (torch.rand(D, generator=torch.Generator().manual_seed(23)) + 0.5).to(torch.bfloat16).to(DEV)
+    r1, r2 = res0.clone(), res0.clone()
+    q, sc = hip.rmsnorm_fp8(x, w, 1e-5, residual=r1 if add else None)
+    y = hip.add_rmsnorm(x, r2, w, 1e-5) if add else hip.rmsnorm(x, w, 1e-5)
+    q2, sc2 = hip.quant_fp8_rows(y)
+    if add:
+        assert torch.equal(r1, r2)
+    torch.testing.assert_close(sc, sc2, rtol=1e-2, atol=0)
+    deq = q.float() * sc[:, None]
+    ref = y.float()
+    # half an e4m3 step of the top binade (32 quantised units) plus the bf16 rounding of the two-pass rows
+    # (<= 2^-8 of 448 units)
+    step = sc[:, None] * 32
+    assert ((deq - ref).abs() <= step * 0.5 + sc[:, None] * 448 * 2 ** -8 + 1e-6).all()
+    assert (q.float() == q2.float()).float().mean() > 0.9
