@@ -2,13 +2,19 @@
 //
 // Packed batch: qkv [T, row_stride] bf16 (Q heads, then K heads, then V
 // heads, D=128 each, already rotated by rope_kv), cu_seqlens [nseq+1].
-// Work item = (sequence, 256-row query block) x query head; items are listed
-// by the host heaviest-first (causal blocks late in a sequence do the most
-// key tiles), blockIdx.y = query head.
+// Work item = (sequence, query block of 256/G positions) x KV HEAD (blockIdx.y), G = Hq / Hkv: the 8 waves
+// of a workgroup run all G query heads of their kv head (wave w: head kvh*G + w%G, rows 32(w/G)..+32), so a
+// staged K/V tile always feeds 256 query rows, and the causal diagonal of a block is only 256/G rows deep
+// (64 for Llama-3-8B, 32 for 70B: waves idle on masked diagonal tiles far less than with 256-row blocks of
+// one head).  Items are listed by the host heaviest-first (blocks late in a sequence do the most key tiles).
 //
-// Workgroup: 8 waves (one per CU, 2 per SIMD at 209 VGPRs), wave w owns query rows [32w, 32w+32) of
-// the block: every staged K/V tile serves 256 query rows (8 x 4000-token / 32k prompts: +4-6 % over two
-// 4-wave 128-row workgroups per CU; 8 x 4096: -2 %, profiles/r2_attn_prefill_8wave_256rows_ab.jsonl).
+// Workgroup: 8 waves (one per CU, 2 per SIMD at ~216 VGPRs).  K/V tiles go through a two-stage LDS ring with
+// one barrier per tile: right after barrier t every wave writes tile t+1 (loaded into registers one tile
+// earlier) into the other stage and issues the global loads of tile t+2, then consumes tile t.  The LDS
+// operand reads run ahead of their MFMAs under sched_group_barrier (8 fragments deep, counted lgkmcnt
+// waits; hipcc otherwise sank each read next to its MFMA behind an lgkmcnt(0)).  GQA packing + ring +
+// read-ahead: 8 x 4k 728 -> 873 TF/s, 1 x 32k 839 -> 1092, 70B heads 1 x 32k 874 -> 1100
+// (profiles/r3_attn_prefill_gqa_ab.jsonl, r3_attn_prefill_stagger_ab.jsonl).
 // Per 64-key tile (K and V staged through LDS, next tile prefetched into
 // registers while the current one is consumed - issue early / write late):
 //
@@ -41,21 +47,32 @@
 
 namespace {
 constexpr int D = 128;
-constexpr int NW = 8;            // waves per workgroup (32 query rows each)
-constexpr int BM = 32 * NW;      // query rows per workgroup
+constexpr int NW = 8;             // waves per workgroup, 32 query rows each
 constexpr int NTHR = 64 * NW;
 constexpr int SROWS = NTHR / 16;  // tile rows staged per load round (16 lanes x 16 B per 256-B row)
-constexpr int BN = 64;   // keys per tile
+constexpr int BN = 64;            // keys per tile
 constexpr int SIT = BN / SROWS;   // load rounds per 64-row tile
+constexpr int STAGE = 2 * BN * 256;  // bytes of one ring stage: K tile | V tile
 constexpr float RESCALE_LOG2 = 8.0f;  // deferred-rescale threshold (log2 units), see the softmax
 
 typedef short v4s __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
 __device__ __forceinline__ int k_off(int row, int chunk) { return row * 256 + ((chunk ^ (row & 15)) << 4); }
 __device__ __forceinline__ int v_off(int row, int chunk) { return row * 256 + ((chunk ^ ((row & 3) << 2)) << 4); }
 
 __device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) { return __builtin_bit_cast(bf16x8, v); }
+
+// v_permlane32_swap of one value with itself: x0 = [lo | lo], x1 = [hi | hi]
+__device__ __forceinline__ float halves_max(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float halves_sum(float v) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 }  // namespace
 
 struct PagedKV {
@@ -67,21 +84,27 @@ struct PagedKV {
     const int* prefix;         // [nseq] tokens already cached before this slice
 };
 
-template <bool PAGED>
+// G = query heads per kv head served by one workgroup: wave w runs query head kvh*G + w%G over query rows
+// [qblock + 32(w/G), +32), so one workgroup covers 256/G query positions of ALL G heads of its kv head and
+// every staged K/V tile feeds 8 x 32 query rows whatever the GQA ratio.
+template <bool PAGED, int G>
 __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __restrict__ qkv, int row_stride,
                                                               const int* __restrict__ cu_seqlens,
                                                               const int2* __restrict__ items,
                                                               bf16* __restrict__ out, int out_stride, int Hq,
                                                               int Hkv, float scale_log2, PagedKV pk) {
-    // one stage of [K tile | V tile]; a 2-stage ring with one barrier per tile measured 2-4 % slower
-    // (its tile writes land between other waves' tile reads instead of behind a barrier)
-    __shared__ __attribute__((aligned(16))) char lds[1][2 * BN * 256];
+    constexpr int BMP = 32 * (NW / G);  // query positions per workgroup
+    // two-stage ring of [K tile | V tile]: tile t+1 is written into the other stage while tile t is
+    // consumed, one barrier per tile
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
 
     const int2 it = items[blockIdx.x];
     const int seq = it.x, qblock = it.y;
-    const int h = blockIdx.y, kvh = h / (Hq / Hkv);
+    const int kvh = blockIdx.y;
+    const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5, r32 = lane & 31;
+    const int w = tid >> 6;  // (readfirstlane here made hipcc spill the staggered loop)
+    const int h = kvh * G + w % G, rb = w / G;
     const int s0 = cu_seqlens[seq], len = cu_seqlens[seq + 1] - s0;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, half = lane >> 5, r32 = lane & 31;
     const bf16* base = qkv + (size_t)s0 * row_stride;
     const int kcol = (Hq + kvh) * D, vcol = (Hq + Hkv + kvh) * D;
     // keys live at absolute positions [0, pre + len); query row qi at pre + qi
@@ -90,7 +113,8 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
     const size_t head_pg = (size_t)kvh * BN * D;  // this kv head's 64-row slab inside a page
 
     // Q^T fragments: lane holds Q[row r32][dims 16ks + 8half .. +8] for ks = 0..7
-    const int qi = qblock + 32 * w + r32;
+    const int q0 = qblock + 32 * rb;  // the wave's first query row
+    const int qi = q0 + r32;
     bf16x8 qf[8];
     {
         const bool ok = qi < len;
@@ -103,13 +127,13 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
         }
     }
 
-    const int kend = pre + min(len, qblock + BM);
+    const int kend = pre + min(len, qblock + BMP);
     const int ntiles = (kend + BN - 1) / BN;
 
     // staging: thread loads rows tid/16 + SROWS i (i < SIT), chunk tid%16.  Named u32x4 registers and
-    // UNCONDITIONAL loads (key clamped to the last row of the sequence; such rows are masked out of
-    // the scores, and V rows stay finite) -- a conditional or lambda-captured prefetch made hipcc
-    // serialise the loop on vmcnt(0).
+    // UNCONDITIONAL loads (tile index clamped to the last tile, key clamped to the last row of the
+    // sequence; such rows are masked out of the scores and V rows stay finite) -- a conditional prefetch
+    // made hipcc serialise the loop on vmcnt(0).
     const int st_chunk = tid & 15, st_row0 = tid >> 4;
     u32x4 kreg[SIT], vreg[SIT];
 #define LOAD_TILE(t)                                                                              \
@@ -127,11 +151,11 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
             vreg[i] = *reinterpret_cast<const u32x4*>(p + vcol);                                 \
         }                                                                                         \
     }
-#define STORE_TILE(stage)                                                                         \
+#define STORE_TILE(st)                                                                            \
     _Pragma("unroll") for (int i = 0; i < SIT; ++i) {                                               \
         const int row = st_row0 + SROWS * i;                                                         \
-        *reinterpret_cast<u32x4*>(lds[stage] + k_off(row, st_chunk)) = kreg[i];                  \
-        *reinterpret_cast<u32x4*>(lds[stage] + BN * 256 + v_off(row, st_chunk)) = vreg[i];       \
+        *reinterpret_cast<u32x4*>(lds + (st) + k_off(row, st_chunk)) = kreg[i];                    \
+        *reinterpret_cast<u32x4*>(lds + (st) + BN * 256 + v_off(row, st_chunk)) = vreg[i];         \
     }
 
     f32x16 o[4];
@@ -141,153 +165,210 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
 
     LOAD_TILE(0);
     STORE_TILE(0);
-    __syncthreads();
+    LOAD_TILE(min(1, ntiles - 1));
 
-    const int wave_last_q = pre + qblock + 32 * w + 31;  // absolute position of the wave's last row
-    const char* ldsK = lds[0];
-    const char* ldsV = ldsK + BN * 256;
+    const int wave_last_q = pre + q0 + 31;  // absolute position of the wave's last row
+    // PV operand addressing (loop-invariant parts): lane (g, q4, p4) reads V rows 4(g>>1) + q4 (+8) of each
+    // 16-key slab at columns dt*32 + 16(g&1) + 4p4
+    const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+    // (A GEMM-style stagger -- waves 4-7 half a tile behind waves 0-3, two barriers per tile, so one
+    // wave's QK^T runs beside its partner's softmax + P.V -- measured 3-7 % slower than this one-barrier
+    // loop, as did raising waves 0-3's priority: profiles/r3_attn_prefill_stagger_ab.jsonl.)
     for (int t = 0; t < ntiles; ++t) {
-        LOAD_TILE(min(t + 1, ntiles - 1));
+        const int cur = (t & 1) * STAGE;
         const int kv0 = t * BN;
-        if (kv0 <= wave_last_q) {  // wave-uniform: tiles wholly above the diagonal are skipped
-            f32x16 sacc[2];
+        const bool act = kv0 <= wave_last_q;  // wave-uniform: tiles wholly above the diagonal are skipped
+        __syncthreads();  // tile t visible in stage t&1; every wave is done with tile t-1 (stage (t+1)&1)
+        STORE_TILE(STAGE - cur);
+        LOAD_TILE(min(t + 2, ntiles - 1));
+        const char* ldsK = lds + cur;
+        const char* ldsV = ldsK + BN * 256;
+        if (!act) continue;
+        // S^T = K Q^T: all 16 K fragments read up front (64 VGPRs, dead after the QK^T MFMAs), so the
+        // ds_reads run ahead of the MFMA chain instead of one exposed LDS round trip per MFMA
+        uint4 kf[2][8];
+        f32x16 sacc[2];
 #pragma unroll
-            for (int kt = 0; kt < 2; ++kt) {
-                sacc[kt] = f32x16{};
-                const int row = kt * 32 + r32;
+        for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-                for (int ks = 0; ks < 8; ++ks) {
-                    const uint4 kv = *reinterpret_cast<const uint4*>(ldsK + k_off(row, 2 * ks + half));
-                    sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kv), qf[ks], sacc[kt], 0, 0, 0);
-                }
-            }
-            // mask + row max (key index of reg i: kt*32 + (i&3) + 8(i>>2) + 4half).  The causal/length
-            // mask is only needed on tiles that reach past the wave's first query row or the sequence
-            // end (wave-uniform test); scores stay unscaled until the exponent, which is one FMA:
-            // p = 2^(s * scale_log2 - m), with the raw v_exp_f32 (no denormal range reduction: the
-            // library exp2f costs 4 extra VALU ops per score).
-            const int kmax = pre + min(qi, len - 1) - kv0 - 4 * half;  // last valid key offset for row qi
-            if (kv0 + BN - 1 > pre + qblock + 32 * w || kv0 + BN > pre + len) {
+            for (int ks = 0; ks < 8; ++ks)
+                kf[kt][ks] = *reinterpret_cast<const uint4*>(ldsK + k_off(kt * 32 + r32, 2 * ks + half));
 #pragma unroll
-                for (int kt = 0; kt < 2; ++kt)
+        for (int kt = 0; kt < 2; ++kt) {
+            sacc[kt] = f32x16{};
 #pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const int koff = kt * 32 + (i & 3) + 8 * (i >> 2);  // key - kv0 - 4*half
-                        sacc[kt][i] = koff <= kmax ? sacc[kt][i] : -INFINITY;
-                    }
-            }
-            float mt = -INFINITY;
+            for (int ks = 0; ks < 8; ++ks)
+                sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[kt][ks]), qf[ks], sacc[kt], 0, 0, 0);
+        }
+        // schedule (cdna_hip_programming.md T19): 8 reads ahead, then one read per MFMA gap -- without it the
+        // machine scheduler sinks every read next to its MFMA and waits lgkmcnt(0) before each one
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+        // mask + row max (key index of reg i: kt*32 + (i&3) + 8(i>>2) + 4half).  The causal/length mask is
+        // only needed on tiles that reach past the wave's first query row or the sequence end (wave-uniform
+        // test); scores stay unscaled until the exponent, which is one FMA: p = 2^(s * scale_log2 - m), with
+        // the raw v_exp_f32.
+        const int kmax = pre + min(qi, len - 1) - kv0 - 4 * half;  // last valid key offset for row qi
+        if (kv0 + BN - 1 > pre + q0 || kv0 + BN > pre + len) {
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-                for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sacc[kt][i]);
-            mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
-            // deferred rescale: the running max m only moves (and o, l are rescaled) when some row's
-            // max grew by more than RESCALE_LOG2 -- until then p <= 2^RESCALE_LOG2, harmless in fp32
-            // and in the bf16 P operand.  Key 0 is valid for every row, so m is finite after tile 0.
-            // (PAGED: rows past the slice end see keys up to pre + len - 1 only; stale page rows past
-            // that are masked like any key beyond the causal limit.)
-            const float mc = mt * scale_log2;
-            if (__ballot(mc > m + RESCALE_LOG2)) {
-                const float mn = fmaxf(m, mc);
-                const float alpha = __builtin_amdgcn_exp2f(m - mn);  // m = -inf before tile 0 -> 0
-                m = mn;
-                l *= alpha;
-#pragma unroll
-                for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
-            }
-            float ls = 0.f;
-            bf16x8 pf[2][2];
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt) {
-#pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kt][i], scale_log2, -m));
-                    ls += p;
-                    pf[kt][i >> 3][i & 7] = (bf16)p;
+                    const int koff = kt * 32 + (i & 3) + 8 * (i >> 2);  // key - kv0 - 4*half
+                    sacc[kt][i] = koff <= kmax ? sacc[kt][i] : -INFINITY;
                 }
-            }
-            l += ls;
-            // O^T[d][q] += V^T[d][key] P^T[key][q]
-            const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+        }
+        float mt = -INFINITY;
 #pragma unroll
-            for (int dt = 0; dt < 4; ++dt) {
-                const int col = dt * 32 + 16 * (g & 1) + 4 * p4;  // this lane's address column
-                const int chunk = col >> 3, inoff = (col & 7) * 2;
+        for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-                for (int kt = 0; kt < 2; ++kt) {
+            for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sacc[kt][i]);
+        mt = halves_max(mt);
+        // deferred rescale (cdna_hip_programming.md T13): the running max m only moves (and o, l are
+        // rescaled) when some row's max grew by more than RESCALE_LOG2 -- until then p <= 2^RESCALE_LOG2,
+        // harmless in fp32 and in the bf16 P operand.  The previous tile's P.V is complete (program order)
+        // and this tile's P is exponentiated after the decision.  Key 0 is valid for every row, so m is
+        // finite after tile 0.
+        const float mc = mt * scale_log2;
+        if (__ballot(mc > m + RESCALE_LOG2)) {
+            const float mn = fmaxf(m, mc);
+            const float alpha = __builtin_amdgcn_exp2f(m - mn);  // m = -inf before tile 0 -> 0
+            m = mn;
+            l *= alpha;
 #pragma unroll
-                    for (int s = 0; s < 2; ++s) {
-                        const int rowa = kt * 32 + 16 * s + 4 * (g >> 1) + q4;
-                        const int rowb = rowa + 8;
-                        const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                            (lds_v4s*)(ldsV + v_off(rowa, chunk) + inoff));
-                        const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                            (lds_v4s*)(ldsV + v_off(rowb, chunk) + inoff));
-                        typedef short v8s __attribute__((ext_vector_type(8)));
-                        const v8s a = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), pf[kt][s],
-                                                                        o[dt], 0, 0, 0);
-                    }
-                }
+            for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+        }
+        float ls = 0.f;
+        bf16x8 pf[2][2];
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kt][i], scale_log2, -m));
+                ls += p;
+                pf[kt][i >> 3][i & 7] = (bf16)p;
             }
         }
-        __syncthreads();
-        if (t + 1 < ntiles) {
-            STORE_TILE(0);
-            __syncthreads();
+        l += ls;
+        // O^T[d][q] += V^T[d][key] P^T[key][q]: per 32-dim block dt, its 8 transposed reads, then 4 MFMAs
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            const int col = dt * 32 + 16 * (g & 1) + 4 * p4;  // this lane's address column
+            const int chunk = col >> 3, inoff = (col & 7) * 2;
+            v8s va[2][2];
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const int rowa = kt * 32 + 16 * s + 4 * (g >> 1) + q4;
+                    const v4s lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(ldsV + v_off(rowa, chunk) + inoff));
+                    const v4s hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(ldsV + v_off(rowa + 8, chunk) + inoff));
+                    va[kt][s] = v8s{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                }
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va[kt][s]), pf[kt][s],
+                                                                    o[dt], 0, 0, 0);
         }
+        // 8 transposed reads ahead, two per MFMA gap after that
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 1);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);
     }
 #undef LOAD_TILE
 #undef STORE_TILE
 
-    // normalise and store: reg i of tile dt holds d = dt*32 + (i&3) + 8(i>>2) + 4half for query qi
-    const float lt = l + __shfl_xor(l, 32, 64);
-    if (qi < len) {
-        const float inv = 1.f / lt;
-        bf16* op = out + (size_t)(s0 + qi) * out_stride + h * D;
+    // normalise and store.  Reg i of tile dt holds d = dt*32 + (i&3) + 8(i>>2) + 4half for query qi; one
+    // v_permlane32_swap per dword pair regroups two 4-dim groups so every lane stores 16 contiguous bytes
+    // (cdna_hip_programming.md T21): lane < 32 dims 16j..16j+7, lane >= 32 dims 16j+8..16j+15 of row qi.
+    const float lt = halves_sum(l);
+    const float inv = 1.f / lt;
+    uint4 ov[4][2];
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
+    for (int dt = 0; dt < 4; ++dt) {
 #pragma unroll
-            for (int g4 = 0; g4 < 4; ++g4) {
-                const int d = dt * 32 + 8 * g4 + 4 * half;
-                uint2 v;
-                v.x = pack2(o[dt][4 * g4 + 0] * inv, o[dt][4 * g4 + 1] * inv);
-                v.y = pack2(o[dt][4 * g4 + 2] * inv, o[dt][4 * g4 + 3] * inv);
-                *reinterpret_cast<uint2*>(op + d) = v;
-            }
+        for (int j = 0; j < 2; ++j) {  // groups g4 = 2j, 2j+1 of this 32-dim block
+            const uint32_t a0 = pack2(o[dt][8 * j + 0] * inv, o[dt][8 * j + 1] * inv);
+            const uint32_t a1 = pack2(o[dt][8 * j + 2] * inv, o[dt][8 * j + 3] * inv);
+            const uint32_t b0 = pack2(o[dt][8 * j + 4] * inv, o[dt][8 * j + 5] * inv);
+            const uint32_t b1 = pack2(o[dt][8 * j + 6] * inv, o[dt][8 * j + 7] * inv);
+            const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+            const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+            ov[dt][j] = make_uint4(r0[0], r1[0], r0[1], r1[1]);
         }
+    }
+    if (qi < len) {
+        bf16* op = out + (size_t)(s0 + qi) * out_stride + h * D + 8 * half;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) *reinterpret_cast<uint4*>(op + dt * 32 + 16 * j) = ov[dt][j];
     }
 }
 
+template <bool PAGED, int G>
+static void launch_g(dim3 grid, hipStream_t s, const bf16* Q, int row_stride, const int* cu, const int2* it, bf16* out,
+                     int out_stride, int Hq, int Hkv, float sl, const PagedKV& p) {
+    attn_prefill_kernel<PAGED, G><<<grid, NTHR, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq, Hkv, sl, p);
+}
+
+// Query positions per workgroup for a GQA ratio (the host's work list must use the same block size).
+MRSUM_API int mrsum_attn_prefill_block_m(int Hq, int Hkv) {
+    if (Hkv <= 0 || Hq % Hkv) return -1;
+    const int G = Hq / Hkv;
+    return (G == 1 || G == 2 || G == 4 || G == 8) ? 32 * (NW / G) : -1;
+}
+
 static int launch_prefill(const void* qkv, int row_stride, const int* cu_seqlens, const int* items, int n_items,
-                          void* out, int out_stride, int Hq, int Hkv, int Dh, float scale, const PagedKV* pk,
-                          hipStream_t s) {
+                          int block_m, void* out, int out_stride, int Hq, int Hkv, int Dh, float scale,
+                          const PagedKV* pk, hipStream_t s) {
     if (n_items <= 0) return 0;
-    if (Dh != D || Hq % Hkv) return (int)hipErrorInvalidValue;
-    dim3 grid(n_items, Hq), block(NTHR);
+    if (Dh != D || mrsum_attn_prefill_block_m(Hq, Hkv) != block_m) return (int)hipErrorInvalidValue;
+    dim3 grid(n_items, Hkv);
     const float sl = scale * 1.4426950408889634f;
     auto Q = (const bf16*)qkv;
     auto IT = (const int2*)items;
+    auto O = (bf16*)out;
     const PagedKV p = pk ? *pk : PagedKV{nullptr, nullptr, nullptr, 0, nullptr, nullptr};
-    if (pk) attn_prefill_kernel<true><<<grid, block, 0, s>>>(Q, row_stride, cu_seqlens, IT, (bf16*)out, out_stride, Hq, Hkv, sl, p);
-    else attn_prefill_kernel<false><<<grid, block, 0, s>>>(Q, row_stride, cu_seqlens, IT, (bf16*)out, out_stride, Hq, Hkv, sl, p);
+#define DISPATCH(PG)                                                                                         \
+    switch (Hq / Hkv) {                                                                                      \
+        case 1: launch_g<PG, 1>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, sl, p); break; \
+        case 2: launch_g<PG, 2>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, sl, p); break; \
+        case 4: launch_g<PG, 4>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, sl, p); break; \
+        default: launch_g<PG, 8>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, sl, p); break; \
+    }
+    if (pk) { DISPATCH(true) } else { DISPATCH(false) }
+#undef DISPATCH
     return (int)hipGetLastError();
 }
 
+// items: (sequence, first query row) pairs of block_m = mrsum_attn_prefill_block_m(Hq, Hkv) rows each.
 MRSUM_API int mrsum_attn_prefill(const void* qkv, int row_stride, const int* cu_seqlens, const int* items,
-                                 int n_items, void* out, int out_stride, int Hq, int Hkv, int Dh, float scale,
-                                 hipStream_t s) {
-    return launch_prefill(qkv, row_stride, cu_seqlens, items, n_items, out, out_stride, Hq, Hkv, Dh, scale, nullptr, s);
+                                 int n_items, int block_m, void* out, int out_stride, int Hq, int Hkv, int Dh,
+                                 float scale, hipStream_t s) {
+    return launch_prefill(qkv, row_stride, cu_seqlens, items, n_items, block_m, out, out_stride, Hq, Hkv, Dh, scale,
+                          nullptr, s);
 }
 
 // Chunked-prefill attention: q rows of the packed slices (qkv, cu_seqlens), keys / values from the paged
 // cache for absolute positions [0, prefix[seq] + slice length) of every sequence (page size 64).
 MRSUM_API int mrsum_attn_prefill_paged(const void* qkv, int row_stride, const int* cu_seqlens, const int* items,
-                                       int n_items, void* out, int out_stride, int Hq, int Hkv, int Dh, float scale,
-                                       const void* kcache, const void* vcache, const int* block_tables,
+                                       int n_items, int block_m, void* out, int out_stride, int Hq, int Hkv, int Dh,
+                                       float scale, const void* kcache, const void* vcache, const int* block_tables,
                                        int bt_stride, const int* seq_slot, const int* prefix, hipStream_t s) {
     if (!kcache || !vcache || !block_tables || !seq_slot || !prefix) return (int)hipErrorInvalidValue;
     const PagedKV pk{(const bf16*)kcache, (const bf16*)vcache, block_tables, bt_stride, seq_slot, prefix};
-    return launch_prefill(qkv, row_stride, cu_seqlens, items, n_items, out, out_stride, Hq, Hkv, Dh, scale, &pk, s);
+    return launch_prefill(qkv, row_stride, cu_seqlens, items, n_items, block_m, out, out_stride, Hq, Hkv, Dh, scale,
+                          &pk, s);
 }

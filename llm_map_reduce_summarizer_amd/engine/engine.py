@@ -343,7 +343,7 @@ class LLMEngine:
         items = None
         if dev.type == "cuda":
             from ..ops.hip import prefill_items
-            items = prefill_items(lens).to(dev, non_blocking=True)
+            items = prefill_items(lens, self.model.hq // self.model.hkv).to(dev, non_blocking=True)
         pp = None
         if paged:
             pre = [b for b, _ in spans]

@@ -31,8 +31,9 @@ _SIGS = {
     "mrsum_swiglu": [_vp, _vp, _c_int, _c_int, _vp],
     "mrsum_kv_scatter": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp],
     "mrsum_embed": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _vp],
-    "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
-    "mrsum_attn_prefill_paged": [_vp, _c_int, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp,
+    "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
+    "mrsum_attn_prefill_paged": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float,
+                                 _vp,
                                  _vp, _vp, _c_int, _vp, _vp, _vp],
     "mrsum_attn_decode_mfma": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int,
                                _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp],
@@ -255,11 +256,16 @@ def embed(ids: torch.Tensor, table: torch.Tensor, out: Optional[torch.Tensor] = 
 
 
 # ------------------------------------------------------------------ attention
-PREFILL_BLOCK_M = 256  # query rows per prefill-attention workgroup (attn_prefill.hip BM: 8 waves x 32 rows)
+def prefill_block_m(group: int) -> int:
+    """Query positions per prefill-attention workgroup for ``group`` = Hq / Hkv query heads per kv head
+    (attn_prefill.hip: 8 waves x 32 rows cover all ``group`` heads of one kv head)."""
+    _req(group in (1, 2, 4, 8), "attn_prefill: GQA ratio %d not in (1, 2, 4, 8)" % group)
+    return 256 // group
 
 
-def prefill_items(seqlens, block_m: int = PREFILL_BLOCK_M) -> torch.Tensor:
-    """(sequence, query-block start) work list, heaviest (latest) blocks first."""
+def prefill_items(seqlens, group: int = 4) -> torch.Tensor:
+    """(sequence, query-block start) work list for GQA ratio ``group``, heaviest (latest) blocks first."""
+    block_m = prefill_block_m(group)
     items = []
     for s, n in enumerate(seqlens):
         for qb in range(0, int(n), block_m):
@@ -282,8 +288,9 @@ def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int,
         cu = cu_seqlens.cpu().tolist()
         seqlens = [b - a for a, b in zip(cu[:-1], cu[1:])]
         _req(cu[0] == 0 and cu[-1] <= T and all(n >= 0 for n in seqlens), "attn_prefill: bad cu_seqlens")
+    block_m = prefill_block_m(hq // hkv)
     if items is None:
-        items = prefill_items(seqlens).to(qkv.device)
+        items = prefill_items(seqlens, hq // hkv).to(qkv.device)
     _i32(items)
     if out is None:
         out = torch.empty(T, hq * d, dtype=qkv.dtype, device=qkv.device)
@@ -301,11 +308,11 @@ def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int,
             _req(0 <= slot < bt.shape[0] and pre >= 0 and pre + n <= bt.shape[1] * 64,
                  "attn_prefill: slice [%d, %d) beyond block table" % (pre, pre + n))
         _check(_fn("mrsum_attn_prefill_paged")(_p(qkv), qkv.stride(0), _p(cu_seqlens), _p(items), items.shape[0],
-                                               _p(out), out.stride(0), hq, hkv, d, scale, _p(kc), _p(vc), _p(bt),
+                                               block_m, _p(out), out.stride(0), hq, hkv, d, scale, _p(kc), _p(vc), _p(bt),
                                                bt.stride(0), _p(paged.seq_slot), _p(paged.prefix), _stream()),
                "attn_prefill_paged")
         return out
-    _check(_fn("mrsum_attn_prefill")(_p(qkv), qkv.stride(0), _p(cu_seqlens), _p(items), items.shape[0], _p(out),
+    _check(_fn("mrsum_attn_prefill")(_p(qkv), qkv.stride(0), _p(cu_seqlens), _p(items), items.shape[0], block_m, _p(out),
                                      out.stride(0), hq, hkv, d, scale, _stream()), "attn_prefill")
     return out
 

@@ -95,7 +95,7 @@ def test_swiglu_embed():
 
 
 @pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (2, 2)])
-@pytest.mark.parametrize("seqlens", [[1, 37, 130, 300], [64], [129, 256]])
+@pytest.mark.parametrize("seqlens", [[1, 37, 130, 300], [64], [129, 256], [1000, 33, 2100]])
 def test_attn_prefill(hq, hkv, seqlens):
     d = 128
     T = sum(seqlens)
@@ -107,7 +107,7 @@ def test_attn_prefill(hq, hkv, seqlens):
     _close(o1, o2, 2e-2)
 
 
-@pytest.mark.parametrize("hq,hkv", [(4, 1), (8, 2)])
+@pytest.mark.parametrize("hq,hkv", [(4, 1), (8, 2), (8, 1), (2, 2)])
 @pytest.mark.parametrize("spans", [[(0, 200)], [(130, 300), (0, 77), (1000, 1129)], [(64, 128), (2047, 2048)]])
 def test_attn_prefill_paged(hq, hkv, spans):
     """Chunked-prefill attention: slice rows attend to [0, prefix + slice) of their sequence read from the
@@ -136,9 +136,10 @@ def test_attn_prefill_paged(hq, hkv, spans):
     _close(o1, o2, 2e-2)
 
 
-def test_attn_prefill_spike():
+@pytest.mark.parametrize("hq", [4, 8])
+def test_attn_prefill_spike(hq):
     """A key far larger than the rest forces the online-softmax rescale path mid-sequence."""
-    hq, hkv, d = 4, 1, 128
+    hkv, d = 1, 128
     seqlens = [300]
     T = 300
     qkv = _rand(T, (hq + 2 * hkv) * d, scale=0.5, seed=12)

@@ -34,18 +34,22 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", default="1x4096,8x4096,39x4000,1x32768")
     ap.add_argument("--tag", default=os.path.basename(os.getcwd()))
+    ap.add_argument("--hq", type=int, default=32)
+    ap.add_argument("--hkv", type=int, default=8)
     a = ap.parse_args()
-    dev, hq, hkv, d = "cuda:0", 32, 8, 128
+    dev, hq, hkv, d = "cuda:0", a.hq, a.hkv, 128
     torch.manual_seed(0)
     for case in a.cases.split(","):
         nseq, L = (int(v) for v in case.split("x"))
         T = nseq * L
         qkv = torch.randn(T, (hq + 2 * hkv) * d, device=dev, dtype=torch.bfloat16)
         cu = torch.arange(0, T + 1, L, dtype=torch.int32, device=dev)
-        items = hip.prefill_items([L] * nseq).to(dev)
+        # trees before the GQA-packed kernel take 256-row blocks of one head
+        items = (hip.prefill_items([L] * nseq, hq // hkv) if hasattr(hip, "prefill_block_m")
+                 else hip.prefill_items([L] * nseq)).to(dev)
         fl = nseq * 4 * L * L / 2 * d * hq
         ms = timeit(lambda: hip.attn_prefill(qkv, cu, hq, hkv, d, 1 / math.sqrt(d), items=items, seqlens=[L] * nseq))
-        print(json.dumps({"tree": a.tag, "kind": "contiguous", "nseq": nseq, "L": L, "ms": round(ms, 3),
+        print(json.dumps({"tree": a.tag, "kind": "contiguous", "hq": hq, "hkv": hkv, "nseq": nseq, "L": L, "ms": round(ms, 3),
                           "TFLOPs": round(fl / ms / 1e9, 1)}), flush=True)
         # paged: the same keys from a page cache (prefix 0: one slice), pages shuffled
         npg = -(-L // 64)
@@ -57,7 +61,7 @@ def main():
                               kc, vc)
         ms = timeit(lambda: hip.attn_prefill(qkv, cu, hq, hkv, d, 1 / math.sqrt(d), items=items, seqlens=[L] * nseq,
                                              paged=pp))
-        print(json.dumps({"tree": a.tag, "kind": "paged", "nseq": nseq, "L": L, "ms": round(ms, 3),
+        print(json.dumps({"tree": a.tag, "kind": "paged", "hq": hq, "hkv": hkv, "nseq": nseq, "L": L, "ms": round(ms, 3),
                           "TFLOPs": round(fl / ms / 1e9, 1)}), flush=True)
         del qkv, kc, vc
 

@@ -83,7 +83,7 @@ def main():
         T = nseq * L
         qkv = torch.randn(T, (hq + 2 * hkv) * d, device=dev, dtype=torch.bfloat16)
         cu = torch.arange(0, T + 1, L, dtype=torch.int32, device=dev)
-        items = hip.prefill_items([L] * nseq).to(dev)
+        items = hip.prefill_items([L] * nseq, hq // hkv).to(dev)
         t = timeit(lambda: hip.attn_prefill(qkv, cu, hq, hkv, d, 1 / math.sqrt(d), items=items, seqlens=[L] * nseq),
                    iters=20)
         fl = nseq * 4 * L * L / 2 * d * hq
