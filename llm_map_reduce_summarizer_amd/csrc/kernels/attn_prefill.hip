@@ -173,7 +173,10 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
     const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
     // (A GEMM-style stagger -- waves 4-7 half a tile behind waves 0-3, two barriers per tile, so one
     // wave's QK^T runs beside its partner's softmax + P.V -- measured 3-7 % slower than this one-barrier
-    // loop, as did raising waves 0-3's priority: profiles/r3_attn_prefill_stagger_ab.jsonl.)
+    // loop, as did raising waves 0-3's priority: profiles/r3_attn_prefill_stagger_ab.jsonl.  A T15 software
+    // pipeline -- QK^T of tile t+1 in one scheduling region with tile t's exponentials, P.V(t) beside tile
+    // t+1's mask + max, three-stage ring, 246 VGPRs -- measured 7-9 % slower on every shape:
+    // profiles/r3_attn_prefill_pipelined_experiment.jsonl.)
     for (int t = 0; t < ntiles; ++t) {
         const int cur = (t & 1) * STAGE;
         const int kv0 = t * BN;
