@@ -19,11 +19,18 @@ import build  # noqa: E402
 def main():
     ref, tag = sys.argv[1], sys.argv[2]
     kdir = "llm_map_reduce_summarizer_amd/csrc/kernels"
-    names = subprocess.check_output(["git", "-C", ROOT, "ls-tree", "--name-only", ref, kdir + "/"], text=True).split()
     with tempfile.TemporaryDirectory() as td:
-        for n in names:
-            with open(os.path.join(td, os.path.basename(n)), "wb") as f:
-                f.write(subprocess.check_output(["git", "-C", ROOT, "show", "%s:%s" % (ref, n)]))
+        if os.path.isdir(ref):  # a directory of (patched) kernel sources instead of a git ref
+            names = sorted(os.listdir(ref))
+            for n in names:
+                with open(os.path.join(ref, n), "rb") as fi, open(os.path.join(td, n), "wb") as f:
+                    f.write(fi.read())
+        else:
+            names = subprocess.check_output(["git", "-C", ROOT, "ls-tree", "--name-only", ref, kdir + "/"],
+                                            text=True).split()
+            for n in names:
+                with open(os.path.join(td, os.path.basename(n)), "wb") as f:
+                    f.write(subprocess.check_output(["git", "-C", ROOT, "show", "%s:%s" % (ref, n)]))
         objs = []
         for n in names:
             if not n.endswith(".hip"):
