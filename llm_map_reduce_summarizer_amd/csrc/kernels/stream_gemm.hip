@@ -625,19 +625,29 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_fp8_kernel(const bf16* __r
         if (j + D - 1 < nkb) ISSUE8((j + D - 1) % D, (j + D - 1) * KB8);
         const char* wl = lds + (j % D) * SLOT;
         const char* xl = wl + WBYTES;
+        // MFMA steps in pairs (2p, 2p+1): lane (r, g) reads the 16-B chunk 4p + g of its weight row (fp8 k =
+        // 64p + 16g .. +16) with one ds_read_b128 and feeds its low 8 bytes to step 2p and its high 8 bytes
+        // to step 2p+1; the x operand takes the same k permutation (the MFMA k order is free).  8-byte A
+        // reads were merged by hipcc into ds_read2st64_b64, whose lost alias info made the waitcnt pass drain
+        // vmcnt(0) -- every in-flight ring slot -- before each slot's first read (XR variant).  Same-box A/B:
+        // neutral to +7 % (profiles/r3_fp8_stream_vmcnt_fix_ab.jsonl; 6.2 TB/s on the 70B down shape on
+        // that box, 4.8 on another: compare only same-box numbers).
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {  // 32-k MFMA steps: fp8 bytes 32 i + 8 g .. +8 of the row
-            const uint2 araw = *reinterpret_cast<const uint2*>(wl + img_off(16 * w + r, 2 * i + (g >> 1)) + 8 * (g & 1));
-            const bf16x8 av = fp8x8_bf16(araw);
-            if constexpr (XR) {  // every lane reads row 0 (broadcast); rows >= M are never stored
-                const u32x4 bv = *reinterpret_cast<const u32x4*>(xres + 2 * (KB8 * j + 32 * i + 8 * g));
-                acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, bv), acc[0], 0, 0, 0);
-            } else {
+        for (int p = 0; p < 4; ++p) {
+            const u32x4 a4 = *reinterpret_cast<const u32x4*>(wl + img_off(16 * w + r, 4 * p + g));
 #pragma unroll
-                for (int m = 0; m < MT; ++m) {
-                    const u32x4 bv = *reinterpret_cast<const u32x4*>(xl + (i >> 2) * XBYTES +
-                                                                     img_off(16 * m + r, 4 * (i & 3) + g));
-                    acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, bv), acc[m], 0, 0, 0);
+            for (int h = 0; h < 2; ++h) {
+                const bf16x8 av = fp8x8_bf16(make_uint2(a4[2 * h], a4[2 * h + 1]));
+                if constexpr (XR) {  // every lane reads row 0 (broadcast); rows >= M are never stored
+                    const u32x4 bv = *reinterpret_cast<const u32x4*>(xres + 2 * (KB8 * j + 64 * p + 16 * g + 8 * h));
+                    acc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, bv), acc[0], 0, 0, 0);
+                } else {
+#pragma unroll
+                    for (int m = 0; m < MT; ++m) {
+                        const u32x4 bv = *reinterpret_cast<const u32x4*>(xl + (p >> 1) * XBYTES +
+                                                                         img_off(16 * m + r, 8 * (p & 1) + 2 * g + h));
+                        acc[m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, __builtin_bit_cast(bf16x8, bv), acc[m], 0, 0, 0);
+                    }
                 }
             }
         }

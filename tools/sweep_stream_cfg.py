@@ -36,7 +36,8 @@ def main():
     ap.add_argument("--ops", default="o,down,qkv")
     a = ap.parse_args()
     dev = "cuda:0"
-    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "down": (4096, 14336), "gate_up": (28672, 4096)}
+    shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "down": (4096, 14336), "gate_up": (28672, 4096),
+              "o70": (8192, 8192), "down70h": (8192, 14336)}  # 70B o; the fp8 70B down's row bytes in bf16
     for name in a.ops.split(","):
         N, K = shapes[name]
         ncopy = max(2, int(1.2e9 // (N * K * 2)))
