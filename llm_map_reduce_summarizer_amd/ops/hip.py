@@ -396,7 +396,10 @@ def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
     else:
         fused = groups <= 128
         if fused:
-            splits = min(splits, 8 if pages <= 96 else 4)  # B=5 at 4k: 6 splits fused 22.6 us, unfused 23.3
+            # B=5 at 4k: 6 splits fused 22.6 us, unfused 23.3; a TP shard's one or two kv heads at B=20 (20 groups,
+            # 4k) take 12 fused splits: 1.971 / 1.971 ms per TP=8 shard step vs 8 fused 2.020 / 2.016, 12
+            # separate 1.984 (in situ, profiles/r3_plans_insitu_tp8_b39_b20.jsonl)
+            splits = min(splits, (12 if hkv <= 2 else 8) if pages <= 96 else 4)
     return splits, fused
 
 
