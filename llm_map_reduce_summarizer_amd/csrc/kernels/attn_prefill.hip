@@ -2,7 +2,7 @@
 //
 // Packed batch: qkv [T, row_stride] bf16 (Q heads, then K heads, then V
 // heads, D=128 each, already rotated by rope_kv), cu_seqlens [nseq+1].
-// Work item = (sequence, query block of 256/G positions) x KV HEAD (blockIdx.y), G = Hq / Hkv: the 8 waves
+// Work item = (sequence, query block of 256/G positions) x KV HEAD, G = Hq / Hkv: the 8 waves
 // of a workgroup run all G query heads of their kv head (wave w: head kvh*G + w%G, rows 32(w/G)..+32), so a
 // staged K/V tile always feeds 256 query rows, and the causal diagonal of a block is only 256/G rows deep
 // (64 for Llama-3-8B, 32 for 70B: waves idle on masked diagonal tiles far less than with 256-row blocks of
@@ -92,15 +92,22 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
                                                               const int* __restrict__ cu_seqlens,
                                                               const int2* __restrict__ items,
                                                               bf16* __restrict__ out, int out_stride, int Hq,
-                                                              int Hkv, float scale_log2, PagedKV pk) {
+                                                              int Hkv, float scale_log2, PagedKV pk, int kv_major) {
     constexpr int BMP = 32 * (NW / G);  // query positions per workgroup
     // two-stage ring of [K tile | V tile]: tile t+1 is written into the other stage while tile t is
     // consumed, one barrier per tile
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
 
-    const int2 it = items[blockIdx.x];
+    // Block order.  Small grids (kv_major = 0): block b = item b / Hkv x kv head b % Hkv, the host's heaviest-
+    // first order across ALL kv heads -- kv-head-major order started kv head 7's heaviest blocks only after
+    // kv head 0-6's lists (1 x 4k: 580 vs 870 TF/s).  Large grids (kv_major = 1): block b = kv head
+    // b / n_items x item b % n_items, so the blocks in flight share one kv head and its K/V stays in the
+    // Infinity Cache (39 x 4k: 912 vs 815 TF/s); profiles/r3_attn_prefill_grid_order_ab.jsonl.
+    const int n_items = gridDim.x / Hkv;
+    const int item = kv_major ? blockIdx.x % n_items : blockIdx.x / Hkv;
+    const int2 it = items[item];
     const int seq = it.x, qblock = it.y;
-    const int kvh = blockIdx.y;
+    const int kvh = kv_major ? blockIdx.x / n_items : blockIdx.x % Hkv;
     const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5, r32 = lane & 31;
     const int w = tid >> 6;  // (readfirstlane here made hipcc spill the staggered loop)
     const int h = kvh * G + w % G, rb = w / G;
@@ -323,7 +330,9 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
 template <bool PAGED, int G>
 static void launch_g(dim3 grid, hipStream_t s, const bf16* Q, int row_stride, const int* cu, const int2* it, bf16* out,
                      int out_stride, int Hq, int Hkv, float sl, const PagedKV& p) {
-    attn_prefill_kernel<PAGED, G><<<grid, NTHR, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq, Hkv, sl, p);
+    // kv-head-major order from 8 blocks per CU up (measured crossover: 4096 blocks neutral, 19656 kv-major)
+    const int kv_major = grid.x > 8 * 256;
+    attn_prefill_kernel<PAGED, G><<<grid, NTHR, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq, Hkv, sl, p, kv_major);
 }
 
 // Query positions per workgroup for a GQA ratio (the host's work list must use the same block size).
@@ -338,7 +347,7 @@ static int launch_prefill(const void* qkv, int row_stride, const int* cu_seqlens
                           const PagedKV* pk, hipStream_t s) {
     if (n_items <= 0) return 0;
     if (Dh != D || mrsum_attn_prefill_block_m(Hq, Hkv) != block_m) return (int)hipErrorInvalidValue;
-    dim3 grid(n_items, Hkv);
+    dim3 grid(n_items * Hkv);
     const float sl = scale * 1.4426950408889634f;
     auto Q = (const bf16*)qkv;
     auto IT = (const int2*)items;

@@ -263,8 +263,9 @@ def prefill_block_m(group: int) -> int:
     return 256 // group
 
 
-def prefill_items(seqlens, group: int = 4) -> torch.Tensor:
-    """(sequence, query-block start) work list for GQA ratio ``group``, heaviest (latest) blocks first."""
+def prefill_items(seqlens, group: int) -> torch.Tensor:
+    """(sequence, query-block start) work list for GQA ratio ``group`` = Hq / Hkv, heaviest (latest) blocks
+    first."""
     block_m = prefill_block_m(group)
     items = []
     for s, n in enumerate(seqlens):
@@ -291,6 +292,10 @@ def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int,
     block_m = prefill_block_m(hq // hkv)
     if items is None:
         items = prefill_items(seqlens, hq // hkv).to(qkv.device)
+    # a list built for another GQA ratio has another block count (same-count collisions need every
+    # sequence shorter than both block sizes, where the blocks cover the same rows anyway)
+    _req(items.shape[0] == sum(-(-int(n) // block_m) for n in seqlens),
+         "attn_prefill: work list not built for GQA ratio %d (prefill_items(seqlens, %d))" % (hq // hkv, hq // hkv))
     _i32(items)
     if out is None:
         out = torch.empty(T, hq * d, dtype=qkv.dtype, device=qkv.device)

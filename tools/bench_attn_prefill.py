@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--tag", default=os.path.basename(os.getcwd()))
     ap.add_argument("--hq", type=int, default=32)
     ap.add_argument("--hkv", type=int, default=8)
+    ap.add_argument("--prefix", type=int, default=0, help="paged case: cached tokens before each slice")
     a = ap.parse_args()
     dev, hq, hkv, d = "cuda:0", a.hq, a.hkv, 128
     torch.manual_seed(0)
@@ -51,18 +52,20 @@ def main():
         ms = timeit(lambda: hip.attn_prefill(qkv, cu, hq, hkv, d, 1 / math.sqrt(d), items=items, seqlens=[L] * nseq))
         print(json.dumps({"tree": a.tag, "kind": "contiguous", "hq": hq, "hkv": hkv, "nseq": nseq, "L": L, "ms": round(ms, 3),
                           "TFLOPs": round(fl / ms / 1e9, 1)}), flush=True)
-        # paged: the same keys from a page cache (prefix 0: one slice), pages shuffled
-        npg = -(-L // 64)
+        # paged: the same keys from a page cache (``--prefix`` cached tokens before each slice), pages shuffled
+        P = a.prefix
+        npg = -(-(P + L) // 64)
         kc = torch.randn(nseq * npg + 1, hkv, 64, d, device=dev, dtype=torch.bfloat16)
         vc = torch.randn_like(kc)
         bt = (torch.randperm(nseq * npg, device=dev).to(torch.int32) + 1).view(nseq, npg)
         pp = ops.PagedPrefill(bt, torch.arange(nseq, dtype=torch.int32, device=dev),
-                              torch.zeros(nseq, dtype=torch.int32, device=dev), list(range(nseq)), [0] * nseq,
+                              torch.full((nseq,), P, dtype=torch.int32, device=dev), list(range(nseq)), [P] * nseq,
                               kc, vc)
         ms = timeit(lambda: hip.attn_prefill(qkv, cu, hq, hkv, d, 1 / math.sqrt(d), items=items, seqlens=[L] * nseq,
                                              paged=pp))
-        print(json.dumps({"tree": a.tag, "kind": "paged", "hq": hq, "hkv": hkv, "nseq": nseq, "L": L, "ms": round(ms, 3),
-                          "TFLOPs": round(fl / ms / 1e9, 1)}), flush=True)
+        flp = nseq * 4 * (P * L + L * L / 2) * d * hq
+        print(json.dumps({"tree": a.tag, "kind": "paged", "hq": hq, "hkv": hkv, "nseq": nseq, "L": L, "prefix": P,
+                          "ms": round(ms, 3), "TFLOPs": round(flp / ms / 1e9, 1)}), flush=True)
         del qkv, kc, vc
 
 

@@ -46,7 +46,7 @@ def main():
     lens = [4096] * 4
     qkv = torch.randn(sum(lens), 48 * hd, **bf)
     cu = torch.tensor([0, 4096, 8192, 12288, 16384], dtype=torch.int32, device=dev)
-    items = hip.prefill_items(lens).to(dev)
+    items = hip.prefill_items(lens, 4).to(dev)
     for _ in range(3):
         hip.attn_prefill(qkv, cu, 32, 8, hd, 1 / math.sqrt(hd), seqlens=lens, items=items)
     # prefill GEMMs (gemm.hip, 256 x 256 tiles): bf16 qkv / gate_up + SwiGLU at M = 16384, fp8 gate_up at
