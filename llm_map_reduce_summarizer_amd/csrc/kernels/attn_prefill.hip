@@ -183,7 +183,9 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
     // loop, as did raising waves 0-3's priority: profiles/r3_attn_prefill_stagger_ab.jsonl.  A T15 software
     // pipeline -- QK^T of tile t+1 in one scheduling region with tile t's exponentials, P.V(t) beside tile
     // t+1's mask + max, three-stage ring, 246 VGPRs -- measured 7-9 % slower on every shape:
-    // profiles/r3_attn_prefill_pipelined_experiment.jsonl.)
+    // profiles/r3_attn_prefill_pipelined_experiment.jsonl.  Issuing tile 1's and Q's loads with tile 0's
+    // (one exposed memory latency in the prologue instead of two) measured neutral to -1 %:
+    // profiles/r3_attn_prefill_prologue_experiment.jsonl.)
     for (int t = 0; t < ntiles; ++t) {
         const int cur = (t & 1) * STAGE;
         const int kv0 = t * BN;
