@@ -380,7 +380,7 @@ def _resid_plan(hip, a, w, role, tp=False):
         p = hip.plan(role, M, N, K)
         cfg = p[1:] if p[0] == "stream" else None
         env = os.environ.get("MRSUM_RESID_SKINNY_" + role.upper())  # measurement override (exp_plans_insitu.py)
-        if not tp and N % 512 == 0 and (env == "1" or (env is None and role == "o" and K <= 4096)):
+        if not tp and M <= 16 and N % 512 == 0 and (env == "1" or (env is None and role == "o" and K <= 4096)):
             # TP=1 o projection on the register-streaming producer (no split-K tail), in situ 4k context
             # (profiles/r3_tp1_resid_skinny_insitu.jsonl): B=1 3.336 vs 3.380 ms per step, B=10 4.078 vs 4.087;
             # down (K 14336) loses (3.50 / 4.32)
