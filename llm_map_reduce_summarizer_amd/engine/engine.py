@@ -207,7 +207,7 @@ class LLMEngine:
         self.max_model_len = min(max_model_len, cfg.max_position)
         self.max_num_seqs = min(max_num_seqs, BUCKETS[-1])
         self.max_new_cap = max_new_cap
-        self.max_prefill_tokens = max_prefill_tokens
+        self.max_prefill_tokens = int(os.environ.get("MRSUM_MAX_PREFILL_TOKENS", max_prefill_tokens))
         self.prefill_chunk = int(os.environ.get("MRSUM_PREFILL_CHUNK", prefill_chunk))
         # one-pass prefill attention reads the packed qkv rows (the paged-cache path measured equal:
         # profiles/r2_chunked_prefill_32k_ab.jsonl); tools/bench_prefill.py flips this for the A/B
