@@ -154,22 +154,38 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16* __restrict
 
     // wave w takes k blocks ks + (w + 4j) * KB.  Issue order per block: x fragments of THIS block,
     // then W of the NEXT block, then the MFMAs -- vmcnt retires loads in issue order, so waiting
-    // for x must not also wait for the prefetched W (which would serialise the stream).
-    int kb = ks + w * KB;
+    // for x must not also wait for the prefetched W (which would serialise the stream).  The steady
+    // loop issues every next-block load unconditionally and the last one or two blocks run in
+    // straight-line tails: with the next-block loads under a branch, the waitcnt pass merged the
+    // branch's two vmcnt states into the smaller count and waited for the prefetched W before every
+    // MFMA of the block, one exposed memory round trip per block.  Same-box A/B: TP=8 shard B=10 -1.4 %,
+    // 70B fp8 B=1 -0.5 %, TP=1 B=1/10 unchanged -- the many resident waves had hidden most of it
+    // (profiles/r3_skinny_prefetch_fix_ab.jsonl).
+    const int kb0 = ks + w * KB;
+    const int nb = kb0 < ke ? (ke - kb0 + 4 * KB - 1) / (4 * KB) : 0;  // this wave's k blocks
     AFrag<NT> a0, a1;
     BFrag<MT> b;
-    if (kb < ke) load_a<NT>(a0, W, K, n0, kb, lane);
-    while (kb < ke) {
-        const int kb1 = kb + 4 * KB;
+    if (nb > 0) load_a<NT>(a0, W, K, n0, kb0, lane);
+    int i = 0;
+    for (; i + 2 < nb; i += 2) {  // blocks i and i + 1, each with a successor
+        const int kb = kb0 + i * 4 * KB;
         load_b<MT>(b, x, ldx, M, kb, lane);
-        if (kb1 < ke) load_a<NT>(a1, W, K, n0, kb1, lane);
+        load_a<NT>(a1, W, K, n0, kb + 4 * KB, lane);
         mma_block<NT, MT>(acc, a0, b);
-        if (kb1 >= ke) break;
-        const int kb2 = kb1 + 4 * KB;
-        load_b<MT>(b, x, ldx, M, kb1, lane);
-        if (kb2 < ke) load_a<NT>(a0, W, K, n0, kb2, lane);
+        load_b<MT>(b, x, ldx, M, kb + 4 * KB, lane);
+        load_a<NT>(a0, W, K, n0, kb + 8 * KB, lane);
         mma_block<NT, MT>(acc, a1, b);
-        kb = kb2;
+    }
+    if (nb - i == 2) {
+        const int kb = kb0 + i * 4 * KB;
+        load_b<MT>(b, x, ldx, M, kb, lane);
+        load_a<NT>(a1, W, K, n0, kb + 4 * KB, lane);
+        mma_block<NT, MT>(acc, a0, b);
+        load_b<MT>(b, x, ldx, M, kb + 4 * KB, lane);
+        mma_block<NT, MT>(acc, a1, b);
+    } else if (nb - i == 1) {
+        load_b<MT>(b, x, ldx, M, kb0 + i * 4 * KB, lane);
+        mma_block<NT, MT>(acc, a0, b);
     }
 
     // C layout (16x16x32): lane holds C[row 4(lane>>4)+j][col lane&15] = out^T[n][m]
@@ -590,21 +606,32 @@ __global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict_
 #pragma unroll
         for (int m = 0; m < MT; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    int kb = ks + w * KB;
+    // unconditional next-block loads in the steady loop, straight-line tails (as skinny_gemm_kernel)
+    const int kb0 = ks + w * KB;
+    const int nb = kb0 < ke ? (ke - kb0 + 4 * KB - 1) / (4 * KB) : 0;
     A8Frag<NT> a0, a1;
     BFrag<MT> b;
-    if (kb < ke) load_a8<NT>(a0, W, K, n0, kb, lane);
-    while (kb < ke) {
-        const int kb1 = kb + 4 * KB;
+    if (nb > 0) load_a8<NT>(a0, W, K, n0, kb0, lane);
+    int i = 0;
+    for (; i + 2 < nb; i += 2) {
+        const int kb = kb0 + i * 4 * KB;
         load_b(b, kb);
-        if (kb1 < ke) load_a8<NT>(a1, W, K, n0, kb1, lane);
+        load_a8<NT>(a1, W, K, n0, kb + 4 * KB, lane);
         mma_block8<NT, MT>(acc, a0, b);
-        if (kb1 >= ke) break;
-        const int kb2 = kb1 + 4 * KB;
-        load_b(b, kb1);
-        if (kb2 < ke) load_a8<NT>(a0, W, K, n0, kb2, lane);
+        load_b(b, kb + 4 * KB);
+        load_a8<NT>(a0, W, K, n0, kb + 8 * KB, lane);
         mma_block8<NT, MT>(acc, a1, b);
-        kb = kb2;
+    }
+    if (nb - i == 2) {
+        const int kb = kb0 + i * 4 * KB;
+        load_b(b, kb);
+        load_a8<NT>(a1, W, K, n0, kb + 4 * KB, lane);
+        mma_block8<NT, MT>(acc, a0, b);
+        load_b(b, kb + 4 * KB);
+        mma_block8<NT, MT>(acc, a1, b);
+    } else if (nb - i == 1) {
+        load_b(b, kb0 + i * 4 * KB);
+        mma_block8<NT, MT>(acc, a0, b);
     }
 
     const int cn = 4 * (lane >> 4), cm = lane & 15;
