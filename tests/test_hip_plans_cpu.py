@@ -1,0 +1,40 @@
+"""Host-side work lists and launch plans of the HIP ops (no GPU needed): the prefill-attention item list
+covers every query row of every sequence exactly once at each GQA ratio, heaviest blocks first, and the
+decode-attention split plan keeps its measured choices (ops/hip.py)."""
+import pytest
+
+from llm_map_reduce_summarizer_amd.ops import hip
+
+
+@pytest.mark.parametrize("group", [1, 2, 4, 8])
+def test_prefill_items_cover_every_row_once(group):
+    seqlens = [1, 63, 64, 65, 300, 4096]
+    bm = hip.prefill_block_m(group)
+    assert bm == 256 // group
+    items = hip.prefill_items(seqlens, group).tolist()
+    assert len(items) == sum(-(-n // bm) for n in seqlens)
+    seen = {s: [0] * n for s, n in enumerate(seqlens)}
+    for s, qb in items:
+        assert qb % bm == 0 and 0 <= qb < seqlens[s]
+        for r in range(qb, min(qb + bm, seqlens[s])):
+            seen[s][r] += 1
+    assert all(c == 1 for rows in seen.values() for c in rows)
+    starts = [qb for _, qb in items]
+    assert starts == sorted(starts, reverse=True)  # heaviest (latest) blocks first
+
+
+def test_prefill_block_m_rejects_other_ratios():
+    for g in (3, 16):
+        with pytest.raises(ValueError):
+            hip.prefill_block_m(g)
+
+
+def test_decode_attn_plan_measured_choices():
+    # a TP shard's single kv head at B=20, 4k context: 12 fused splits (profiles/r3_plans_insitu_tp8_b39_b20.jsonl)
+    assert hip.decode_attn_plan(20, 1, 4096) == (12, True)
+    # the same batch over 8 kv heads (TP=1) keeps at most 8 fused splits
+    s, fused = hip.decode_attn_plan(20, 8, 4096)
+    assert fused is False or s <= 8
+    # B=1 at TP=8 (one kv head, 4k): one workgroup per page, separate merge
+    s, fused = hip.decode_attn_plan(1, 1, 4096)
+    assert not fused and s == 64
