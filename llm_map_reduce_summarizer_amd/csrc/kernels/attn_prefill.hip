@@ -23,7 +23,7 @@
 //                   16-lane group hits 16 distinct slots), B = Q^T fragments
 //                   held in VGPRs for the whole loop.  The "swapped" product
 //                   puts one query row per lane (col = lane&31), so the row
-//                   max is 31 in-lane fmax + one xor-32 shuffle.
+//                   max is 31 in-lane fmax + one v_permlane32_swap.
 //   softmax         online, log2 domain; causal + length mask only on tiles that reach the
 //                   diagonal or the sequence end; one FMA + raw v_exp_f32 per score; the running
 //                   max (and the o/l rescale) only moves when it grows by > 2^8 (deferred rescale).
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
     const int seq = it.x, qblock = it.y;
     const int kvh = kv_major ? blockIdx.x / n_items : blockIdx.x % Hkv;
     const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5, r32 = lane & 31;
-    const int w = tid >> 6;  // (readfirstlane here made hipcc spill the staggered loop)
+    const int w = tid >> 6;
     const int h = kvh * G + w % G, rb = w / G;
     const int s0 = cu_seqlens[seq], len = cu_seqlens[seq + 1] - s0;
     const bf16* base = qkv + (size_t)s0 * row_stride;
