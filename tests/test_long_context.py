@@ -89,6 +89,47 @@ def test_attn_prefill_long_sequence():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("paged", [False, True])
+def test_attn_prefill_large_grid_kv_major(paged):
+    """A packed prefill whose grid exceeds 2048 blocks runs in kv-head-major block order (attn_prefill.hip):
+    3 x 6000 tokens at Llama-3-8B heads (2256 blocks), sampled rows of every sequence vs fp32; the paged
+    variant reads the same keys from a shuffled page cache."""
+    from llm_map_reduce_summarizer_amd import ops
+    from llm_map_reduce_summarizer_amd.ops import hip
+    dev = "cuda:0"
+    hq, hkv, d, L, nseq = 32, 8, 128, 6000, 3
+    assert nseq * -(-L // hip.prefill_block_m(hq // hkv)) * hkv > 2048
+    T = nseq * L
+    g = torch.Generator(device="cpu").manual_seed(7)
+    qkv = (torch.randn(T, (hq + 2 * hkv) * d, generator=g) * 0.5).to(torch.bfloat16).to(dev)
+    cu = torch.arange(0, T + 1, L, dtype=torch.int32, device=dev)
+    sc = 1.0 / math.sqrt(d)
+    pp = None
+    if paged:
+        npg = -(-L // 64)
+        kc = torch.zeros(nseq * npg + 1, hkv, 64, d, dtype=torch.bfloat16, device=dev)
+        vc = torch.zeros_like(kc)
+        perm = torch.randperm(nseq * npg, generator=g) + 1
+        bt = perm.view(nseq, npg).to(torch.int32).to(dev)
+        for s in range(nseq):
+            rows = qkv[s * L:(s + 1) * L]
+            kk = torch.zeros(npg * 64, hkv, d, dtype=torch.bfloat16, device=dev)
+            vv = torch.zeros_like(kk)
+            kk[:L] = rows[:, hq * d:(hq + hkv) * d].view(L, hkv, d)
+            vv[:L] = rows[:, (hq + hkv) * d:].view(L, hkv, d)
+            kc[bt[s].long()] = kk.view(npg, 64, hkv, d).transpose(1, 2)
+            vc[bt[s].long()] = vv.view(npg, 64, hkv, d).transpose(1, 2)
+        i32 = lambda x: torch.tensor(x, dtype=torch.int32, device=dev)  # noqa: E731
+        pp = ops.PagedPrefill(bt, i32(list(range(nseq))), i32([0] * nseq), list(range(nseq)), [0] * nseq, kc, vc)
+    out = hip.attn_prefill(qkv, cu, hq, hkv, d, sc, paged=pp)
+    for s in range(nseq):
+        rows = torch.tensor([0, 64, 2047, 4100, L - 1], device=dev)
+        ref = _ref_causal_rows(qkv[s * L:(s + 1) * L], rows, hq, hkv, d, sc)
+        err = (out[s * L + rows].float() - ref).abs()
+        assert err.max().item() < 3e-2, (s, err.max().item())
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("ctx", [65536, 100001])
 def test_attn_decode_long_context(ctx):
     """Decode attention over a 64k / 100k-token paged context with the engine's split plan vs fp32."""
