@@ -100,7 +100,7 @@ __device__ __forceinline__ void tile_of(int bid, int nwg, int tiles_m, int tiles
 }
 }  // namespace
 
-template <bool FP8, int EPI, int NS, bool LEPI>
+template <bool FP8, int EPI, int NS, bool LEPI, bool M32>
 __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
     // NS = half-tile slots of the LDS ring: half-tile h (K-tile h / 4, part h % 4) lives in slot h % NS.
     // NS = 8 (128 KiB, 2 K-tiles): staged LK = 6 ahead; NS = 10 (160 KiB): LK = 8 ahead.  A slot is
@@ -143,12 +143,20 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
         }
     };
 
-    // fragment reads: row (lane & 15) of a 16-row block, chunk (lane >> 4) (k-step 0) or 4 + (lane >> 4)
-    const int lo0 = (lane & 15) * 128 + (((lane >> 4) ^ ((lane >> 1) & 7)) << 4);
-    const int lo1 = (lane & 15) * 128 + (((4 + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4);
+    // fragment reads.  16x16 MFMA: row (lane & 15) of a 16-row block, chunk (lane >> 4) (k-step 0) or
+    // 4 + (lane >> 4).  32x32 MFMA (M32): row (lane & 31) of a 32-row block, read r = chunk 2 r + (lane >> 5);
+    // any k order shared by the A and B operands gives the same dot product, and each ds_read_b128 lane
+    // group still covers 16 distinct slots of a bank row (rows r, r + 1 share the swizzle, 8 slots apart).
+    int lo[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        lo[r] = M32 ? (lane & 31) * 128 + (((2 * r + (lane >> 5)) ^ ((lane >> 1) & 7)) << 4)
+                    : (lane & 15) * 128 + (((4 * (r & 1) + (lane >> 4)) ^ ((lane >> 1) & 7)) << 4);
     const int xbase = (64 * wr) * 128, wbase = (32 * wc) * 128;
 
+    // per quadrant: 16x16 -- [x block b 0..3][w block i 0..1] f32x4; 32x32 -- [x block b 0..1] f32x16
     f32x4 acc[2][4][2][2];
+    f32x16 acc32[2][2][2];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -156,8 +164,12 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
 #pragma unroll
             for (int j = 0; j < 2; ++j)
 #pragma unroll
-                for (int k = 0; k < 2; ++k) acc[i][b][j][k] = f32x4{0.f, 0.f, 0.f, 0.f};
-    u32x4 xf[4][2], wf0[2][2], wf1[2][2];
+                for (int k = 0; k < 2; ++k) {
+                    if constexpr (M32) { if (b < 2 && k == 0) acc32[i][b][j] = f32x16{}; }
+                    else acc[i][b][j][k] = f32x4{0.f, 0.f, 0.f, 0.f};
+                }
+    // xf[2 b + ks] (16x16) | xf[4 b + r] (32x32); wf[2 i + ks] | wf[r]
+    u32x4 xf[8], wf0[4], wf1[4];
 
     // prologue: half-tiles 0 .. LK-1 in flight, wait for the phase 0 reads (h <= 1 | h <= 2)
 #pragma unroll
@@ -167,41 +179,59 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
     bar();
     if (wr == 1) bar();  // stagger: waves 4-7 run one barrier (half a phase) behind waves 0-3
 
+    // 16x16: block b (16 rows) read ks at b * 2048 + lo[ks];  32x32: block b (32 rows) read r at b * 4096 + lo[r]
     auto read_x = [&](const char* base) {
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            xf[b][0] = *reinterpret_cast<const u32x4*>(base + xbase + b * 2048 + lo0);
-            xf[b][1] = *reinterpret_cast<const u32x4*>(base + xbase + b * 2048 + lo1);
-        }
+        for (int j = 0; j < 8; ++j)
+            xf[j] = *reinterpret_cast<const u32x4*>(base + xbase + (M32 ? (j >> 2) * 4096 + lo[j & 3]
+                                                                        : (j >> 1) * 2048 + lo[j & 1]));
     };
-    auto read_w = [&](const char* base, u32x4 (&wf)[2][2]) {
+    auto read_w = [&](const char* base, u32x4 (&wf)[4]) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            wf[i][0] = *reinterpret_cast<const u32x4*>(base + wbase + i * 2048 + lo0);
-            wf[i][1] = *reinterpret_cast<const u32x4*>(base + wbase + i * 2048 + lo1);
-        }
+        for (int j = 0; j < 4; ++j)
+            wf[j] = *reinterpret_cast<const u32x4*>(base + wbase + (M32 ? lo[j] : (j >> 1) * 2048 + lo[j & 1]));
     };
-    auto mfma_q = [&](int qm, int qn, const u32x4 (&wf)[2][2]) {
+    auto cat8 = [](const u32x4& p, const u32x4& q) -> i32x8 {
+        return i32x8{(int)p[0], (int)p[1], (int)p[2], (int)p[3], (int)q[0], (int)q[1], (int)q[2], (int)q[3]};
+    };
+    auto mfma_q = [&](int qm, int qn, const u32x4 (&wf)[4]) {
         __builtin_amdgcn_s_setprio(1);
+        if constexpr (M32) {
+            if constexpr (FP8) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+                for (int s = 0; s < 2; ++s)
 #pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                if constexpr (FP8) {
-                    const i32x8 av = {(int)wf[i][0][0], (int)wf[i][0][1], (int)wf[i][0][2], (int)wf[i][0][3],
-                                      (int)wf[i][1][0], (int)wf[i][1][1], (int)wf[i][1][2], (int)wf[i][1][3]};
-                    const i32x8 bv = {(int)xf[b][0][0], (int)xf[b][0][1], (int)xf[b][0][2], (int)xf[b][0][3],
-                                      (int)xf[b][1][0], (int)xf[b][1][1], (int)xf[b][1][2], (int)xf[b][1][3]};
-                    acc[qm][b][qn][i] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
-                        av, bv, acc[qm][b][qn][i], 0, 0, 0, 127, 0, 127);
-                } else {
+                    for (int b = 0; b < 2; ++b)
+                        acc32[qm][b][qn] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
+                            cat8(wf[2 * s], wf[2 * s + 1]), cat8(xf[4 * b + 2 * s], xf[4 * b + 2 * s + 1]),
+                            acc32[qm][b][qn], 0, 0, 0, 127, 0, 127);
+            } else {
 #pragma unroll
-                    for (int ks = 0; ks < 2; ++ks)
-                        acc[qm][b][qn][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                            __builtin_bit_cast(bf16x8, wf[i][ks]), __builtin_bit_cast(bf16x8, xf[b][ks]),
-                            acc[qm][b][qn][i], 0, 0, 0);
-                }
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int b = 0; b < 2; ++b)
+                        acc32[qm][b][qn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                            __builtin_bit_cast(bf16x8, wf[r]), __builtin_bit_cast(bf16x8, xf[4 * b + r]),
+                            acc32[qm][b][qn], 0, 0, 0);
             }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) {
+                    if constexpr (FP8) {
+                        acc[qm][b][qn][i] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+                            cat8(wf[2 * i], wf[2 * i + 1]), cat8(xf[2 * b], xf[2 * b + 1]), acc[qm][b][qn][i],
+                            0, 0, 0, 127, 0, 127);
+                    } else {
+#pragma unroll
+                        for (int ks = 0; ks < 2; ++ks)
+                            acc[qm][b][qn][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                                __builtin_bit_cast(bf16x8, wf[2 * i + ks]), __builtin_bit_cast(bf16x8, xf[2 * b + ks]),
+                                acc[qm][b][qn][i], 0, 0, 0);
+                    }
+                }
+        }
         __builtin_amdgcn_s_setprio(0);
     };
     // stage the half-tile LK ahead of phase P = 4 kt + p, then wait for what phase P + 1 reads.  In the
@@ -255,56 +285,96 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
     // (16-B unit u of row r at u ^ (r & 7): 2-way ds_write_b64, conflict-free ds_read_b128), then each
     // wave stores 32 whole rows with 16-B lanes (full-row segments instead of 32-B pieces per row).
     constexpr int RB = EPI == GEPI_SWIGLU ? 256 : 512;
-    const int g4 = lane >> 4;
+    // fp8: v *= activation row scale x weight row scales of tile columns c4 .. c4+3
+    auto scale4 = [&](f32x4& v, float rs, int c4) {
+        if constexpr (FP8) {
+            const float4 s4 = *reinterpret_cast<const float4*>(a.sw + min(n0 + c4, a.N - 4));
+            v[0] *= rs * s4.x; v[1] *= rs * s4.y; v[2] *= rs * s4.z; v[3] *= rs * s4.w;
+        }
+    };
+    auto silu_mul = [](const f32x4& g, const f32x4& u) {
+        f32x4 r;
 #pragma unroll
-    for (int qm = 0; qm < 2; ++qm)
+        for (int j = 0; j < 4; ++j) r[j] = g[j] / (1.f + __expf(-g[j])) * u[j];
+        return r;
+    };
+    // 4 bf16 outputs of tile row rl at byte cbyte of the output tile row; gcol = first weight column of
+    // the 16-column group they come from (N % 16 == 0, so the group is wholly in or out of range)
+    auto store4 = [&](int rl, int cbyte, const f32x4& v, int gcol) {
+        const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        if constexpr (LEPI) {
+            *reinterpret_cast<uint2*>(lds + rl * RB + (((cbyte >> 4) ^ (rl & 7)) << 4) + (cbyte & 15)) = pk;
+        } else if (m0 + rl < a.M && n0 + gcol < a.N) {
+            char* o = reinterpret_cast<char*>(a.c) + ((size_t)(m0 + rl) * a.ldc) * 2 +
+                      (EPI == GEPI_SWIGLU ? n0 : 2 * n0) + cbyte;
+            *reinterpret_cast<uint2*>(o) = pk;
+        }
+    };
+    if constexpr (M32) {
+        // lane holds C[m][n .. n+3] of every 32 x 32 block: m = .. + (lane & 31), register group gi covers
+        // n = .. + 8 gi + 4 (lane >> 5).  SwiGLU: groups 0 / 2 are gate, 1 / 3 the matching up columns.
+        const int h = lane >> 5;
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int rl = 128 * qm + 64 * wr + 16 * b + (lane & 15);  // row within the tile
-            const int m = m0 + rl;
-            float rs = 1.f;
-            if constexpr (FP8) rs = a.sx[min(m, a.M - 1)];
+        for (int qm = 0; qm < 2; ++qm)
 #pragma unroll
-            for (int qn = 0; qn < 2; ++qn)
+            for (int b = 0; b < 2; ++b) {
+                const int rl = 128 * qm + 64 * wr + 32 * b + (lane & 31);
+                float rs = 1.f;
+                if constexpr (FP8) rs = a.sx[min(m0 + rl, a.M - 1)];
 #pragma unroll
-                for (int i = 0; i < 2; ++i) {
-                    const int cb = 128 * qn + 32 * wc + 16 * i;  // 16-column block within the tile
-                    const int nb = n0 + cb;
-                    const int n = nb + 4 * g4;
-                    f32x4 v = acc[qm][b][qn][i];
-                    if constexpr (FP8) {
-                        const int nn = min(n, a.N - 4);
-                        const float4 s4 = *reinterpret_cast<const float4*>(a.sw + nn);
-                        v[0] *= rs * s4.x; v[1] *= rs * s4.y; v[2] *= rs * s4.z; v[3] *= rs * s4.w;
+                for (int qn = 0; qn < 2; ++qn) {
+                    const int cb = 128 * qn + 32 * wc;
+                    f32x4 v[4];
+#pragma unroll
+                    for (int gi = 0; gi < 4; ++gi) {
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) v[gi][t] = acc32[qm][b][qn][4 * gi + t];
+                        scale4(v[gi], rs, cb + 8 * gi + 4 * h);
                     }
-                    uint2 pk;
-                    int cbyte;  // byte offset of this lane's 4 outputs within the tile row
-                    bool have;
                     if constexpr (EPI == GEPI_SWIGLU) {
-                        f32x4 up;
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) up[j] = __shfl_xor(v[j], 32, 64);
-                        float r[4];
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) r[j] = v[j] / (1.f + __expf(-v[j])) * up[j];
-                        pk = make_uint2(pack2(r[0], r[1]), pack2(r[2], r[3]));
-                        cbyte = ((cb >> 1) + 4 * g4) * 2;
-                        have = g4 < 2;
+                        for (int gp = 0; gp < 2; ++gp) {
+                            const int gcol = cb + 16 * gp;
+                            store4(rl, ((gcol >> 1) + 4 * h) * 2, silu_mul(v[2 * gp], v[2 * gp + 1]), gcol);
+                        }
                     } else {
-                        pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-                        cbyte = (cb + 4 * g4) * 2;
-                        have = true;
-                    }
-                    if constexpr (LEPI) {
-                        if (have)
-                            *reinterpret_cast<uint2*>(lds + rl * RB + (((cbyte >> 4) ^ (rl & 7)) << 4) + (cbyte & 15)) = pk;
-                    } else if (have && m < a.M && nb < a.N) {
-                        char* o = reinterpret_cast<char*>(a.c) + ((size_t)m * a.ldc) * 2 +
-                                  (EPI == GEPI_SWIGLU ? n0 : 2 * n0) + cbyte;
-                        *reinterpret_cast<uint2*>(o) = pk;
+#pragma unroll
+                        for (int gi = 0; gi < 4; ++gi) {
+                            const int c4 = cb + 8 * gi + 4 * h;
+                            store4(rl, c4 * 2, v[gi], c4);
+                        }
                     }
                 }
-        }
+            }
+    } else {
+        // lane holds C[m][n .. n+3] of every 16 x 16 block, m = .. + (lane & 15), n = .. + 4 (lane >> 4).
+        // SwiGLU: the up columns 8-15 of a 16-column group sit in lane xor 32.
+        const int g4 = lane >> 4;
+#pragma unroll
+        for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int rl = 128 * qm + 64 * wr + 16 * b + (lane & 15);
+                float rs = 1.f;
+                if constexpr (FP8) rs = a.sx[min(m0 + rl, a.M - 1)];
+#pragma unroll
+                for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const int cb = 128 * qn + 32 * wc + 16 * i;  // 16-column block within the tile
+                        f32x4 v = acc[qm][b][qn][i];
+                        scale4(v, rs, cb + 4 * g4);
+                        if constexpr (EPI == GEPI_SWIGLU) {
+                            f32x4 up;
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) up[j] = __shfl_xor(v[j], 32, 64);
+                            if (g4 < 2) store4(rl, ((cb >> 1) + 4 * g4) * 2, silu_mul(v, up), cb);
+                        } else {
+                            store4(rl, (cb + 4 * g4) * 2, v, cb);
+                        }
+                    }
+            }
+    }
     if constexpr (LEPI) {
         __syncthreads();
         constexpr int UPR = RB / 16, RPI = 1024 / RB;
@@ -336,6 +406,11 @@ MRSUM_API int mrsum_gemm(const void* x, int ldx, const void* w, int ldw, void* c
     a.ldx_b = ldx * es; a.ldw_b = ldw * es; a.ldc = ldc;
     a.M = M; a.N = N; a.kb = K * es / 128;
     a.tiles_m = ceil_div(M, 256); a.tiles_n = ceil_div(N, 256);
+    // group_m bits 0-7: tile rows per raster group (0 = 4); bit 8: 32x32 MFMA tiles instead of 16x16.
+    // Measured (profiles/r3_gemm_mfma32_experiment.jsonl, same box, interleaved): 32x32 is 0-9 % slower on
+    // the 8B bf16 projections and -1.4..+2.7 % on the 70B fp8 ones, so 16x16 stays the default.
+    const bool m32 = (group_m >> 8) & 1;
+    group_m &= 255;
     a.group_m = group_m > 0 ? group_m : 4;
     const dim3 grid(a.tiles_m * a.tiles_n), block(512);
     // measured (profiles/r2_gemm_variants_ab.jsonl, r2_gemm_ring10_ab.jsonl): the staggered 8-slot ring
@@ -344,8 +419,13 @@ MRSUM_API int mrsum_gemm(const void* x, int ldx, const void* w, int ldw, void* c
     // aligned (strided views).
     const bool lepi = ldc % 8 == 0 && (uintptr_t)c % 16 == 0;
 #define GEMM_LAUNCH(F, E)                                                          \
-    if (lepi) gemm_kernel<F, E, 8, true><<<grid, block, 0, s>>>(a);               \
-    else gemm_kernel<F, E, 8, false><<<grid, block, 0, s>>>(a);
+    if (m32) {                                                                     \
+        if (lepi) gemm_kernel<F, E, 8, true, true><<<grid, block, 0, s>>>(a);      \
+        else gemm_kernel<F, E, 8, false, true><<<grid, block, 0, s>>>(a);          \
+    } else {                                                                       \
+        if (lepi) gemm_kernel<F, E, 8, true, false><<<grid, block, 0, s>>>(a);     \
+        else gemm_kernel<F, E, 8, false, false><<<grid, block, 0, s>>>(a);         \
+    }
     if (fp8) {
         if (epi == GEPI_SWIGLU) { GEMM_LAUNCH(true, GEPI_SWIGLU) } else { GEMM_LAUNCH(true, GEPI_BF16) }
     } else {

@@ -100,6 +100,33 @@ def test_gemm_fp8(M, N, K, swiglu):
     _check(out, ref, tol=3e-2)
 
 
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("swiglu", [False, True])
+@pytest.mark.parametrize("aligned", [True, False])
+def test_gemm_mfma32_variant(fp8, swiglu, aligned):
+    """The 32x32-MFMA tile variant (group_m bit 8; measured slower for bf16, not the default --
+    profiles/r3_gemm_mfma32_experiment.jsonl) against fp32, ragged M and an N % 32 == 16 tail."""
+    M, N, K = 777, 1040 if not swiglu else 1056, 1024
+    x = _rand(M, K, seed=10, scale=0.5, offset=0.02)
+    wb = _rand(N, K, seed=11, scale=0.03, offset=0.001)
+    n_out = N // 2 if swiglu else N
+    big = torch.zeros(M, n_out + 8, dtype=torch.bfloat16, device=DEV)
+    out = big[:, :n_out] if aligned else big[:, 4:4 + n_out]
+    if fp8:
+        w = Fp8Weight.quantize(wb)
+        xq, xs = hip.quant_fp8_rows(x)
+        hip.gemm_fp8(xq, xs, w, out=out, swiglu=swiglu, group_m=4 | 256)
+        y = (xq.float() * xs[:, None]) @ w.dequant().t()
+    else:
+        hip.gemm(x, wb, out=out, swiglu=swiglu, group_m=4 | 256)
+        y = x.float() @ wb.float().t()
+    torch.cuda.synchronize()
+    if swiglu:
+        g = y.reshape(M, -1, 2, 8)
+        y = (torch.nn.functional.silu(g[:, :, 0]) * g[:, :, 1]).reshape(M, -1)
+    _check(out, y, tol=3e-2)
+
+
 def test_gemm_graph_capture():
     x, w = _rand(512, 1024, seed=10), _rand(768, 1024, seed=11, scale=0.05)
     out = torch.empty(512, 768, dtype=torch.bfloat16, device=DEV)
