@@ -157,8 +157,11 @@ def main() -> int:
     t0 = time.perf_counter()
     reports = []
     with maybe_profile(args.profile, rank):
-        for _ in range(args.steps):
+        for i in range(args.steps):
+            ts = time.perf_counter()
             reports.append(one())
+            if rank == 0:  # progress on stderr (a 20-step run is minutes long); stdout keeps the one JSON line
+                print("step %d: %.2f s" % (i, time.perf_counter() - ts), file=sys.stderr, flush=True)
     pdist.barrier()
     if torch.cuda.is_available():
         torch.cuda.synchronize()
