@@ -35,6 +35,9 @@
 //   * the MFMA computes the transposed tile (A = W fragment, B = X fragment) so each lane ends with 4
 //     consecutive output columns of one row: 8-byte bf16 stores, and the fused SwiGLU epilogue of the
 //     [8 gate | 8 up]-interleaved gate_up weight is a lane-xor-32 exchange.
+//   * M32 variant: the same ring, phases and quadrants on 32x32 MFMA tiles (v_mfma_f32_32x32x16_bf16 /
+//     v_mfma_scale_f32_32x32x64_f8f6f4); a lane then holds 4 register groups of 4 consecutive columns,
+//     and the SwiGLU gate / up halves of a 16-column group sit in adjacent groups of the same lane.
 #include "common.h"
 
 #include <type_traits>
@@ -408,7 +411,8 @@ MRSUM_API int mrsum_gemm(const void* x, int ldx, const void* w, int ldw, void* c
     a.tiles_m = ceil_div(M, 256); a.tiles_n = ceil_div(N, 256);
     // group_m bits 0-7: tile rows per raster group (0 = 4); bit 8: 32x32 MFMA tiles instead of 16x16.
     // Measured (profiles/r3_gemm_mfma32_experiment.jsonl, same box, interleaved): 32x32 is 0-9 % slower on
-    // the 8B bf16 projections and -1.4..+2.7 % on the 70B fp8 ones, so 16x16 stays the default.
+    // the 8B bf16 projections and about equal on the 70B fp8 qkv / o / down, so 16x16 stays the default;
+    // the fp8 gate_up + SwiGLU GEMM gains 1.7-3.8 % at M = 4k-32k and takes it (ops/hip.py gemm_fp8).
     const bool m32 = (group_m >> 8) & 1;
     group_m &= 255;
     a.group_m = group_m > 0 ? group_m : 4;

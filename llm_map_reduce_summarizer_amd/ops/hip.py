@@ -525,6 +525,10 @@ def sample_tp(logits: torch.Tensor, st, tok_offset: int, max_reduce) -> None:
 # ------------------------------------------------------------------ large-M GEMM (prefill, M > 64)
 GEMM_GROUP_M = 4  # tile rows per raster group (4 x 8 tiles per XCD at a time; 8 measured equal)
 GEMM_EPI_BF16, GEMM_EPI_SWIGLU = 0, 1
+# group_m bit 8: 32x32-MFMA tiles.  Taken by the fp8 gate_up + SwiGLU GEMM only: +1.7..3.8 % at M = 4k-32k on
+# the 70B shape on two boxes; the 70B fp8 qkv / o / down and every bf16 projection are equal or slower
+# (profiles/r3_gemm_mfma32_experiment.jsonl, r3_gemm_mfma32_fp8_70b.jsonl)
+GEMM_MFMA32 = 256
 
 
 def _gemm(xp, ldx, wp, ldw, out, M, N, K, fp8, epi, sx, sw, group_m):
@@ -560,7 +564,7 @@ def gemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, s
 def gemm_fp8(xq: torch.Tensor, xs: torch.Tensor, w, out: Optional[torch.Tensor] = None, swiglu: bool = False,
              group_m: Optional[int] = None) -> torch.Tensor:
     """(xs[:, None] * xq) @ (w.scale[:, None] * w.q)^T on the fp8 MFMA path of the same kernel
-    (v_mfma_scale_f32_16x16x128_f8f6f4, OCP e4m3fn operands), bf16 out."""
+    (v_mfma_scale_f32_16x16x128_f8f6f4, OCP e4m3fn operands; the SwiGLU form on the 32x32x64 tiles), bf16 out."""
     _req(xq.is_cuda and xq.dtype == torch.float8_e4m3fn and xq.dim() == 2 and xq.stride(1) == 1
          and xq.stride(0) % 16 == 0 and xq.data_ptr() % 16 == 0, "gemm_fp8: x must be e4m3fn rows, 16-B aligned")
     M, K = xq.shape
@@ -578,6 +582,8 @@ def gemm_fp8(xq: torch.Tensor, xs: torch.Tensor, w, out: Optional[torch.Tensor] 
     _req(out.shape == (M, n_out), "gemm_fp8: bad out shape")
     if M == 0:
         return out
+    if group_m is None and swiglu:
+        group_m = GEMM_GROUP_M | GEMM_MFMA32
     return _gemm(_p(xq), xq.stride(0), _p(q), K, out, M, N, K, 1, GEMM_EPI_SWIGLU if swiglu else GEMM_EPI_BF16,
                  _p(xs), _p(sc), group_m)
 

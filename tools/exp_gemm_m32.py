@@ -86,8 +86,10 @@ def timeit(fn, iters):
     return ev[0].elapsed_time(ev[1]) * 1000.0 / iters
 
 
-def ab(dev, model, ms, fp8, rounds=5, iters=10):
+def ab(dev, model, ms, fp8, rounds=5, iters=10, roles=None):
     for role, (N, K) in SHAPES[model].items():
+        if roles and role not in roles:
+            continue
         w = (torch.randn(N, K, device=dev) * 0.02).to(torch.bfloat16)
         wq = Fp8Weight.quantize(w) if fp8 else None
         swiglu = role == "gate_up"
@@ -122,14 +124,20 @@ def main():
     ap.add_argument("--ms", default="4096,16384")
     ap.add_argument("--fp8-model", default="llama3-70b")
     ap.add_argument("--fp8-ms", default="8192")
+    ap.add_argument("--fp8-roles", default="", help="comma list (default: all four)")
+    ap.add_argument("--skip-check", action="store_true")
+    ap.add_argument("--skip-bf16", action="store_true")
+    ap.add_argument("--rounds", type=int, default=5)
     a = ap.parse_args()
     dev = "cuda:0"
-    if not check(dev):
+    if not a.skip_check and not check(dev):
         print(json.dumps({"check": "FAILED"}), flush=True)
         sys.exit(1)
-    ab(dev, "llama3-8b", [int(m) for m in a.ms.split(",")], False)
+    if not a.skip_bf16:
+        ab(dev, "llama3-8b", [int(m) for m in a.ms.split(",")], False, a.rounds)
     if a.fp8_model:
-        ab(dev, a.fp8_model, [int(m) for m in a.fp8_ms.split(",")], True)
+        ab(dev, a.fp8_model, [int(m) for m in a.fp8_ms.split(",")], True, a.rounds,
+           roles=[r for r in a.fp8_roles.split(",") if r])
 
 
 if __name__ == "__main__":
