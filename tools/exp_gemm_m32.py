@@ -127,6 +127,7 @@ def main():
     ap.add_argument("--fp8-roles", default="", help="comma list (default: all four)")
     ap.add_argument("--skip-check", action="store_true")
     ap.add_argument("--skip-bf16", action="store_true")
+    ap.add_argument("--bf16-roles", default="", help="comma list (default: all four)")
     ap.add_argument("--rounds", type=int, default=5)
     a = ap.parse_args()
     dev = "cuda:0"
@@ -134,7 +135,8 @@ def main():
         print(json.dumps({"check": "FAILED"}), flush=True)
         sys.exit(1)
     if not a.skip_bf16:
-        ab(dev, "llama3-8b", [int(m) for m in a.ms.split(",")], False, a.rounds)
+        ab(dev, "llama3-8b", [int(m) for m in a.ms.split(",")], False, a.rounds,
+           roles=[r for r in a.bf16_roles.split(",") if r])
     if a.fp8_model:
         ab(dev, a.fp8_model, [int(m) for m in a.fp8_ms.split(",")], True, a.rounds,
            roles=[r for r in a.fp8_roles.split(",") if r])
