@@ -21,6 +21,7 @@ from llm_map_reduce_summarizer_amd.ops import hip  # noqa: E402
 from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight  # noqa: E402
 
 M32 = 256
+VARIANTS = [("m16g4", 4), ("m32g4", 4 | M32)]
 SHAPES = {
     "llama3-8b": {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)},
     "llama3-70b": {"qkv": (10240, 8192), "o": (8192, 8192), "gate_up": (57344, 8192), "down": (8192, 28672)},
@@ -51,14 +52,14 @@ def check(dev):
                     out = buf[:, 4:]
                 else:
                     out = torch.empty(M, n_out, dtype=torch.bfloat16, device=dev)
-                for gm in (4, 4 | M32):
+                for gm in [g for _, g in VARIANTS]:
                     out.fill_(float("nan"))
                     hip.gemm(x, w, out=out, swiglu=swiglu, group_m=gm)
                     err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
                     good = err < 1e-2
                     ok &= good
                     print(json.dumps({"check": "bf16", "M": M, "N": N, "K": K, "swiglu": swiglu, "strided": strided,
-                                      "m32": gm >= M32, "rel_err": round(err, 5), "ok": good}), flush=True)
+                                      "group_m": gm, "rel_err": round(err, 5), "ok": good}), flush=True)
         wq = Fp8Weight.quantize(w)
         xq, xs = hip.quant_fp8_rows(x)
         deq = (xq.float() * xs.view(-1, 1)) @ (wq.q.float() * wq.scale.view(-1, 1)).t()
@@ -71,7 +72,7 @@ def check(dev):
                 err = ((out.float() - ref).abs().max() / ref.abs().max()).item()
                 good = err < 1e-2
                 ok &= good
-                print(json.dumps({"check": "fp8", "M": M, "N": N, "K": K, "swiglu": swiglu, "m32": gm >= M32,
+                print(json.dumps({"check": "fp8", "M": M, "N": N, "K": K, "swiglu": swiglu, "group_m": gm,
                                   "rel_err": round(err, 5), "ok": good}), flush=True)
     return ok
 
@@ -98,7 +99,7 @@ def ab(dev, model, ms, fp8, rounds=5, iters=10, roles=None):
             out = torch.empty(M, N // 2 if swiglu else N, dtype=torch.bfloat16, device=dev)
             xq, xs = hip.quant_fp8_rows(x) if fp8 else (None, None)
             fns = {}
-            for name, gm in (("m16g4", 4), ("m32g4", 4 | M32)):
+            for name, gm in VARIANTS:
                 if fp8:
                     fns[name] = (lambda gm=gm: hip.gemm_fp8(xq, xs, wq, out=out, swiglu=swiglu, group_m=gm))
                 else:
@@ -129,7 +130,9 @@ def main():
     ap.add_argument("--skip-bf16", action="store_true")
     ap.add_argument("--bf16-roles", default="", help="comma list (default: all four)")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--variants", default="m16g4=4,m32g4=260", help="name=group_m list (bit 8: 32x32 tiles)")
     a = ap.parse_args()
+    VARIANTS[:] = [(v.split("=")[0], int(v.split("=")[1])) for v in a.variants.split(",")]
     dev = "cuda:0"
     if not a.skip_check and not check(dev):
         print(json.dumps({"check": "FAILED"}), flush=True)
