@@ -154,6 +154,7 @@ def main() -> int:
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     from llm_map_reduce_summarizer_amd.utils.profiling import maybe_profile
+    work0 = dict(provider.work)
     t0 = time.perf_counter()
     reports = []
     with maybe_profile(args.profile, rank):
@@ -173,6 +174,10 @@ def main() -> int:
         ranks_seen, backend = tdist.get_world_size(), tdist.get_backend()
     else:
         ranks_seen, backend = 1, "none"
+    # the timed work must be the pinned work: every generation of every timed step produced exactly its
+    # max_new_tokens and none failed (the provider counts from the all-gathered results, same on every rank)
+    work = {k: provider.work[k] - work0[k] for k in work0}
+    work_ok = work["errors"] == 0 and (args.stop_at_eos or work["completion_tokens"] == work["requested_tokens"])
     rep = reports[-1]
     ms = elapsed / max(1, args.steps) * 1000.0
     n_chunks = rep["chunks"]
@@ -209,11 +214,16 @@ def main() -> int:
         "map_chunks_per_s": round(rep["chunks_per_second"] or 0.0, 3),
         "reduce_plan": rep.get("reduce_plan"),
         "tokens_used": rep.get("tokens_used"),
+        "timed_work": dict(work, pinned_ok=work_ok),
         "engine_rank0": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in eng.items()},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
     pdist.shutdown()
+    if not work_ok:
+        print("bench: timed work is not the pinned work: %d of %d requested tokens generated, %d failed requests"
+              % (work["completion_tokens"], work["requested_tokens"], work["errors"]), file=sys.stderr)
+        return 3
     return 0
 
 

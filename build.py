@@ -6,8 +6,13 @@
   CUDA paths) and linked into one shared object.
 * ``_native/libmrsum_runtime.so``: ``csrc/runtime/*.cpp`` host runtime (g++).
 
-Objects are rebuilt only when their source (or a header in the same
-directory) is newer.  Usage: ``python build.py [--force] [-j N]``.
+Objects are rebuilt when the content hash of their source, the headers of
+its directory and the flags differs from the one recorded next to the object
+(not by mtime: a snapshot copied to another machine keeps no useful mtimes).
+Each library gets a ``<lib>.stamp.json`` (``llm_map_reduce_summarizer_amd/
+_stamp.py``): sha256 over its sources + flags, checked by ``ops/_lib.py`` at
+load time, which refuses a library built from other sources.
+Usage: ``python build.py [--force] [-j N]``.
 """
 
 from __future__ import annotations
@@ -21,25 +26,34 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+from llm_map_reduce_summarizer_amd import _stamp  # noqa: E402  (stdlib only)
+
 PKG = os.path.join(ROOT, "llm_map_reduce_summarizer_amd")
-CSRC = os.path.join(PKG, "csrc")
-NATIVE = os.path.join(PKG, "_native")
+CSRC = _stamp.CSRC
+NATIVE = _stamp.NATIVE
 OBJ = os.path.join(ROOT, "build", "obj")
 
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CXX = os.environ.get("CXX", "g++")
-ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
-HIP_FLAGS = ["--offload-arch=%s" % ARCH, "-O3", "-std=c++17", "-fPIC", "-ffp-contract=fast",
-             "-mcode-object-version=5", "-Wno-unused-result", "-munsafe-fp-atomics",
-             "-Rpass-analysis=kernel-resource-usage"]
-CXX_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-sign-compare"]
+ARCH = _stamp.ARCH
+HIP_FLAGS = _stamp.HIP_FLAGS
+CXX_FLAGS = _stamp.CXX_FLAGS
 
 
-def _newer(src: str, dst: str, deps) -> bool:
-    if not os.path.exists(dst):
+def _stale(src: str, dst: str, deps, flags) -> bool:
+    """Whether object ``dst`` must be rebuilt: missing, or built from other source/header/flag content."""
+    key = _stamp.digest([src] + list(deps), flags)
+    try:
+        with open(dst + ".sha") as f:
+            return not os.path.exists(dst) or f.read().strip() != key
+    except OSError:
         return True
-    t = os.path.getmtime(dst)
-    return any(os.path.getmtime(p) > t for p in [src] + list(deps))
+
+
+def _mark(src: str, dst: str, deps, flags) -> None:
+    with open(dst + ".sha", "w") as f:
+        f.write(_stamp.digest([src] + list(deps), flags))
 
 
 def _run(cmd):
@@ -65,9 +79,10 @@ def _check_resources(src: str, remarks: str) -> None:
         raise RuntimeError("scratch (private memory) in %s:\n  %s" % (os.path.basename(src), "\n  ".join(bad)))
 
 
-def _compile_hip(cmd_src):
-    cmd, src = cmd_src
+def _compile_hip(job):
+    cmd, src, obj, deps = job
     _check_resources(src, _run(cmd))
+    _mark(src, obj, deps, HIP_FLAGS)
 
 
 def build_kernels(force: bool = False, jobs: int = 8) -> str:
@@ -80,26 +95,37 @@ def build_kernels(force: bool = False, jobs: int = 8) -> str:
     for s in srcs:
         o = os.path.join(OBJ, os.path.basename(s) + ".o")
         objs.append(o)
-        if force or _newer(s, o, hdrs):
-            todo.append(([HIPCC] + HIP_FLAGS + ["-I", os.path.join(CSRC, "kernels"), "-c", s, "-o", o], s))
+        if force or _stale(s, o, hdrs, HIP_FLAGS):
+            todo.append(([HIPCC] + HIP_FLAGS + ["-I", os.path.join(CSRC, "kernels"), "-c", s, "-o", o], s, o, hdrs))
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         list(ex.map(_compile_hip, todo))
     out = os.path.join(NATIVE, "libmrsum_kernels.so")
-    if force or todo or not os.path.exists(out):
+    if force or todo or not os.path.exists(out) or _stamp.check("kernels"):
         tmp = out + ".tmp"
         _run([HIPCC, "--offload-arch=%s" % ARCH, "-shared", "-fPIC", "-o", tmp] + objs)
         os.replace(tmp, out)
+        _stamp.write_stamp("kernels", {"compiler": _tool_version(HIPCC)})
     return out
+
+
+def _tool_version(tool: str) -> str:
+    try:
+        r = subprocess.run([tool, "--version"], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                           timeout=60)
+        return " | ".join(ln.strip() for ln in r.stdout.splitlines()[:2])
+    except Exception:  # noqa: BLE001 -- informational only
+        return "unknown"
 
 
 def build_runtime(force: bool = False) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "runtime", "*.cpp")))
     os.makedirs(NATIVE, exist_ok=True)
     out = os.path.join(NATIVE, "libmrsum_runtime.so")
-    if force or any(_newer(s, out, []) for s in srcs):
+    if force or not os.path.exists(out) or _stamp.check("runtime"):
         tmp = out + ".tmp"
         _run([CXX] + CXX_FLAGS + ["-shared", "-o", tmp] + srcs + ["-lpthread"])
         os.replace(tmp, out)
+        _stamp.write_stamp("runtime", {"compiler": _tool_version(CXX)})
     return out
 
 

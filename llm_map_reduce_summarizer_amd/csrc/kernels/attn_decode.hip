@@ -206,6 +206,10 @@ __global__ __launch_bounds__(256) void attn_decode_combine_kernel(const float* _
 // Softmax is per head column: 4 in-lane values + two xor shuffles per 16 keys.  No q.k lane
 // reductions, no per-key VALU dot products -- the VALU only does the online softmax.
 // Heads G <= 16 (columns >= G are computed on zero q and never stored).
+// GQA ratios other than 1/2/4/8/16 (e.g. Llama-3.2-3B: 24 / 8 = 3) run the G = 1 instantiation over
+// Hkv = Hq "virtual kv heads" (grid.y), one per query head, each streaming the pages of its cache kv head
+// kvr = kvh / gq of Hc (gq = Hq / Hc); for them the split holding the new token writes the same K/V row
+// from each of the gq virtual heads (identical bytes; every reader patches that row from LDS anyway).
 namespace {
 typedef short s4v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s4v lds_s4v;
@@ -228,13 +232,14 @@ struct RopeArgs {
     const float2* cos_sin;  // [max_pos, D/2]
 };
 
-// The fp32 slab sums the ROPE variant needs, by all 256 threads: q of the G heads of kv head ``kvh``
-// (G D floats) and, with ``with_kv``, the new token's K and V rows (D floats each), into ``sq``.
+// The fp32 slab sums the ROPE variant needs, by all 256 threads: q of the G heads of head group ``kvh``
+// (G D floats) and, with ``with_kv``, the new token's K and V rows of cache kv head ``kvr`` (of ``Hc``;
+// kvr = kvh except for the per-query-head fallback of other GQA ratios) (D floats each), into ``sq``.
 // Work items = float4 columns x slab subsets (NH subsets when there are fewer than 256 columns), so
 // every thread has its loads in flight at once; the subsets are merged through LDS.
 template <int G>
-__device__ __forceinline__ void rope_slab_sums(const RopeArgs& ra, const float* prow, int kvh, int Hkv, bool with_kv,
-                                               float* sq) {
+__device__ __forceinline__ void rope_slab_sums(const RopeArgs& ra, const float* prow, int kvh, int kvr, int Hc,
+                                               bool with_kv, float* sq) {
     constexpr int D = 128;
     const int tid = threadIdx.x;
     const int nq = G * D / 4;                    // q float4 columns
@@ -245,8 +250,8 @@ __device__ __forceinline__ void rope_slab_sums(const RopeArgs& ra, const float* 
         const int item = it % nv, h = it / nv;
         int colf;
         if (item < nq) colf = kvh * G * D + 4 * item;
-        else if (item < nq + D / 4) colf = (ra.hq_total + kvh) * D + 4 * (item - nq);
-        else colf = (ra.hq_total + Hkv + kvh) * D + 4 * (item - nq - D / 4);
+        else if (item < nq + D / 4) colf = (ra.hq_total + kvr) * D + 4 * (item - nq);
+        else colf = (ra.hq_total + Hc + kvr) * D + 4 * (item - nq - D / 4);
         const float* src = prow + colf;
         float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 8
@@ -281,7 +286,7 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     const bf16* __restrict__ q, int q_stride, bf16* __restrict__ kc, bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ positions,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int S, float scale_log2, RopeArgs ra,
-    int* __restrict__ counters, bf16* __restrict__ out, int out_stride) {
+    int* __restrict__ counters, bf16* __restrict__ out, int out_stride, int Hc_rt, int gq) {
     constexpr int D = 128, PG = 64;
     __shared__ __attribute__((aligned(16))) char lds[2 * PG * 256 + 2 * 4 * 16 * 4];
     __shared__ __attribute__((aligned(16))) bf16 lds_new[2 * D];  // ROPE: the new token's K | V row (bf16)
@@ -295,6 +300,9 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
 
     const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
     const int Hq = Hkv * G;
+    // cache kv head / cache kv heads (the per-query-head fallback exists only as G = 1)
+    const int kvr = G == 1 ? kvh / gq : kvh;
+    const int Hc = G == 1 ? Hc_rt : Hkv;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 15, grp = lane >> 4;
     const int ctx = positions[b] + 1;
     int chunk = (ctx + S - 1) / S;
@@ -320,7 +328,7 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     const float2* cs = ROPE ? ra.cos_sin + (size_t)(ctx - 1) * (D / 2) : nullptr;
     const int* bt = block_tables + (size_t)b * bt_stride + ks / PG;
     const int st_row = tid >> 4, st_chunk = tid & 15;
-    const size_t head_off = (size_t)kvh * PG * D + (size_t)st_row * D + st_chunk * 8;
+    const size_t head_off = (size_t)kvr * PG * D + (size_t)st_row * D + st_chunk * 8;
     // staging registers are plain named arrays indexed only by unrolled constants (a lambda
     // capturing them by reference put them in scratch), and the prefetch is unconditional (no
     // branch around the loads) so hipcc keeps them in flight.
@@ -334,7 +342,7 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
 #define KV_ISSUE(KR, VR, TILE)                                                          \
     {                                                                                   \
         const int pg_ = bt[min((TILE), ntiles - 1)];                                    \
-        const size_t base_ = (size_t)((TILE) < ntiles ? pg_ : 0) * Hkv * PG * D + head_off; \
+        const size_t base_ = (size_t)((TILE) < ntiles ? pg_ : 0) * Hc * PG * D + head_off;  \
         _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                 \
             KR[i] = ld_kv<NT>(kc + base_ + (size_t)16 * i * D);                         \
             VR[i] = ld_kv<NT>(vc + base_ + (size_t)16 * i * D);                         \
@@ -351,14 +359,14 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     const bool has_pos = ROPE && ks <= ctx - 1 && ctx - 1 < ke;
     if constexpr (ROPE) {
         if (has_pos) {
-            rope_slab_sums<G>(ra, prow, kvh, Hkv, true, sq);
+            rope_slab_sums<G>(ra, prow, kvh, kvr, Hc, true, sq);
             // the new token's K (rotated) and V row of this kv head -> paged cache for the next steps;
             // THIS launch never reads it back from memory (no store drain on the critical path): the
             // staging of the page that holds it patches the row into LDS from the fp32 image
             // (lds_new); only this split reads that page in this launch
             const int pos = ctx - 1;
             const int page = block_tables[(size_t)b * bt_stride + pos / PG];
-            const size_t dst = ((size_t)page * Hkv * PG + (size_t)kvh * PG + (pos % PG)) * D;
+            const size_t dst = ((size_t)page * Hc * PG + (size_t)kvr * PG + (pos % PG)) * D;
             const float* kr = sq + G * D;
             if (tid < D / 8) {  // rotated K chunk tid (8 dims), into the cache and the LDS patch row
                 const int c = tid * 8, cl = c & (D / 2 - 1);
@@ -387,7 +395,7 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     if constexpr (ROPE) {
         // dims 32k + 8grp + j (k = 0, 1) pair with dims 64 + the same (k = 2, 3): the rotation of a
         // lane's q values needs only the lane's own values
-        if (!has_pos) rope_slab_sums<G>(ra, prow, kvh, Hkv, false, sq);  // overlaps the first page's loads
+        if (!has_pos) rope_slab_sums<G>(ra, prow, kvh, kvr, Hc, false, sq);  // overlaps the first page's loads
         float a[4][8];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -535,12 +543,25 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
 // (profiles/r1_decode_nt_ab.jsonl)
 constexpr int NT_MIN_GROUPS = 64;
 
+static bool decode_packed(int G) { return G == 1 || G == 2 || G == 4 || G == 8 || G == 16; }
+
+// Head groups (grid.y) the decode attention runs for Hq query / Hkv kv heads: Hkv for the packed GQA ratios,
+// Hq (one per query head) for the fallback -- the split workspace and merge tickets are sized by it.
+MRSUM_API int mrsum_attn_decode_groups(int Hq, int Hkv) {
+    if (Hkv <= 0 || Hq % Hkv || Hq / Hkv > 64) return -1;
+    return decode_packed(Hq / Hkv) ? Hkv : Hq;
+}
+
 static int launch_mfma(const void* q, int q_stride, const void* kcache, const void* vcache, const int* block_tables,
                        int bt_stride, const int* positions, void* part_o, void* part_ml, void* out, int out_stride,
                        int B, int Hq, int Hkv, int D, int P, int S, float scale, const RopeArgs* rope, int* counters,
                        hipStream_t s) {
     if (B <= 0) return 0;
-    if (D != 128 || P != 64 || Hq % Hkv || Hq / Hkv > 16 || S < 1 || S > MAX_SPLITS) return (int)hipErrorInvalidValue;
+    if (D != 128 || P != 64 || Hkv <= 0 || Hq % Hkv || Hq / Hkv > 64 || S < 1 || S > MAX_SPLITS)
+        return (int)hipErrorInvalidValue;
+    const int Hc = Hkv;                          // kv heads of the cache
+    const int gq = decode_packed(Hq / Hc) ? 1 : Hq / Hc;
+    Hkv = Hq / (decode_packed(Hq / Hc) ? Hq / Hc : 1);  // head groups of the grid (virtual kv heads)
     const int G = Hq / Hkv;
     const float sl = scale * 1.4426950408889634f;
     dim3 grid(S, Hkv, B), block(256);
@@ -552,11 +573,11 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
         if (B * Hkv >= NT_MIN_GROUPS)                                                                       \
             attn_decode_mfma_kernel<G_, R_, true><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, \
                                                                          positions, PO, PM, Hkv, S, sl, ra, counters, \
-                                                                         (bf16*)out, out_stride);             \
+                                                                         (bf16*)out, out_stride, Hc, gq);     \
         else                                                                                                  \
             attn_decode_mfma_kernel<G_, R_, false><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, \
                                                                           positions, PO, PM, Hkv, S, sl, ra, counters, \
-                                                                          (bf16*)out, out_stride);            \
+                                                                          (bf16*)out, out_stride, Hc, gq);    \
     } while (0)
 #define MFMA_G(R_)                            \
     switch (G) {                              \

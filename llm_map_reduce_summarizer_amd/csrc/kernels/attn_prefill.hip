@@ -87,12 +87,16 @@ struct PagedKV {
 // G = query heads per kv head served by one workgroup: wave w runs query head kvh*G + w%G over query rows
 // [qblock + 32(w/G), +32), so one workgroup covers 256/G query positions of ALL G heads of its kv head and
 // every staged K/V tile feeds 8 x 32 query rows whatever the GQA ratio.
+// Other GQA ratios (e.g. Llama-3.2-3B: 24 / 8 = 3) run the G = 1 instantiation over Hg = Hq "virtual kv
+// heads", one per query head, each reading the K/V columns of its real kv head h / gq (gq = Hq / Hkv):
+// no K/V reuse across the group inside a workgroup, but any ratio works.  Hg = Hkv and gq = 1 otherwise.
 template <bool PAGED, int G>
 __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __restrict__ qkv, int row_stride,
                                                               const int* __restrict__ cu_seqlens,
                                                               const int2* __restrict__ items,
                                                               bf16* __restrict__ out, int out_stride, int Hq,
-                                                              int Hkv, float scale_log2, PagedKV pk, int kv_major) {
+                                                              int Hkv, int Hg, int gq, float scale_log2, PagedKV pk,
+                                                              int kv_major) {
     constexpr int BMP = 32 * (NW / G);  // query positions per workgroup
     // two-stage ring of [K tile | V tile]: tile t+1 is written into the other stage while tile t is
     // consumed, one barrier per tile
@@ -103,14 +107,15 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
     // kv head 0-6's lists (1 x 4k: 580 vs 870 TF/s).  Large grids (kv_major = 1): block b = kv head
     // b / n_items x item b % n_items, so the blocks in flight share one kv head and its K/V stays in the
     // Infinity Cache (39 x 4k: 912 vs 815 TF/s); profiles/r3_attn_prefill_grid_order_ab.jsonl.
-    const int n_items = gridDim.x / Hkv;
-    const int item = kv_major ? blockIdx.x % n_items : blockIdx.x / Hkv;
+    const int n_items = gridDim.x / Hg;
+    const int item = kv_major ? blockIdx.x % n_items : blockIdx.x / Hg;
     const int2 it = items[item];
     const int seq = it.x, qblock = it.y;
-    const int kvh = kv_major ? blockIdx.x / n_items : blockIdx.x % Hkv;
+    const int kvg = kv_major ? blockIdx.x / n_items : blockIdx.x % Hg;  // head group of this workgroup
+    const int kvh = G == 1 ? kvg / gq : kvg;                             // its real kv head
     const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5, r32 = lane & 31;
     const int w = tid >> 6;
-    const int h = kvh * G + w % G, rb = w / G;
+    const int h = G == 1 ? kvg : kvh * G + w % G, rb = w / G;
     const int s0 = cu_seqlens[seq], len = cu_seqlens[seq + 1] - s0;
     const bf16* base = qkv + (size_t)s0 * row_stride;
     const int kcol = (Hq + kvh) * D, vcol = (Hq + Hkv + kvh) * D;
@@ -331,17 +336,21 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
 
 template <bool PAGED, int G>
 static void launch_g(dim3 grid, hipStream_t s, const bf16* Q, int row_stride, const int* cu, const int2* it, bf16* out,
-                     int out_stride, int Hq, int Hkv, float sl, const PagedKV& p) {
+                     int out_stride, int Hq, int Hkv, int Hg, int gq, float sl, const PagedKV& p) {
     // kv-head-major order from 8 blocks per CU up (measured crossover: 4096 blocks neutral, 19656 kv-major)
     const int kv_major = grid.x > 8 * 256;
-    attn_prefill_kernel<PAGED, G><<<grid, NTHR, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq, Hkv, sl, p, kv_major);
+    attn_prefill_kernel<PAGED, G><<<grid, NTHR, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq, Hkv, Hg, gq, sl, p,
+                                                        kv_major);
 }
 
-// Query positions per workgroup for a GQA ratio (the host's work list must use the same block size).
+static bool packed_ratio(int G) { return G == 1 || G == 2 || G == 4 || G == 8; }
+
+// Query positions per workgroup for a GQA ratio (the host's work list must use the same block size):
+// 256 / G for the packed ratios, 256 for the per-query-head fallback of any other ratio.
 MRSUM_API int mrsum_attn_prefill_block_m(int Hq, int Hkv) {
-    if (Hkv <= 0 || Hq % Hkv) return -1;
+    if (Hkv <= 0 || Hq % Hkv || Hq / Hkv > 64) return -1;
     const int G = Hq / Hkv;
-    return (G == 1 || G == 2 || G == 4 || G == 8) ? 32 * (NW / G) : -1;
+    return packed_ratio(G) ? 32 * (NW / G) : 32 * NW;
 }
 
 static int launch_prefill(const void* qkv, int row_stride, const int* cu_seqlens, const int* items, int n_items,
@@ -349,18 +358,21 @@ static int launch_prefill(const void* qkv, int row_stride, const int* cu_seqlens
                           const PagedKV* pk, hipStream_t s) {
     if (n_items <= 0) return 0;
     if (Dh != D || mrsum_attn_prefill_block_m(Hq, Hkv) != block_m) return (int)hipErrorInvalidValue;
-    dim3 grid(n_items * Hkv);
+    const int G = Hq / Hkv;
+    const int Hg = packed_ratio(G) ? Hkv : Hq;  // head groups per work item (see the kernel's header)
+    const int gq = packed_ratio(G) ? 1 : G;
+    dim3 grid(n_items * Hg);
     const float sl = scale * 1.4426950408889634f;
     auto Q = (const bf16*)qkv;
     auto IT = (const int2*)items;
     auto O = (bf16*)out;
     const PagedKV p = pk ? *pk : PagedKV{nullptr, nullptr, nullptr, 0, nullptr, nullptr};
-#define DISPATCH(PG)                                                                                         \
-    switch (Hq / Hkv) {                                                                                      \
-        case 1: launch_g<PG, 1>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, sl, p); break; \
-        case 2: launch_g<PG, 2>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, sl, p); break; \
-        case 4: launch_g<PG, 4>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, sl, p); break; \
-        default: launch_g<PG, 8>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, sl, p); break; \
+#define DISPATCH(PG)                                                                                                 \
+    switch (packed_ratio(G) ? G : 1) {                                                                               \
+        case 1: launch_g<PG, 1>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p); break; \
+        case 2: launch_g<PG, 2>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p); break; \
+        case 4: launch_g<PG, 4>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p); break; \
+        default: launch_g<PG, 8>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p); break; \
     }
     if (pk) { DISPATCH(true) } else { DISPATCH(false) }
 #undef DISPATCH

@@ -331,6 +331,22 @@ MRSUM_API int mrsum_ar_add_rmsnorm(void* hv, const void* parts, int S, int T, vo
     return (int)hipGetLastError();
 }
 
+// Clear this rank's whole allocation (flags, one-shot / push-row / granule-push slots) and every local
+// counter (epochs, the sticky error word, push-row and granule epochs).  COLLECTIVE at the host level
+// (parallel/custom_ar.py CustomAllReduce.reset): every rank of the group must be idle (no kernel of this
+// handle in flight anywhere) before, and must not launch one before every rank has returned -- then all
+// ranks restart from epoch 1 against zeroed slots, so no stale tag or flag can match a new epoch.
+MRSUM_API int mrsum_ar_reset(void* hv) {
+    auto h = (ArHandle*)hv;
+    if (!h) return (int)hipErrorInvalidValue;
+    constexpr size_t n_ctr = MAX_BLOCKS + 16 + MAX_ROWS + MAX_GRAN;
+    hipError_t e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemset(h->mine, 0, alloc_bytes(h->max_bytes, h->world));
+    if (e == hipSuccess) e = hipMemset(h->epochs, 0, n_ctr * sizeof(unsigned));
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    return (int)e;
+}
+
 MRSUM_API int mrsum_ar_error(void* hv) {
     auto h = (ArHandle*)hv;
     unsigned v = 0;

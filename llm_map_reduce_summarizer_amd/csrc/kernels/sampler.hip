@@ -12,13 +12,19 @@
 // finish:  one lane per row: decode the winner, reset result[b] to 0 for
 //          the next launch, append the token to out_tokens, feed it as the
 //          next input id, advance the position, and retire the row on EOS or
-//          max_new.  A retired row keeps its position, so a captured decode
+//          max_new.  The stop ids are read from device memory at EVERY launch
+//          (EOS_SLOTS ints, -1 = unused slot), never passed by value: a
+//          captured decode graph then follows whatever stop set the engine
+//          holds when it is replayed (generate(ignore_eos=True) writes -1s),
+//          not the one it held when the graph was captured.  A retired row keeps its position, so a captured decode
 //          graph can keep running it harmlessly until the host drops it.
 // Tensor parallel (vocab-parallel LM head): each rank scans its vocab shard with
 // tok_offset = rank * V_local -- the noise is a function of the GLOBAL token id, so the
 // per-rank winners max-reduced across ranks (8 bytes per row, parallel/custom_ar.py) give the
 // same token as one GPU scanning the whole row, without gathering the logits.
 #include "common.h"
+
+constexpr int EOS_SLOTS = 4;  // engine DecodeState.eos: 4 device ints, -1 = unused
 
 __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
     x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ULL;
@@ -86,7 +92,7 @@ __global__ __launch_bounds__(256) void sample_kernel(const bf16* __restrict__ lo
 __global__ void sample_finish_kernel(unsigned long long* __restrict__ result, int* __restrict__ next_ids,
                                      int* __restrict__ positions, int* __restrict__ gen_count,
                                      const int* __restrict__ max_new, int* __restrict__ out_tokens, int out_stride,
-                                     int* __restrict__ done, const int* __restrict__ eos, int n_eos, int B) {
+                                     int* __restrict__ done, const int* __restrict__ eos, int B) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     const unsigned long long r = result[b];
@@ -98,7 +104,8 @@ __global__ void sample_finish_kernel(unsigned long long* __restrict__ result, in
     gen_count[b] = g + 1;
     next_ids[b] = tok;
     bool stop = g + 1 >= max_new[b];
-    for (int i = 0; i < n_eos; ++i) stop |= tok == eos[i];
+#pragma unroll
+    for (int i = 0; i < EOS_SLOTS; ++i) stop |= tok == eos[i];  // tok >= 0 never matches a -1 slot
     if (stop) done[b] = 1;
     else positions[b] += 1;
 }
@@ -122,24 +129,22 @@ MRSUM_API int mrsum_sample_keys(const void* logits, int ld, int B, int V, int to
 }
 
 MRSUM_API int mrsum_sample_finish(void* result, int* next_ids, int* positions_rw, int* gen_count, const int* max_new,
-                                  int* out_tokens, int out_stride, int* done, const int* eos, int n_eos, int B,
+                                  int* out_tokens, int out_stride, int* done, const int* eos, int B,
                                   hipStream_t s) {
     if (B <= 0) return 0;
     sample_finish_kernel<<<ceil_div(B, 64), 64, 0, s>>>((unsigned long long*)result, next_ids, positions_rw,
-                                                        gen_count, max_new, out_tokens, out_stride, done, eos,
-                                                        n_eos, B);
+                                                        gen_count, max_new, out_tokens, out_stride, done, eos, B);
     return (int)hipGetLastError();
 }
 
 MRSUM_API int mrsum_sample(const void* logits, int ld, int B, int V, const float* temps, const long long* seeds,
                            const int* positions, void* result, int* next_ids, int* positions_rw, int* gen_count,
-                           const int* max_new, int* out_tokens, int out_stride, int* done, const int* eos, int n_eos,
+                           const int* max_new, int* out_tokens, int out_stride, int* done, const int* eos,
                            hipStream_t s) {
     if (B <= 0) return 0;
     int e = launch_keys(logits, ld, B, V, 0, temps, seeds, positions, result, s);
     if (e) return e;
     sample_finish_kernel<<<ceil_div(B, 64), 64, 0, s>>>((unsigned long long*)result, next_ids, positions_rw,
-                                                        gen_count, max_new, out_tokens, out_stride, done, eos,
-                                                        n_eos, B);
+                                                        gen_count, max_new, out_tokens, out_stride, done, eos, B);
     return (int)hipGetLastError();
 }

@@ -58,6 +58,9 @@ PRESETS = {
     "tiny": ModelConfig("tiny", hidden=256, n_layers=2, n_heads=2, n_kv_heads=1, ffn=512, max_position=8192),
     "tiny-gqa4": ModelConfig("tiny-gqa4", hidden=512, n_layers=2, n_heads=8, n_kv_heads=2, ffn=1024,
                              max_position=8192),
+    # GQA 3:1 (Llama-3.2-3B's ratio, 24 / 8): the attention kernels' per-query-head fallback
+    "tiny-gqa3": ModelConfig("tiny-gqa3", hidden=768, n_layers=2, n_heads=6, n_kv_heads=2, ffn=1024,
+                             max_position=8192),
     # 8 KV heads (GQA 2:1) with heads / ffn / vocab divisible by 8: the TP=4 / TP=8 sharding paths of an
     # 8-GPU node (one or two KV heads per rank, 16032-row vocab shards, 8-way KV hand-off) on CPU ranks
     "tiny-kv8": ModelConfig("tiny-kv8", hidden=512, n_layers=2, n_heads=16, n_kv_heads=8, ffn=1024,

@@ -97,9 +97,19 @@ class DecodeState:
         self.result = torch.zeros(max_seqs, dtype=torch.int64, device=device)
         self.temps = torch.zeros(max_seqs, dtype=torch.float32, device=device)
         self.seeds = torch.zeros(max_seqs, dtype=torch.int64, device=device)
-        eos = list(eos)[:4]
-        self.eos = torch.tensor(eos + [-1] * (4 - len(eos)), **i32)
-        self.n_eos = len(eos)
+        # the sampler's finish kernel reads these 4 stop ids from device memory at every launch (-1 =
+        # unused slot), so captured decode graphs follow the stop set at REPLAY time (set_eos)
+        self.eos = torch.full((4,), -1, **i32)
+        self.eos_ids: List[int] = []
+        self.set_eos(eos)
+
+    def set_eos(self, ids: Sequence[int]) -> None:
+        """Stop ids of every later sampler launch, captured graphs included (at most 4; [] = none)."""
+        ids = [int(x) for x in ids]
+        if len(ids) > 4 or any(x < 0 for x in ids):
+            raise ValueError("at most 4 non-negative EOS ids, got %s" % ids)
+        self.eos.copy_(torch.tensor(ids + [-1] * (4 - len(ids)), dtype=torch.int32), non_blocking=False)
+        self.eos_ids = ids
 
     _ROW_FIELDS = ("next_ids", "positions", "block_tables", "gen_count", "max_new", "out_tokens", "done", "result",
                    "temps", "seeds")
@@ -110,7 +120,7 @@ class DecodeState:
         for f in self._ROW_FIELDS:
             setattr(v, f, getattr(self, f)[start:start + n])
         v.seq_idx = self.seq_idx[:n]
-        v.eos, v.n_eos = self.eos, self.n_eos
+        v.eos, v.eos_ids = self.eos, self.eos_ids
         return v
 
     def move_row(self, src: int, dst: int) -> None:
@@ -231,6 +241,10 @@ class LLMEngine:
         # decode slot until their last slice has run, so no decode step can touch their pages)
         self.pf_tables = torch.zeros(self.max_num_seqs, self.max_pages, dtype=torch.int32, device=self.device)
         self.interleave = os.environ.get("MRSUM_INTERLEAVE", "1") == "1"
+        # test hook (SURVEY §5.3 fault injection): "rank:seconds" -- TP rank ``rank`` sleeps on the host
+        # before its first decode window, so its peers' P2P all-reduce waits time out (recovery test)
+        spec = os.environ.get("MRSUM_FAULT_AR_DELAY", "")
+        self._fault_delay = tuple(float(x) for x in spec.split(":")) if spec else None
         self.use_graphs = use_graphs and self.device.type == "cuda"
         if self.use_graphs and self.model.tp_size > 1 and self.model.custom_ar is None:
             # TP without the P2P all-reduce would put RCCL collectives inside the captured graphs;
@@ -264,10 +278,10 @@ class LLMEngine:
         key = (B, self._ctx_cls)
         ws = self._workspaces.get(key)
         if ws is None:
-            from ..ops.hip import CTX_CLASSES, DecodeWorkspace, decode_attn_plan
-            s, fused = decode_attn_plan(B, self.model.hkv, min(CTX_CLASSES[self._ctx_cls], self.max_model_len))
-            ws = DecodeWorkspace(B, self.model.hq, self.cfg.head_dim, s, self.device, self.model.hkv,
-                                 fused_combine=fused)
+            from ..ops.hip import CTX_CLASSES, DecodeWorkspace, decode_attn_plan, decode_groups
+            ng = decode_groups(self.model.hq, self.model.hkv)  # kv heads, or query heads for odd GQA ratios
+            s, fused = decode_attn_plan(B, ng, min(CTX_CLASSES[self._ctx_cls], self.max_model_len))
+            ws = DecodeWorkspace(B, self.model.hq, self.cfg.head_dim, s, self.device, ng, fused_combine=fused)
             self._workspaces[key] = ws
         return ws
 
@@ -387,6 +401,11 @@ class LLMEngine:
         self._sample(logits, st.view(0, B))
 
     def _decode_steps(self, B: int, steps: int) -> None:
+        if self._fault_delay is not None and int(self._fault_delay[0]) == self.model.tp_rank \
+                and self.model.custom_ar is not None:
+            delay, self._fault_delay = self._fault_delay[1], None  # once
+            log.warning("fault injection: TP rank %d sleeps %.1f s before a decode window", self.model.tp_rank, delay)
+            time.sleep(delay)
         if not self.use_graphs:
             for _ in range(steps):
                 self._decode_once(B)
@@ -467,16 +486,40 @@ class LLMEngine:
         summarised)"""
         if len(prompts) != len(params):
             raise ValueError("prompts and params differ in length")
-        n_eos = self.state.n_eos
-        if ignore_eos:
-            self.state.n_eos = 0
+        eos = list(self.state.eos_ids)
+        if ignore_eos:  # device-side stop set: captured graphs see it at replay (sampler.hip EOS_SLOTS)
+            self.state.set_eos([])
         try:
             out = self._generate(prompts, params, imported or {}, on_prefill, feeder, on_sync)
+            ar = self.model.custom_ar
+            if ar is not None and ar.agree_error():
+                out = self._recover_custom_ar(prompts, params, imported or {}, on_prefill, feeder, on_sync)
         finally:
-            self.state.n_eos = n_eos
-        if self.model.custom_ar is not None and self.model.custom_ar.error():
-            raise RuntimeError("custom all-reduce: a wait for a peer timed out during this generate; "
-                               "results are invalid (set MRSUM_CUSTOM_AR=0 to use RCCL)")
+            if ignore_eos:
+                self.state.set_eos(eos)
+        return out
+
+    def _recover_custom_ar(self, prompts, params, imported, on_prefill, feeder, on_sync) -> List[GenOutput]:
+        """A wait of the P2P all-reduce timed out on some rank during this generate (a peer stalled > 4 s:
+        host jitter, a slow rank), so its results are garbage on every rank.  Every rank got here (the error
+        vote is collective): clear the all-reduce state on the whole group, then run the SAME requests again
+        on RCCL (torch.distributed, eager: RCCL never runs inside a captured graph) -- the retry of the
+        reference's executor (llm_executor.py:198-228), done inside the engine so it hits a working path.
+        The handle is usable again afterwards; later generates use it."""
+        if feeder is not None or on_sync is not None:
+            # streamed requests were already handed out: they cannot be taken back
+            raise RuntimeError("custom all-reduce: a wait for a peer timed out during a streamed generate")
+        ar = self.model.custom_ar
+        log.error("custom all-reduce: a wait for a peer timed out (TP rank %d); resetting the P2P buffers and "
+                  "re-running %d requests on RCCL", self.model.tp_rank, len(prompts))
+        self.stats["custom_ar_recoveries"] = self.stats.get("custom_ar_recoveries", 0) + 1
+        ar.reset()
+        graphs = self.use_graphs
+        self.model.custom_ar, self.use_graphs = None, False
+        try:
+            out = self._generate(prompts, params, imported, on_prefill, None, None)
+        finally:
+            self.model.custom_ar, self.use_graphs = ar, graphs
         return out
 
     def _new_seq(self, i: int, p: Sequence[int], sp: SamplingParams, imported=None) -> _Seq:
@@ -509,7 +552,7 @@ class LLMEngine:
             if s.imported is not None:
                 tok = int(s.imported.first_token)
                 mn = s.params.max_new_tokens
-                if mn == 1 or tok in set(self.state.eos.tolist()[: self.state.n_eos]):
+                if mn == 1 or tok in self.state.eos_ids:
                     results[i] = GenOutput([tok], len(s.prompt), "length" if mn == 1 else "stop")  # done at prefill
                     finished.append(i)
                     continue
@@ -679,26 +722,41 @@ class LLMEngine:
         st.seeds[s.slot] = int(s.params.seed)
         st.result[s.slot] = 0
 
-    def _interleaved_pass(self, prefilling: List[_Seq], active: List[_Seq]) -> None:
+    def _interleaved_pass(self, prefilling: List[_Seq], active: List[_Seq], max_parts: Optional[int] = None) -> None:
         """One packed forward of the next slices of the prefilling requests (at most ``prefill_chunk``
-        tokens, or ``max_prefill_tokens`` without chunking; always at least one slice).  Requests whose
-        LAST slice ran take the next decode slots and sample their first token there."""
+        tokens, or ``max_prefill_tokens`` without chunking; always at least one slice; at most
+        ``max_parts`` slices).  Requests whose LAST slice ran take the next decode slots and sample their
+        first token there.  A device out-of-memory error in the forward (TP=1) re-runs the pass with half
+        as many slices, down to one -- the running decode batch and the other joiners are unaffected
+        (SURVEY §5.3 failure isolation, as ``_prefill_isolated`` for blocking admission)."""
         budget = self.prefill_chunk or self.max_prefill_tokens
         part, spans, tokens = [], [], 0
         for s in prefilling:
             b, e = s.spans[0]
-            if part and tokens + (e - b) > budget:
+            if part and (tokens + (e - b) > budget or (max_parts is not None and len(part) >= max_parts)):
                 break
             part.append(s)
             spans.append((b, e))
             tokens += e - b
         final = [len(s.spans) == 1 for s in part]
         t0 = time.perf_counter()
-        x = self._pass_inputs(part, spans, paged=True, tables=self.pf_tables, slots=[s.pf_slot for s in part],
-                              sample=final)
-        logits = self.model.prefill(x.ids, x.positions, x.seq_idx, x.cu_seqlens, x.last_rows, self.pf_tables,
-                                    self.kv.k, self.kv.v, seqlens=x.seqlens, items=x.items,
-                                    gather=not self.model.tp_sampling, paged=x.paged, logits=any(final))
+        try:
+            x = self._pass_inputs(part, spans, paged=True, tables=self.pf_tables, slots=[s.pf_slot for s in part],
+                                  sample=final)
+            logits = self.model.prefill(x.ids, x.positions, x.seq_idx, x.cu_seqlens, x.last_rows, self.pf_tables,
+                                        self.kv.k, self.kv.v, seqlens=x.seqlens, items=x.items,
+                                        gather=not self.model.tp_sampling, paged=x.paged, logits=any(final))
+        except torch.OutOfMemoryError:
+            # nothing of this pass is committed yet (spans are popped and slots taken only below; the K/V
+            # rows it may have written are rewritten by the retry)
+            if len(part) == 1 or self.model.tp_size > 1:
+                raise
+            if self.device.type == "cuda":
+                torch.cuda.empty_cache()
+            self.stats["prefill_oom_splits"] = self.stats.get("prefill_oom_splits", 0) + 1
+            log.warning("interleaved prefill pass of %d slices ran out of device memory: retrying with %d",
+                        len(part), len(part) // 2)
+            return self._interleaved_pass(prefilling, active, max_parts=len(part) // 2)
         self.stats["prefill_tokens"] += tokens
         self.stats["prefill_slices"] = self.stats.get("prefill_slices", 0) + len(part)
         for s in part:

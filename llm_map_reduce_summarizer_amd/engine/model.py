@@ -70,7 +70,7 @@ class _TPReduce:
 
     def fused_ok(self, rows: int, hidden: int) -> bool:
         ar = self.model.custom_ar
-        return self.fused and rows <= ar.MAX_ROWS and hidden % 4 == 0 and hidden <= 8192 and \
+        return self.fused and ar is not None and rows <= ar.MAX_ROWS and hidden % 4 == 0 and hidden <= 8192 and \
             rows * hidden * 2 <= ar.max_bytes
 
     def add_rmsnorm(self, parts, residual, ln, eps):
@@ -297,6 +297,13 @@ class LlamaModel:
         if self.tp_size == 1:
             return logits
         B, vl = logits.shape
+        if logits.is_cuda and torch.distributed.get_backend(self.tp_group) != "nccl":
+            # gloo group over GPU tensors (ranks sharing one GPU: the rehearsals, the custom all-reduce
+            # recovery test): gather through host memory
+            cpu = torch.empty(self.tp_size * B, vl, dtype=logits.dtype)
+            torch.distributed.all_gather_into_tensor(cpu, logits.cpu().contiguous(), group=self.tp_group)
+            out = cpu.to(logits.device)
+            return out.view(self.tp_size, B, vl).permute(1, 0, 2).reshape(B, self.tp_size * vl)
         out = torch.empty(self.tp_size * B, vl, dtype=logits.dtype, device=logits.device)
         torch.distributed.all_gather_into_tensor(out, logits.contiguous(), group=self.tp_group)
         return out.view(self.tp_size, B, vl).permute(1, 0, 2).reshape(B, self.tp_size * vl)

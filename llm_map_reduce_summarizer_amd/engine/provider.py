@@ -146,6 +146,9 @@ class LocalEngineProvider(Provider):
         if max_num_seqs is not None:
             self._engine_options.setdefault("max_num_seqs", max_num_seqs)
         self.timings: Dict[str, float] = {"generate_s": 0.0, "allgather_s": 0.0}
+        # work actually done, from the all-gathered results (identical on every rank): bench.py checks that
+        # a pinned run generated exactly its requested tokens (no generation cut short inside the timed work)
+        self.work: Dict[str, int] = {"requests": 0, "errors": 0, "completion_tokens": 0, "requested_tokens": 0}
         self.par = pdist.setup_parallel(tp)
         # parallel policy (module docstring); the legacy reduce_tp flag maps onto it
         if parallel is None:
@@ -451,6 +454,17 @@ class LocalEngineProvider(Provider):
     async def generate(self, req: GenRequest) -> GenResult:
         return (await self.generate_batch([req]))[0]
 
+    def _tally(self, results: Sequence[Optional[GenResult]], max_tokens: Sequence[int]) -> None:
+        for r, mt in zip(results, max_tokens):
+            if r is None:
+                continue
+            self.work["requests"] += 1
+            if r.error:
+                self.work["errors"] += 1
+                continue
+            self.work["completion_tokens"] += int(r.completion_tokens)
+            self.work["requested_tokens"] += int(mt)
+
     def _generate_tp_groups(self, prompts, reqs, k: int, sp, stage: str) -> List[GenResult]:
         """TP=k x DP=world/k: requests LPT-balanced over the world / k groups of k consecutive ranks, each
         group runs its share on its TP=k engine (disaggregated / context-parallel prefill inside the group
@@ -523,6 +537,7 @@ class LocalEngineProvider(Provider):
             # TP=tp groups (tp = world: every rank runs every request); the TP ranks sample identically
             res = self._generate_tp(prompts, reqs, handoff, tp, stage)
             self.timings["generate_s"] += time.perf_counter() - t0
+            self._tally(res, [r.max_tokens for r in reqs])
             return res
         dp, dp_rank = self.par.dp, self.par.dp_rank
         owner = assign_balanced([len(p) + r.max_tokens for p, r in zip(prompts, reqs)], dp)
@@ -571,8 +586,10 @@ class LocalEngineProvider(Provider):
         else:
             merged = {r["i"]: r for r in local}
         self.timings["allgather_s"] += time.perf_counter() - t1
-        return [_result(merged[i]) if i in merged else GenResult("", error="request %d produced no result" % i)
-                for i in range(len(reqs))]
+        res = [_result(merged[i]) if i in merged else GenResult("", error="request %d produced no result" % i)
+               for i in range(len(reqs))]
+        self._tally(res, [r.max_tokens for r in reqs])
+        return res
 
     async def generate_groups(self, reqs: Sequence[GenRequest], groups: Sequence[Sequence[int]], build):
         """Streamed two-stage generate (map -> level-1 reduce): ``groups`` partitions
@@ -607,6 +624,7 @@ class LocalEngineProvider(Provider):
         first: Dict[int, Dict[str, Any]] = {}
         second: Dict[int, Dict[str, Any]] = {}
         fed: List[int] = []  # engine request index len(mine) + k -> group fed[k]
+        fed_mt: Dict[int, int] = {}  # group -> max_tokens of its follow-up request
 
         def rec(key, idx, o):
             return {key: idx, "text": self.tokenizer.decode(o.token_ids), "pt": o.prompt_len, "ct": len(o.token_ids),
@@ -617,7 +635,7 @@ class LocalEngineProvider(Provider):
             for rid, o in done:
                 if rid >= len(mine):
                     g = fed[rid - len(mine)]
-                    second[g] = rec("g", g, o)
+                    second[g] = dict(rec("g", g, o), mt=fed_mt[g])
                     continue
                 i = mine[rid]
                 first[i] = rec("i", i, o)
@@ -629,6 +647,7 @@ class LocalEngineProvider(Provider):
                 if r2 is None:
                     continue
                 fed.append(g)
+                fed_mt[g] = r2.max_tokens
                 new.append((self.encode_request(r2),
                             SamplingParams(r2.max_tokens, r2.temperature, _req_seed(self.seed, r2))))
             return new
@@ -657,6 +676,8 @@ class LocalEngineProvider(Provider):
         res1 = [_result(m1[i]) if i in m1 else GenResult("", error="request %d produced no result" % i)
                 for i in range(len(reqs))]
         res2 = [_result(m2[g]) if g in m2 else None for g in range(len(groups))]
+        self._tally(res1, [r.max_tokens for r in reqs])
+        self._tally([res2[g] for g in m2], [int(m2[g].get("mt", 0)) for g in m2])
         return res1, res2
 
     def stats(self) -> Dict[str, Any]:

@@ -15,6 +15,11 @@ our library link ``libamdhip64.so.7`` (same SONAME), and loading torch first
 makes the dynamic loader bind ours to torch's already-mapped HIP runtime so
 streams and device pointers are shared.
 
+Provenance: each library carries ``<lib>.stamp.json`` (``_stamp.py``: sha256 of
+the sources + flags it was built from); the default in-tree libraries are
+refused when that stamp does not match this tree's sources, so stale binaries
+never run silently.
+
 On a machine with a GPU the kernel library is REQUIRED (``kernels_lib()``
 raises if it is missing) -- there is deliberately no silent PyTorch fallback
 for the hot path.  ``MRSUM_OPS=torch`` selects the pure-PyTorch reference ops
@@ -28,10 +33,13 @@ import os
 import threading
 from typing import Optional
 
+from .. import _stamp
+
 NATIVE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native")
 # MRSUM_KERNELS_SO: an alternative build of the kernel library (A/B experiments of two kernel versions
 # in one process tree); default the in-tree build
-KERNELS_SO = os.environ.get("MRSUM_KERNELS_SO") or os.path.join(NATIVE_DIR, "libmrsum_kernels.so")
+_KERNELS_OVERRIDE = os.environ.get("MRSUM_KERNELS_SO")
+KERNELS_SO = _KERNELS_OVERRIDE or os.path.join(NATIVE_DIR, "libmrsum_kernels.so")
 RUNTIME_SO = os.path.join(NATIVE_DIR, "libmrsum_runtime.so")
 
 _lock = threading.Lock()
@@ -55,6 +63,10 @@ def kernels_lib() -> ctypes.CDLL:
             if not os.path.isfile(KERNELS_SO):
                 raise NativeLibraryMissing(
                     "%s not found: run `python build.py` (hipcc --offload-arch=gfx950) first" % KERNELS_SO)
+            if not _KERNELS_OVERRIDE:  # an explicit A/B build carries its own provenance
+                why = _stamp.check("kernels")
+                if why:
+                    raise NativeLibraryMissing("refusing a stale kernel library: " + why)
             _kernels = ctypes.CDLL(KERNELS_SO, mode=ctypes.RTLD_LOCAL)
     return _kernels
 
@@ -68,7 +80,22 @@ def runtime_lib(required: bool = True) -> Optional[ctypes.CDLL]:
         if _runtime is None and not _runtime_tried:
             _runtime_tried = True
             if os.path.isfile(RUNTIME_SO):
-                _runtime = ctypes.CDLL(RUNTIME_SO, mode=ctypes.RTLD_LOCAL)
+                why = _stamp.check("runtime")
+                if why and required:
+                    raise NativeLibraryMissing("refusing a stale runtime library: " + why)
+                if not why:
+                    _runtime = ctypes.CDLL(RUNTIME_SO, mode=ctypes.RTLD_LOCAL)
     if _runtime is None and required:
-        raise NativeLibraryMissing("%s not found: run `python build.py` first" % RUNTIME_SO)
+        raise NativeLibraryMissing("%s not found or stale: run `python build.py` first" % RUNTIME_SO)
     return _runtime
+
+
+def native_stamps() -> dict:
+    """{kind: stamp record + "matches_tree"} of the in-tree libraries (smoke() prints it)."""
+    out = {}
+    for kind in _stamp.LIBS:
+        rec = dict(_stamp.read_stamp(kind) or {})
+        rec.pop("files", None)
+        rec["matches_tree"] = _stamp.check(kind) is None
+        out[kind] = rec
+    return out

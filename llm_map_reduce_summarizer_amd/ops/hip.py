@@ -51,11 +51,11 @@ _SIGS = {
     "mrsum_quant_fp8_rows": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_sample_keys": [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
-    "mrsum_sample_finish": [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
+    "mrsum_sample_finish": [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_int, _vp],
     "mrsum_gemm": [_vp, _c_int, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int,
                    _vp],
     "mrsum_sample": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp,
-                     _c_int, _vp],
+                     _vp],
 }
 
 _fns = {}
@@ -258,9 +258,10 @@ def embed(ids: torch.Tensor, table: torch.Tensor, out: Optional[torch.Tensor] = 
 # ------------------------------------------------------------------ attention
 def prefill_block_m(group: int) -> int:
     """Query positions per prefill-attention workgroup for ``group`` = Hq / Hkv query heads per kv head
-    (attn_prefill.hip: 8 waves x 32 rows cover all ``group`` heads of one kv head)."""
-    _req(group in (1, 2, 4, 8), "attn_prefill: GQA ratio %d not in (1, 2, 4, 8)" % group)
-    return 256 // group
+    (attn_prefill.hip: 8 waves x 32 rows cover all ``group`` heads of one kv head; any other ratio, e.g.
+    Llama-3.2-3B's 3, runs one query head per workgroup over 256 positions)."""
+    _req(1 <= group <= 64, "attn_prefill: GQA ratio %d out of range" % group)
+    return 256 // group if group in (1, 2, 4, 8) else 256
 
 
 def prefill_items(seqlens, group: int) -> torch.Tensor:
@@ -408,6 +409,13 @@ def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
     return splits, fused
 
 
+def decode_groups(hq: int, hkv: int) -> int:
+    """Head groups the decode attention runs (attn_decode.hip mrsum_attn_decode_groups): hkv for GQA ratios
+    1/2/4/8/16, hq (one per query head) for any other ratio -- size workspaces / split plans by it."""
+    _req(hkv > 0 and hq % hkv == 0 and hq // hkv <= 64, "decode attention: bad head config %d / %d" % (hq, hkv))
+    return hkv if hq // hkv in (1, 2, 4, 8, 16) else hq
+
+
 class DecodeWorkspace:
     """Split-K partial buffers + per-(seq, kv head) arrival counters for attn_decode
     (allocated once per batch bucket; counters start at 0 and every launch re-arms them)."""
@@ -436,8 +444,9 @@ def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.T
     _req(parts.is_cuda and parts.dtype == torch.float32 and parts.is_contiguous() and parts.dim() == 3,
          "attn_decode_rope: parts must be fp32 [S, B, width]")
     SP, B, width = parts.shape
-    _req(width == (hq + 2 * hkv) * d and d == 128 and page == 64 and hq % hkv == 0 and hq // hkv <= 16,
+    _req(width == (hq + 2 * hkv) * d and d == 128 and page == 64 and hq % hkv == 0 and hq // hkv <= 64,
          "attn_decode_rope: unsupported config")
+    ng = decode_groups(hq, hkv)
     _bf16_cuda(kcache, vcache)
     _req(tuple(kcache.shape[1:]) == (hkv, page, d) and kcache.is_contiguous() and vcache.is_contiguous(),
          "attn_decode_rope: cache must be [pages, Hkv, P, D]")
@@ -446,9 +455,9 @@ def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.T
     _i32(block_tables, positions)
     _req(block_tables.dim() == 2 and block_tables.shape[0] >= B and positions.numel() >= B, "attn_decode_rope: tables")
     if workspace is None:
-        workspace = DecodeWorkspace(B, hq, d, decode_splits(B, hkv, block_tables.shape[1] * page), parts.device, hkv)
+        workspace = DecodeWorkspace(B, hq, d, decode_splits(B, ng, block_tables.shape[1] * page), parts.device, ng)
     _req(workspace.part_o.numel() >= B * hq * workspace.splits * d and workspace.part_ml.numel() >=
-         B * hq * workspace.splits * 2 and (workspace.counters is None or workspace.counters.numel() >= B * hkv),
+         B * hq * workspace.splits * 2 and (workspace.counters is None or workspace.counters.numel() >= B * ng),
          "attn_decode_rope: workspace")
     if out is None:
         out = torch.empty(B, hq * d, dtype=torch.bfloat16, device=parts.device)
@@ -470,16 +479,17 @@ def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, blo
     _bf16_cuda(q, kcache, vcache)
     _rows_ok(q)
     B = q.shape[0]
-    _req(d == 128 and hq % hkv == 0 and hq // hkv <= 16 and page == 64, "attn_decode: bad config")
+    _req(d == 128 and hq % hkv == 0 and hq // hkv <= 64 and page == 64, "attn_decode: bad config")
+    ng = decode_groups(hq, hkv)
     _req(tuple(kcache.shape[1:]) == (hkv, page, d) and kcache.is_contiguous() and vcache.is_contiguous(),
          "attn_decode: cache must be [pages, Hkv, P, D]")
     _i32(block_tables, positions)
     _req(block_tables.dim() == 2 and block_tables.shape[0] >= B and positions.numel() >= B, "attn_decode: tables")
     if workspace is None:
-        s = num_splits or decode_splits(B, hkv, block_tables.shape[1] * page)
-        workspace = DecodeWorkspace(B, hq, d, s, q.device, hkv)
+        s = num_splits or decode_splits(B, ng, block_tables.shape[1] * page)
+        workspace = DecodeWorkspace(B, hq, d, s, q.device, ng)
     _req(workspace.part_o.numel() >= B * hq * workspace.splits * d, "attn_decode: workspace too small")
-    _req(workspace.counters is None or workspace.counters.numel() >= B * hkv, "attn_decode: counters too small")
+    _req(workspace.counters is None or workspace.counters.numel() >= B * ng, "attn_decode: counters too small")
     if out is None:
         out = torch.empty(B, hq * d, dtype=q.dtype, device=q.device)
     _rows_ok(out)
@@ -492,6 +502,13 @@ def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, blo
 
 
 # ------------------------------------------------------------------ sampler
+def _eos_ok(st) -> None:
+    # the finish kernel reads EOS_SLOTS (4) stop ids from device memory at every launch (-1 = unused):
+    # the stop set is state, never a by-value launch argument a captured graph would freeze
+    _req(st.eos.is_cuda and st.eos.dtype == torch.int32 and st.eos.is_contiguous() and st.eos.numel() == 4,
+         "sample: eos must be 4 int32 device slots")
+
+
 def sample(logits: torch.Tensor, st) -> None:
     """Sample one token per row of ``logits`` into decode state ``st`` (see engine.state)."""
     _bf16_cuda(logits)
@@ -499,9 +516,10 @@ def sample(logits: torch.Tensor, st) -> None:
     B, V = logits.shape
     _req(st.temps.numel() >= B and st.next_ids.numel() >= B and st.out_tokens.shape[0] >= B,
          "sample: state smaller than batch")
+    _eos_ok(st)
     _check(_fn("mrsum_sample")(_p(logits), logits.stride(0), B, V, _p(st.temps), _p(st.seeds), _p(st.positions),
                                _p(st.result), _p(st.next_ids), _p(st.positions), _p(st.gen_count), _p(st.max_new),
-                               _p(st.out_tokens), st.out_tokens.stride(0), _p(st.done), _p(st.eos), st.n_eos,
+                               _p(st.out_tokens), st.out_tokens.stride(0), _p(st.done), _p(st.eos),
                                _stream()), "sample")
 
 
@@ -514,12 +532,13 @@ def sample_tp(logits: torch.Tensor, st, tok_offset: int, max_reduce) -> None:
     B, V = logits.shape
     _req(st.temps.numel() >= B and st.next_ids.numel() >= B and st.out_tokens.shape[0] >= B,
          "sample_tp: state smaller than batch")
+    _eos_ok(st)
     _check(_fn("mrsum_sample_keys")(_p(logits), logits.stride(0), B, V, tok_offset, _p(st.temps), _p(st.seeds),
                                     _p(st.positions), _p(st.result), _stream()), "sample_keys")
     max_reduce(st.result[:B])
     _check(_fn("mrsum_sample_finish")(_p(st.result), _p(st.next_ids), _p(st.positions), _p(st.gen_count),
                                       _p(st.max_new), _p(st.out_tokens), st.out_tokens.stride(0), _p(st.done),
-                                      _p(st.eos), st.n_eos, B, _stream()), "sample_finish")
+                                      _p(st.eos), B, _stream()), "sample_finish")
 
 
 # ------------------------------------------------------------------ large-M GEMM (prefill, M > 64)

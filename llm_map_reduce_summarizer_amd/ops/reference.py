@@ -330,7 +330,7 @@ def sample_tokens(logits: torch.Tensor, temps: torch.Tensor, seeds: torch.Tensor
 def sample_finish(tokens: torch.Tensor, st) -> None:
     """Bookkeeping identical to the finish kernel (st = engine DecodeState)."""
     B = tokens.shape[0]
-    eos = set(int(x) for x in st.eos.tolist()[: st.n_eos])
+    eos = set(int(x) for x in st.eos.tolist() if int(x) >= 0)
     for b in range(B):
         if int(st.done[b]):
             continue

@@ -48,6 +48,7 @@ _SIGS = {
                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                               ctypes.c_void_p], ctypes.c_int),
     "mrsum_ar_error": ([ctypes.c_void_p], ctypes.c_int),
+    "mrsum_ar_reset": ([ctypes.c_void_p], ctypes.c_int),
     "mrsum_ar_destroy": ([ctypes.c_void_p], None),
 }
 
@@ -208,7 +209,32 @@ class CustomAllReduce:
             ok = False
         votes = [None] * self.world
         dist.all_gather_object(votes, ok, group=self.group)
+        # the test's tagged words sit at offsets that later belong to other granules / rows: start the real
+        # traffic from zeroed slots and epoch 1 on every rank, whatever the test's iteration count
+        self.reset()
         return all(votes)
+
+    def reset(self) -> None:
+        """COLLECTIVE: clear the flags, slots, epochs and the sticky error word on every rank of the group
+        (after a timed-out wait: the handle is usable again).  Every rank must call it at the same point
+        with no kernel of this handle queued; the barriers around the local clear keep a fast rank from
+        pushing into a peer's region before that peer has cleared it."""
+        dist.barrier(group=self.group)
+        rc = self._lib.mrsum_ar_reset(self._h)
+        oks = [None] * self.world
+        dist.all_gather_object(oks, rc == 0, group=self.group)
+        if not all(oks):
+            raise RuntimeError("custom all-reduce: reset failed on some rank (rc %d here)" % rc)
+
+    def agree_error(self) -> int:
+        """COLLECTIVE: the error words of every rank, OR-ed (a rank whose own waits all succeeded may still
+        hold garbage pushed by a timed-out peer, so the group decides together)."""
+        errs = [None] * self.world
+        dist.all_gather_object(errs, self.error(), group=self.group)
+        out = 0
+        for e in errs:
+            out |= int(e) if e is not None and e >= 0 else 1
+        return out
 
     def _test_fused(self, dev, iters: int, T: int = 5, D: int = 512, S: int = 2) -> bool:
         """add_rmsnorm against (collective sum of the slabs) + the fp32 reference add_rmsnorm, eager
@@ -414,6 +440,11 @@ class LocalPush:
     add_rmsnorm = CustomAllReduce.add_rmsnorm
     error = CustomAllReduce.error
     close = CustomAllReduce.close
+
+    def reset(self) -> None:
+        rc = self._lib.mrsum_ar_reset(self._h)
+        if rc:
+            raise RuntimeError("LocalPush: reset failed (%d)" % rc)
     __del__ = CustomAllReduce.__del__
 
 

@@ -159,18 +159,31 @@ class Batcher:
         self.stats = {"requests": 0, "batches": 0, "errors": 0, "prompt_tokens": 0, "completion_tokens": 0,
                       "engine_s": 0.0, "max_batch_seen": 0}
         self._thread: Optional[threading.Thread] = None
+        # enqueue vs drain: once _drain has closed the queue no request may enter it (its client would wait
+        # on its future forever), so the closed check and the put happen under the lock _drain takes
+        self._qlock = threading.Lock()
+        self._closed = False
+
+    def _enqueue(self, item) -> bool:
+        """Queue ``item`` unless the server is stopping / drained (False: answer the client yourself)."""
+        with self._qlock:
+            if self._closed or self.stop.is_set():
+                return False
+            self.q.put(item)
+            return True
 
     async def submit(self, req: GenRequest) -> GenResult:
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
-        if self.stop.is_set():
+        if not self._enqueue((req, loop, fut)):
             return GenResult("", error="server shutting down")
-        self.q.put((req, loop, fut))
         return await fut
 
     def _drain(self) -> None:
         """Answer every request still queued when the engine thread stops (its client would otherwise
-        wait on its future until the process dies)."""
+        wait on its future until the process dies); no request can be queued after this."""
+        with self._qlock:
+            self._closed = True
         while True:
             try:
                 it = self.q.get_nowait()
@@ -255,10 +268,9 @@ class ContinuousBatcher(Batcher):
         loop = asyncio.get_running_loop()
         fut = loop.create_future()
         sq: "asyncio.Queue[str]" = asyncio.Queue()
-        if self.stop.is_set():
+        if not self._enqueue((req, loop, fut, sq)):
             yield "done", GenResult("", error="server shutting down")
             return
-        self.q.put((req, loop, fut, sq))
         while True:
             getter = asyncio.ensure_future(sq.get())
             await asyncio.wait([getter, fut], return_when=asyncio.FIRST_COMPLETED)

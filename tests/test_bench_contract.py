@@ -55,6 +55,10 @@ def test_bench_prints_one_json_line(world, extra):
         assert "tp2" in cfg["parallelism"]
     assert out["ranks_seen"] == world
     assert out["backend"] == ("gloo" if world > 1 else "none")
+    # the timed work is the pinned work: every generation produced exactly max_new tokens
+    tw = out["timed_work"]
+    assert tw["pinned_ok"] and tw["errors"] == 0 and tw["requests"] > 0
+    assert tw["completion_tokens"] == tw["requested_tokens"] > 0
 
 
 def test_bench_self_launches_ranks():

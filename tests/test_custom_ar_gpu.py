@@ -46,3 +46,15 @@ def test_tp2_push_decode_one_gpu():
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=400)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert r.stdout.count("tp push ok") == 2, r.stdout[-2000:]
+
+
+@pytest.mark.gpu
+def test_custom_ar_timeout_recovery():
+    """A peer stalled past the P2P wait bound: the TP engine resets the all-reduce state on every rank and
+    re-runs the stage on the torch.distributed path (VERDICT r3 #5; reference retry llm_executor.py:198-228)."""
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+           "--master-port", str(_port()), os.path.join(ROOT, "tests", "_ar_recover_worker.py")]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.stdout.count("ar recovery ok") == 2, r.stdout[-2000:]

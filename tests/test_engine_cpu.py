@@ -59,15 +59,16 @@ def test_eos_stops(eng):
     # force EOS: find the greedy first token of a prompt and declare it EOS
     p = _prompts(1)
     first = eng.generate(p, [SamplingParams(1, 0.0, 0)])[0].token_ids[0]
-    eos_backup = eng.state.eos.clone(), eng.state.n_eos
-    eng.state.eos[0] = first
-    eng.state.n_eos = 1
+    eos_backup = list(eng.state.eos_ids)
+    eng.state.set_eos([first])
     try:
         o = eng.generate(p, [SamplingParams(10, 0.0, 0)])[0]
+        pinned = eng.generate(p, [SamplingParams(10, 0.0, 0)], ignore_eos=True)[0]
+        assert eng.state.eos_ids == [first]  # restored after the ignore_eos call
     finally:
-        eng.state.eos.copy_(eos_backup[0])
-        eng.state.n_eos = eos_backup[1]
+        eng.state.set_eos(eos_backup)
     assert o.token_ids == [first] and o.finish_reason == "stop"
+    assert len(pinned.token_ids) == 10 and pinned.finish_reason == "length"
 
 
 def test_rejects_bad_requests(eng):
@@ -218,6 +219,52 @@ def test_prefill_oom_is_isolated(monkeypatch):
     monkeypatch.setattr(e, "_prefill", always)
     with pytest.raises(torch.OutOfMemoryError):
         e.generate(_prompts(1), ps[:1])
+
+
+def test_interleaved_prefill_oom_is_isolated(monkeypatch):
+    """Requests joining a RUNNING batch (interleaved prefill): a device OOM in a packed slice pass re-runs
+    the pass with half as many slices, down to one -- same tokens as without the fault, the running
+    sequence keeps decoding, and a single slice that still does not fit re-raises."""
+    def run(e):
+        fed = []
+
+        def feeder(done):
+            if fed:
+                return []
+            fed.append(1)
+            return [(p, SamplingParams(5, 0.3, 60 + i)) for i, p in enumerate(_prompts(4))]
+        return e.generate(_prompts(1), [SamplingParams(12, 0.3, 59)], feeder=feeder)
+
+    mk = lambda: LLMEngine(get_model_config("tiny", init_std=0.05), device="cpu", max_model_len=512,  # noqa: E731
+                           max_num_seqs=8, kv_pages=64, sync_every=3, max_prefill_tokens=4096)
+    ref = run(mk())
+    e = mk()
+    assert e.interleave
+    real = e.model.prefill
+    sizes = []
+
+    def flaky(ids, positions, seq_idx, cu, last, tables, *a, **kw):
+        if tables is e.pf_tables:
+            sizes.append(len(kw["seqlens"]))
+            if len(kw["seqlens"]) > 1:
+                raise torch.OutOfMemoryError("simulated HIP out of memory")
+        return real(ids, positions, seq_idx, cu, last, tables, *a, **kw)
+
+    monkeypatch.setattr(e.model, "prefill", flaky)
+    got = run(e)
+    assert [o.token_ids for o in got] == [o.token_ids for o in ref]
+    assert sizes[:3] == [4, 2, 1] and e.stats["prefill_oom_splits"] >= 2
+    assert e.stats.get("interleaved_prefills", 0) == 4
+    assert e.kv.alloc.available() == e.kv.num_pages - 1
+
+    def always(ids, positions, seq_idx, cu, last, tables, *a, **kw):
+        if tables is e.pf_tables:
+            raise torch.OutOfMemoryError("simulated HIP out of memory")
+        return real(ids, positions, seq_idx, cu, last, tables, *a, **kw)
+
+    monkeypatch.setattr(e.model, "prefill", always)
+    with pytest.raises(torch.OutOfMemoryError):
+        run(e)
 
 
 @pytest.mark.parametrize("chunk", [64, 192])

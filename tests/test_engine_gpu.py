@@ -202,3 +202,54 @@ def test_32k_prompt_joins_running_batch_interleaved():
     assert st_i["max_window_gap_s"] <= 1.5 * slice_s, (st_i["max_window_gap_s"], slice_s)
     # the blocking admission stalled the running rows for the whole (8-slice) prefill
     assert st_b["max_window_gap_s"] > 4 * slice_s, (st_b["max_window_gap_s"], slice_s)
+
+
+@pytest.mark.parametrize("capture_first", ["ignore", "honour"])
+def test_eos_is_read_at_graph_replay(capture_first):
+    """EOS handling must not depend on which generate captured the decode graphs (the stop ids are
+    device state read by the sampler at every replay, sampler.hip EOS_SLOTS): a decode-produced greedy
+    token declared EOS stops an EOS-honouring call and is ignored by an ignore_eos call, whichever of
+    the two ran (and captured) first -- and after an explicit capture_graphs() at start-up."""
+    def fresh():
+        e = LLMEngine(get_model_config("tiny-gqa4", init_std=0.05), device="cuda:0", max_model_len=1024,
+                      max_num_seqs=8, kv_pages=64, sync_every=4)
+        e.state.set_eos([])
+        return e
+
+    prompt = [[128000] + [(j * 29) % 50000 + 11 for j in range(60)]]
+    probe = fresh()
+    probe.use_graphs = False
+    ref = probe.generate(prompt, [SamplingParams(12, 0.0, 0)])[0].token_ids
+    k = next((i for i in range(3, 12) if ref[i] not in ref[:i]), None)
+    assert k is not None, "greedy sequence without a fresh decode-produced token"
+    stop = ref[k]
+    del probe
+    for eager_capture in (False, True):
+        eng = fresh()
+        eng.state.set_eos([stop])
+        if eager_capture:
+            assert eng.capture_graphs(max_batch=1) >= 1
+        calls = [("ignore", True), ("honour", False)]
+        if capture_first == "honour":
+            calls.reverse()
+        for name, ign in calls:
+            o = eng.generate(prompt, [SamplingParams(12, 0.0, 0)], ignore_eos=ign)[0]
+            if ign:
+                assert o.token_ids == ref and o.finish_reason == "length", (name, eager_capture)
+            else:
+                assert o.token_ids == ref[:k + 1] and o.finish_reason == "stop", (name, eager_capture)
+        assert eng.state.eos_ids == [stop]
+        assert eng.stats["graph_captures"] >= 1
+
+
+def test_gqa_ratio3_model_runs():
+    """A GQA 3:1 model (Llama-3.2-3B's ratio) prefills and decodes through the attention kernels'
+    per-query-head fallback; greedy decode agrees with a teacher-forced prefill."""
+    e = LLMEngine(get_model_config("tiny-gqa3", init_std=0.05), device="cuda:0", max_model_len=2048,
+                  max_num_seqs=8, kv_pages=128, sync_every=4)
+    prompts = _prompts()
+    outs = e.generate(prompts, [SamplingParams(8, 0.0, 0)] * len(prompts))
+    assert all(len(o.token_ids) == 8 for o in outs)
+    agree = sum(e.generate([p + o.token_ids[:-1]], [SamplingParams(1, 0.0, 0)])[0].token_ids[0] == o.token_ids[-1]
+                for p, o in zip(prompts, outs))
+    assert agree >= len(prompts) - 1

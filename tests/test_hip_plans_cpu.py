@@ -6,11 +6,12 @@ import pytest
 from llm_map_reduce_summarizer_amd.ops import hip
 
 
-@pytest.mark.parametrize("group", [1, 2, 4, 8])
+@pytest.mark.parametrize("group", [1, 2, 4, 8, 3, 5, 16])
 def test_prefill_items_cover_every_row_once(group):
     seqlens = [1, 63, 64, 65, 300, 4096]
     bm = hip.prefill_block_m(group)
-    assert bm == 256 // group
+    # packed GQA ratios: 256 / G positions per workgroup; others: per-query-head fallback, 256 positions
+    assert bm == (256 // group if group in (1, 2, 4, 8) else 256)
     items = hip.prefill_items(seqlens, group).tolist()
     assert len(items) == sum(-(-n // bm) for n in seqlens)
     seen = {s: [0] * n for s, n in enumerate(seqlens)}
@@ -23,10 +24,17 @@ def test_prefill_items_cover_every_row_once(group):
     assert starts == sorted(starts, reverse=True)  # heaviest (latest) blocks first
 
 
-def test_prefill_block_m_rejects_other_ratios():
-    for g in (3, 16):
+def test_prefill_block_m_rejects_bad_ratios():
+    for g in (0, 65):
         with pytest.raises(ValueError):
             hip.prefill_block_m(g)
+
+
+def test_decode_groups():
+    assert hip.decode_groups(32, 8) == 8 and hip.decode_groups(64, 8) == 8 and hip.decode_groups(16, 1) == 1
+    assert hip.decode_groups(24, 8) == 24  # ratio 3: one group per query head
+    with pytest.raises(ValueError):
+        hip.decode_groups(24, 7)
 
 
 def test_decode_attn_plan_measured_choices():

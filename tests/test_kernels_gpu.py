@@ -94,7 +94,8 @@ def test_swiglu_embed():
     assert torch.equal(hip.embed(ids, table), reference.embed(ids, table))
 
 
-@pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (2, 2)])
+# (6, 2) / (24, 8) / (10, 2): GQA ratios 3 and 5 (Llama-3.2-3B is 24 / 8) take the per-query-head fallback
+@pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (2, 2), (6, 2), (24, 8), (10, 2)])
 @pytest.mark.parametrize("seqlens", [[1, 37, 130, 300], [64], [129, 256], [1000, 33, 2100]])
 def test_attn_prefill(hq, hkv, seqlens):
     d = 128
@@ -107,7 +108,7 @@ def test_attn_prefill(hq, hkv, seqlens):
     _close(o1, o2, 2e-2)
 
 
-@pytest.mark.parametrize("hq,hkv", [(4, 1), (8, 2), (8, 1), (2, 2)])
+@pytest.mark.parametrize("hq,hkv", [(4, 1), (8, 2), (8, 1), (2, 2), (6, 2)])
 @pytest.mark.parametrize("spans", [[(0, 200)], [(130, 300), (0, 77), (1000, 1129)], [(64, 128), (2047, 2048)]])
 def test_attn_prefill_paged(hq, hkv, spans):
     """Chunked-prefill attention: slice rows attend to [0, prefix + slice) of their sequence read from the
@@ -151,7 +152,7 @@ def test_attn_prefill_spike(hq):
     _close(hip.attn_prefill(qkv, cu, hq, hkv, d, sc), reference.attn_prefill(qkv, cu, hq, hkv, d, sc), 2e-2)
 
 
-@pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (4, 4), (16, 1)])
+@pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (4, 4), (16, 1), (6, 2), (24, 8), (10, 2)])
 @pytest.mark.parametrize("splits", [1, 3, 16, 48])
 @pytest.mark.parametrize("fused", [False, True])
 def test_attn_decode(hq, hkv, splits, fused):
@@ -173,7 +174,7 @@ def test_attn_decode(hq, hkv, splits, fused):
     pos = torch.tensor([c - 1 for c in ctxs], dtype=torch.int32, device=DEV)
     q = _rand(B, (hq + 2 * hkv) * d, seed=14)
     sc = 1.0 / math.sqrt(d)
-    ws = hip.DecodeWorkspace(B, hq, d, splits, DEV, hkv, fused_combine=fused)
+    ws = hip.DecodeWorkspace(B, hq, d, splits, DEV, hip.decode_groups(hq, hkv), fused_combine=fused)
     # poisoned workspace (a reused allocation may hold NaN / inf): splits past a short context must not
     # leave stale slabs for the merge to multiply by a zero weight (0 x NaN = NaN)
     ws.part_o.fill_(float("nan"))
@@ -199,7 +200,6 @@ class _St:
         self.temps = torch.tensor(temps, dtype=torch.float32, device=DEV)
         self.seeds = torch.tensor(seeds, dtype=torch.int64, device=DEV)
         self.eos = torch.tensor([7, -1, -1, -1], **i32)
-        self.n_eos = 1
 
 
 def test_sampler_greedy_and_gumbel():
@@ -457,7 +457,7 @@ def test_fp8_swiglu_and_quant():
     assert (q.float() == ref_q.float()).float().mean().item() > 0.98
 
 
-@pytest.mark.parametrize("hq,hkv,S", [(32, 8, 4), (4, 1, 1), (16, 1, 3), (8, 2, 2), (4, 1, 16)])
+@pytest.mark.parametrize("hq,hkv,S", [(32, 8, 4), (4, 1, 1), (16, 1, 3), (8, 2, 2), (4, 1, 16), (6, 2, 2), (24, 8, 4)])
 @pytest.mark.parametrize("fused_combine", [False, True])
 def test_attn_decode_rope_fused(hq, hkv, S, fused_combine):
     """attn_decode_rope (q/k RoPE + new K/V written into the cache + attention, from the QKV GEMM's
@@ -487,7 +487,8 @@ def test_attn_decode_rope_fused(hq, hkv, S, fused_combine):
     qkv = reference.rope_kv_parts(parts, pos, sidx, bt, k2, v2, cs, hq, hkv, d, page)
     o2 = reference.attn_decode(qkv, k2, v2, bt, pos, hq, hkv, d, page, sc)
     k1, v1 = kc0.clone().to(DEV), vc0.clone().to(DEV)
-    ws = hip.DecodeWorkspace(B, hq, d, hip.decode_splits(B, hkv, 20 * page), DEV, hkv, fused_combine=fused_combine)
+    ng = hip.decode_groups(hq, hkv)
+    ws = hip.DecodeWorkspace(B, hq, d, hip.decode_splits(B, ng, 20 * page), DEV, ng, fused_combine=fused_combine)
     ws.part_o.fill_(float("nan"))  # poisoned workspace: empty splits must publish zero slabs
     for _ in range(3):  # idempotent: later calls rewrite the same K/V row (and re-armed merge tickets)
         o1 = hip.attn_decode_rope(parts, cs, k1, v1, bt, pos, hq, hkv, d, page, sc, workspace=ws)

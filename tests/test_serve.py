@@ -169,6 +169,24 @@ def test_shutdown_answers_queued_requests():
     assert r1.error == r2.error == "server shutting down"
 
 
+def test_enqueue_after_drain_is_refused():
+    """The stop check and the put are atomic against the drain: once _drain ran (even with the stop flag
+    not yet set, the window of the submit / stop race), nothing can enter the queue unanswered."""
+    class _Prov:
+        class par:
+            world = 1
+        tp = 1
+    b = ContinuousBatcher(_Prov(), max_batch=4)
+    b._drain()
+    assert not b.stop.is_set()
+    assert b._enqueue(("late", None, None)) is False and b.q.empty()
+
+    async def run():
+        return await b.submit(GenRequest(user="late")), [x async for x in b.stream(GenRequest(user="late"))]
+    r, st = asyncio.run(run())
+    assert r.error == "server shutting down" and st[-1][1].error == "server shutting down"
+
+
 def test_multi_turn_stream_models_health_metrics(server):
     _, _, base = server
     body = {"messages": [{"role": "system", "content": "s"}, {"role": "user", "content": "hi"},
