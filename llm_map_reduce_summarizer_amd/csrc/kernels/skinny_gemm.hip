@@ -28,6 +28,14 @@
 //    the TP push all-reduce when ``tp.world`` > 0, ar_common.h), per-tile row sums of squares to ssp.
 //    A TP-shard row-parallel projection (K <= 2048) keeps this kernel's launch floor instead of the
 //    stream kernel's ring ramp.
+//    Progress of the TP push here: EVERY workgroup pushes its tile and then spins on its peers' copies
+//    of the same tile (no split-K, so no "one spinner per tile" bound as in stream_gemm.hip).  A rank's
+//    spinners wait only for tiles its peers' workgroups push BEFORE spinning, so the grid completes on
+//    every rank iff each peer eventually dispatches every workgroup -- guaranteed when the whole grid is
+//    resident at once (dispatch never waits for a spinner to retire).  The launcher therefore refuses a
+//    TP-push grid larger than the device's resident capacity for this kernel (occupancy x CUs,
+//    mrsum_skinny_resid_capacity; ops/__init__.py picks the stream producer then), and the 4 s wait bound
+//    + the engine's collective reset / RCCL re-run (parallel/custom_ar.py) cover a stall anyway.
 #include "ar_common.h"
 
 namespace {
@@ -276,6 +284,22 @@ static int launch_mt(int mt, dim3 grid, hipStream_t s, const bf16* x, int ldx, c
     return (int)hipGetLastError();
 }
 
+// Workgroups of the residual-update (TP push) instantiation that can be resident on this device at once:
+// occupancy per CU x CUs (header: a TP-push grid must fit, every workgroup spins on its peers).
+MRSUM_API int mrsum_skinny_resid_capacity() {
+    static int cap = -1;
+    if (cap < 0) {
+        int dev = 0, cus = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, skinny_gemm_kernel<1, 1, EPI_RESID>, 256, 0) !=
+                hipSuccess)
+            return 0;
+        cap = cus * per;
+    }
+    return cap;
+}
+
 // epi: 0 bf16 [M, ldo], 1 fp32 partial [S, M, ldo], 2 swiglu bf16 [M, ldo] (ldo >= N/2), 3 residual update
 // (resid [M, ldr] bf16 += x W^T, ssp fp32 [M, N / 16] per-tile row sums of squares of the new residual;
 // nt 1, splits 1, M <= 16; ``ar`` non-null: all-reduced over that custom all-reduce group first (TP push,
@@ -300,6 +324,7 @@ MRSUM_API int mrsum_skinny_gemm(const void* x, int ldx, const void* W, int N, in
         for (int r = 0; r < h->world; ++r)
             if (!h->peers.base[r]) return (int)hipErrorInvalidValue;
     }
+    if (ar && N / 16 > mrsum_skinny_resid_capacity()) return (int)hipErrorInvalidValue;  // header: progress
     SkinnyNorm e;
     e.ssq = ssq; e.ssq_tiles = ssq_tiles; e.inv_k = 1.f / (float)K; e.eps = eps;
     e.resid = (bf16*)resid; e.ldr = ldr; e.ssp = ssp;

@@ -387,7 +387,8 @@ def _resid_plan(hip, a, w, role, tp=False):
             return ("skinny",)
         if tp:
             force = os.environ.get("MRSUM_TP_RESID_KERNEL", "auto")
-            if (force == "skinny" or (force == "auto" and p[0] == "skinny")) and N % 512 == 0:
+            if (force == "skinny" or (force == "auto" and p[0] == "skinny")) and N % 512 == 0 \
+                    and N // 16 <= hip.skinny_resid_capacity():  # every pushing workgroup resident at once
                 return ("skinny",)
             if cfg is None or force == "stream":
                 cfg = hip.tp_resid_config(N, K)

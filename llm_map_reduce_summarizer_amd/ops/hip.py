@@ -41,6 +41,7 @@ _SIGS = {
                                _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp],
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int,
                           _c_float, _vp, _c_int, _vp, _vp, _vp],
+    "mrsum_skinny_resid_capacity": [],
     "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_stream_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp,
                           _vp, _c_int, _c_float, _vp, _c_int, _vp, _c_int, _vp, _vp],
@@ -833,6 +834,17 @@ def stream_resid(x: torch.Tensor, w, residual: torch.Tensor, wpb: int, splits: i
     return ssp
 
 
+_RESID_CAP = []
+
+
+def skinny_resid_capacity() -> int:
+    """Workgroups of the register-streaming residual producer resident at once on this device (a TP-push
+    grid of N / 16 workgroups must fit: every one spins on its peers' copies of its tile)."""
+    if not _RESID_CAP:
+        _RESID_CAP.append(int(_fn("mrsum_skinny_resid_capacity")()))
+    return _RESID_CAP[0]
+
+
 def skinny_resid(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, tp=None) -> torch.Tensor:
     """Deferred-RMSNorm producer on the register-streaming kernel (one 16-row tile per workgroup, no
     split-K, M <= 16): residual += x @ w^T -- all-reduced over the custom all-reduce group ``tp`` first
@@ -841,6 +853,8 @@ def skinny_resid(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, tp=No
     N = w.shape[0]
     ssp = torch.empty(M, N // 16, dtype=torch.float32, device=x.device)
     if tp is not None:
+        _req(N // 16 <= skinny_resid_capacity(), "skinny_resid: TP-push grid of %d workgroups is not fully "
+             "resident (capacity %d)" % (N // 16, skinny_resid_capacity()))
         STATS["tp_push"] += 1
     _skinny(x, w, None, EPI_SKINNY_RESID, 1, 1, 0, resid=residual, ssp=ssp, ar=tp)
     return ssp
