@@ -252,11 +252,14 @@ class LlamaModel:
     # next column-parallel GEMM -- the same bytes on the links as the all-reduce, 1 / TP of the norm work
     # and residual memory.  Rows are padded to a multiple of TP.
     def _sp_backend_ok(self) -> bool:
-        """Reduce-scatter of device tensors needs RCCL (gloo takes CPU tensors only: CPU ranks, or the
-        shared-GPU rehearsals, which then keep the all-reduces)."""
-        if self.device.type != "cuda":
-            return True
-        return torch.distributed.get_backend(self.tp_group) == "nccl"
+        """Sequence parallelism runs on every backend: RCCL natively, gloo on CPU tensors, and gloo over GPU
+        tensors (ranks sharing one GPU: rehearsals, the TP parity test) through host-staged collectives
+        (_sp_host)."""
+        return True
+
+    def _sp_host(self) -> bool:
+        """Device tensors over a non-RCCL group (gloo): stage the SP collectives through host memory."""
+        return self.device.type == "cuda" and torch.distributed.get_backend(self.tp_group) != "nccl"
 
     def _sp_rows(self, T: int):
         Tp = -(-T // self.tp_size) * self.tp_size
@@ -279,11 +282,19 @@ class LlamaModel:
         Tp, Ts = self._sp_rows(T)
         if Tp != T:
             t = torch.cat([t, torch.zeros(Tp - T, t.shape[1], dtype=t.dtype, device=t.device)])
+        if self._sp_host():  # gloo: synchronous, through host memory
+            cpu = torch.empty(Ts, t.shape[1], dtype=t.dtype)
+            torch.distributed.reduce_scatter_tensor(cpu, t.contiguous().cpu(), group=self.tp_group)
+            return cpu.to(t.device), None
         out = torch.empty(Ts, t.shape[1], dtype=t.dtype, device=t.device)
         h = torch.distributed.reduce_scatter_tensor(out, t.contiguous(), group=self.tp_group, async_op=True)
         return out, h
 
     def _sp_all_gather(self, shard: torch.Tensor, T: int) -> torch.Tensor:
+        if self._sp_host():
+            cpu = torch.empty(shard.shape[0] * self.tp_size, shard.shape[1], dtype=shard.dtype)
+            torch.distributed.all_gather_into_tensor(cpu, shard.contiguous().cpu(), group=self.tp_group)
+            return cpu.to(shard.device)[:T]
         out = torch.empty(shard.shape[0] * self.tp_size, shard.shape[1], dtype=shard.dtype, device=shard.device)
         torch.distributed.all_gather_into_tensor(out, shard.contiguous(), group=self.tp_group)
         return out[:T]
