@@ -100,6 +100,9 @@ def main() -> int:
                     help="single-pass reduce over every summary (use a long-context model, e.g. llama3.1-8b)")
     ap.add_argument("--stream-reduce", action="store_true",
                     help="start each level-1 reduce batch as soon as its chunks are summarised (no map barrier)")
+    ap.add_argument("--kv-dtype", choices=["bf16", "fp8"], default="bf16",
+                    help="KV cache format; fp8 (e4m3 rows, power-of-two row scales) is a LABELLED variant: the "
+                         "headline is bf16 KV")
     ap.add_argument("--profile", default=None, metavar="DIR", help="torch.profiler trace of the timed steps")
     ap.add_argument("--log-level", default="WARNING")
     args = ap.parse_args()
@@ -130,7 +133,7 @@ def main() -> int:
 
     cfg = LLMConfig(MAX_TOKENS=args.max_new_tokens, TEMPERATURE=0.3, REDUCE_TEMPERATURE=0.2)
     provider = LocalEngineProvider(args.model, cfg, use_graphs=not args.no_graphs, ignore_eos=not args.stop_at_eos,
-                                   parallel=args.parallel)
+                                   parallel=args.parallel, kv_dtype=args.kv_dtype)
     executor = LLMExecutor(config=cfg, provider_obj=provider)
     summarizer = TranscriptSummarizer(executor=executor, max_tokens_per_chunk=args.chunk_tokens,
                                       hierarchical_aggregation=not args.no_hierarchical,
@@ -186,10 +189,11 @@ def main() -> int:
     out = {
         "metric": "chunks/sec (whole node) + end-to-end wall-clock, 10h transcript, Llama-3-8B"
                   + ("" if args.model == "llama3-8b" and args.hours == 10.0 and not args.no_hierarchical
-                     and not args.stream_reduce
-                     else " [variant: %s, %gh%s%s]" % (args.model, args.hours,
-                                                       ", single-pass reduce" if args.no_hierarchical else "",
-                                                       ", streamed level-1 reduce" if args.stream_reduce else "")),
+                     and not args.stream_reduce and args.kv_dtype == "bf16"
+                     else " [variant: %s, %gh%s%s%s]" % (args.model, args.hours,
+                                                         ", single-pass reduce" if args.no_hierarchical else "",
+                                                         ", streamed level-1 reduce" if args.stream_reduce else "",
+                                                         ", fp8 KV cache" if args.kv_dtype == "fp8" else "")),
         "value": round(value, 4),
         "unit": "chunks/s",
         "n_gpus": world,
@@ -200,6 +204,7 @@ def main() -> int:
         "scaling": "strong",
         "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
         "dtype": "bf16",
+        "kv_dtype": args.kv_dtype,
         "data": ("synthetic %gh transcript (utils/synth.py, seed 0); random-init weights; every generation "
                  "pinned to max_new_tokens%s" % (args.hours, " (EOS honoured)" if args.stop_at_eos else "")),
         "config": {"model": args.model, "global_batch": n_chunks, "seq_len": args.chunk_tokens,

@@ -76,6 +76,9 @@ def build_parser() -> argparse.ArgumentParser:
     e.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (ranks per model replica)")
     e.add_argument("--seed", type=int, default=None)
     e.add_argument("--kv-fraction", type=float, default=None, help="fraction of free HBM for the KV cache")
+    e.add_argument("--kv-dtype", choices=["bf16", "fp8"], default=None,
+                   help="KV cache format: bf16 (default, $ENGINE_KV_DTYPE) or fp8 = OCP e4m3fn rows with power-of-two "
+                        "row scales (half the KV bytes per decode step; no context-parallel prefill)")
     e.add_argument("--no-graphs", action="store_true", help="disable hipGraph capture of decode steps")
     e.add_argument("--max-model-len", type=int, default=None,
                    help="context budget per request (default: 32k for llama3-*, the model window for llama3.1-*); "
@@ -139,6 +142,7 @@ async def async_main(args: argparse.Namespace) -> int:
         popts["fault_rate"] = args.fault_inject
     if provider == "local":
         popts.update({"dtype": args.dtype, "tp": args.tp, "seed": args.seed, "kv_fraction": args.kv_fraction,
+                      "kv_dtype": args.kv_dtype,
                       "use_graphs": not args.no_graphs, "tokenizer": args.tokenizer,
                       "max_num_seqs": args.max_concurrent_requests, "reduce_tp": args.reduce_tp,
                       "parallel": args.parallel,

@@ -61,6 +61,7 @@ class LLMConfig:
         # engine (new)
         "LOCAL_MODEL": ("llama3-8b", str), "ENGINE_DTYPE": ("bf16", str), "ENGINE_SEED": ("0", int),
         "ENGINE_MAX_NUM_SEQS": ("256", int), "ENGINE_KV_FRACTION": ("0.6", float),
+        "ENGINE_KV_DTYPE": ("bf16", str),
         "REDUCE_TEMPERATURE": ("0.2", float),
         # hosted-provider endpoints (new): point the adapters at any compatible server
         "OPENAI_BASE_URL": ("https://api.openai.com/v1", str),

@@ -22,7 +22,7 @@
 // With no counter buffer a separate combine kernel is launched instead.
 // Context length = positions[b] + 1 is read on the device, so the launch
 // shape is fixed and the kernel can live inside a captured decode graph.
-#include "common.h"
+#include "kv8.h"
 
 constexpr int MAX_SPLITS = 64;
 
@@ -275,13 +275,19 @@ __device__ __forceinline__ void rope_slab_sums(const RopeArgs& ra, const float* 
 }
 
 // KV page loads: nontemporal (each page is read once per step by one workgroup) when NT
-template <bool NT>
-__device__ __forceinline__ u32x4 ld_kv(const bf16* p) {
+template <bool NT, typename T>
+__device__ __forceinline__ u32x4 ld_kv(const T* p) {
     if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
     else return *reinterpret_cast<const u32x4*>(p);
 }
 
-template <int G, bool ROPE, bool NT = false>
+// KV8 (FP8 KV cache, kv8.h): each (page, kv head) is an 8.25 KiB slab of e4m3 rows + fp32 row scales.
+// The staging loads half the bytes (thread -> row tid / 8 + 32 i, 16-B chunk tid % 8 = 16 dims, 2 rows per
+// tile per thread) plus each row's scale, and converts every row to bf16 exactly (power-of-two scales)
+// while writing it into the SAME LDS image the bf16 cache fills: QK^T, softmax and PV are unchanged.
+// The fused RoPE writer quantises the new token's rows (kv8 row rule) and patches their DEQUANTISED
+// values into the tile, so this step and later steps see the same K/V.
+template <int G, bool ROPE, bool NT = false, bool KV8 = false>
 __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     const bf16* __restrict__ q, int q_stride, bf16* __restrict__ kc, bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ positions,
@@ -329,6 +335,12 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     const int* bt = block_tables + (size_t)b * bt_stride + ks / PG;
     const int st_row = tid >> 4, st_chunk = tid & 15;
     const size_t head_off = (size_t)kvr * PG * D + (size_t)st_row * D + st_chunk * 8;
+    // KV8 staging: row r8 + 32 i, 16-B fp8 chunk c8 (dims 16 c8 .. +16) of the (page, head) slab
+    const int r8 = tid >> 3, c8 = tid & 7;
+    const size_t head8 = (size_t)kvr * kv8::SLAB;
+    const unsigned char* kc8 = reinterpret_cast<const unsigned char*>(kc);
+    const unsigned char* vc8 = reinterpret_cast<const unsigned char*>(vc);
+    float ksc[2], vsc[2], ksc2[2], vsc2[2];  // KV8: row scales of register sets A and B
     // staging registers are plain named arrays indexed only by unrolled constants (a lambda
     // capturing them by reference put them in scratch), and the prefetch is unconditional (no
     // branch around the loads) so hipcc keeps them in flight.
@@ -339,17 +351,28 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     // overshoot shares and so stays in L2 (re-reading the workgroup's own last tile cost ~9 % extra HBM
     // traffic at B=39, PMC FETCH_SIZE).
     u32x4 kreg[4], vreg[4], kreg2[4], vreg2[4];
-#define KV_ISSUE(KR, VR, TILE)                                                          \
-    {                                                                                   \
-        const int pg_ = bt[min((TILE), ntiles - 1)];                                    \
-        const size_t base_ = (size_t)((TILE) < ntiles ? pg_ : 0) * Hc * PG * D + head_off;  \
-        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                 \
-            KR[i] = ld_kv<NT>(kc + base_ + (size_t)16 * i * D);                         \
-            VR[i] = ld_kv<NT>(vc + base_ + (size_t)16 * i * D);                         \
-        }                                                                               \
+#define KV_ISSUE(KR, VR, KS, VS, TILE)                                                              \
+    {                                                                                               \
+        const int pg_ = bt[min((TILE), ntiles - 1)];                                                \
+        if constexpr (KV8) {                                                                        \
+            const size_t base_ = (size_t)((TILE) < ntiles ? pg_ : 0) * Hc * kv8::SLAB + head8;      \
+            _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                         \
+                const size_t ro_ = base_ + (size_t)(r8 + 32 * i) * D + 16 * c8;                      \
+                KR[i] = ld_kv<NT>(kc8 + ro_);                                                       \
+                VR[i] = ld_kv<NT>(vc8 + ro_);                                                       \
+                KS[i] = *reinterpret_cast<const float*>(kc8 + base_ + PG * D + 4 * (r8 + 32 * i));  \
+                VS[i] = *reinterpret_cast<const float*>(vc8 + base_ + PG * D + 4 * (r8 + 32 * i));  \
+            }                                                                                       \
+        } else {                                                                                    \
+            const size_t base_ = (size_t)((TILE) < ntiles ? pg_ : 0) * Hc * PG * D + head_off;      \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                         \
+                KR[i] = ld_kv<NT>(kc + base_ + (size_t)16 * i * D);                                 \
+                VR[i] = ld_kv<NT>(vc + base_ + (size_t)16 * i * D);                                 \
+            }                                                                                       \
+        }                                                                                           \
     }
-    KV_ISSUE(kreg, vreg, 0)
-    KV_ISSUE(kreg2, vreg2, 1)
+    KV_ISSUE(kreg, vreg, ksc, vsc, 0)
+    KV_ISSUE(kreg2, vreg2, ksc2, vsc2, 1)
     // ROPE: the q rows of this group (and, for the split holding the new token, its K and V rows)
     // summed over the SP slabs by ALL 256 threads in one round of independent loads into an fp32
     // LDS image (aliasing the K/V tile buffers, which are first written after it is consumed):
@@ -368,23 +391,47 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
             const int page = block_tables[(size_t)b * bt_stride + pos / PG];
             const size_t dst = ((size_t)page * Hc * PG + (size_t)kvr * PG + (pos % PG)) * D;
             const float* kr = sq + G * D;
-            if (tid < D / 8) {  // rotated K chunk tid (8 dims), into the cache and the LDS patch row
-                const int c = tid * 8, cl = c & (D / 2 - 1);
+            if (tid < D / 4) {  // lanes 0-15: rotated K chunk (8 dims); 16-31: V chunk -> cache + LDS patch row
+                const bool isk = tid < D / 8;
+                const int c = (isk ? tid : tid - D / 8) * 8, cl = c & (D / 2 - 1);
                 float kv[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const float2 e = cs[cl + j];
-                    const float lo = kr[cl + j], hi = kr[cl + j + D / 2];
-                    kv[j] = c < D / 2 ? lo * e.x - hi * e.y : hi * e.x + lo * e.y;
+                    if (isk) {
+                        const float2 e = cs[cl + j];
+                        const float lo = kr[cl + j], hi = kr[cl + j + D / 2];
+                        kv[j] = c < D / 2 ? lo * e.x - hi * e.y : hi * e.x + lo * e.y;
+                    } else {
+                        kv[j] = kr[D + c + j];
+                    }
                 }
-                const uint4 pk = pack8(kv);
-                *reinterpret_cast<uint4*>(kc + dst + c) = pk;
-                *reinterpret_cast<uint4*>(lds_new + c) = pk;
-            } else if (tid < D / 4) {
-                const int c = (tid - D / 8) * 8;
-                const uint4 pv = pack8(kr + D + c);
-                *reinterpret_cast<uint4*>(vc + dst + c) = pv;
-                *reinterpret_cast<uint4*>(lds_new + D + c) = pv;
+                bf16* pdst = lds_new + (isk ? 0 : D) + c;
+                if constexpr (KV8) {
+                    // quantise the bf16-rounded row, as every other writer does (rope_kv.hip), then the row's 16
+                    // lanes (K: 0-15, V: 16-31) reduce max|x| (kv8.h row rule)
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) kv[j] = (float)(bf16)kv[j];
+                    float amax = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(kv[j]));
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+                    const float sc = kv8::row_scale(amax), inv = 1.f / sc;
+                    const uint2 q = make_uint2(kv8::pack4(kv[0] * inv, kv[1] * inv, kv[2] * inv, kv[3] * inv),
+                                               kv8::pack4(kv[4] * inv, kv[5] * inv, kv[6] * inv, kv[7] * inv));
+                    unsigned char* cb = reinterpret_cast<unsigned char*>(isk ? kc : vc) +
+                                        (size_t)page * Hc * kv8::SLAB + head8;
+                    *reinterpret_cast<uint2*>(cb + (size_t)(pos % PG) * D + c) = q;
+                    if (c == 0) *reinterpret_cast<float*>(cb + PG * D + 4 * (pos % PG)) = sc;
+                    // patch row = the dequantised values later steps read back
+                    u32x4 lo, hi;
+                    kv8::dequant16(u32x4{q.x, q.y, 0u, 0u}, sc, lo, hi);
+                    *reinterpret_cast<u32x4*>(pdst) = lo;
+                } else {
+                    const uint4 pk = pack8(kv);
+                    *reinterpret_cast<uint4*>((isk ? kc : vc) + dst + c) = pk;
+                    *reinterpret_cast<uint4*>(pdst) = pk;
+                }
             }
         }
     }
@@ -425,20 +472,40 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     // the new token's row (row pr of tile ptile) is staged from lds_new, not from the page loads
     const int ptile = has_pos ? (ctx - 1 - ks) / PG : -1;
     const int pr = (ctx - 1 - ks) % PG;
-    const bool patcher = has_pos && st_row == (pr & 15);
+    const bool patcher = has_pos && (KV8 ? r8 == (pr & 31) : st_row == (pr & 15));
     if constexpr (ROPE) {
         __syncthreads();  // every lane has its q out of the fp32 image the tiles overwrite
     }
-#define KV_WRITE(KR, VR, TILE)                                                                                  \
-    _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                             \
-        const bool pt = ROPE && ptile == (TILE) && patcher && i == (pr >> 4);                                   \
-        *reinterpret_cast<u32x4*>(ldsK + dk_off(st_row + 16 * i, st_chunk)) =                                   \
-            pt ? *reinterpret_cast<const u32x4*>(lds_new + st_chunk * 8) : KR[i];                               \
-        *reinterpret_cast<u32x4*>(ldsV + dv_off(st_row + 16 * i, st_chunk)) =                                   \
-            pt ? *reinterpret_cast<const u32x4*>(lds_new + D + st_chunk * 8) : VR[i];                           \
+#define KV_WRITE(KR, VR, KS, VS, TILE)                                                                          \
+    if constexpr (KV8) {                                                                                        \
+        _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                                         \
+            const bool pt = ROPE && ptile == (TILE) && patcher && i == (pr >> 5);                               \
+            const int row_ = r8 + 32 * i;                                                                       \
+            u32x4 klo, khi, vlo, vhi;                                                                           \
+            kv8::dequant16(KR[i], KS[i], klo, khi);                                                             \
+            kv8::dequant16(VR[i], VS[i], vlo, vhi);                                                             \
+            if (pt) {                                                                                           \
+                klo = *reinterpret_cast<const u32x4*>(lds_new + 16 * c8);                                       \
+                khi = *reinterpret_cast<const u32x4*>(lds_new + 16 * c8 + 8);                                   \
+                vlo = *reinterpret_cast<const u32x4*>(lds_new + D + 16 * c8);                                   \
+                vhi = *reinterpret_cast<const u32x4*>(lds_new + D + 16 * c8 + 8);                               \
+            }                                                                                                   \
+            *reinterpret_cast<u32x4*>(ldsK + dk_off(row_, 2 * c8)) = klo;                                      \
+            *reinterpret_cast<u32x4*>(ldsK + dk_off(row_, 2 * c8 + 1)) = khi;                                  \
+            *reinterpret_cast<u32x4*>(ldsV + dv_off(row_, 2 * c8)) = vlo;                                      \
+            *reinterpret_cast<u32x4*>(ldsV + dv_off(row_, 2 * c8 + 1)) = vhi;                                  \
+        }                                                                                                       \
+    } else {                                                                                                    \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                         \
+            const bool pt = ROPE && ptile == (TILE) && patcher && i == (pr >> 4);                               \
+            *reinterpret_cast<u32x4*>(ldsK + dk_off(st_row + 16 * i, st_chunk)) =                               \
+                pt ? *reinterpret_cast<const u32x4*>(lds_new + st_chunk * 8) : KR[i];                           \
+            *reinterpret_cast<u32x4*>(ldsV + dv_off(st_row + 16 * i, st_chunk)) =                               \
+                pt ? *reinterpret_cast<const u32x4*>(lds_new + D + st_chunk * 8) : VR[i];                       \
+        }                                                                                                       \
     }
-    KV_WRITE(kreg, vreg, 0)
-    KV_ISSUE(kreg, vreg, 2)
+    KV_WRITE(kreg, vreg, ksc, vsc, 0)
+    KV_ISSUE(kreg, vreg, ksc, vsc, 2)
 
     f32x4 o[8];
 #pragma unroll
@@ -487,15 +554,15 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
         compute(t);
         __syncthreads();
         if (t + 1 < ntiles) {
-            KV_WRITE(kreg2, vreg2, t + 1)
-            KV_ISSUE(kreg2, vreg2, t + 3)
+            KV_WRITE(kreg2, vreg2, ksc2, vsc2, t + 1)
+            KV_ISSUE(kreg2, vreg2, ksc2, vsc2, t + 3)
             __syncthreads();
             compute(t + 1);
             __syncthreads();
         }
         if (t + 2 < ntiles) {
-            KV_WRITE(kreg, vreg, t + 2)
-            KV_ISSUE(kreg, vreg, t + 4)
+            KV_WRITE(kreg, vreg, ksc, vsc, t + 2)
+            KV_ISSUE(kreg, vreg, ksc, vsc, t + 4)
             __syncthreads();
         }
     }
@@ -555,7 +622,7 @@ MRSUM_API int mrsum_attn_decode_groups(int Hq, int Hkv) {
 static int launch_mfma(const void* q, int q_stride, const void* kcache, const void* vcache, const int* block_tables,
                        int bt_stride, const int* positions, void* part_o, void* part_ml, void* out, int out_stride,
                        int B, int Hq, int Hkv, int D, int P, int S, float scale, const RopeArgs* rope, int* counters,
-                       hipStream_t s) {
+                       int kv8, hipStream_t s) {
     if (B <= 0) return 0;
     if (D != 128 || P != 64 || Hkv <= 0 || Hq % Hkv || Hq / Hkv > 64 || S < 1 || S > MAX_SPLITS)
         return (int)hipErrorInvalidValue;
@@ -568,16 +635,15 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
     auto Qp = (const bf16*)q; auto K = (bf16*)kcache; auto V = (bf16*)vcache;
     auto PO = (float*)part_o; auto PM = (float*)part_ml;
     const RopeArgs ra = rope ? *rope : RopeArgs{nullptr, 0, 0, 0, 0, nullptr};
+#define MFMA_K(G_, R_, NT_, K8_)                                                                                \
+    attn_decode_mfma_kernel<G_, R_, NT_, K8_><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride,  \
+                                                                     positions, PO, PM, Hkv, S, sl, ra, counters, \
+                                                                     (bf16*)out, out_stride, Hc, gq)
 #define MFMA_L(G_, R_)                                                                                        \
     do {                                                                                                      \
-        if (B * Hkv >= NT_MIN_GROUPS)                                                                       \
-            attn_decode_mfma_kernel<G_, R_, true><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, \
-                                                                         positions, PO, PM, Hkv, S, sl, ra, counters, \
-                                                                         (bf16*)out, out_stride, Hc, gq);     \
-        else                                                                                                  \
-            attn_decode_mfma_kernel<G_, R_, false><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, \
-                                                                          positions, PO, PM, Hkv, S, sl, ra, counters, \
-                                                                          (bf16*)out, out_stride, Hc, gq);    \
+        const bool nt_ = B * Hkv >= NT_MIN_GROUPS;                                                            \
+        if (kv8) { if (nt_) MFMA_K(G_, R_, true, true); else MFMA_K(G_, R_, false, true); }                   \
+        else { if (nt_) MFMA_K(G_, R_, true, false); else MFMA_K(G_, R_, false, false); }                     \
     } while (0)
 #define MFMA_G(R_)                            \
     switch (G) {                              \
@@ -591,6 +657,7 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
     if (rope) { MFMA_G(true) } else { MFMA_G(false) }
 #undef MFMA_G
 #undef MFMA_L
+#undef MFMA_K
     int e = (int)hipGetLastError();
     if (e || counters) return e;
     if (S > 16) {
@@ -613,9 +680,9 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
 MRSUM_API int mrsum_attn_decode_mfma(const void* q, int q_stride, const void* kcache, const void* vcache,
                                      const int* block_tables, int bt_stride, const int* positions, void* part_o,
                                      void* part_ml, void* out, int out_stride, int B, int Hq, int Hkv, int D, int P,
-                                     int S, float scale, int* counters, hipStream_t s) {
+                                     int S, float scale, int* counters, int kv8, hipStream_t s) {
     return launch_mfma(q, q_stride, kcache, vcache, block_tables, bt_stride, positions, part_o, part_ml, out,
-                       out_stride, B, Hq, Hkv, D, P, S, scale, nullptr, counters, s);
+                       out_stride, B, Hq, Hkv, D, P, S, scale, nullptr, counters, kv8, s);
 }
 
 // Decode attention straight from the QKV GEMM's fp32 split-K slabs [SP, B, (Hq + 2 Hkv) D]: RoPE on q,
@@ -623,10 +690,10 @@ MRSUM_API int mrsum_attn_decode_mfma(const void* q, int q_stride, const void* kc
 MRSUM_API int mrsum_attn_decode_rope(const void* qkv_parts, int SP, const void* cos_sin, void* kcache, void* vcache,
                                      const int* block_tables, int bt_stride, const int* positions, void* part_o,
                                      void* part_ml, void* out, int out_stride, int B, int Hq, int Hkv, int D, int P,
-                                     int S, float scale, int* counters, hipStream_t s) {
+                                     int S, float scale, int* counters, int kv8, hipStream_t s) {
     if (SP < 1 || !qkv_parts || !cos_sin) return (int)hipErrorInvalidValue;
     const int width = (Hq + 2 * Hkv) * D;
     const RopeArgs ra{(const float*)qkv_parts, (size_t)B * width, SP, width, Hq, (const float2*)cos_sin};
     return launch_mfma(nullptr, 0, kcache, vcache, block_tables, bt_stride, positions, part_o, part_ml, out,
-                       out_stride, B, Hq, Hkv, D, P, S, scale, &ra, counters, s);
+                       out_stride, B, Hq, Hkv, D, P, S, scale, &ra, counters, kv8, s);
 }

@@ -42,8 +42,12 @@
 // contiguous -- for positions [0, prefix + slice), and query row qi sits at absolute position
 // prefix + qi (causal offset).  With prefix = 0 it is the same attention as the contiguous path.
 //
+// PAGED + KV8 (fp8 KV cache, kv8.h): a 64-key tile is one (page, head) slab of e4m3 rows + row scales;
+// each thread loads one 16-B chunk (16 dims) of one row of K and of V plus the two row scales, and the
+// store converts them exactly to bf16 into the same LDS image (the rest of the kernel is unchanged).
+//
 // Numerics: bf16 inputs, fp32 accumulation and softmax, bf16 output.
-#include "common.h"
+#include "kv8.h"
 
 namespace {
 constexpr int D = 128;
@@ -90,7 +94,7 @@ struct PagedKV {
 // Other GQA ratios (e.g. Llama-3.2-3B: 24 / 8 = 3) run the G = 1 instantiation over Hg = Hq "virtual kv
 // heads", one per query head, each reading the K/V columns of its real kv head h / gq (gq = Hq / Hkv):
 // no K/V reuse across the group inside a workgroup, but any ratio works.  Hg = Hkv and gq = 1 otherwise.
-template <bool PAGED, int G>
+template <bool PAGED, int G, bool KV8 = false>
 __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __restrict__ qkv, int row_stride,
                                                               const int* __restrict__ cu_seqlens,
                                                               const int2* __restrict__ items,
@@ -148,8 +152,20 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
     // made hipcc serialise the loop on vmcnt(0).
     const int st_chunk = tid & 15, st_row0 = tid >> 4;
     u32x4 kreg[SIT], vreg[SIT];
+    // KV8: row tid / 8 (0..63) of the slab, 16-B chunk tid % 8; one round per tile
+    const int r8 = tid >> 3, c8 = tid & 7;
+    float ks8 = 1.f, vs8 = 1.f;
+    static_assert(!KV8 || NTHR / 8 == BN, "KV8 staging: one slab row per 8 threads");
 #define LOAD_TILE(t)                                                                              \
-    if constexpr (PAGED) {                                                                        \
+    if constexpr (PAGED && KV8) {                                                                 \
+        const size_t sb = kv8::slab_off(btab[t], Hkv, kvh);                                       \
+        const unsigned char* kb_ = reinterpret_cast<const unsigned char*>(pk.kc) + sb;           \
+        const unsigned char* vb_ = reinterpret_cast<const unsigned char*>(pk.vc) + sb;           \
+        kreg[0] = *reinterpret_cast<const u32x4*>(kb_ + r8 * D + 16 * c8);                        \
+        vreg[0] = *reinterpret_cast<const u32x4*>(vb_ + r8 * D + 16 * c8);                        \
+        ks8 = *reinterpret_cast<const float*>(kb_ + BN * D + 4 * r8);                             \
+        vs8 = *reinterpret_cast<const float*>(vb_ + BN * D + 4 * r8);                             \
+    } else if constexpr (PAGED) {                                                                 \
         const size_t pg = (size_t)btab[t] * Hkv * BN * D + head_pg + st_chunk * 8;                \
         _Pragma("unroll") for (int i = 0; i < SIT; ++i) {                                           \
             kreg[i] = *reinterpret_cast<const u32x4*>(pk.kc + pg + (size_t)(st_row0 + SROWS * i) * D); \
@@ -164,6 +180,15 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
         }                                                                                         \
     }
 #define STORE_TILE(st)                                                                            \
+    if constexpr (KV8) {                                                                          \
+        u32x4 lo_, hi_;                                                                           \
+        kv8::dequant16(kreg[0], ks8, lo_, hi_);                                                   \
+        *reinterpret_cast<u32x4*>(lds + (st) + k_off(r8, 2 * c8)) = lo_;                          \
+        *reinterpret_cast<u32x4*>(lds + (st) + k_off(r8, 2 * c8 + 1)) = hi_;                      \
+        kv8::dequant16(vreg[0], vs8, lo_, hi_);                                                   \
+        *reinterpret_cast<u32x4*>(lds + (st) + BN * 256 + v_off(r8, 2 * c8)) = lo_;               \
+        *reinterpret_cast<u32x4*>(lds + (st) + BN * 256 + v_off(r8, 2 * c8 + 1)) = hi_;           \
+    } else                                                                                        \
     _Pragma("unroll") for (int i = 0; i < SIT; ++i) {                                               \
         const int row = st_row0 + SROWS * i;                                                         \
         *reinterpret_cast<u32x4*>(lds + (st) + k_off(row, st_chunk)) = kreg[i];                    \
@@ -336,11 +361,18 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
 
 template <bool PAGED, int G>
 static void launch_g(dim3 grid, hipStream_t s, const bf16* Q, int row_stride, const int* cu, const int2* it, bf16* out,
-                     int out_stride, int Hq, int Hkv, int Hg, int gq, float sl, const PagedKV& p) {
+                     int out_stride, int Hq, int Hkv, int Hg, int gq, float sl, const PagedKV& p, int kv8) {
     // kv-head-major order from 8 blocks per CU up (measured crossover: 4096 blocks neutral, 19656 kv-major)
     const int kv_major = grid.x > 8 * 256;
-    attn_prefill_kernel<PAGED, G><<<grid, NTHR, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq, Hkv, Hg, gq, sl, p,
-                                                        kv_major);
+    if constexpr (PAGED) {
+        if (kv8) {
+            attn_prefill_kernel<PAGED, G, true><<<grid, NTHR, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq, Hkv,
+                                                                      Hg, gq, sl, p, kv_major);
+            return;
+        }
+    }
+    attn_prefill_kernel<PAGED, G, false><<<grid, NTHR, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq, Hkv, Hg,
+                                                                   gq, sl, p, kv_major);
 }
 
 static bool packed_ratio(int G) { return G == 1 || G == 2 || G == 4 || G == 8; }
@@ -355,7 +387,7 @@ MRSUM_API int mrsum_attn_prefill_block_m(int Hq, int Hkv) {
 
 static int launch_prefill(const void* qkv, int row_stride, const int* cu_seqlens, const int* items, int n_items,
                           int block_m, void* out, int out_stride, int Hq, int Hkv, int Dh, float scale,
-                          const PagedKV* pk, hipStream_t s) {
+                          const PagedKV* pk, int kv8, hipStream_t s) {
     if (n_items <= 0) return 0;
     if (Dh != D || mrsum_attn_prefill_block_m(Hq, Hkv) != block_m) return (int)hipErrorInvalidValue;
     const int G = Hq / Hkv;
@@ -369,10 +401,10 @@ static int launch_prefill(const void* qkv, int row_stride, const int* cu_seqlens
     const PagedKV p = pk ? *pk : PagedKV{nullptr, nullptr, nullptr, 0, nullptr, nullptr};
 #define DISPATCH(PG)                                                                                                 \
     switch (packed_ratio(G) ? G : 1) {                                                                               \
-        case 1: launch_g<PG, 1>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p); break; \
-        case 2: launch_g<PG, 2>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p); break; \
-        case 4: launch_g<PG, 4>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p); break; \
-        default: launch_g<PG, 8>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p); break; \
+        case 1: launch_g<PG, 1>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p, kv8); break; \
+        case 2: launch_g<PG, 2>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p, kv8); break; \
+        case 4: launch_g<PG, 4>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p, kv8); break; \
+        default: launch_g<PG, 8>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p, kv8); break; \
     }
     if (pk) { DISPATCH(true) } else { DISPATCH(false) }
 #undef DISPATCH
@@ -384,7 +416,7 @@ MRSUM_API int mrsum_attn_prefill(const void* qkv, int row_stride, const int* cu_
                                  int n_items, int block_m, void* out, int out_stride, int Hq, int Hkv, int Dh,
                                  float scale, hipStream_t s) {
     return launch_prefill(qkv, row_stride, cu_seqlens, items, n_items, block_m, out, out_stride, Hq, Hkv, Dh, scale,
-                          nullptr, s);
+                          nullptr, 0, s);
 }
 
 // Chunked-prefill attention: q rows of the packed slices (qkv, cu_seqlens), keys / values from the paged
@@ -392,9 +424,9 @@ MRSUM_API int mrsum_attn_prefill(const void* qkv, int row_stride, const int* cu_
 MRSUM_API int mrsum_attn_prefill_paged(const void* qkv, int row_stride, const int* cu_seqlens, const int* items,
                                        int n_items, int block_m, void* out, int out_stride, int Hq, int Hkv, int Dh,
                                        float scale, const void* kcache, const void* vcache, const int* block_tables,
-                                       int bt_stride, const int* seq_slot, const int* prefix, hipStream_t s) {
+                                       int bt_stride, const int* seq_slot, const int* prefix, int kv8, hipStream_t s) {
     if (!kcache || !vcache || !block_tables || !seq_slot || !prefix) return (int)hipErrorInvalidValue;
     const PagedKV pk{(const bf16*)kcache, (const bf16*)vcache, block_tables, bt_stride, seq_slot, prefix};
     return launch_prefill(qkv, row_stride, cu_seqlens, items, n_items, block_m, out, out_stride, Hq, Hkv, Dh, scale,
-                          &pk, s);
+                          &pk, kv8, s);
 }

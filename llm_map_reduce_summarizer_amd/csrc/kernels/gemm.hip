@@ -6,7 +6,12 @@
 //   * OCP e4m3fn x e4m3fn on v_mfma_scale_f32_16x16x128_f8f6f4 with unit block scales (E8M0 127): the
 //     block-scaled form runs at twice the bf16 rate (MI355X_MICROARCH.md "Matrix cores"), so the plain
 //     per-row quantisation (activation row scale sx[m] x weight row scale sw[n]) is applied in the
-//     epilogue and the MX block scales stay 1.0.
+//     epilogue and the MX block scales stay 1.0.  (Per-32 E8M0 activation scales measured WORSE than the
+//     fp32 row scale: power-of-two scales waste up to a bit of e4m3's range -- 2.67 vs 2.29 % element
+//     error, 25.6 vs 24.3 % on the fp8 parity logits, profiles/r4_fp8_activation_emulation.txt.)
+//   * two-term fp8 activations (norm.hip Q8 == 2, the fp8 model's QKV input): X rows hold [hi | lo] over
+//     2K bytes, W keeps K; the K-tiles kt >= kbw (the lo half) re-read W's tile kt - kbw and run with the
+//     X block scale E8M0 123 = 2^-4, so one launch computes hi W^T + lo W^T / 16.
 //
 // Structure (cdna_hip_programming.md §5 "The 256^2 8-phase template", re-derived for this layout):
 //   * one 256 x 256 output tile per 512-thread workgroup (8 waves, one workgroup per CU), K-tiles of 128
@@ -59,6 +64,7 @@ struct GemmArgs {
     const float* sw;  // fp8: per-row weight scale [N]
     int ldx_b, ldw_b, ldc;  // X / W row strides in bytes, C row stride in elements
     int M, N, kb;           // kb = K-tiles (128 bytes of every row each)
+    int kbw;                // W's K-tiles: kb, or kb / 2 for two-term X (X tiles kt >= kbw re-read W tile kt - kbw)
     int tiles_m, tiles_n, group_m;
 };
 
@@ -141,8 +147,9 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
             dma16(rx, dst + 1024, vx1 + o, soff);
         } else {
             const int o = part == 2 ? wh : 0;
-            dma16(rw, dst, vw0 + o, soff);
-            dma16(rw, dst + 1024, vw1 + o, soff);
+            const int sw = (kt >= a.kbw ? kt - a.kbw : kt) * 128;
+            dma16(rw, dst, vw0 + o, sw);
+            dma16(rw, dst + 1024, vw1 + o, sw);
         }
     };
 
@@ -197,7 +204,7 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
     auto cat8 = [](const u32x4& p, const u32x4& q) -> i32x8 {
         return i32x8{(int)p[0], (int)p[1], (int)p[2], (int)p[3], (int)q[0], (int)q[1], (int)q[2], (int)q[3]};
     };
-    auto mfma_q = [&](int qm, int qn, const u32x4 (&wf)[4]) {
+    auto mfma_q = [&](int qm, int qn, const u32x4 (&wf)[4], int xsc) {
         __builtin_amdgcn_s_setprio(1);
         if constexpr (M32) {
             if constexpr (FP8) {
@@ -207,7 +214,7 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
                     for (int b = 0; b < 2; ++b)
                         acc32[qm][b][qn] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(
                             cat8(wf[2 * s], wf[2 * s + 1]), cat8(xf[4 * b + 2 * s], xf[4 * b + 2 * s + 1]),
-                            acc32[qm][b][qn], 0, 0, 0, 127, 0, 127);
+                            acc32[qm][b][qn], 0, 0, 0, 127, 0, xsc);
             } else {
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
@@ -225,7 +232,7 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
                     if constexpr (FP8) {
                         acc[qm][b][qn][i] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
                             cat8(wf[2 * i], wf[2 * i + 1]), cat8(xf[2 * b], xf[2 * b + 1]), acc[qm][b][qn][i],
-                            0, 0, 0, 127, 0, 127);
+                            0, 0, 0, 127, 0, xsc);
                     } else {
 #pragma unroll
                         for (int ks = 0; ks < 2; ++ks)
@@ -252,29 +259,30 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
     };
     auto slot = [&](int kt, int part) -> const char* { return lds + ((4 * kt + part) % NS) * HALF; };
     auto ktile = [&](int kt, auto tail) {
+        const int xsc = FP8 && kt >= a.kbw ? 123 : 127;  // E8M0 2^-4 on the lo half of two-term X
         // phase 0: quadrant (0, 0) -- X0, W0
         read_x(slot(kt, 0));
         read_w(slot(kt, 1), wf0);
         stage_and_wait(kt, 0, tail);
         bar();
-        mfma_q(0, 0, wf0);
+        mfma_q(0, 0, wf0, xsc);
         bar();
         // phase 1: quadrant (0, 1) -- W1
         read_w(slot(kt, 2), wf1);
         stage_and_wait(kt, 1, tail);
         bar();
-        mfma_q(0, 1, wf1);
+        mfma_q(0, 1, wf1, xsc);
         bar();
         // phase 2: quadrant (1, 1) -- X1
         read_x(slot(kt, 3));
         stage_and_wait(kt, 2, tail);
         bar();
-        mfma_q(1, 1, wf1);
+        mfma_q(1, 1, wf1, xsc);
         bar();
         // phase 3: quadrant (1, 0) -- registers only
         stage_and_wait(kt, 3, tail);
         bar();
-        mfma_q(1, 0, wf0);
+        mfma_q(1, 0, wf0, xsc);
         bar();
     };
     // steady state while every phase's stage exists: P + LK < htot for P <= 4 kt + 3
@@ -395,10 +403,11 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
 
 // x [M, K] (row stride ldx elements), w [N, K] (ldw), c [M, N] bf16 (ldc) -- or [M, N / 2] for
 // epi 1 (SwiGLU of the [8 gate | 8 up]-interleaved gate_up rows).  fp8: x, w are e4m3fn bytes,
-// sx [M] / sw [N] fp32 row scales.  Requirements (checked by the Python wrapper too): K % 64 (bf16) /
-// K % 128 (fp8), N % 16, 16-byte aligned rows.
+// sx [M] / sw [N] fp32 row scales; split: x is two-term [hi | lo] of 2K bytes per row over w's K.
+// Requirements (checked by the Python wrapper too): K % 64 (bf16) / K % 128 (fp8), N % 16, 16-byte
+// aligned rows.
 MRSUM_API int mrsum_gemm(const void* x, int ldx, const void* w, int ldw, void* c, int ldc, int M, int N, int K,
-                         int fp8, int epi, const float* sx, const float* sw, int group_m, hipStream_t s) {
+                         int fp8, int epi, const float* sx, const float* sw, int group_m, int split, hipStream_t s) {
     if (M <= 0 || N <= 0) return 0;
     const int es = fp8 ? 1 : 2;
     if ((K * es) % 128 || N % 16 || (ldx * es) % 16 || (ldw * es) % 16 || ldc % 4) return (int)hipErrorInvalidValue;
@@ -408,6 +417,9 @@ MRSUM_API int mrsum_gemm(const void* x, int ldx, const void* w, int ldw, void* c
     a.x = (const char*)x; a.w = (const char*)w; a.c = c; a.sx = sx; a.sw = sw;
     a.ldx_b = ldx * es; a.ldw_b = ldw * es; a.ldc = ldc;
     a.M = M; a.N = N; a.kb = K * es / 128;
+    if (split && (!fp8 || ldx < 2 * K)) return (int)hipErrorInvalidValue;
+    a.kbw = a.kb;
+    if (split) a.kb *= 2;  // X K-tiles: hi then lo
     a.tiles_m = ceil_div(M, 256); a.tiles_n = ceil_div(N, 256);
     // group_m bits 0-7: tile rows per raster group (0 = 4); bit 8: 32x32 MFMA tiles instead of 16x16.
     // Measured (profiles/r3_gemm_mfma32_experiment.jsonl, same box, interleaved): 32x32 is 0-9 % slower on

@@ -11,9 +11,15 @@
 // Q8 (the fp8 prefill GEMMs' input): the normalised row is quantised in the same pass -- row-wise
 // dynamic OCP e4m3fn as quant.hip (scale = max|y| / 448, from the fp32 values) -- so neither the bf16
 // normalised rows nor a separate quantisation pass over them exist.
+// Q8 == 2 (two-term fp8, the QKV input of the fp8 model): the row is written as [hi | lo], 2 D bytes, on
+// the same row scale: hi = e4m3(y / s), lo = e4m3((y / s - hi) x 16) -- the residual of the first rounding
+// at 16x, inside e4m3's range since |y / s - hi| <= 16 (half an e4m3 step at 448).  The fp8 GEMM takes the
+// pair as a 2K-deep product with the lo half scaled by 2^-4 through the MFMA's E8M0 block scale (gemm.hip),
+// so x is carried to ~2^-8 relative precision: the attention scores computed from q / k stop amplifying
+// e4m3's 2-3 % activation rounding (fp8 parity 24 % -> ~10 % rel L2, profiles/r4_fp8_activation_emulation.txt).
 #include "common.h"
 
-template <int VPT, bool ADD, bool Q8 = false>
+template <int VPT, bool ADD, int Q8 = 0>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16* __restrict__ x, bf16* __restrict__ residual,
                                                       const bf16* __restrict__ w, bf16* __restrict__ out,
                                                       int D, int x_stride, int out_stride, float eps,
@@ -77,19 +83,37 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16* __restrict__ x
         for (int i = 0; i < VPT; ++i) {
             const int c = threadIdx.x + i * 256;
             if (c < nvec) {
+                float y[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) y[j] = v[i][j] * qi;
                 int lo = 0, hi = 0;
-                lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][0] * qi, v[i][1] * qi, lo, false);
-                lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][2] * qi, v[i][3] * qi, lo, true);
-                hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][4] * qi, v[i][5] * qi, hi, false);
-                hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[i][6] * qi, v[i][7] * qi, hi, true);
+                lo = __builtin_amdgcn_cvt_pk_fp8_f32(y[0], y[1], lo, false);
+                lo = __builtin_amdgcn_cvt_pk_fp8_f32(y[2], y[3], lo, true);
+                hi = __builtin_amdgcn_cvt_pk_fp8_f32(y[4], y[5], hi, false);
+                hi = __builtin_amdgcn_cvt_pk_fp8_f32(y[6], y[7], hi, true);
                 qr[c] = make_uint2((unsigned)lo, (unsigned)hi);
+                if constexpr (Q8 == 2) {  // the second term: 16 x (y - e4m3(y)) on the same scale
+                    float r[8];
+                    const auto a0 = __builtin_amdgcn_cvt_pk_f32_fp8(lo, false), a1 = __builtin_amdgcn_cvt_pk_f32_fp8(lo, true);
+                    const auto b0 = __builtin_amdgcn_cvt_pk_f32_fp8(hi, false), b1 = __builtin_amdgcn_cvt_pk_f32_fp8(hi, true);
+                    r[0] = (y[0] - a0[0]) * 16.f; r[1] = (y[1] - a0[1]) * 16.f;
+                    r[2] = (y[2] - a1[0]) * 16.f; r[3] = (y[3] - a1[1]) * 16.f;
+                    r[4] = (y[4] - b0[0]) * 16.f; r[5] = (y[5] - b0[1]) * 16.f;
+                    r[6] = (y[6] - b1[0]) * 16.f; r[7] = (y[7] - b1[1]) * 16.f;
+                    int l2 = 0, h2 = 0;
+                    l2 = __builtin_amdgcn_cvt_pk_fp8_f32(r[0], r[1], l2, false);
+                    l2 = __builtin_amdgcn_cvt_pk_fp8_f32(r[2], r[3], l2, true);
+                    h2 = __builtin_amdgcn_cvt_pk_fp8_f32(r[4], r[5], h2, false);
+                    h2 = __builtin_amdgcn_cvt_pk_fp8_f32(r[6], r[7], h2, true);
+                    qr[nvec + c] = make_uint2((unsigned)l2, (unsigned)h2);  // lo half starts at byte D
+                }
             }
         }
     }
 }
 
-// Q8: ``out`` is e4m3fn [T, out_stride bytes], ``qscale`` fp32 [T]
-template <bool ADD, bool Q8 = false>
+// Q8: ``out`` is e4m3fn [T, out_stride bytes] ([hi | lo], 2 D bytes, when Q8 == 2), ``qscale`` fp32 [T]
+template <bool ADD, int Q8 = 0>
 static int launch_rmsnorm(const void* x, void* residual, const void* w, void* out, int T, int D, int x_stride,
                           int out_stride, float eps, hipStream_t s, float* qscale = nullptr) {
     if (T <= 0) return 0;
@@ -104,11 +128,17 @@ static int launch_rmsnorm(const void* x, void* residual, const void* w, void* ou
     return (int)hipGetLastError();
 }
 
-// rmsnorm / residual-add + rmsnorm whose output rows are e4m3fn (q [T, ldq bytes]) with row scales [T]
+// rmsnorm / residual-add + rmsnorm whose output rows are e4m3fn (q [T, ldq bytes]) with row scales [T];
+// split: two-term rows [hi | lo] (2 D bytes, ldq >= 2 D)
 MRSUM_API int mrsum_rmsnorm_fp8(const void* x, void* residual, const void* w, void* q, float* qscale, int T, int D,
-                                int x_stride, int ldq, float eps, hipStream_t s) {
-    if (residual) return launch_rmsnorm<true, true>(x, residual, w, q, T, D, x_stride, ldq, eps, s, qscale);
-    return launch_rmsnorm<false, true>(x, nullptr, w, q, T, D, x_stride, ldq, eps, s, qscale);
+                                int x_stride, int ldq, float eps, int split, hipStream_t s) {
+    if (split) {
+        if (ldq < 2 * D) return (int)hipErrorInvalidValue;
+        if (residual) return launch_rmsnorm<true, 2>(x, residual, w, q, T, D, x_stride, ldq, eps, s, qscale);
+        return launch_rmsnorm<false, 2>(x, nullptr, w, q, T, D, x_stride, ldq, eps, s, qscale);
+    }
+    if (residual) return launch_rmsnorm<true, 1>(x, residual, w, q, T, D, x_stride, ldq, eps, s, qscale);
+    return launch_rmsnorm<false, 1>(x, nullptr, w, q, T, D, x_stride, ldq, eps, s, qscale);
 }
 
 MRSUM_API int mrsum_rmsnorm(const void* x, const void* w, void* out, int T, int D, int x_stride, int out_stride,

@@ -13,8 +13,15 @@
 //          (i, i + D/2), precomputed on the host (no device trig).
 //
 // One 256-thread block per token; a work item is 8 rotary pairs of one head
-// (two 16-B loads, two 16-B stores) or one 16-B V vector.
-#include "common.h"
+// (two 16-B loads, two 16-B stores) or 16 dims of one V head (two 16-B vectors): 8 items per
+// head for K and for V, so the 8 lanes of a head's row sit together (fp8 row scale below).
+//
+// FP8 KV cache (KV8): the cache is byte slabs [num_pages, Hkv, SLAB], SLAB = P * D + 4 * P (kv8.h):
+// row r of a (page, head) slab is D OCP e4m3fn bytes at r * D, its fp32 scale at P * D + 4 r.  A
+// row is quantised as a whole (rotated K, raw V): scale = the power of two >= max|x| / 448 (the
+// 8 lanes of the row reduce the max with xor shuffles), q = e4m3(x / scale).  Power-of-two scales
+// make the decode-side dequantisation (cvt_scalef32 to bf16) exact.
+#include "kv8.h"
 
 // Source of one token row: the bf16 qkv row itself, or (PARTS) the sum of S
 // fp32 split-K slabs of the decode QKV GEMM -- the GEMM's split-K reduction
@@ -53,7 +60,7 @@ struct RowSrc {
     }
 };
 
-template <int D, bool PARTS>
+template <int D, bool PARTS, bool KV8>
 __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ qkv_in, const float* __restrict__ parts,
                                                       int S, int T, bf16* __restrict__ qkv_out, int row_stride,
                                                       const int* __restrict__ positions,
@@ -64,7 +71,8 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
                                                       int P, int write_cache) {
     constexpr int HALF = D / 2;
     constexpr int RI = HALF / 8;   // rotation items per head
-    constexpr int VI = D / 8;      // copy items per v head
+    constexpr int VI = D / 16;     // copy items per v head (16 dims each)
+    static_assert(RI == VI, "K and V rows must take the same number of lanes");
     const int t = blockIdx.x;  // blockIdx.y: 256-item slice of the token's work (one item per thread)
     const int pos = positions[t];
     const int width = (Hq + 2 * Hkv) * D;
@@ -80,8 +88,9 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
     size_t page_base = 0;
     // seq_idx < 0: a padding token of the prefill batch (engine._prefill) -- rotated, never cached
     write_cache = write_cache && seq_idx[t] >= 0;
+    int page = 0;
     if (write_cache) {
-        const int page = block_tables[(size_t)seq_idx[t] * bt_stride + pos / P];
+        page = block_tables[(size_t)seq_idx[t] * bt_stride + pos / P];
         page_base = (size_t)page * Hkv * P + (pos % P);
     }
     const float2* cs = cos_sin + (size_t)pos * HALF;
@@ -104,26 +113,48 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
             bf16* hp = row + h * D;
             *reinterpret_cast<uint4*>(hp + c) = pa;
             *reinterpret_cast<uint4*>(hp + c + HALF) = pb;
-            if (write_cache && h >= Hq) {
+            if constexpr (KV8) {
+                if (h >= Hq) {  // head-uniform over the row's RI lanes: the shuffles stay inside the row
+                    float f[16];
+                    unpack8(pa, f);
+                    unpack8(pb, f + 8);
+                    kv8::put_row16(kcache, page, Hkv, h - Hq, pos % P, P, D, c, c + HALF, f, write_cache);
+                }
+            } else if (write_cache && h >= Hq) {
                 bf16* kp = kcache + (page_base + (size_t)(h - Hq) * P) * D;
                 *reinterpret_cast<uint4*>(kp + c) = pa;
                 *reinterpret_cast<uint4*>(kp + c + HALF) = pb;
             }
         } else {
             const int i = it - n_rot;
-            const int h = i / VI, c = (i % VI) * 8;
+            const int h = i / VI, c = (i % VI) * 16;
             const int col = (Hq + Hkv + h) * D + c;
-            uint4 v;
+            uint4 v[2];
             if constexpr (PARTS) {
                 float f[8];
-                src.load8(col, f);
-                v = pack8(f);
-                *reinterpret_cast<uint4*>(row + col) = v;
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    src.load8(col + 8 * u, f);
+                    v[u] = pack8(f);
+                    *reinterpret_cast<uint4*>(row + col + 8 * u) = v[u];
+                }
             } else {
-                v = *reinterpret_cast<const uint4*>(src.row + col);
-                if (qkv_out != qkv_in) *reinterpret_cast<uint4*>(row + col) = v;
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    v[u] = *reinterpret_cast<const uint4*>(src.row + col + 8 * u);
+                    if (qkv_out != qkv_in) *reinterpret_cast<uint4*>(row + col + 8 * u) = v[u];
+                }
             }
-            if (write_cache) *reinterpret_cast<uint4*>(vcache + (page_base + (size_t)h * P) * D + c) = v;
+            if constexpr (KV8) {
+                float f[16];
+                unpack8(v[0], f);
+                unpack8(v[1], f + 8);
+                kv8::put_row16(vcache, page, Hkv, h, pos % P, P, D, c, c + 8, f, write_cache);
+            } else if (write_cache) {
+#pragma unroll
+                for (int u = 0; u < 2; ++u)
+                    *reinterpret_cast<uint4*>(vcache + (page_base + (size_t)h * P) * D + c + 8 * u) = v[u];
+            }
         }
     }
 }
@@ -132,39 +163,44 @@ template <bool PARTS>
 static int launch_rope(const void* qkv_in, const void* parts, int S, void* qkv_out, int T, int row_stride,
                        const int* positions, const int* seq_idx, const int* block_tables, int bt_stride,
                        void* kcache, void* vcache, const void* cos_sin, int Hq, int Hkv, int D, int P,
-                       int write_cache, hipStream_t s) {
+                       int write_cache, int kv8, hipStream_t s) {
     if (T <= 0) return 0;
-    const int items = (Hq + Hkv) * (D / 16) + Hkv * (D / 8);
+    if (kv8 && D != 128) return (int)hipErrorInvalidValue;
+    const int items = (Hq + 2 * Hkv) * (D / 16);
     dim3 g(T, ceil_div(items, 256)), b(256);
     auto QI = (const bf16*)qkv_in; auto PA = (const float*)parts; auto QO = (bf16*)qkv_out;
     auto K = (bf16*)kcache; auto V = (bf16*)vcache; auto CS = (const float2*)cos_sin;
-    if (D == 128)
-        rope_kv_kernel<128, PARTS><<<g, b, 0, s>>>(QI, PA, S, T, QO, row_stride, positions, seq_idx, block_tables,
-                                                   bt_stride, K, V, CS, Hq, Hkv, P, write_cache);
+    if (kv8)
+        rope_kv_kernel<128, PARTS, true><<<g, b, 0, s>>>(QI, PA, S, T, QO, row_stride, positions, seq_idx,
+                                                         block_tables, bt_stride, K, V, CS, Hq, Hkv, P, write_cache);
+    else if (D == 128)
+        rope_kv_kernel<128, PARTS, false><<<g, b, 0, s>>>(QI, PA, S, T, QO, row_stride, positions, seq_idx,
+                                                          block_tables, bt_stride, K, V, CS, Hq, Hkv, P, write_cache);
     else if (D == 64)
-        rope_kv_kernel<64, PARTS><<<g, b, 0, s>>>(QI, PA, S, T, QO, row_stride, positions, seq_idx, block_tables,
-                                                  bt_stride, K, V, CS, Hq, Hkv, P, write_cache);
+        rope_kv_kernel<64, PARTS, false><<<g, b, 0, s>>>(QI, PA, S, T, QO, row_stride, positions, seq_idx,
+                                                         block_tables, bt_stride, K, V, CS, Hq, Hkv, P, write_cache);
     else
         return (int)hipErrorInvalidValue;
     return (int)hipGetLastError();
 }
 
+// kv8: the cache is the fp8 byte-slab layout (kv8.h), else bf16 [pages, Hkv, P, D]
 MRSUM_API int mrsum_rope_kv(void* qkv, int T, int row_stride, const int* positions, const int* seq_idx,
                             const int* block_tables, int bt_stride, void* kcache, void* vcache,
-                            const void* cos_sin, int Hq, int Hkv, int D, int P, int write_cache,
+                            const void* cos_sin, int Hq, int Hkv, int D, int P, int write_cache, int kv8,
                             hipStream_t s) {
     return launch_rope<false>(qkv, nullptr, 1, qkv, T, row_stride, positions, seq_idx, block_tables, bt_stride,
-                              kcache, vcache, cos_sin, Hq, Hkv, D, P, write_cache, s);
+                              kcache, vcache, cos_sin, Hq, Hkv, D, P, write_cache, kv8, s);
 }
 
 // parts: fp32 [S, T, (Hq+2Hkv)*D] split-K slabs; qkv_out: bf16 [T, row_stride]
 MRSUM_API int mrsum_rope_kv_parts(const void* parts, int S, void* qkv_out, int T, int row_stride,
                                   const int* positions, const int* seq_idx, const int* block_tables, int bt_stride,
                                   void* kcache, void* vcache, const void* cos_sin, int Hq, int Hkv, int D, int P,
-                                  hipStream_t s) {
+                                  int kv8, hipStream_t s) {
     if (S < 1) return (int)hipErrorInvalidValue;
     return launch_rope<true>(nullptr, parts, S, qkv_out, T, row_stride, positions, seq_idx, block_tables, bt_stride,
-                             kcache, vcache, cos_sin, Hq, Hkv, D, P, 1, s);
+                             kcache, vcache, cos_sin, Hq, Hkv, D, P, 1, kv8, s);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -199,8 +199,12 @@ class LLMEngine:
                  kv_pages: Optional[int] = None, kv_fraction: float = 0.6, page_size: int = 64,
                  max_prefill_tokens: int = 16384, use_graphs: bool = True, sync_every: int = 16,
                  eos_ids: Sequence[int] = (128001, 128009), tp_rank: int = 0, tp_size: int = 1, tp_group=None,
-                 weight_dtype: str = "bf16", weights_path: Optional[str] = None, prefill_chunk: int = 4096):
-        """``prefill_chunk``: cut prompts longer than this many tokens into slices prefilled one pass
+                 weight_dtype: str = "bf16", weights_path: Optional[str] = None, prefill_chunk: int = 4096,
+                 kv_dtype: Optional[str] = None):
+        """``kv_dtype``: "bf16" (default, $MRSUM_KV_DTYPE) or "fp8" -- e4m3fn K/V rows with power-of-two
+        row scales (engine/kv_cache.py): half the KV bytes per decode step; no context-parallel prefill.
+
+        ``prefill_chunk``: cut prompts longer than this many tokens into slices prefilled one pass
         after the other through the paged cache (chunked prefill; 0 = one pass per prompt).  At 32k
         tokens on Llama-3-8B 4096-token slices took 0.669 s vs 0.701 s in one pass; 70B fp8 8192-token
         slices 3.53 vs 3.52 s (profiles/r2_chunked_prefill_32k_ab.jsonl)."""
@@ -209,6 +213,7 @@ class LLMEngine:
         self.dtype = dtype
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
+        self.kv_dtype = kv_dtype or os.environ.get("MRSUM_KV_DTYPE", "bf16")
         t0 = time.perf_counter()
         self.model = LlamaModel(cfg, self.device, dtype, seed, tp_rank, tp_size, tp_group, weight_dtype=weight_dtype,
                                  weights_path=weights_path)
@@ -231,10 +236,12 @@ class LLMEngine:
                 budget = int(free * kv_fraction)
             else:
                 budget = 256 << 20
-            kv_pages = PagedKVCache.size_pages(budget, cfg.n_layers, self.model.hkv, page_size, cfg.head_dim)
+            kv_pages = PagedKVCache.size_pages(budget, cfg.n_layers, self.model.hkv, page_size, cfg.head_dim,
+                                               kv_dtype=self.kv_dtype)
             # no point holding more than every slot at full length
             kv_pages = min(kv_pages, 1 + self.max_num_seqs * -(-self.max_model_len // page_size))
-        self.kv = PagedKVCache(cfg.n_layers, kv_pages, self.model.hkv, page_size, cfg.head_dim, dtype, self.device)
+        self.kv = PagedKVCache(cfg.n_layers, kv_pages, self.model.hkv, page_size, cfg.head_dim, dtype, self.device,
+                               kv_dtype=self.kv_dtype)
         self.max_pages = -(-self.max_model_len // page_size)
         self.state = DecodeState(self.max_num_seqs, self.max_pages, max_new_cap, self.device, eos_ids)
         # block tables of requests whose prefill is interleaved with the running decode (they hold no
@@ -782,8 +789,8 @@ class LLMEngine:
         n = len(s.prompt)
         npg = self.kv.pages_for(n)
         if imp.kv is not None:
-            if tuple(imp.kv.shape) != (2, self.cfg.n_layers, npg, self.model.hkv, self.page, self.cfg.head_dim):
-                raise ValueError("imported KV has shape %s" % (tuple(imp.kv.shape),))
+            if tuple(imp.kv.shape) != self.import_shape(n) or imp.kv.dtype != self.kv.k.dtype:
+                raise ValueError("imported KV has shape %s %s" % (tuple(imp.kv.shape), imp.kv.dtype))
             idx = torch.tensor(s.pages[:npg], dtype=torch.long, device=self.device)
             kv = imp.kv.to(self.device, non_blocking=True)
             self.kv.k.index_copy_(1, idx, kv[0])
@@ -850,7 +857,7 @@ class LLMEngine:
         outs = self.generate(prompts, one, ignore_eos=ignore_eos, on_prefill=grab)
         firsts = [o.token_ids[0] for o in outs]
         packs = [torch.cat([chunks[i][g] for i in range(len(prompts))]) if prompts else
-                 torch.empty(0, dtype=self.dtype, device=self.device) for g in range(groups)]
+                 torch.empty(0, dtype=self.kv.k.dtype, device=self.device) for g in range(groups)]
         return firsts, packs
 
     @staticmethod
@@ -870,6 +877,8 @@ class LLMEngine:
             return str(e)
         if self.model.tp_size != 1 or self.model.hkv % world:
             return "needs a TP=1 engine and Hkv divisible by %d" % world
+        if self.kv.fp8:
+            return "the fp8 KV cache has no context-parallel K/V exchange"
         if len(prompt) < 2 * world:
             return "prompt of %d tokens is too short for %d ranks" % (len(prompt), world)
         if self.kv.pages_for(len(prompt) + 1) > self.kv.alloc.available():
@@ -889,8 +898,8 @@ class LLMEngine:
         Returns ``(first_token, kv)`` with kv [2, n_layers, pages, Hkv / world, page, head_dim] (this
         rank's heads), the ImportedPrefill layout of the TP engine."""
         import torch.distributed as dist
-        if self.model.tp_size != 1 or self.model.hkv % world:
-            raise ValueError("prefill_export_cp needs a TP=1 engine and Hkv divisible by %d" % world)
+        if self.model.tp_size != 1 or self.model.hkv % world or self.kv.fp8:
+            raise ValueError("prefill_export_cp needs a TP=1 bf16-KV engine and Hkv divisible by %d" % world)
         s = self._new_seq(0, prompt, SamplingParams(1, params.temperature, params.seed))
         n = len(s.prompt)
         if n < 2 * world:
@@ -946,8 +955,9 @@ class LLMEngine:
             st.park_row(0)  # slot 0 was borrowed: idle again (stopped, pages -> scratch page 0)
 
     def import_shape(self, prompt_len: int):
-        """Shape of this engine's ImportedPrefill.kv for a prompt of ``prompt_len`` tokens."""
-        return (2, self.cfg.n_layers, self.kv.pages_for(prompt_len), self.model.hkv, self.page, self.cfg.head_dim)
+        """Shape of this engine's ImportedPrefill.kv for a prompt of ``prompt_len`` tokens (its cache layout:
+        [.., hkv, page, head_dim] bf16 or [.., hkv, slab bytes] fp8)."""
+        return (2, self.cfg.n_layers, self.kv.pages_for(prompt_len)) + tuple(self.kv.k.shape[2:])
 
     def _compact(self, active: List[_Seq], fin: set) -> None:
         st = self.state
@@ -966,6 +976,7 @@ class LLMEngine:
         s["prefill_tok_s"] = s["prefill_tokens"] / s["prefill_s"] if s["prefill_s"] else 0.0
         s["decode_tok_s"] = s["decode_tokens"] / s["decode_s"] if s["decode_s"] else 0.0
         s["kv_pages"] = self.kv.num_pages
+        s["kv_dtype"] = self.kv.kv_dtype
         s["weights_gib"] = self.model.weight_bytes() / 2 ** 30
         if self.device.type == "cuda":
             s["hbm_peak_gib"] = torch.cuda.max_memory_allocated(self.device) / 2 ** 30

@@ -5,6 +5,11 @@ holds P consecutive positions of ONE kv head contiguously (16 KiB at P=64,
 hd=128) -- the unit the decode-attention workgroups stream.  Page 0 is a
 scratch page: idle decode slots point at it, real sequences never do.
 
+``kv_dtype="fp8"``: ``k``/``v`` are uint8 [num_pages, Hkv, SLAB] byte slabs,
+SLAB = P * hd + 4 * P -- the P rows of e4m3fn bytes then the P fp32 row scales
+of one (page, kv head) (csrc/kernels/kv8.h): 8.25 KiB instead of 16 KiB, so a
+decode step streams half the KV bytes and the cache holds ~1.94x the tokens.
+
 Allocation is whole-sequence: a request reserves ceil((prompt + max_new) / P)
 pages at admission, so a captured decode graph can run many steps without
 the host touching block tables.  The free list is the native C++ allocator
@@ -89,12 +94,20 @@ class PageAllocator:
 
 class PagedKVCache:
     def __init__(self, n_layers: int, num_pages: int, n_kv_heads: int, page: int, head_dim: int,
-                 dtype: torch.dtype, device: torch.device):
+                 dtype: torch.dtype, device: torch.device, kv_dtype: str = "bf16"):
         if num_pages < 2:
             raise ValueError("need at least 2 KV pages (page 0 is scratch)")
+        if kv_dtype not in ("bf16", "fp8"):
+            raise ValueError("kv_dtype must be bf16 or fp8")
+        if kv_dtype == "fp8" and (page, head_dim) != (64, 128):
+            raise ValueError("the fp8 KV cache needs page 64 and head dim 128")
         self.page = page
         self.num_pages = num_pages
+        self.kv_dtype = kv_dtype
         shape = (n_layers, num_pages, n_kv_heads, page, head_dim)
+        if kv_dtype == "fp8":
+            from ..ops.reference import kv8_slab
+            shape, dtype = (n_layers, num_pages, n_kv_heads, kv8_slab(page, head_dim)), torch.uint8
         # zeroed, not empty: attention kernels read whole pages and mask the scores of rows past a
         # sequence's end (p = 0), and 0 x a stale NaN bit pattern in such a V row would still be NaN
         self.k = torch.zeros(shape, dtype=dtype, device=device)
@@ -106,8 +119,13 @@ class PagedKVCache:
     def pages_for(self, n_tokens: int) -> int:
         return -(-n_tokens // self.page)
 
+    @property
+    def fp8(self) -> bool:
+        return self.kv_dtype == "fp8"
+
     @staticmethod
     def size_pages(bytes_budget: int, n_layers: int, n_kv_heads: int, page: int, head_dim: int,
-                   dtype_bytes: int = 2) -> int:
-        per_page = 2 * n_layers * n_kv_heads * page * head_dim * dtype_bytes
+                   dtype_bytes: int = 2, kv_dtype: str = "bf16") -> int:
+        per_head = page * head_dim * dtype_bytes if kv_dtype != "fp8" else page * head_dim + 4 * page
+        per_page = 2 * n_layers * n_kv_heads * per_head
         return max(2, bytes_budget // per_page)

@@ -88,6 +88,21 @@ class _TPReduce:
 _QUANT_NORM = os.environ.get("MRSUM_QUANT_NORM", "1") == "1"
 
 
+def _page_of(kcache: torch.Tensor, head_dim: int) -> int:
+    """Page size (tokens) of a whole-model cache: bf16 [L, pages, hkv, P, D] or the fp8 byte slabs
+    [L, pages, hkv, P * D + 4 P] (engine/kv_cache.py)."""
+    if kcache.dtype == torch.uint8:
+        return kcache.shape[3] // (head_dim + 4)
+    return kcache.shape[3]
+
+
+# fp8 prefill: the QKV projection's input as two-term fp8 ([hi | lo], ops.hip.rmsnorm_fp8 split) -- the
+# attention scores computed from q / k amplify e4m3's 2-3 % row rounding into ~24 % relative logit error on
+# the parity checkpoint; two-term QKV input brings it to ~10 % for ~1.1x the QKV GEMM's cost (the o / gate_up /
+# down inputs stay single-term)  (CPU emulation: profiles/r4_fp8_activation_emulation.txt)
+_QKV_SPLIT = os.environ.get("MRSUM_FP8_QKV_SPLIT", "1") == "1"
+
+
 def _tp_push_enabled() -> bool:
     return os.environ.get("MRSUM_TP_PUSH", "1") == "1"
 
@@ -335,8 +350,9 @@ class LlamaModel:
         residual = ops.embed(ids, self.embed)
         # fp8 prefill: the norms feeding the fp8 GEMMs quantise their rows in the same pass (ops.QuantRows)
         q8 = not decode and self.weight_dtype == "fp8" and _QUANT_NORM
-        x = ops.rmsnorm(residual, None, c.rms_eps, quant=q8)  # gains folded into the consumer weights
-        page = kcache.shape[3]
+        q8qkv = ("split" if _QKV_SPLIT else True) if q8 else False  # the QKV projection's input
+        x = ops.rmsnorm(residual, None, c.rms_eps, quant=q8qkv)  # gains folded into the consumer weights
+        page = _page_of(kcache, self.hd)
         ar = _TPReduce(self) if self.tp_size > 1 else (LocalReduce(self) if self.emulate_tp_reduce else None)
         last = len(self.layers) - 1
         for i, lw in enumerate(self.layers):
@@ -346,7 +362,7 @@ class LlamaModel:
             x = ops.proj_add_rmsnorm(a, lw.wo, residual, None, c.rms_eps, "o", ar, quant=q8)
             act = ops.gate_up_swiglu(x, lw.wgu)
             x = ops.proj_add_rmsnorm(act, lw.wdown, residual, None, c.rms_eps, "down", ar,
-                                     quant=q8 and i < last)  # the last one feeds the bf16 LM head
+                                     quant=q8qkv if i < last else False)  # the last one feeds the bf16 LM head
         return x
 
     def logits(self, x: torch.Tensor, gather: bool = True) -> torch.Tensor:
@@ -389,7 +405,7 @@ class LlamaModel:
         of the last pass's last rows."""
         c = self.cfg
         eps = c.rms_eps
-        page = kcache.shape[3]
+        page = _page_of(kcache, self.hd)
         sp = self.sequence_parallel and self.tp_size > 1 and self._sp_backend_ok()
         st = []
         for p in passes:
@@ -446,7 +462,7 @@ class LlamaModel:
         rank holding the prompt's end), else None."""
         c = self.cfg
         eps = c.rms_eps
-        page = kcache.shape[3]
+        page = _page_of(kcache, self.hd)
         st = []
         for p in passes:
             res = ops.embed(p.ids, self.embed)
@@ -474,7 +490,7 @@ class LlamaModel:
                kcache: torch.Tensor, vcache: torch.Tensor, workspace=None, gather: bool = True) -> torch.Tensor:
         """One token per sequence; context = positions + 1.  Returns logits [B, vocab] (or the local
         vocab shard when ``gather`` is False)."""
-        page = kcache.shape[3]
+        page = _page_of(kcache, self.hd)
 
         def attention(i, qkv):
             return ops.attn_decode(qkv, kcache[i], vcache[i], block_tables, positions, self.hq, self.hkv, self.hd,

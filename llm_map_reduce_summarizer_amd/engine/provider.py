@@ -114,7 +114,7 @@ class LocalEngineProvider(Provider):
                  kv_fraction: Optional[float] = None, use_graphs: bool = True, max_num_seqs: Optional[int] = None,
                  tokenizer: Optional[str] = None, ignore_eos: bool = False, reduce_tp: Optional[bool] = None,
                  weights: Optional[str] = None, parallel: Optional[str] = None,
-                 fault_inject: Optional[str] = None, **_ignored):
+                 fault_inject: Optional[str] = None, kv_dtype: Optional[str] = None, **_ignored):
         super().__init__(model, config)
         spec = fault_inject or os.environ.get("MRSUM_FAULT_INJECT", "")
         self._fault_rank, self._fault_left = (int(x) for x in spec.split(":")) if spec else (-1, 0)
@@ -143,6 +143,10 @@ class LocalEngineProvider(Provider):
             self._engine_options.setdefault("weight_dtype", "fp8")
         if kv_fraction is not None:
             self._engine_options.setdefault("kv_fraction", kv_fraction)
+        kv_dtype = kv_dtype or self.config.ENGINE_KV_DTYPE
+        if kv_dtype not in ("bf16", "fp8"):
+            raise ValueError("kv_dtype must be bf16 or fp8, got %s" % kv_dtype)
+        self._engine_options.setdefault("kv_dtype", kv_dtype)
         if max_num_seqs is not None:
             self._engine_options.setdefault("max_num_seqs", max_num_seqs)
         self.timings: Dict[str, float] = {"generate_s": 0.0, "allgather_s": 0.0}
@@ -378,7 +382,7 @@ class LocalEngineProvider(Provider):
         world = k or self.par.world  # the TP group: ranks [world * g, world * (g + 1))
         rank = self.par.rank % world
         group = pdist.tp_group_for(world)
-        if len(prompts) == 1 and len(prompts[0]) >= 2 * world:
+        if len(prompts) == 1 and len(prompts[0]) >= 2 * world and not self.engine.kv.fp8:
             # one prompt (the final reduce): context-parallel prefill over every rank instead of one rank
             # prefilling it alone; every rank ends with its TP shard's KV heads, no all-to-all
             # (rank-local faults were agreed on by the caller; the pre-flight check makes the ranks agree
@@ -403,14 +407,14 @@ class LocalEngineProvider(Provider):
             self._maybe_fault()
             firsts, packs = self.engine.prefill_export([prompts[i] for i in mine], [sp[i] for i in mine], world,
                                                        ignore_eos=self.ignore_eos)
-            send = torch.cat(packs) if packs else torch.empty(0, dtype=torch.bfloat16)
+            send = torch.cat(packs) if packs else torch.empty(0, dtype=self.engine.kv.k.dtype)
             send_sizes = [p.numel() for p in packs]
         except Exception as e:  # noqa: BLE001 -- still enter the all-to-all with the sizes the peers expect
             err = "rank %d prefill: %s: %s" % (self.par.rank, type(e).__name__, e)
             log.error("%s", err)
             firsts = [0] * len(mine)
             send_sizes = [sum(numel[i] for i in mine)] * world
-            send = torch.zeros(sum(send_sizes), dtype=torch.bfloat16,
+            send = torch.zeros(sum(send_sizes), dtype=self.engine.kv.k.dtype,
                                device=torch.device(self._device) if nccl else "cpu")
         dev = send.device if nccl else torch.device("cpu")
         send = send.to(dev)

@@ -51,12 +51,12 @@ def unit_gain(hidden, device):
 
 def rmsnorm(x, w, eps, out=None, quant=False):
     """``w`` None: unit gain.  ``quant`` (the consumer is an fp8 GEMM): on the GPU at prefill sizes the
-    rows come back quantised (QuantRows)."""
+    rows come back quantised (QuantRows); ``quant="split"``: as two-term fp8 rows (ops.hip.rmsnorm_fp8)."""
     if w is None:
         w = unit_gain(x.shape[-1], x.device)
     if quant and out is None and _quant_ok(x):
         from . import hip
-        return QuantRows(*hip.rmsnorm_fp8(x, w, eps))
+        return QuantRows(*hip.rmsnorm_fp8(x, w, eps, split=quant == "split"))
     return _impl(x).rmsnorm(x, w, eps, out)
 
 
@@ -86,8 +86,8 @@ class NormRows:
 
 class QuantRows:
     """Normalised prefill rows already quantised to row-wise e4m3fn by their producer (ops.hip.rmsnorm_fp8:
-    the norm and the quantisation in one pass) for an fp8-weight GEMM: ``q`` [T, K] float8_e4m3fn,
-    ``scale`` [T] fp32."""
+    the norm and the quantisation in one pass) for an fp8-weight GEMM: ``q`` [T, K] float8_e4m3fn (or
+    two-term [T, 2K] = [hi | lo]), ``scale`` [T] fp32."""
 
     def __init__(self, q, scale):
         self.q, self.scale = q, scale
@@ -436,7 +436,7 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None, quant=F
         if all_reduce:
             all_reduce(o)
         if quant and _quant_ok(o):
-            return QuantRows(*hip.rmsnorm_fp8(o, ln, eps, residual=residual))
+            return QuantRows(*hip.rmsnorm_fp8(o, ln, eps, residual=residual, split=quant == "split"))
         return hip.add_rmsnorm(o, residual, ln, eps)
     if _use_hip(a):
         from . import hip
@@ -454,7 +454,7 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None, quant=F
         if all_reduce:
             all_reduce(o)
         if quant and _quant_ok(o):
-            return QuantRows(*hip.rmsnorm_fp8(o, ln, eps, residual=residual))
+            return QuantRows(*hip.rmsnorm_fp8(o, ln, eps, residual=residual, split=quant == "split"))
         return hip.add_rmsnorm(o, residual, ln, eps)
     o = reference.linear(a, w)
     if all_reduce:

@@ -23,22 +23,22 @@ _c_int, _c_float, _vp = ctypes.c_int, ctypes.c_float, ctypes.c_void_p
 _SIGS = {
     "mrsum_rmsnorm": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_add_rmsnorm": [_vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
-    "mrsum_rmsnorm_fp8": [_vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
+    "mrsum_rmsnorm_fp8": [_vp, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int, _vp],
     "mrsum_rope_kv": [_vp, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int,
-                      _c_int, _vp],
+                      _c_int, _c_int, _vp],
     "mrsum_rope_kv_parts": [_vp, _c_int, _vp, _c_int, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _c_int,
-                            _c_int, _c_int, _c_int, _vp],
+                            _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_swiglu": [_vp, _vp, _c_int, _c_int, _vp],
     "mrsum_kv_scatter": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp],
     "mrsum_embed": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _vp],
     "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_attn_prefill_paged": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float,
                                  _vp,
-                                 _vp, _vp, _c_int, _vp, _vp, _vp],
+                                 _vp, _vp, _c_int, _vp, _vp, _c_int, _vp],
     "mrsum_attn_decode_mfma": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int,
-                               _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp],
+                               _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _c_int, _vp],
     "mrsum_attn_decode_rope": [_vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int,
-                               _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _vp],
+                               _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _c_int, _vp],
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int,
                           _c_float, _vp, _c_int, _vp, _vp, _vp],
     "mrsum_skinny_resid_capacity": [],
@@ -54,7 +54,7 @@ _SIGS = {
     "mrsum_sample_keys": [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
     "mrsum_sample_finish": [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_int, _vp],
     "mrsum_gemm": [_vp, _c_int, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int,
-                   _vp],
+                   _c_int, _vp],
     "mrsum_sample": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp,
                      _vp],
 }
@@ -146,9 +146,12 @@ def add_rmsnorm(x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: f
     return out
 
 
-def rmsnorm_fp8(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None):
+def rmsnorm_fp8(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
+                split: bool = False):
     """rmsnorm(x) * w -- or residual += x; rmsnorm(residual) * w -- quantised in the same pass to row-wise
-    e4m3fn (the fp8 prefill GEMM's input, as quant_fp8_rows): returns (q [T, D] float8_e4m3fn, scale [T])."""
+    e4m3fn (the fp8 prefill GEMM's input, as quant_fp8_rows): returns (q [T, D] float8_e4m3fn, scale [T]).
+    ``split``: two-term rows q [T, 2 D] = [hi | lo], lo = e4m3(16 (y / s - hi)) (norm.hip Q8 == 2), which
+    gemm_fp8 takes as a 2D-deep product with the lo half scaled by 2^-4."""
     _bf16_cuda(x, w)
     _rows_ok(x)
     T, D = x.shape
@@ -156,11 +159,31 @@ def rmsnorm_fp8(x: torch.Tensor, w: torch.Tensor, eps: float, residual: Optional
     if residual is not None:
         _bf16_cuda(residual)
         _req(residual.shape == (T, D) and residual.is_contiguous(), "rmsnorm_fp8: residual must be [T, D] contiguous")
-    q = torch.empty(T, D, dtype=torch.float8_e4m3fn, device=x.device)
+    q = torch.empty(T, 2 * D if split else D, dtype=torch.float8_e4m3fn, device=x.device)
     sc = torch.empty(T, dtype=torch.float32, device=x.device)
-    _check(_fn("mrsum_rmsnorm_fp8")(_p(x), _p(residual), _p(w), _p(q), _p(sc), T, D, x.stride(0), D, eps,
-                                    _stream()), "rmsnorm_fp8")
+    _check(_fn("mrsum_rmsnorm_fp8")(_p(x), _p(residual), _p(w), _p(q), _p(sc), T, D, x.stride(0), q.shape[1], eps,
+                                    1 if split else 0, _stream()), "rmsnorm_fp8")
     return q, sc
+
+
+# ------------------------------------------------------------------ kv cache formats
+KV8_PAGE, KV8_D = 64, 128
+KV8_SLAB = KV8_PAGE * KV8_D + 4 * KV8_PAGE  # csrc/kernels/kv8.h: e4m3 rows then fp32 row scales
+
+
+def _cache_kind(kcache: torch.Tensor, vcache: torch.Tensor, hkv: int, page: int, d: int, what: str) -> int:
+    """1 for the fp8 byte-slab cache [pages, hkv, KV8_SLAB] uint8 (kv8.h), 0 for bf16 [pages, hkv, page, d];
+    validates shape / dtype / contiguity either way."""
+    _req(kcache is not None and vcache is not None and kcache.is_cuda and vcache.is_cuda
+         and kcache.is_contiguous() and vcache.is_contiguous() and kcache.shape == vcache.shape
+         and kcache.dtype == vcache.dtype, "%s: K / V caches must be matching contiguous CUDA tensors" % what)
+    if kcache.dtype == torch.uint8:
+        _req(page == KV8_PAGE and d == KV8_D and tuple(kcache.shape[1:]) == (hkv, KV8_SLAB),
+             "%s: fp8 cache must be uint8 [pages, Hkv, %d] (page 64, head dim 128)" % (what, KV8_SLAB))
+        return 1
+    _req(kcache.dtype == torch.bfloat16 and tuple(kcache.shape[1:]) == (hkv, page, d),
+         "%s: cache must be bf16 [pages, Hkv, P, D] (or the fp8 slab layout)" % what)
+    return 0
 
 
 # ------------------------------------------------------------------ rope + kv
@@ -177,10 +200,9 @@ def rope_kv(qkv: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, b
     _req(positions.numel() >= T and seq_idx.numel() >= T, "rope_kv: positions/seq_idx shorter than T")
     _req(cos_sin.is_cuda and cos_sin.dtype == torch.float32 and cos_sin.is_contiguous()
          and cos_sin.shape[1:] == (d // 2, 2), "rope_kv: cos_sin must be [max_pos, D/2, 2] fp32")
+    kv8 = 0
     if write_cache:
-        _bf16_cuda(kcache, vcache)
-        _req(kcache.is_contiguous() and vcache.is_contiguous() and kcache.shape == vcache.shape
-             and tuple(kcache.shape[1:]) == (hkv, page, d), "rope_kv: cache must be [pages, Hkv, P, D]")
+        kv8 = _cache_kind(kcache, vcache, hkv, page, d, "rope_kv")
         _req(block_tables.dim() == 2, "rope_kv: block_tables must be 2-D")
     if check_bounds:  # host sync; used by tests and prefill (positions live on the host there anyway)
         pmax = int(positions[:T].max())
@@ -191,7 +213,7 @@ def rope_kv(qkv: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, b
     _check(_fn("mrsum_rope_kv")(_p(qkv), T, qkv.stride(0), _p(positions), _p(seq_idx), _p(block_tables),
                                 block_tables.stride(0), _p(kcache) if write_cache else None,
                                 _p(vcache) if write_cache else None, _p(cos_sin), hq, hkv, d, page,
-                                1 if write_cache else 0, _stream()), "rope_kv")
+                                1 if write_cache else 0, kv8, _stream()), "rope_kv")
 
 
 def rope_kv_parts(parts: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, block_tables: torch.Tensor,
@@ -205,21 +227,21 @@ def rope_kv_parts(parts: torch.Tensor, positions: torch.Tensor, seq_idx: torch.T
     _i32(positions, seq_idx, block_tables)
     _req(positions.numel() >= T and seq_idx.numel() >= T and block_tables.dim() == 2, "rope_kv_parts: tables")
     _req(cos_sin.is_cuda and cos_sin.dtype == torch.float32 and cos_sin.shape[1:] == (d // 2, 2), "cos_sin")
-    _bf16_cuda(kcache, vcache)
-    _req(kcache.is_contiguous() and vcache.is_contiguous() and tuple(kcache.shape[1:]) == (hkv, page, d), "cache")
+    kv8 = _cache_kind(kcache, vcache, hkv, page, d, "rope_kv_parts")
     if out is None:
         out = torch.empty(T, W, dtype=torch.bfloat16, device=parts.device)
     _rows_ok(out)
     _check(_fn("mrsum_rope_kv_parts")(_p(parts), S, _p(out), T, out.stride(0), _p(positions), _p(seq_idx),
                                       _p(block_tables), block_tables.stride(0), _p(kcache), _p(vcache), _p(cos_sin),
-                                      hq, hkv, d, page, _stream()), "rope_kv_parts")
+                                      hq, hkv, d, page, kv8, _stream()), "rope_kv_parts")
     return out
 
 
 def kv_scatter(rows: torch.Tensor, page: torch.Tensor, slot: torch.Tensor, kcache: torch.Tensor,
                vcache: torch.Tensor) -> None:
     """kcache / vcache [pages, hkv, P, d] at (page[i], slot[i]) <- rows[i, 0] / rows[i, 1] ([n, 2, hkv, d] bf16;
-    page < 0: skipped).  The K/V rows a context-parallel prefill all-gathers from the other ranks."""
+    page < 0: skipped).  The K/V rows a context-parallel prefill all-gathers from the other ranks (bf16
+    caches only: an fp8-KV engine does not run the context-parallel prefill)."""
     _bf16_cuda(rows, kcache, vcache)
     _i32(page, slot)
     n = rows.shape[0]
@@ -305,9 +327,7 @@ def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int,
     _req(out.shape[0] >= T and out.shape[1] >= hq * d, "attn_prefill: bad out")
     if paged is not None:
         kc, vc, bt = paged.kcache, paged.vcache, paged.block_tables
-        _bf16_cuda(kc, vc)
-        _req(kc.is_contiguous() and vc.is_contiguous() and tuple(kc.shape[1:]) == (hkv, 64, d),
-             "attn_prefill: paged cache must be [pages, Hkv, 64, D]")
+        kv8 = _cache_kind(kc, vc, hkv, 64, d, "attn_prefill")
         _i32(bt, paged.seq_slot, paged.prefix)
         _req(bt.dim() == 2 and len(paged.prefix_host) == len(seqlens) == paged.seq_slot.numel(),
              "attn_prefill: paged tables")
@@ -316,7 +336,7 @@ def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int,
                  "attn_prefill: slice [%d, %d) beyond block table" % (pre, pre + n))
         _check(_fn("mrsum_attn_prefill_paged")(_p(qkv), qkv.stride(0), _p(cu_seqlens), _p(items), items.shape[0],
                                                block_m, _p(out), out.stride(0), hq, hkv, d, scale, _p(kc), _p(vc), _p(bt),
-                                               bt.stride(0), _p(paged.seq_slot), _p(paged.prefix), _stream()),
+                                               bt.stride(0), _p(paged.seq_slot), _p(paged.prefix), kv8, _stream()),
                "attn_prefill_paged")
         return out
     _check(_fn("mrsum_attn_prefill")(_p(qkv), qkv.stride(0), _p(cu_seqlens), _p(items), items.shape[0], block_m, _p(out),
@@ -448,9 +468,7 @@ def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.T
     _req(width == (hq + 2 * hkv) * d and d == 128 and page == 64 and hq % hkv == 0 and hq // hkv <= 64,
          "attn_decode_rope: unsupported config")
     ng = decode_groups(hq, hkv)
-    _bf16_cuda(kcache, vcache)
-    _req(tuple(kcache.shape[1:]) == (hkv, page, d) and kcache.is_contiguous() and vcache.is_contiguous(),
-         "attn_decode_rope: cache must be [pages, Hkv, P, D]")
+    kv8 = _cache_kind(kcache, vcache, hkv, page, d, "attn_decode_rope")
     _req(cos_sin.dtype == torch.float32 and cos_sin.is_contiguous() and cos_sin.shape[-2:] == (d // 2, 2),
          "attn_decode_rope: cos_sin [max_pos, d/2, 2] fp32")
     _i32(block_tables, positions)
@@ -466,7 +484,7 @@ def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.T
     _check(_fn("mrsum_attn_decode_rope")(_p(parts), SP, _p(cos_sin), _p(kcache), _p(vcache), _p(block_tables),
                                          block_tables.stride(0), _p(positions), _p(workspace.part_o),
                                          _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
-                                         workspace.splits, scale, _p(workspace.counters), _stream()),
+                                         workspace.splits, scale, _p(workspace.counters), kv8, _stream()),
            "attn_decode_rope")
     return out
 
@@ -477,13 +495,12 @@ def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, blo
                 workspace: Optional[DecodeWorkspace] = None) -> torch.Tensor:
     """Paged decode attention on MFMA (page 64, G = hq / hkv <= 16): K/V pages staged through LDS,
     QK^T and PV on MFMA, split-K over the context with a fused or separate split merge."""
-    _bf16_cuda(q, kcache, vcache)
+    _bf16_cuda(q)
     _rows_ok(q)
     B = q.shape[0]
     _req(d == 128 and hq % hkv == 0 and hq // hkv <= 64 and page == 64, "attn_decode: bad config")
     ng = decode_groups(hq, hkv)
-    _req(tuple(kcache.shape[1:]) == (hkv, page, d) and kcache.is_contiguous() and vcache.is_contiguous(),
-         "attn_decode: cache must be [pages, Hkv, P, D]")
+    kv8 = _cache_kind(kcache, vcache, hkv, page, d, "attn_decode")
     _i32(block_tables, positions)
     _req(block_tables.dim() == 2 and block_tables.shape[0] >= B and positions.numel() >= B, "attn_decode: tables")
     if workspace is None:
@@ -497,7 +514,7 @@ def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, blo
     _check(_fn("mrsum_attn_decode_mfma")(_p(q), q.stride(0), _p(kcache), _p(vcache), _p(block_tables),
                                          block_tables.stride(0), _p(positions), _p(workspace.part_o),
                                          _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
-                                         workspace.splits, scale, _p(workspace.counters), _stream()),
+                                         workspace.splits, scale, _p(workspace.counters), kv8, _stream()),
            "attn_decode_mfma")
     return out
 
@@ -551,10 +568,10 @@ GEMM_EPI_BF16, GEMM_EPI_SWIGLU = 0, 1
 GEMM_MFMA32 = 256
 
 
-def _gemm(xp, ldx, wp, ldw, out, M, N, K, fp8, epi, sx, sw, group_m):
+def _gemm(xp, ldx, wp, ldw, out, M, N, K, fp8, epi, sx, sw, group_m, split=0):
     _req(out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 8 == 0, "gemm: bad out layout")
     _check(_fn("mrsum_gemm")(xp, ldx, wp, ldw, _p(out), out.stride(0), M, N, K, fp8, epi, sx, sw,
-                             GEMM_GROUP_M if group_m is None else group_m, _stream()), "gemm")
+                             GEMM_GROUP_M if group_m is None else group_m, split, _stream()), "gemm")
     return out
 
 
@@ -587,11 +604,12 @@ def gemm_fp8(xq: torch.Tensor, xs: torch.Tensor, w, out: Optional[torch.Tensor] 
     (v_mfma_scale_f32_16x16x128_f8f6f4, OCP e4m3fn operands; the SwiGLU form on the 32x32x64 tiles), bf16 out."""
     _req(xq.is_cuda and xq.dtype == torch.float8_e4m3fn and xq.dim() == 2 and xq.stride(1) == 1
          and xq.stride(0) % 16 == 0 and xq.data_ptr() % 16 == 0, "gemm_fp8: x must be e4m3fn rows, 16-B aligned")
-    M, K = xq.shape
+    M, KX = xq.shape
     q, sc = w.q, w.scale
-    N = q.shape[0]
-    _req(q.is_cuda and q.dtype == torch.float8_e4m3fn and q.is_contiguous() and q.shape[1] == K,
-         "gemm_fp8: weight must be e4m3fn [N, K] contiguous")
+    N, K = q.shape
+    split = KX == 2 * K  # two-term activations [hi | lo] (rmsnorm_fp8 split)
+    _req(q.is_cuda and q.dtype == torch.float8_e4m3fn and q.is_contiguous() and (KX == K or split),
+         "gemm_fp8: weight must be e4m3fn [N, K] contiguous, x [M, K] or two-term [M, 2K]")
     _req(xs.dtype == torch.float32 and xs.is_contiguous() and xs.numel() >= M and sc.dtype == torch.float32
          and sc.is_contiguous() and sc.numel() == N, "gemm_fp8: scales")
     _req(K % 128 == 0 and N % (32 if swiglu else 16) == 0, "gemm_fp8: unsupported shape M=%d N=%d K=%d" % (M, N, K))
@@ -605,7 +623,7 @@ def gemm_fp8(xq: torch.Tensor, xs: torch.Tensor, w, out: Optional[torch.Tensor] 
     if group_m is None and swiglu:
         group_m = GEMM_GROUP_M | GEMM_MFMA32
     return _gemm(_p(xq), xq.stride(0), _p(q), K, out, M, N, K, 1, GEMM_EPI_SWIGLU if swiglu else GEMM_EPI_BF16,
-                 _p(xs), _p(sc), group_m)
+                 _p(xs), _p(sc), group_m, 1 if split else 0)
 
 
 # ------------------------------------------------------------------ decode GEMMs (M <= 64)

@@ -12,6 +12,9 @@ Layouts shared with the kernels (``csrc/kernels/*.hip``):
   token at position ``p`` of a sequence lives in page
   ``block_tables[row, p // P]`` at offset ``p % P``.
 * ``cos_sin`` [max_pos, D/2, 2] fp32 (cos, sin), HF rotate-half pairing.
+* fp8 KV cache (``--kv-dtype fp8``, csrc/kernels/kv8.h): per layer uint8 [num_pages, Hkv, SLAB],
+  SLAB = P * D + 4 * P -- a (page, head) slab holds P rows of D e4m3fn bytes, then P fp32 row scales;
+  a row is quantised whole with the power-of-two scale >= max|x| / 448.
 """
 
 from __future__ import annotations
@@ -65,6 +68,54 @@ def rope_cos_sin(max_pos: int, head_dim: int, theta: float, device=None, scaling
     return torch.stack([ang.cos(), ang.sin()], dim=-1).float().contiguous().to(device)
 
 
+def kv8_slab(page: int, d: int) -> int:
+    return page * d + 4 * page
+
+
+def kv8_quant_rows(x: torch.Tensor):
+    """Rows [..., d] -> (e4m3fn bytes [..., d] uint8, fp32 scales [...]): scale = the power of two >= max|x| / 448
+    (1 for a zero row), q = RNE e4m3(x / scale) -- kv8.h's row rule."""
+    xf = x.float()
+    amax = xf.abs().amax(-1)
+    m, e = torch.frexp(amax / 448.0)
+    e = torch.where(m == 0.5, e - 1, e)
+    sc = torch.where(amax > 0, torch.ldexp(torch.ones_like(amax), e), torch.ones_like(amax))
+    q = (xf / sc[..., None]).to(torch.float8_e4m3fn).view(torch.uint8)
+    return q, sc
+
+
+def kv8_from_bf16(cache: torch.Tensor) -> torch.Tensor:
+    """A bf16 cache [pages, Hkv, P, d] in the fp8 slab layout [pages, Hkv, P * d + 4 P] (every row quantised)."""
+    n, hkv, page, d = cache.shape
+    q, sc = kv8_quant_rows(cache)
+    return torch.cat([q.reshape(n, hkv, page * d), sc.contiguous().view(torch.uint8).reshape(n, hkv, 4 * page)], -1)
+
+
+def cache_pages(cache: torch.Tensor, pages: torch.Tensor, page: int, d: int) -> torch.Tensor:
+    """fp32 [len(pages), Hkv, P, d] of a bf16 or fp8-slab cache."""
+    c = cache.index_select(0, pages)
+    if cache.dtype != torch.uint8:
+        return c.float()
+    q = c[..., : page * d].reshape(*c.shape[:2], page, d).contiguous().view(torch.float8_e4m3fn).float()
+    sc = c[..., page * d:].contiguous().view(torch.float32)
+    return q * sc[..., None]
+
+
+def cache_write(cache: torch.Tensor, pages: torch.Tensor, offs: torch.Tensor, rows: torch.Tensor, page: int,
+                d: int) -> None:
+    """cache[pages[i], :, offs[i]] = rows[i] ([n, Hkv, d]) for a bf16 or fp8-slab cache."""
+    if cache.dtype != torch.uint8:
+        cache[pages, :, offs] = rows.to(cache.dtype)
+        return
+    q, sc = kv8_quant_rows(rows)  # [n, Hkv, d] bytes, [n, Hkv]
+    n, hkv = rows.shape[0], rows.shape[1]
+    col = offs[:, None] * d + torch.arange(d, device=offs.device)[None, :]  # [n, d] byte columns
+    for h in range(hkv):
+        cache[pages[:, None], h, col] = q[:, h]
+        sb = page * d + 4 * offs[:, None] + torch.arange(4, device=offs.device)[None, :]
+        cache[pages[:, None], h, sb] = sc[:, h].contiguous().view(torch.uint8).view(n, 4)
+
+
 def rope_kv(qkv: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, block_tables: torch.Tensor,
             kcache: Optional[torch.Tensor], vcache: Optional[torch.Tensor], cos_sin: torch.Tensor,
             hq: int, hkv: int, d: int, page: int, write_cache: bool = True) -> None:
@@ -88,8 +139,8 @@ def rope_kv(qkv: torch.Tensor, positions: torch.Tensor, seq_idx: torch.Tensor, b
         pages = block_tables[rows, p_ // page].long()
         offs = p_ % page
         v = qkv[:, (hq + hkv) * d: (hq + 2 * hkv) * d].view(T, hkv, d)[keep]
-        kcache[pages, :, offs] = k
-        vcache[pages, :, offs] = v
+        cache_write(kcache, pages, offs, k, page, d)
+        cache_write(vcache, pages, offs, v, page, d)
 
 
 def rope_kv_parts(parts: torch.Tensor, positions, seq_idx, block_tables, kcache, vcache, cos_sin, hq, hkv, d, page,
@@ -105,6 +156,8 @@ def rope_kv_parts(parts: torch.Tensor, positions, seq_idx, block_tables, kcache,
 def kv_scatter(rows: torch.Tensor, page: torch.Tensor, slot: torch.Tensor, kcache: torch.Tensor,
                vcache: torch.Tensor) -> None:
     """Reference of ops.hip.kv_scatter: cache[page[i], :, slot[i], :] = rows[i, 0 | 1] (page < 0 skipped)."""
+    if kcache.dtype == torch.uint8:
+        raise ValueError("kv_scatter: the context-parallel K/V exchange takes bf16 caches only")
     keep = page[: rows.shape[0]].long() >= 0
     pg, sl, r = page[: rows.shape[0]].long()[keep], slot[: rows.shape[0]].long()[keep], rows[keep]
     kcache[pg, :, sl, :] = r[:, 0].to(kcache.dtype)
@@ -234,7 +287,7 @@ def attn_prefill_paged(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv
         out = torch.empty(T, hq * d, dtype=qkv.dtype, device=qkv.device)
     cu = cu_seqlens.tolist()
     g = hq // hkv
-    P = paged.kcache.shape[2]
+    P = 64 if paged.kcache.dtype == torch.uint8 else paged.kcache.shape[2]
     for i in range(len(cu) - 1):
         s, e = cu[i], cu[i + 1]
         if e <= s:
@@ -242,8 +295,8 @@ def attn_prefill_paged(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv
         n, pre, slot = e - s, paged.prefix_host[i], paged.slot_host[i]
         tot = pre + n
         pages = paged.block_tables[slot, : -(-tot // P)].long()
-        k = paged.kcache.index_select(0, pages).permute(1, 0, 2, 3).reshape(hkv, -1, d)[:, :tot].float()
-        v = paged.vcache.index_select(0, pages).permute(1, 0, 2, 3).reshape(hkv, -1, d)[:, :tot].float()
+        k = cache_pages(paged.kcache, pages, P, d).permute(1, 0, 2, 3).reshape(hkv, -1, d)[:, :tot]
+        v = cache_pages(paged.vcache, pages, P, d).permute(1, 0, 2, 3).reshape(hkv, -1, d)[:, :tot]
         q = qkv[s:e, : hq * d].view(n, hq, d).float().transpose(0, 1)
         k = k.repeat_interleave(g, dim=0)
         v = v.repeat_interleave(g, dim=0)
@@ -268,8 +321,8 @@ def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, blo
         ctx = int(positions[b]) + 1
         npg = (ctx + page - 1) // page
         pages = block_tables[b, :npg].long()
-        k = kcache[pages].permute(1, 0, 2, 3).reshape(hkv, npg * page, d)[:, :ctx].float()
-        v = vcache[pages].permute(1, 0, 2, 3).reshape(hkv, npg * page, d)[:, :ctx].float()
+        k = cache_pages(kcache, pages, page, d).permute(1, 0, 2, 3).reshape(hkv, npg * page, d)[:, :ctx]
+        v = cache_pages(vcache, pages, page, d).permute(1, 0, 2, 3).reshape(hkv, npg * page, d)[:, :ctx]
         qq = q[b, : hq * d].view(hkv, g, d).float()
         sc = torch.matmul(qq, k.transpose(1, 2)) * scale
         p = torch.softmax(sc, dim=-1)

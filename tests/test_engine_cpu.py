@@ -345,3 +345,32 @@ def test_joining_prompt_prefills_between_decode_windows():
     assert before_join(res[True][1]) - before_join(res[False][1]) >= n_slices - 1
     assert res[True][2]["interleaved_prefills"] == 1 and res[False][2].get("interleaved_prefills", 0) == 0
     assert res[True][2]["prefill_slices"] >= n_slices
+
+
+def test_fp8_kv_cache_cpu():
+    """The fp8 slab cache on the CPU reference path: rows round-trip within e4m3 precision, the layout sizes
+    pages at ~1.94x per byte, and an fp8-KV engine's prefill logits stay close to the bf16-KV engine's."""
+    from llm_map_reduce_summarizer_amd.engine.kv_cache import PagedKVCache
+    from llm_map_reduce_summarizer_amd.ops import reference as R
+    x = torch.randn(9, 2, 128) * 5
+    x[3] = 0.0
+    q, sc = R.kv8_quant_rows(x)
+    assert torch.all(torch.log2(sc) == torch.round(torch.log2(sc)))  # powers of two
+    deq = q.view(torch.float8_e4m3fn).float() * sc[..., None]
+    assert float((deq - x).norm() / x.norm()) < 0.04 and float(deq[3].abs().sum()) == 0.0
+    assert float(((x.abs().amax(-1) / sc)[torch.arange(9) != 3]).max()) <= 448.0
+    b = PagedKVCache.size_pages(1 << 30, 32, 8, 64, 128)
+    f = PagedKVCache.size_pages(1 << 30, 32, 8, 64, 128, kv_dtype="fp8")
+    assert 1.9 < f / b < 2.0
+    prompts = [[128000] + [(i * 37 + j * 11) % 120000 + 5 for j in range(n)] for i, n in enumerate((300, 129))]
+    rec = {}
+    for kvd in ("bf16", "fp8"):
+        e = LLMEngine(get_model_config("tiny-gqa4", init_std=0.05), device="cpu", max_model_len=1024,
+                      max_num_seqs=4, kv_pages=32, kv_dtype=kvd, prefill_chunk=128)
+        r = []
+        orig = e._sample
+        e._sample = lambda lg, v, r=r, orig=orig: (r.append(lg.float().clone()), orig(lg, v))
+        e.generate(prompts, [SamplingParams(1, 0.0, 0)] * 2)
+        rec[kvd] = r[-1]
+    a, b = rec["bf16"], rec["fp8"]
+    assert float((a - b).norm() / a.norm()) < 0.15

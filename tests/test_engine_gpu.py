@@ -253,3 +253,17 @@ def test_gqa_ratio3_model_runs():
     agree = sum(e.generate([p + o.token_ids[:-1]], [SamplingParams(1, 0.0, 0)])[0].token_ids[0] == o.token_ids[-1]
                 for p, o in zip(prompts, outs))
     assert agree >= len(prompts) - 1
+
+
+def test_fp8_kv_cache_engine():
+    """--kv-dtype fp8: graph-replayed decode over the fp8 cache agrees with a teacher-forced prefill of the
+    same engine (chunked through the fp8 cache), and the cache holds ~1.94x the tokens per byte."""
+    e = LLMEngine(get_model_config("tiny-gqa4", init_std=0.05), device="cuda:0", max_model_len=2048,
+                  max_num_seqs=8, kv_pages=128, sync_every=4, kv_dtype="fp8", prefill_chunk=128)
+    assert e.kv.k.dtype == torch.uint8 and e.kv.k.shape[-1] == 64 * 128 + 4 * 64
+    prompts = _prompts()
+    outs = e.generate(prompts, [SamplingParams(8, 0.0, 0)] * len(prompts))
+    assert all(len(o.token_ids) == 8 for o in outs) and e.stats["graph_captures"] >= 1
+    agree = sum(e.generate([p + o.token_ids[:-1]], [SamplingParams(1, 0.0, 0)])[0].token_ids[0] == o.token_ids[-1]
+                for p, o in zip(prompts, outs))
+    assert agree >= len(prompts) - 1

@@ -237,3 +237,24 @@ def test_llama3_8b_dims_fp8_parity(monkeypatch):
     print("fp8 parity: max rel err %.4f, top-1 %d/%d, per prompt %s" % (
         err, exact, total, {i: [round(x, 3) for x in v] for i, v in pp.items()}))
     assert max(pp[0]) <= FP8_W8A16_TOL, pp[0]  # the 1-token prompt: weight-only fp8 (W8A16) kernels throughout
+
+
+# fp8 KV cache (e4m3 rows, power-of-two row scales: ~2.7 % RMS per element, kv8.h): the decode rows and the
+# chunked-prefill rows attend over dequantised K/V, which the peaked attention of these checkpoints amplifies
+# like the fp8 activations above; one-pass prefill rows read the bf16 qkv rows and stay at the bf16 level.
+FP8_KV_TOL = 0.3
+
+
+def test_llama3_8b_dims_fp8_kv_parity(monkeypatch):
+    """--kv-dtype fp8: packed + chunked prefill (slices attend to their prefix through the fp8 cache) and
+    decode over the fp8 cache, vs the textbook fp32 forward (bf16 weights)."""
+    cfg = get_model_config("llama3-8b", n_layers=2)
+    ckpt = _checkpoint(cfg, 7)
+    prompts = _prompts((1, 40, 333, 700, 1300), 8)
+    toks, rows, _ = _engine_run(monkeypatch, cfg, ckpt, prompts, 4, max_model_len=2048, kv_pages=256,
+                                kv_dtype="fp8", prefill_chunk=512)
+    pp = {}
+    err, exact, total = _compare(cfg, ckpt, prompts, toks, rows, FP8_KV_TOL, torch.device("cuda:0"),
+                                 min_exact=0.8, per_prompt=pp)
+    print("fp8 KV parity: max rel err %.4f, top-1 %d/%d, per prompt %s" % (
+        err, exact, total, {i: [round(x, 3) for x in v] for i, v in pp.items()}))

@@ -108,9 +108,37 @@ def test_attn_prefill(hq, hkv, seqlens):
     _close(o1, o2, 2e-2)
 
 
+@pytest.mark.parametrize("parts", [False, True])
+def test_rope_kv_fp8_cache(parts):
+    """rope_kv / rope_kv_parts writing the fp8 slab cache (kv8.h: e4m3 rows + power-of-two row scales) ==
+    the reference quantiser on the same rotated rows; rows of padding tokens (seq_idx < 0) are not written."""
+    hq, hkv, d, page, T = 8, 2, 128, 64, 150
+    g = torch.Generator().manual_seed(31)
+    cs = reference.rope_cos_sin(4096, d, 500000.0, DEV)
+    bt = (torch.randperm(40, generator=g)[:24] + 1).view(2, 12).to(torch.int32).to(DEV)
+    pos = torch.cat([torch.arange(100), torch.arange(700, 750)]).to(torch.int32).to(DEV)
+    sidx = torch.tensor([0] * 100 + [1] * 49 + [-1], dtype=torch.int32, device=DEV)
+    c0 = torch.zeros(48, hkv, reference.kv8_slab(page, d), dtype=torch.uint8, device=DEV)
+    k1, v1, k2, v2 = c0.clone(), c0.clone(), c0.clone(), c0.clone()
+    if parts:
+        pr = (torch.randn(3, T, (hq + 2 * hkv) * d, generator=g) * 0.7).to(DEV)
+        q1 = hip.rope_kv_parts(pr, pos, sidx, bt, k1, v1, cs, hq, hkv, d, page)
+        q2 = reference.rope_kv_parts(pr, pos, sidx, bt, k2, v2, cs, hq, hkv, d, page)
+    else:
+        q1 = _rand(T, (hq + 2 * hkv) * d, seed=32)
+        q2 = q1.clone()
+        hip.rope_kv(q1, pos, sidx, bt, k1, v1, cs, hq, hkv, d, page)
+        reference.rope_kv(q2, pos, sidx, bt, k2, v2, cs, hq, hkv, d, page)
+    _close(q1, q2, 2e-2)
+    _kv8_close(k1, k2, page, d)
+    _kv8_close(v1, v2, page, d)
+    assert int(k1[0].sum()) == 0  # page 0 (scratch) untouched
+
+
 @pytest.mark.parametrize("hq,hkv", [(4, 1), (8, 2), (8, 1), (2, 2), (6, 2)])
 @pytest.mark.parametrize("spans", [[(0, 200)], [(130, 300), (0, 77), (1000, 1129)], [(64, 128), (2047, 2048)]])
-def test_attn_prefill_paged(hq, hkv, spans):
+@pytest.mark.parametrize("kv8", [False, True])
+def test_attn_prefill_paged(hq, hkv, spans, kv8):
     """Chunked-prefill attention: slice rows attend to [0, prefix + slice) of their sequence read from the
     paged cache (random non-contiguous pages, stale rows past the slice end), vs the fp32 reference."""
     from llm_map_reduce_summarizer_amd.ops import PagedPrefill
@@ -119,6 +147,8 @@ def test_attn_prefill_paged(hq, hkv, spans):
     n_pages, maxp = 160, 40
     kc = (torch.randn(n_pages, hkv, page, d, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
     vc = torch.randn(n_pages, hkv, page, d, generator=g).to(torch.bfloat16).to(DEV)
+    if kv8:
+        kc, vc = reference.kv8_from_bf16(kc.cpu()).to(DEV), reference.kv8_from_bf16(vc.cpu()).to(DEV)
     nseq = len(spans)
     perm = torch.randperm(n_pages - 1, generator=g)[: nseq * maxp] + 1
     bt = perm.view(nseq, maxp).to(torch.int32).to(DEV)
@@ -155,7 +185,8 @@ def test_attn_prefill_spike(hq):
 @pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (4, 4), (16, 1), (6, 2), (24, 8), (10, 2)])
 @pytest.mark.parametrize("splits", [1, 3, 16, 48])
 @pytest.mark.parametrize("fused", [False, True])
-def test_attn_decode(hq, hkv, splits, fused):
+@pytest.mark.parametrize("kv8", [False, True])
+def test_attn_decode(hq, hkv, splits, fused, kv8):
     d, page = 128, 64
     ctxs = [1, 65, 700, 129, 64, 1000]
     B = len(ctxs)
@@ -163,6 +194,8 @@ def test_attn_decode(hq, hkv, splits, fused):
     g = torch.Generator().manual_seed(13)
     kc = (torch.randn(n_pages, hkv, page, d, generator=g)).to(torch.bfloat16).to(DEV)
     vc = (torch.randn(n_pages, hkv, page, d, generator=g)).to(torch.bfloat16).to(DEV)
+    if kv8:  # the fp8 slab cache (kv8.h); the reference dequantises the same bytes
+        kc, vc = reference.kv8_from_bf16(kc.cpu()).to(DEV), reference.kv8_from_bf16(vc.cpu()).to(DEV)
     perm = torch.randperm(n_pages - 1, generator=g) + 1
     bt = torch.zeros(B, 20, dtype=torch.int32)
     used = 0
@@ -459,7 +492,8 @@ def test_fp8_swiglu_and_quant():
 
 @pytest.mark.parametrize("hq,hkv,S", [(32, 8, 4), (4, 1, 1), (16, 1, 3), (8, 2, 2), (4, 1, 16), (6, 2, 2), (24, 8, 4)])
 @pytest.mark.parametrize("fused_combine", [False, True])
-def test_attn_decode_rope_fused(hq, hkv, S, fused_combine):
+@pytest.mark.parametrize("kv8", [False, True])
+def test_attn_decode_rope_fused(hq, hkv, S, fused_combine, kv8):
     """attn_decode_rope (q/k RoPE + new K/V written into the cache + attention, from the QKV GEMM's
     fp32 split-K slabs) == reference rope_kv_parts followed by reference attention."""
     d, page = 128, 64
@@ -483,6 +517,8 @@ def test_attn_decode_rope_fused(hq, hkv, S, fused_combine):
     cs = reference.rope_cos_sin(2048, d, 500000.0, DEV)
     sc = 1.0 / math.sqrt(d)
     sidx = torch.arange(B, dtype=torch.int32, device=DEV)
+    if kv8:
+        kc0, vc0 = reference.kv8_from_bf16(kc0), reference.kv8_from_bf16(vc0)
     k2, v2 = kc0.clone().to(DEV), vc0.clone().to(DEV)
     qkv = reference.rope_kv_parts(parts, pos, sidx, bt, k2, v2, cs, hq, hkv, d, page)
     o2 = reference.attn_decode(qkv, k2, v2, bt, pos, hq, hkv, d, page, sc)
@@ -492,11 +528,33 @@ def test_attn_decode_rope_fused(hq, hkv, S, fused_combine):
     ws.part_o.fill_(float("nan"))  # poisoned workspace: empty splits must publish zero slabs
     for _ in range(3):  # idempotent: later calls rewrite the same K/V row (and re-armed merge tickets)
         o1 = hip.attn_decode_rope(parts, cs, k1, v1, bt, pos, hq, hkv, d, page, sc, workspace=ws)
-        _close(o1, o2, 2e-2)
+        if kv8:  # the kernel rotates the fp32 slab sums, the reference their bf16 rounding: an element of the
+            # new row on an e4m3 rounding boundary may land one step apart, so compare in relative L2
+            a, b = o1.float().cpu(), o2.float().cpu()
+            assert float((a - b).norm() / b.norm()) < 2e-2
+        else:
+            _close(o1, o2, 2e-2)
     if fused_combine:
         assert int(ws.counters.abs().sum()) == 0
-    _close(k1, k2, 3e-2)
-    _close(v1, v2, 3e-2)
+    if kv8:
+        _kv8_close(k1, k2, page, d)
+        _kv8_close(v1, v2, page, d)
+    else:
+        _close(k1, k2, 3e-2)
+        _close(v1, v2, 3e-2)
+
+
+def _kv8_close(c1, c2, page, d):
+    """Two fp8 slab caches hold the same rows: dequantised within 2 % relative L2 (the kernels rotate / sum
+    in fp32 where the reference rounds to bf16 first, so an element on an e4m3 rounding boundary may land
+    one step -- 6-12 % -- apart) and >= 95 % of the row bytes identical."""
+    allp = torch.arange(c1.shape[0])
+    a = reference.cache_pages(c1.cpu(), allp, page, d)
+    b = reference.cache_pages(c2.cpu(), allp, page, d)
+    assert float((a - b).norm() / b.norm().clamp_min(1e-12)) <= 2e-2
+    written = (c2.cpu()[..., :page * d] != 0) | (c1.cpu()[..., :page * d] != 0)
+    same = (c1.cpu()[..., :page * d] == c2.cpu()[..., :page * d])[written].float().mean()
+    assert float(same) >= 0.95, float(same)
 
 
 @pytest.mark.parametrize("tp", [2, 4, 8])
@@ -832,3 +890,29 @@ def test_rmsnorm_fp8_matches_norm_then_quant(add, D):
     step = sc[:, None] * 32
     assert ((deq - ref).abs() <= step * 0.5 + sc[:, None] * 448 * 2 ** -8 + 1e-6).all()
     assert (q.float() == q2.float()).float().mean() > 0.9
+
+
+@pytest.mark.parametrize("add", [False, True])
+def test_rmsnorm_fp8_two_term(add):
+    """Two-term fp8 rows (norm.hip Q8 == 2): [hi | lo] on one row scale, hi + lo / 16 reproduces the
+    normalised row to ~2^-8 of its magnitude (16x finer than the single-term rows), and the two-term GEMM
+    (gemm.hip: the lo K-tiles re-read W with E8M0 block scale 2^-4) equals (hi + lo / 16) s @ W^T."""
+    T, D, N = 300, 4096, 1280
+    x = _rand(T, D, seed=41)
+    res0 = _rand(T, D, seed=42)
+    w = (torch.rand(D, generator=torch.Generator().manual_seed(43)) + 0.5).to(torch.bfloat16).to(DEV)
+    r1, r2 = res0.clone(), res0.clone()
+    q, sc = hip.rmsnorm_fp8(x, w, 1e-5, residual=r1 if add else None, split=True)
+    q1, sc1 = hip.rmsnorm_fp8(x, w, 1e-5, residual=r2 if add else None)
+    assert q.shape == (T, 2 * D) and torch.equal(sc, sc1) and torch.equal(q[:, :D].float(), q1.float())
+    y = hip.add_rmsnorm(x, res0.clone(), w, 1e-5) if add else hip.rmsnorm(x, w, 1e-5)
+    two = (q[:, :D].float() + q[:, D:].float() / 16) * sc[:, None]
+    one = q1.float() * sc[:, None]
+    e2 = float((two - y.float()).norm() / y.float().norm())
+    e1 = float((one - y.float()).norm() / y.float().norm())
+    assert e2 < e1 / 6, (e1, e2)  # bf16 rounding of the reference row bounds e2 from below
+    from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight
+    wq = Fp8Weight.quantize(_rand(N, D, seed=44, scale=0.02))
+    out = hip.gemm_fp8(q, sc, wq)
+    ref = two @ wq.dequant().t()
+    _close(out, ref, 2e-2)

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--batches", default="1,5,10,39")
     ap.add_argument("--ctx", type=int, default=4000)
     ap.add_argument("--new", type=int, default=256)
+    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--tp-shard", type=int, default=1,
                     help="run ONE rank's shard shapes of TP=K (heads, ffn and vocab / K) on this GPU with no "
                          "all-reduce: the compute + launch floor of a TP=K decode step")
@@ -34,7 +35,7 @@ def main():
         cfg = get_model_config(a.model, n_heads=cfg.n_heads // k, n_kv_heads=cfg.n_kv_heads // k,
                                ffn=cfg.ffn // k, vocab_size=cfg.vocab_size // k)
     eng = LLMEngine(cfg, device="cuda:0", max_model_len=a.ctx + a.new + 64,
-                    max_num_seqs=64, kv_fraction=0.5, weight_dtype=a.dtype, sync_every=32)
+                    max_num_seqs=64, kv_fraction=0.5, weight_dtype=a.dtype, sync_every=32, kv_dtype=a.kv_dtype)
     eng.model.emulate_tp_reduce = a.tp_shard > 1 and not a.deferred_norm
     res = []
     for B in (int(b) for b in a.batches.split(",")):
@@ -50,7 +51,7 @@ def main():
         st = eng.stats
         steps = st["decode_steps"] - s0["decode_steps"]
         dec = st["decode_s"] - s0["decode_s"]
-        res.append({"B": B, "ctx": a.ctx, "tp_shard": a.tp_shard, "decode_ms_per_step": round(1000 * dec / max(1, steps), 3),
+        res.append({"B": B, "ctx": a.ctx, "tp_shard": a.tp_shard, "kv_dtype": a.kv_dtype, "decode_ms_per_step": round(1000 * dec / max(1, steps), 3),
                     "prefill_s": round(st["prefill_s"] - s0["prefill_s"], 3), "wall_s": round(wall, 3)})
         print(json.dumps(res[-1]), flush=True)
 
