@@ -287,7 +287,7 @@ class LLMEngine:
         if ws is None:
             from ..ops.hip import CTX_CLASSES, DecodeWorkspace, decode_attn_plan, decode_groups
             ng = decode_groups(self.model.hq, self.model.hkv)  # kv heads, or query heads for odd GQA ratios
-            s, fused = decode_attn_plan(B, ng, min(CTX_CLASSES[self._ctx_cls], self.max_model_len))
+            s, fused = decode_attn_plan(B, ng, min(CTX_CLASSES[self._ctx_cls], self.max_model_len), kv8=self.kv.fp8)
             ws = DecodeWorkspace(B, self.model.hq, self.cfg.head_dim, s, self.device, ng, fused_combine=fused)
             self._workspaces[key] = ws
         return ws

@@ -370,7 +370,27 @@ def ctx_class(ctx: int) -> int:
 ATTN_SLOTS = 768  # resident decode-attention workgroups (3 per CU, 162 VGPRs; 512 / 1024 measured equal or worse)
 
 
-def decode_attn_plan(batch: int, hkv: int, max_ctx: int):
+# fp8 KV cache: a page is half the bytes, so the same split plan keeps half the bytes in flight per CU.  Whole
+# decode steps at 4.4k context with the splits x 1 / 2 / 3 (profiles/r4_kv8_split_sweep.jsonl): B = 10 (80
+# groups) 4.036 / 3.901 / 3.996 ms, B = 20 4.469 / 4.705 / 4.639, B = 39 5.649 / 5.942 / 6.187 -- so twice the
+# splits up to KV8_SPLIT_GROUPS (sequence, kv head) groups, the bf16 plan above them ($MRSUM_KV8_SPLIT_MULT
+# overrides the factor, for measurements)
+KV8_SPLIT_GROUPS = 96
+_KV8_MULT_ENV = os.environ.get("MRSUM_KV8_SPLIT_MULT")
+
+
+def decode_attn_plan(batch: int, hkv: int, max_ctx: int, kv8: bool = False):
+    """(splits, fused) of decode_attn_plan_bf16; with ``kv8`` (fp8 KV cache) the measured split multiplier
+    (at most one page per split; a fused merge keeps its 16-split cap)."""
+    s, fused = decode_attn_plan_bf16(batch, hkv, max_ctx)
+    if kv8:
+        mult = float(_KV8_MULT_ENV) if _KV8_MULT_ENV else (2.0 if batch * hkv <= KV8_SPLIT_GROUPS else 1.0)
+        pages = max(1, -(-max_ctx // 64))
+        s = max(1, min(int(round(s * mult)), pages, 64, 16 if fused else 64))
+    return s, fused
+
+
+def decode_attn_plan_bf16(batch: int, hkv: int, max_ctx: int):
     """(splits, fused_combine) of the decode attention of ``batch`` sequences x ``hkv`` kv heads whose
     contexts reach ``max_ctx`` tokens (the engine passes its context class's upper bound).
 

@@ -173,10 +173,14 @@ def _compare(cfg, ref_ckpt, prompts, toks, rows, rel_tol, dev, min_exact=0.9, pe
 # 0.9-3.5 % on the same model and prompts (the GPU at 0.7-4.2 %), while a wrong RoPE table puts rows
 # at 30 %+ -- the bounds sit between.  fp8 adds the e4m3 activation rounding of the prefill GEMMs.
 BF16_TOL = 0.07
-# fp8: prefill GEMMs round the activations to e4m3 per row (3 mantissa bits, ~3.6 % RMS per element),
-# which the peaked attention amplifies to 20-26 % on prefilled rows; the W8A16 decode kernels keep bf16
-# activations (a one-token prompt's rows: 2-8 %).  A wrong row-scale order is O(1).
-FP8_TOL = 0.4
+# fp8: prefill GEMMs round the activations to e4m3 per row (3 mantissa bits, ~2.3 % RMS per element);
+# the peaked attention amplifies that on prefilled rows -- 20-26 % when the QKV input was single-term (round
+# 3).  The QKV input is now two-term fp8 (hi + lo / 16, ops.hip.rmsnorm_fp8 split): measured 9.5-10.9 % on
+# prefilled rows, 1-7 % on decode rows (profiles/r4_gpu_tests_fp8kv_twoterm.txt; the CPU emulation of the
+# same checkpoint predicts 10.1 %, profiles/r4_fp8_activation_emulation.txt).  The W8A16 decode kernels keep
+# bf16 activations (a one-token prompt's rows: 1-7 %).  A wrong row-scale order or a lost lo half is O(0.2+).
+FP8_TOL = 0.15
+FP8_MIN_EXACT = 0.9
 FP8_W8A16_TOL = 0.1
 
 
@@ -232,17 +236,19 @@ def test_llama3_8b_dims_fp8_parity(monkeypatch):
         ref[p + "post_attention_layernorm.weight"] = ones
     assert hd == 128
     pp = {}
-    err, exact, total = _compare(cfg, ref, prompts, toks, rows, FP8_TOL, torch.device("cuda:0"), min_exact=0.75,
-                                 per_prompt=pp)
+    err, exact, total = _compare(cfg, ref, prompts, toks, rows, FP8_TOL, torch.device("cuda:0"),
+                                 min_exact=FP8_MIN_EXACT, per_prompt=pp)
     print("fp8 parity: max rel err %.4f, top-1 %d/%d, per prompt %s" % (
         err, exact, total, {i: [round(x, 3) for x in v] for i, v in pp.items()}))
     assert max(pp[0]) <= FP8_W8A16_TOL, pp[0]  # the 1-token prompt: weight-only fp8 (W8A16) kernels throughout
 
 
-# fp8 KV cache (e4m3 rows, power-of-two row scales: ~2.7 % RMS per element, kv8.h): the decode rows and the
-# chunked-prefill rows attend over dequantised K/V, which the peaked attention of these checkpoints amplifies
-# like the fp8 activations above; one-pass prefill rows read the bf16 qkv rows and stay at the bf16 level.
-FP8_KV_TOL = 0.3
+# fp8 KV cache (e4m3 rows, power-of-two row scales: ~2.7 % RMS per element, kv8.h): every row here attends
+# over dequantised K/V (the 1300-token prompt makes every prefill pass chunked, through the cache), and the
+# peaked attention of this checkpoint (score std ~6) amplifies the K error like it amplifies fp8 activations
+# (single-term: 24 %): measured 13-22 % on prompts with history, 3.8 % on the one-token prompt, top-1 20/20
+# (profiles/r4_gpu_tests_fp8kv_twoterm.txt).  The bf16-KV headline is unaffected; fp8 KV is a labelled variant.
+FP8_KV_TOL = 0.25
 
 
 def test_llama3_8b_dims_fp8_kv_parity(monkeypatch):
