@@ -373,7 +373,10 @@ class LocalEngineProvider(Provider):
         its full (TP=1) engine -- no activation all-reduces -- and ships each prompt's KV heads to the
         TP rank that owns them in ONE all-to-all (RCCL over xGMI: ~prompt tokens x 128 KiB x
         (world-1)/world per Llama-3-8B prompt); first tokens are all-gathered.  Returns the
-        ImportedPrefill map for the TP engine's generate."""
+        ImportedPrefill map for the TP engine's generate -- or None when the single-prompt context-parallel
+        prefill cannot run here (every rank's pre-flight verdict, agreed: a prompt too short for the group,
+        an fp8 KV cache, a DP engine whose KV pool cannot hold the prompt); the TP engine then prefills the
+        prompt itself (a TP forward, nothing lost but the hand-off's speed)."""
         import torch
         import torch.distributed as dist
 
@@ -389,8 +392,11 @@ class LocalEngineProvider(Provider):
             # on their local resources BEFORE the per-layer all-gathers, which no rank may leave early)
             pre = self.engine.cp_preflight(prompts[0], world)
             errs = [x for x in pdist.all_gather_json(pre and "rank %d: %s" % (self.par.rank, pre), group) if x]
-            if errs:
-                raise RuntimeError("context-parallel prefill: " + "; ".join(errs))
+            if errs:  # every rank of the group saw the same verdicts: all fall back alike
+                log.warning("context-parallel prefill not possible (%s): the TP engine prefills the prompt",
+                            "; ".join(errs))
+                self.timings["cp_fallbacks"] = self.timings.get("cp_fallbacks", 0) + 1
+                return None
             first, kv = self.engine.prefill_export_cp(prompts[0], sp[0], rank, world, group=group)
             self.timings["handoff_s"] = self.timings.get("handoff_s", 0.0) + time.perf_counter() - t0
             self.timings["cp_prefills"] = self.timings.get("cp_prefills", 0) + 1

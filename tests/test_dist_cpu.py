@@ -203,3 +203,32 @@ def test_all_stages_tp2():
         outs.append(json.loads([l for l in o.splitlines() if l.startswith("RESULT ")][-1][7:]))
     assert outs[0]["summary"] == outs[1]["summary"] and outs[0]["plan"]["levels"] >= 2
     assert outs[0]["imported"] > 0  # TP stages prefilled data-parallel and imported their KV
+
+
+CPFALL_SCRIPT = TPALL_SCRIPT.replace(
+    'ex = LLMExecutor(config=cfg, provider_obj=prov)',
+    'if int(os.environ.get("RANK", 0)) == 1:  # one rank cannot run the context-parallel prefill\n'
+    '    prov.engine.cp_preflight = lambda prompt, world: "injected: KV pool too small"\n'
+    'ex = LLMExecutor(config=cfg, provider_obj=prov)').replace(
+    '"imported": prov.stats()["tp_engine"].get("imported_prefills", 0)}',
+    '"imported": prov.stats()["tp_engine"].get("imported_prefills", 0), '
+    '"cp_fallbacks": prov.stats().get("cp_fallbacks", 0), "failed": ex.failed_requests}')
+
+
+@pytest.mark.slow
+def test_cp_prefill_refused_falls_back_to_tp_prefill():
+    """The single-prompt (final reduce) context-parallel prefill is refused by one rank's pre-flight: every
+    rank agrees and the TP engine prefills the prompt itself -- the stage succeeds, no failed requests."""
+    code = CPFALL_SCRIPT % {"root": ROOT}
+    assert "injected" in code
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), WORLD_SIZE="2",
+               OMP_NUM_THREADS="2")
+    procs = [subprocess.Popen([sys.executable, "-c", code], env=dict(env, RANK=str(r), LOCAL_RANK=str(r)),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = []
+    for p in procs:
+        o, err = p.communicate(timeout=600)
+        assert p.returncode == 0, err[-3000:]
+        outs.append(json.loads([l for l in o.splitlines() if l.startswith("RESULT ")][-1][7:]))
+    assert outs[0]["summary"] == outs[1]["summary"] and outs[0]["failed"] == 0
+    assert all(o["cp_fallbacks"] >= 1 for o in outs)
