@@ -497,10 +497,23 @@ class LLMEngine:
         if ignore_eos:  # device-side stop set: captured graphs see it at replay (sampler.hip EOS_SLOTS)
             self.state.set_eos([])
         try:
-            out = self._generate(prompts, params, imported or {}, on_prefill, feeder, on_sync)
             ar = self.model.custom_ar
-            if ar is not None and ar.agree_error():
-                out = self._recover_custom_ar(prompts, params, imported or {}, on_prefill, feeder, on_sync)
+            failed: Optional[BaseException] = None
+            try:
+                out = self._generate(prompts, params, imported or {}, on_prefill, feeder, on_sync)
+            except Exception as e:  # noqa: BLE001 -- re-raised below, after the group's vote
+                failed = e
+            if ar is not None:
+                # every TP rank votes whatever happened locally, so the group's collective sequence stays
+                # aligned: a local exception fails the call on every rank; a timed-out P2P wait anywhere
+                # (the sticky error word) makes every rank re-run the requests on RCCL
+                ar_err, peer_failed = ar.agree_error(failed is not None)
+                if failed is None and peer_failed:
+                    raise RuntimeError("a tensor-parallel peer failed during this generate")
+                if failed is None and ar_err:
+                    out = self._recover_custom_ar(prompts, params, imported or {}, on_prefill, feeder, on_sync)
+            if failed is not None:
+                raise failed
         finally:
             if ignore_eos:
                 self.state.set_eos(eos)

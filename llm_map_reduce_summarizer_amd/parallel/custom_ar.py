@@ -226,15 +226,18 @@ class CustomAllReduce:
         if not all(oks):
             raise RuntimeError("custom all-reduce: reset failed on some rank (rc %d here)" % rc)
 
-    def agree_error(self) -> int:
-        """COLLECTIVE: the error words of every rank, OR-ed (a rank whose own waits all succeeded may still
-        hold garbage pushed by a timed-out peer, so the group decides together)."""
-        errs = [None] * self.world
-        dist.all_gather_object(errs, self.error(), group=self.group)
-        out = 0
-        for e in errs:
-            out |= int(e) if e is not None and e >= 0 else 1
-        return out
+    def agree_error(self, local_failed: bool = False):
+        """COLLECTIVE: (the error words of every rank OR-ed, whether any rank reports ``local_failed``).  A rank
+        whose own waits all succeeded may still hold garbage pushed by a timed-out peer, and a rank whose
+        call raised must not leave its peers alone in the next collective, so the group decides together."""
+        votes = [None] * self.world
+        dist.all_gather_object(votes, (self.error(), bool(local_failed)), group=self.group)
+        err, failed = 0, False
+        for v in votes:
+            e, f = v if v is not None else (1, True)
+            err |= int(e) if e is not None and e >= 0 else 1
+            failed |= bool(f)
+        return err, failed
 
     def _test_fused(self, dev, iters: int, T: int = 5, D: int = 512, S: int = 2) -> bool:
         """add_rmsnorm against (collective sum of the slabs) + the fp32 reference add_rmsnorm, eager
