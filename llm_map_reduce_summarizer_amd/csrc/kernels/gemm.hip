@@ -66,6 +66,9 @@ struct GemmArgs {
     int M, N, kb;           // kb = K-tiles (128 bytes of every row each)
     int kbw;                // W's K-tiles: kb, or kb / 2 for two-term X (X tiles kt >= kbw re-read W tile kt - kbw)
     int tiles_m, tiles_n, group_m;
+#ifdef MRSUM_CLOCK_STAMPS
+    unsigned long long* stamps;  // diagnostic build only (tools/gemm_clock.py): [grid][2] shader / 100 MHz ticks
+#endif
 };
 
 template <int N>
@@ -116,6 +119,9 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
     // restaged at phase h + NS - LK >= 2 phases after the last phase that read half-tile h (<= h).
     constexpr int LK = NS - 2;
     static_assert(NS * HALF <= 160 * 1024 && NS * HALF >= 2 * TILE, "LDS ring size");
+#ifdef MRSUM_CLOCK_STAMPS
+    const unsigned long long clk0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
+#endif
     __shared__ __attribute__((aligned(1024))) char lds[NS * HALF];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -399,7 +405,30 @@ __global__ __launch_bounds__(512, 1) void gemm_kernel(const GemmArgs a) {
             if (ok) *reinterpret_cast<u32x4*>(reinterpret_cast<bf16*>(a.c) + (size_t)m * a.ldc + col) = val;
         }
     }
+#ifdef MRSUM_CLOCK_STAMPS
+    // in-kernel clock = shader ticks / 100 MHz ticks (MI355X_MICROARCH.md, DVFS give-back item 6); lane 0's
+    // vector store to a buffer no other code reads
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned long long clk = __builtin_amdgcn_s_memtime() - clk0, rt = __builtin_amdgcn_s_memrealtime() - rt0;
+        a.stamps[2 * blockIdx.x] = clk;
+        a.stamps[2 * blockIdx.x + 1] = rt;
+    }
+#endif
 }
+
+#ifdef MRSUM_CLOCK_STAMPS
+static unsigned long long* g_stamps = nullptr;
+static int g_nstamps = 0;
+// copies the last launch's [grid][2] stamps to host memory; returns the count of u64 words (diagnostic build)
+MRSUM_API int mrsum_gemm_stamps(unsigned long long* host, int max_words) {
+    const int n = std::min(max_words, g_nstamps);
+    if (!g_stamps || n <= 0 || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(host, g_stamps, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    return n;
+}
+#endif
 
 // x [M, K] (row stride ldx elements), w [N, K] (ldw), c [M, N] bf16 (ldc) -- or [M, N / 2] for
 // epi 1 (SwiGLU of the [8 gate | 8 up]-interleaved gate_up rows).  fp8: x, w are e4m3fn bytes,
@@ -429,6 +458,18 @@ MRSUM_API int mrsum_gemm(const void* x, int ldx, const void* w, int ldw, void* c
     group_m &= 255;
     a.group_m = group_m > 0 ? group_m : 4;
     const dim3 grid(a.tiles_m * a.tiles_n), block(512);
+#ifdef MRSUM_CLOCK_STAMPS
+    static unsigned long long* stamps = nullptr;
+    static size_t nstamps = 0;
+    if (nstamps < 2 * grid.x) {
+        if (stamps) (void)hipFree(stamps);
+        nstamps = 2 * grid.x;
+        if (hipMalloc(&stamps, nstamps * 8) != hipSuccess) return (int)hipErrorOutOfMemory;
+    }
+    a.stamps = stamps;
+    g_stamps = stamps;
+    g_nstamps = 2 * (int)grid.x;
+#endif
     // measured (profiles/r2_gemm_variants_ab.jsonl, r2_gemm_ring10_ab.jsonl): the staggered 8-slot ring
     // (LOOK 6) with the LDS-staged epilogue is the fastest; the 2-phase / 10-slot rings and the
     // unstaggered schedule lost 5-25 %.  The register epilogue remains for outputs that are not 16-B

@@ -360,9 +360,8 @@ class LlamaModel:
                                self.hq, self.hkv, self.hd, page, defer=decode)
             a = attention(i, qkv)
             x = ops.proj_add_rmsnorm(a, lw.wo, residual, None, c.rms_eps, "o", ar, quant=q8)
-            act = ops.gate_up_swiglu(x, lw.wgu)
-            x = ops.proj_add_rmsnorm(act, lw.wdown, residual, None, c.rms_eps, "down", ar,
-                                     quant=q8qkv if i < last else False)  # the last one feeds the bf16 LM head
+            x = ops.mlp(x, lw.wgu, lw.wdown, residual, c.rms_eps, ar,
+                        quant=q8qkv if i < last else False)  # the last one feeds the bf16 LM head
         return x
 
     def logits(self, x: torch.Tensor, gather: bool = True) -> torch.Tensor:

@@ -462,6 +462,28 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None, quant=F
     return reference.add_rmsnorm(o, residual, ln, eps)
 
 
+MLP_FUSED = os.environ.get("MRSUM_MLP_FUSED", "0") == "1"  # measured: see docs/decode_latency.md
+
+
+def mlp(x, wgu, wdown, residual, eps, all_reduce=None, quant=False):
+    """The decode/prefill MLP block: residual += swiglu(x wgu^T) wdown^T (TP-all-reduced when
+    ``all_reduce``); returns the next layer's normed input as proj_add_rmsnorm does.
+
+    GPU decode rows of a tensor-parallel shard (bf16, F = ffn / TP <= 2048, M <= 16, ``x`` a NormRows) run
+    the one-launch fused MLP (ops.hip.mlp_fused: gate_up + SwiGLU -> in-launch granule hand-off -> down +
+    residual update + TP push); everything else runs gate_up_swiglu then proj_add_rmsnorm."""
+    if MLP_FUSED and isinstance(x, NormRows) and not quant and not isinstance(wgu, Fp8Weight) and _use_hip(x.h):
+        from . import hip
+        M, H = x.shape
+        F = wdown.shape[1]
+        ok = getattr(all_reduce, "push_ok", None)
+        push = all_reduce.push_handle() if ok is not None and ok(M, H) else None
+        if (all_reduce is None or push is not None) and hip.mlp_fused_ok(M, H, F):
+            return NormRows(residual, hip.mlp_fused(x.h, wgu, wdown, residual, norm=x.norm, tp=push), eps)
+    act = gate_up_swiglu(x, wgu)
+    return proj_add_rmsnorm(act, wdown, residual, None, eps, "down", all_reduce, quant=quant)
+
+
 def gate_up_swiglu(x, wgu):
     """silu(gate) * up of the fused, [8 gate | 8 up]-blocked gate_up projection; ``x`` may be a
     NormRows (deferred RMSNorm) or QuantRows (fp8 prefill rows quantised by the norm)."""

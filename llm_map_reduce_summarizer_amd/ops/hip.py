@@ -42,6 +42,9 @@ _SIGS = {
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int,
                           _c_float, _vp, _c_int, _vp, _vp, _vp],
     "mrsum_skinny_resid_capacity": [],
+    "mrsum_mlp_fused": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_float, _vp, _c_int, _vp, _vp,
+                        _vp, _vp, _vp, _vp],
+    "mrsum_mlp_fused_capacity": [],
     "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_stream_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp,
                           _vp, _c_int, _c_float, _vp, _c_int, _vp, _c_int, _vp, _vp],
@@ -881,6 +884,74 @@ def skinny_resid_capacity() -> int:
     if not _RESID_CAP:
         _RESID_CAP.append(int(_fn("mrsum_skinny_resid_capacity")()))
     return _RESID_CAP[0]
+
+
+_MLP_CAP = []
+_MLP_WS = {}
+MLP_FUSED_MAX_M = 16
+MLP_FUSED_MAX_F = 2048  # skinny_gemm.hip MLP_MAXB: the down tile's k blocks held in registers
+
+
+def mlp_fused_capacity() -> int:
+    """Workgroups of the fused MLP kernel resident at once (its grid of max(F / 8, H / 16) must fit)."""
+    if not _MLP_CAP:
+        _MLP_CAP.append(int(_fn("mrsum_mlp_fused_capacity")()))
+    return _MLP_CAP[0]
+
+
+def mlp_fused_ok(M: int, H: int, F: int) -> bool:
+    """Shapes the one-launch decode MLP takes (a TP shard's: F = ffn / TP <= 2048)."""
+    return (1 <= M <= MLP_FUSED_MAX_M and H % 128 == 0 and F % 128 == 0 and F <= MLP_FUSED_MAX_F
+            and max(F // 8, H // 16) <= min(mlp_fused_capacity(), _MLP_MAX_GRID))
+
+
+_MLP_MAX_GRID = 1024
+
+
+def _mlp_workspace(device, grid: int):
+    """Granule buffer + per-workgroup epoch words of mlp_fused, one set per (device, grid size): the epoch
+    words of one grid size advance in lockstep (skinny_gemm.hip), so launches of another grid size must
+    not share them, nor the granules their tags guard.  Zeroed once; word _MLP_MAX_GRID is the timeout word."""
+    key = (str(device), int(grid))
+    ws = _MLP_WS.get(key)
+    if ws is None:
+        h = torch.zeros(MLP_FUSED_MAX_M * MLP_FUSED_MAX_F // 2, dtype=torch.int64, device=device)
+        words = torch.zeros(_MLP_MAX_GRID + 4, dtype=torch.int32, device=device)
+        ws = _MLP_WS[key] = (h, words)
+    return ws
+
+
+def mlp_fused_error(device) -> int:
+    """The fused MLP's sticky timeout words (non-TP launches; a TP launch uses its group's error word)."""
+    return sum(int(w[_MLP_MAX_GRID].item()) for (d, _), (_, w) in _MLP_WS.items() if d == str(device))
+
+
+def mlp_fused(x: torch.Tensor, w_gu: torch.Tensor, w_down: torch.Tensor, residual: torch.Tensor, norm=None,
+              tp=None) -> torch.Tensor:
+    """One-launch decode MLP (skinny_gemm.hip mlp_fused_kernel): residual += swiglu(x w_gu^T) w_down^T --
+    all-reduced over the custom all-reduce group ``tp`` first when given (TP push); ``norm`` (ssq, eps): the
+    deferred RMSNorm of ``x`` (the un-normalised residual rows).  Returns the fp32 [M, H / 16] per-tile row
+    sums of squares of the new residual (the next consumer's deferred norm)."""
+    _bf16_cuda(x, w_gu, w_down, residual)
+    _rows_ok(x)
+    _rows_ok(residual)
+    M, H = x.shape
+    F = w_down.shape[1]
+    _req(w_gu.is_contiguous() and w_down.is_contiguous() and tuple(w_gu.shape) == (2 * F, H)
+         and tuple(w_down.shape) == (H, F) and tuple(residual.shape) == (M, H),
+         "mlp_fused: w_gu [2F, H], w_down [H, F], residual [M, H]")
+    _req(mlp_fused_ok(M, H, F), "mlp_fused: unsupported M=%d H=%d F=%d (capacity %d)"
+         % (M, H, F, mlp_fused_capacity()))
+    sq, tiles, eps = _norm_args(x, norm)
+    h, words = _mlp_workspace(x.device, max(F // 8, H // 16))
+    ssp = torch.empty(M, H // 16, dtype=torch.float32, device=x.device)
+    if tp is not None:
+        STATS["tp_push"] += 1
+    wp = words.data_ptr()
+    _check(_fn("mrsum_mlp_fused")(_p(x), x.stride(0), _p(w_gu), _p(w_down), H, F, M, sq, tiles, eps, _p(residual),
+                                  residual.stride(0), _p(ssp), _p(h), ctypes.c_void_p(wp), ctypes.c_void_p(wp + 4 * _MLP_MAX_GRID),
+                                  tp, _stream()), "mlp_fused")
+    return ssp
 
 
 def skinny_resid(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, tp=None) -> torch.Tensor:

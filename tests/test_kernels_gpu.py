@@ -866,6 +866,64 @@ def test_skinny_resid_producer(M, tp):
             h.close()
 
 
+@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("tp", [False, True])
+@pytest.mark.parametrize("H,F", [(4096, 1792), (1024, 512)])
+def test_mlp_fused(M, tp, H, F):
+    """One-launch decode MLP of a TP shard (skinny_gemm.hip mlp_fused_kernel): gate_up + SwiGLU under the
+    deferred norm, the in-launch granule hand-off of h, down + residual update (+ the TP push over a group of
+    one) -- against the fp32 reference, and BIT-EXACT against the two-launch composition it replaces (skinny
+    SwiGLU + skinny residual producer: same tiles, same summation order); repeated launches and hipGraph
+    replays with changing inputs advance the epoch words."""
+    from llm_map_reduce_summarizer_amd.parallel.custom_ar import LocalPush
+    h = LocalPush(max_bytes=1 << 20) if tp else None
+    try:
+        eps = 1e-5
+        tph = h.push_handle() if tp else None
+        wg = _rand(F, H, scale=0.03, seed=32)
+        wu = _rand(F, H, scale=0.03, seed=33)
+        wgu = reference.interleave_gate_up(wg, wu).contiguous()
+        wd = _rand(H, F, scale=0.03, seed=34)
+
+        def ref_of(x0):
+            hf = x0.float()
+            xn = hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + eps)
+            g, u = xn @ wg.float().t(), xn @ wu.float().t()
+            act = (g * torch.sigmoid(g) * u).to(torch.bfloat16).float()
+            return (hf + act @ wd.float().t()).to(torch.bfloat16)
+
+        def ssq_of(t):  # the producer's per-16-column-tile row sums of squares (deferred-norm input)
+            return t.float().pow(2).reshape(M, -1, 16).sum(-1).contiguous()
+
+        for it in range(3):
+            x0 = _rand(M, H, scale=0.5, seed=31 + it)
+            res, r2 = x0.clone(), x0.clone()
+            ssp = hip.mlp_fused(res, wgu, wd, res, norm=(ssq_of(x0), eps), tp=tph)
+            _close(res, ref_of(x0), 3e-2, 2e-2)
+            act = hip.linear_swiglu(r2, wgu, kernel="skinny", norm=(ssq_of(x0), eps))
+            ss2 = hip.skinny_resid(act, wd, r2, tp=tph)
+            assert torch.equal(res, r2), "fused MLP differs from the two-launch composition"
+            assert torch.equal(ssp, ss2)
+        # graph capture: static operands, replayed with new contents
+        xs = _rand(M, H, scale=0.5, seed=40)
+        ss_s = ssq_of(xs)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            ssp_s = hip.mlp_fused(xs, wgu, wd, xs, norm=(ss_s, eps), tp=tph)
+        for it in range(3):
+            x0 = _rand(M, H, scale=0.5, seed=50 + it)
+            xs.copy_(x0)
+            ss_s.copy_(ssq_of(x0))
+            g.replay()
+            torch.cuda.synchronize()
+            _close(xs, ref_of(x0), 3e-2, 2e-2)
+            _close(ssp_s, xs.float().pow(2).reshape(M, H // 16, 16).sum(-1), 1e-2, 1e-3)
+        assert (h.error() if tp else hip.mlp_fused_error(DEV)) == 0
+    finally:
+        if h is not None:
+            h.close()
+
+
 @pytest.mark.parametrize("add", [False, True])
 @pytest.mark.parametrize("D", [4096, 8192])
 def test_rmsnorm_fp8_matches_norm_then_quant(add, D):
