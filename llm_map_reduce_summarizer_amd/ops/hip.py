@@ -56,6 +56,7 @@ _SIGS = {
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_sample_keys": [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
     "mrsum_sample_finish": [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_int, _vp],
+    "mrsum_gemm4w": [_vp, _c_int, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_gemm": [_vp, _c_int, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int,
                    _c_int, _vp],
     "mrsum_sample": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp,
@@ -599,7 +600,7 @@ def _gemm(xp, ldx, wp, ldw, out, M, N, K, fp8, epi, sx, sw, group_m, split=0):
 
 
 def gemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, swiglu: bool = False,
-         group_m: Optional[int] = None) -> torch.Tensor:
+         group_m: Optional[int] = None, kernel: Optional[str] = None) -> torch.Tensor:
     """x [M, K] @ w [N, K]^T in bf16 on the 256 x 256-tile MFMA kernel (csrc/kernels/gemm.hip), any M.
     ``swiglu``: w is the [8 gate | 8 up]-interleaved gate_up weight and the result is silu(gate) * up
     [M, N / 2]."""
@@ -617,8 +618,29 @@ def gemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, s
     _req(out.shape == (M, n_out), "gemm: bad out shape")
     if M == 0:
         return out
+    if kernel is None:
+        kernel = GEMM_KERNEL
+    if kernel in ("4w", "4w5"):
+        return gemm4w(x, w, out, swiglu, group_m, ns=5 if kernel == "4w5" else 4)
     return _gemm(_p(x), x.stride(0), _p(w), w.stride(0), out, M, N, K, 0,
                  GEMM_EPI_SWIGLU if swiglu else GEMM_EPI_BF16, None, None, group_m)
+
+
+# bf16 prefill GEMM kernel: "8w" = gemm.hip (8 waves, 128 x 64 per wave), "4w" / "4w5" = gemm4w.hip (4 waves,
+# 128 x 128 per wave, 4- / 5-step LDS ring); MRSUM_GEMM_KERNEL overrides for measurements
+GEMM_KERNEL = os.environ.get("MRSUM_GEMM_KERNEL", "8w")
+
+
+def gemm4w(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, swiglu: bool = False,
+           group_m: Optional[int] = None, ns: int = 4) -> torch.Tensor:
+    """The four-wave bf16 GEMM (csrc/kernels/gemm4w.hip); same operands as gemm()."""
+    M, K = x.shape
+    N = w.shape[0]
+    _req(out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 8 == 0, "gemm4w: bad out layout")
+    _check(_fn("mrsum_gemm4w")(_p(x), x.stride(0), _p(w), w.stride(0), _p(out), out.stride(0), M, N, K,
+                               GEMM_EPI_SWIGLU if swiglu else GEMM_EPI_BF16,
+                               GEMM_GROUP_M if group_m is None else group_m, ns, _stream()), "gemm4w")
+    return out
 
 
 def gemm_fp8(xq: torch.Tensor, xs: torch.Tensor, w, out: Optional[torch.Tensor] = None, swiglu: bool = False,
@@ -911,7 +933,9 @@ _MLP_MAX_GRID = 1024
 def _mlp_workspace(device, grid: int):
     """Granule buffer + per-workgroup epoch words of mlp_fused, one set per (device, grid size): the epoch
     words of one grid size advance in lockstep (skinny_gemm.hip), so launches of another grid size must
-    not share them, nor the granules their tags guard.  Zeroed once; word _MLP_MAX_GRID is the timeout word."""
+    not share them, nor the granules their tags guard.  Launches sharing a workspace must be ordered (one
+    stream, as the decode graph is): two in flight at once would interleave their epochs.  Zeroed once; word
+    _MLP_MAX_GRID is the timeout word."""
     key = (str(device), int(grid))
     ws = _MLP_WS.get(key)
     if ws is None:
