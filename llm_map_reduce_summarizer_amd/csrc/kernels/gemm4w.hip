@@ -18,8 +18,8 @@
 //     step t + 1 is visible; restage slot t with step t + NS (NS - 1 steps = NS - 1 x 64 MFMA issues of
 //     prefetch distance); then 64 MFMAs on step t's fragments (registers) interleaved with the 16
 //     fragment reads of step t + 1 into the other register set (sched_group_barrier).
-//   * epilogue: gemm.hip's -- transposed tile (A = W fragment), so a lane holds 4 consecutive output
-//     columns of one row; LDS-staged whole-row stores; SwiGLU of the [8 gate | 8 up] rows by lane xor 32.
+//   * epilogue: transposed tile (A = W fragment), so a lane holds 4 consecutive output columns of one row;
+//     LDS-staged whole-row stores; SwiGLU of the [8 gate | 8 up] rows in the store pass.
 #include "common.h"
 
 namespace {
@@ -127,17 +127,23 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const G4Args a) {
         if (t < nk) stage(t);
     vmw_rt(min(NS - 1, nk) - 1);  // step 0 landed
     bar4();
+    // (in the order the loop refills them: the waitcnt pass then sees one outstanding-read order at the loop head)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        xf[j] = *reinterpret_cast<const u32x4*>(lds + xoff + j * 1024);
-        wf[j] = *reinterpret_cast<const u32x4*>(lds + woff + j * 1024);
-    }
+    for (int j = 0; j < 4; ++j) xf[j] = *reinterpret_cast<const u32x4*>(lds + xoff + j * 1024);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wf[j] = *reinterpret_cast<const u32x4*>(lds + woff + j * 1024);
+#pragma unroll
+    for (int j = 4; j < 8; ++j) xf[j] = *reinterpret_cast<const u32x4*>(lds + xoff + j * 1024);
 
     // step t: wait for step t + 1 (the steps staged after it may stay in flight), barrier, restage the slot of step
     // t - 1 (its fragments were consumed by step t - 1's MFMAs) with step t + NS - 1, then the 64 MFMAs of step t,
-    // each fragment register refilled with step t + 1's fragment as soon as its last MFMA has issued: W block i
-    // after row i of the 8 x 8 products, X block b after the last row's product with it.  The last step reads a
+    // each fragment register refilled with step t + 1's fragment right after its last MFMA issued.  Order: X blocks
+    // 0-3 against all W blocks first (X 0-3 refilled early), then W-major over X blocks 4-7 (each W block refilled
+    // as it finishes, X 4-7 at the end) -- the next step starts on X 0-3 and W 0.., which were refilled 7 or more
+    // MFMAs earlier, and the in-order LDS counter lets its first MFMAs wait only for those.  The last step reads a
     // stale slot into registers nothing uses.
+#define G4_MFMA(i, b) acc[i][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[i]),       \
+                                                                        __builtin_bit_cast(bf16x8, xf[b]), acc[i][b], 0, 0, 0);
 #define G4_STEP(T)                                                                                          \
     {                                                                                                      \
         const int t_ = (T);                                                                                \
@@ -145,75 +151,88 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const G4Args a) {
         bar4();                                                                                            \
         if (t_ + NS - 1 < nk) stage(t_ + NS - 1);                                                          \
         const char* s = lds + ((t_ + 1) % NS) * SLOT;                                                      \
-        _Pragma("unroll") for (int i = 0; i < 7; ++i) {                                                    \
-            _Pragma("unroll") for (int b = 0; b < 8; ++b) acc[i][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16( \
-                __builtin_bit_cast(bf16x8, wf[i]), __builtin_bit_cast(bf16x8, xf[b]), acc[i][b], 0, 0, 0); \
-            wf[i] = *reinterpret_cast<const u32x4*>(s + woff + i * 1024);                                  \
-        }                                                                                                  \
-        _Pragma("unroll") for (int b = 0; b < 8; ++b) {                                                    \
-            acc[7][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[7]),         \
-                                                                __builtin_bit_cast(bf16x8, xf[b]), acc[7][b], 0, 0, 0); \
+        _Pragma("unroll") for (int b = 0; b < 4; ++b) {                                                    \
+            _Pragma("unroll") for (int i = 0; i < 8; ++i) { G4_MFMA(i, b) }                                \
             xf[b] = *reinterpret_cast<const u32x4*>(s + xoff + b * 1024);                                  \
         }                                                                                                  \
-        wf[7] = *reinterpret_cast<const u32x4*>(s + woff + 7 * 1024);                                      \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                                    \
+            _Pragma("unroll") for (int b = 4; b < 8; ++b) { G4_MFMA(i, b) }                                \
+            wf[i] = *reinterpret_cast<const u32x4*>(s + woff + i * 1024);                                  \
+        }                                                                                                  \
+        _Pragma("unroll") for (int b = 4; b < 8; ++b)                                                      \
+            xf[b] = *reinterpret_cast<const u32x4*>(s + xoff + b * 1024);                                  \
         /* keep the refills between the MFMAs (hipcc otherwise sinks all 16 reads below the last MFMA) */  \
-        _Pragma("unroll") for (int i = 0; i < 7; ++i) {                                                    \
+        _Pragma("unroll") for (int b = 0; b < 4; ++b) {                                                    \
             __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);                                             \
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                             \
         }                                                                                                  \
-        _Pragma("unroll") for (int b = 0; b < 8; ++b) {                                                    \
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                             \
+        _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                                    \
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                             \
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                             \
         }                                                                                                  \
-        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                                 \
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                                                 \
     }
     for (int t = 0; t < nk; ++t) G4_STEP(t)
 #undef G4_STEP
+#undef G4_MFMA
 
-    // epilogue (gemm.hip): lane holds C[m][n .. n+3] of every 16 x 16 block, m = .. + (lane & 15), n = .. + 4 (lane >> 4)
+    // epilogue: every wave writes its 128 x 128 bf16 results into a [256 rows][512 B] LDS image of the tile
+    // (16-B unit u of row r at u ^ (r & 7): conflict-free), then each wave stores 64 whole rows.  SwiGLU is applied
+    // in the store pass from the image's [8 gate | 8 up] units -- gate and up are rounded to bf16 first (gemm.hip
+    // applies it to the fp32 accumulators; an in-register lane exchange here kept all 256 accumulators live and
+    // spilled).  LEPI: 16-B stores; else the 8-B aligned output takes two 8-B stores per unit.
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     __syncthreads();
-    constexpr int RB = EPI == 1 ? 256 : 512;
-    auto store4 = [&](int rl, int cbyte, const f32x4& v, int gcol) {
-        const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
-        if constexpr (LEPI) {
-            *reinterpret_cast<uint2*>(lds + rl * RB + (((cbyte >> 4) ^ (rl & 7)) << 4) + (cbyte & 15)) = pk;
-        } else if (m0 + rl < a.M && n0 + gcol < a.N) {
-            char* o = reinterpret_cast<char*>(a.c) + ((size_t)(m0 + rl) * a.ldc) * 2 + (EPI == 1 ? n0 : 2 * n0) + cbyte;
-            *reinterpret_cast<uint2*>(o) = pk;
-        }
-    };
+    constexpr int RB = 512;
     const int g4 = lane >> 4;
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
         const int rl = 128 * wr + 16 * b + (lane & 15);
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const int cb = 128 * wc + 16 * i;
+            const int cbyte = (128 * wc + 16 * i + 4 * g4) * 2;
             const f32x4 v = acc[i][b];
-            if constexpr (EPI == 1) {  // SwiGLU: columns 8-15 of the block (up) sit in lane xor 32
-                f32x4 up, r;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) up[j] = __shfl_xor(v[j], 32, 64);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) r[j] = v[j] / (1.f + __expf(-v[j])) * up[j];
-                if (g4 < 2) store4(rl, ((cb >> 1) + 4 * g4) * 2, r, cb);
-            } else {
-                store4(rl, (cb + 4 * g4) * 2, v, cb);
-            }
+            const uint2 pk = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+            *reinterpret_cast<uint2*>(lds + rl * RB + (((cbyte >> 4) ^ (rl & 7)) << 4) + (cbyte & 15)) = pk;
         }
     }
-    if constexpr (LEPI) {
-        __syncthreads();
-        constexpr int UPR = RB / 16, RPI = 1024 / RB;
+    __syncthreads();
+    constexpr int UNITS = EPI == 1 ? 16 : 32;  // output 16-B units per tile row
+    constexpr int RPI = 64 / UNITS;           // rows per wave instruction
+    const int u = lane % UNITS;
+    const int col = (EPI == 1 ? (n0 >> 1) : n0) + 8 * u;  // first output column of the unit
+    const bool cok = (EPI == 1 ? 2 * col : col) < a.N;
 #pragma unroll
-        for (int it = 0; it < 64 / RPI; ++it) {
-            const int rl = 64 * w + RPI * it + lane / UPR, u = lane % UPR;
-            const u32x4 val = *reinterpret_cast<const u32x4*>(lds + rl * RB + ((u ^ (rl & 7)) << 4));
-            const int m = m0 + rl;
-            const int col = (EPI == 1 ? (n0 >> 1) : n0) + 8 * u;
-            const bool ok = m < a.M && (EPI == 1 ? 2 * col : col) < a.N;
-            if (ok) *reinterpret_cast<u32x4*>(reinterpret_cast<bf16*>(a.c) + (size_t)m * a.ldc + col) = val;
+    for (int it0 = 0; it0 < 64 / RPI; it0 += 8) {  // 8 rows in flight, then their stores
+        u32x4 val[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int rl = 64 * w + RPI * (it0 + j) + lane / UNITS;
+            if constexpr (EPI == 1) {
+                const u32x4 gv = *reinterpret_cast<const u32x4*>(lds + rl * RB + (((2 * u) ^ (rl & 7)) << 4));
+                const u32x4 uv = *reinterpret_cast<const u32x4*>(lds + rl * RB + (((2 * u + 1) ^ (rl & 7)) << 4));
+                float g[8], up[8], r[8];
+                unpack8(make_uint4(gv[0], gv[1], gv[2], gv[3]), g);
+                unpack8(make_uint4(uv[0], uv[1], uv[2], uv[3]), up);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) r[e] = g[e] / (1.f + __expf(-g[e])) * up[e];
+                const uint4 o = pack8(r);
+                val[j] = u32x4{o.x, o.y, o.z, o.w};
+            } else {
+                val[j] = *reinterpret_cast<const u32x4*>(lds + rl * RB + ((u ^ (rl & 7)) << 4));
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int m = m0 + 64 * w + RPI * (it0 + j) + lane / UNITS;
+            if (!cok || m >= a.M) continue;
+            bf16* o = reinterpret_cast<bf16*>(a.c) + (size_t)m * a.ldc + col;
+            if constexpr (LEPI) {
+                *reinterpret_cast<u32x4*>(o) = val[j];
+            } else {
+                reinterpret_cast<uint2*>(o)[0] = make_uint2(val[j][0], val[j][1]);
+                reinterpret_cast<uint2*>(o)[1] = make_uint2(val[j][2], val[j][3]);
+            }
         }
     }
 }
