@@ -48,6 +48,11 @@ def main(root):
         wc = a.get("SQ_WAVE_CYCLES", 0.0)
         shares = " ".join("%5.1f" % (100.0 * a[c] / wc) if wc else "-" for c in extra)
         print("%-70s %6d %9.1f %9.1f %8.2f %8s %8s %s" % (k, n, us, rd / 1e6, tbps, mf, lc, shares))
+    shown = {"n", "us", "FETCH_SIZE", "SQ_VALU_MFMA_BUSY_CYCLES", "SQ_LDS_IDX_ACTIVE", "SQ_LDS_BANK_CONFLICT"}
+    for k, a in sorted(agg.items(), key=lambda kv: -kv[1]["us"])[:30]:
+        rest = {c: v / a["n"] for c, v in a.items() if c not in shown and not c.startswith(("SQ_WAIT", "SQ_ACTIVE"))}
+        if rest:  # other counters: mean per dispatch
+            print("  %-68s %s" % (k, " ".join("%s=%.4g" % kv for kv in sorted(rest.items()))))
 
 
 if __name__ == "__main__":
