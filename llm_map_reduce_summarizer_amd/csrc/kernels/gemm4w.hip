@@ -72,7 +72,8 @@ __device__ __forceinline__ void tile_of4(int bid, int nwg, int tiles_m, int tile
 }
 }  // namespace
 
-template <int EPI, int NS, bool LEPI>
+// G4_LAG: MFMAs between a fragment register's last reader and the LDS read that refills it (0 or 4)
+template <int EPI, int NS, bool LEPI, int G4_LAG>
 __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const G4Args a) {
     static_assert(NS >= 4 && NS * SLOT <= 160 * 1024, "LDS ring");
     __shared__ __attribute__((aligned(1024))) char lds[NS * SLOT];
@@ -161,16 +162,31 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const G4Args a) {
         }                                                                                                  \
         _Pragma("unroll") for (int b = 4; b < 8; ++b)                                                      \
             xf[b] = *reinterpret_cast<const u32x4*>(s + xoff + b * 1024);                                  \
-        /* keep the refills between the MFMAs (hipcc otherwise sinks all 16 reads below the last MFMA) */  \
-        _Pragma("unroll") for (int b = 0; b < 4; ++b) {                                                    \
-            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);                                             \
+        /* keep the refills between the MFMAs (hipcc otherwise sinks all 16 reads below the last MFMA); with  \
+           G4_LAG = 4 each refill issues 4 MFMAs after the last MFMA that reads the register it overwrites */  \
+        if constexpr (G4_LAG == 4) {                                                                       \
+            __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);                                            \
             __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                             \
+            _Pragma("unroll") for (int b = 1; b < 4; ++b) {                                                \
+                __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);                                         \
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
+            }                                                                                              \
+            _Pragma("unroll") for (int k = 0; k < 7; ++k) {                                                \
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                         \
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
+            }                                                                                              \
+            __builtin_amdgcn_sched_group_barrier(0x100, 5, 0);                                             \
+        } else {                                                                                           \
+            _Pragma("unroll") for (int b = 0; b < 4; ++b) {                                                \
+                __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);                                         \
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
+            }                                                                                              \
+            _Pragma("unroll") for (int k = 0; k < 8; ++k) {                                                \
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                         \
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                         \
+            }                                                                                              \
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                                             \
         }                                                                                                  \
-        _Pragma("unroll") for (int i = 0; i < 8; ++i) {                                                    \
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);                                             \
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                                             \
-        }                                                                                                  \
-        __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                                                 \
     }
     for (int t = 0; t < nk; ++t) G4_STEP(t)
 #undef G4_STEP
@@ -238,9 +254,11 @@ __global__ __launch_bounds__(256, 1) void gemm4w_kernel(const G4Args a) {
 }
 
 // Same contract as mrsum_gemm's bf16 path (epi 0 plain, 1 SwiGLU of the [8 gate | 8 up] rows): x [M, K] (ldx
-// elements), w [N, K] (ldw), c (ldc).  K % 64 == 0 (an even count of 32-k steps), N % 16 == 0, 16-byte aligned rows.  ns: LDS ring steps (4 or 5).
+// elements), w [N, K] (ldw), c (ldc).  K % 64 == 0 (an even count of 32-k steps), N % 16 == 0, 16-byte aligned rows.  ns: LDS ring steps (4 or 5) | 256 for the lagged refill schedule.
 MRSUM_API int mrsum_gemm4w(const void* x, int ldx, const void* w, int ldw, void* c, int ldc, int M, int N, int K,
                            int epi, int group_m, int ns, hipStream_t s) {
+    const int lag = (ns >> 8) & 1 ? 4 : 0;  // bit 8: refills 4 MFMAs after their registers' last reader
+    ns &= 255;
     if (M <= 0 || N <= 0) return 0;
     if (K % 64 || N % 16 || ldx % 8 || ldw % 8 || ldc % 4 || (epi != 0 && epi != 1) || (ns != 4 && ns != 5))
         return (int)hipErrorInvalidValue;
@@ -253,14 +271,16 @@ MRSUM_API int mrsum_gemm4w(const void* x, int ldx, const void* w, int ldw, void*
     a.group_m = group_m > 0 ? group_m : 4;
     const dim3 grid(a.tiles_m * a.tiles_n), block(256);
     const bool lepi = ldc % 8 == 0 && (uintptr_t)c % 16 == 0;
-#define G4_LAUNCH(E, NS_)                                                       \
-    if (lepi) gemm4w_kernel<E, NS_, true><<<grid, block, 0, s>>>(a);             \
-    else gemm4w_kernel<E, NS_, false><<<grid, block, 0, s>>>(a);
+#define G4_LAUNCH(E, NS_, L)                                                    \
+    if (lepi) gemm4w_kernel<E, NS_, true, L><<<grid, block, 0, s>>>(a);          \
+    else gemm4w_kernel<E, NS_, false, L><<<grid, block, 0, s>>>(a);
+#define G4_BY_LAG(E, NS_) if (lag) { G4_LAUNCH(E, NS_, 4) } else { G4_LAUNCH(E, NS_, 0) }
     if (ns == 4) {
-        if (epi == 1) { G4_LAUNCH(1, 4) } else { G4_LAUNCH(0, 4) }
+        if (epi == 1) { G4_BY_LAG(1, 4) } else { G4_BY_LAG(0, 4) }
     } else {
-        if (epi == 1) { G4_LAUNCH(1, 5) } else { G4_LAUNCH(0, 5) }
+        if (epi == 1) { G4_BY_LAG(1, 5) } else { G4_BY_LAG(0, 5) }
     }
+#undef G4_BY_LAG
 #undef G4_LAUNCH
     return (int)hipGetLastError();
 }

@@ -620,8 +620,8 @@ def gemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, s
         return out
     if kernel is None:
         kernel = GEMM_KERNEL
-    if kernel in ("4w", "4w5"):
-        return gemm4w(x, w, out, swiglu, group_m, ns=5 if kernel == "4w5" else 4)
+    if kernel.startswith("4w"):  # "4w" / "4w5": 4- / 5-step ring; "L": lagged refills
+        return gemm4w(x, w, out, swiglu, group_m, ns=(5 if "5" in kernel else 4) | (256 if kernel.endswith("L") else 0))
     return _gemm(_p(x), x.stride(0), _p(w), w.stride(0), out, M, N, K, 0,
                  GEMM_EPI_SWIGLU if swiglu else GEMM_EPI_BF16, None, None, group_m)
 

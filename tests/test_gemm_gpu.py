@@ -141,7 +141,7 @@ def test_gemm_graph_capture():
     _check(out, x.float() @ w.float().t())
 
 
-@pytest.mark.parametrize("kernel", ["4w", "4w5"])
+@pytest.mark.parametrize("kernel", ["4w", "4w5", "4wL", "4w5L"])
 @pytest.mark.parametrize("M,N,K", [(65, 256, 128), (1000, 1280, 4096), (4097, 6144, 4096), (300, 16032, 1024),
                                    (257, 4096, 14336), (16384 + 13, 4096, 1024)])
 @pytest.mark.parametrize("aligned", [True, False])
@@ -162,7 +162,7 @@ def test_gemm4w_bf16(kernel, M, N, K, aligned):
     _check(out, ref)
 
 
-@pytest.mark.parametrize("kernel", ["4w", "4w5"])
+@pytest.mark.parametrize("kernel", ["4w", "4w5", "4wL", "4w5L"])
 def test_gemm4w_identity_and_swiglu(kernel):
     K = 256
     x = torch.eye(K, dtype=torch.bfloat16, device=DEV)

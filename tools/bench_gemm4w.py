@@ -25,6 +25,8 @@ def main():
         fns = {"8w": lambda: hip.gemm(x, w, out=out, swiglu=sw, kernel="8w"),
                "4w": lambda: hip.gemm(x, w, out=out, swiglu=sw, kernel="4w"),
                "4w5": lambda: hip.gemm(x, w, out=out, swiglu=sw, kernel="4w5"),
+               "4wL": lambda: hip.gemm(x, w, out=out, swiglu=sw, kernel="4wL"),
+               "4w5L": lambda: hip.gemm(x, w, out=out, swiglu=sw, kernel="4w5L"),
                "blas": lambda: torch.matmul(x, w.t(), out=ref)}
         # agreement of the two own kernels (same math, different summation order)
         a = hip.gemm(x, w, swiglu=sw, kernel="8w").float()
