@@ -85,7 +85,7 @@ def main():
         if v.startswith("attn"):
             fused = v.startswith("attnfused")
             S = int(v[len("attnfused"):] if fused else v[len("attnsep"):])
-            hip.decode_attn_plan = lambda B, hkv, ctx: (S, fused) if B == bucket else base_attn(B, hkv, ctx)
+            hip.decode_attn_plan = lambda B, hkv, ctx, **kw: (S, fused) if B == bucket else base_attn(B, hkv, ctx, **kw)
             return
         role, kind, p1, p2 = v.split(":")
         p = (kind, int(p1), int(p2))
