@@ -450,13 +450,13 @@ def decode_attn_plan_bf16(batch: int, hkv: int, max_ctx: int):
             # B=5 at 4k: 6 splits fused 22.6 us, unfused 23.3; a TP shard's one or two kv heads at B=20 (20 groups,
             # 4k) take 12 fused splits: 1.971 / 1.971 ms per TP=8 shard step vs 8 fused 2.020 / 2.016, 12
             # separate 1.984 (in situ, profiles/r3_plans_insitu_tp8_b39_b20.jsonl).  Longer contexts (the <= 12k
-            # class: the level-1 reduce) take about one workgroup per CU, in situ at ~6k
-            # (profiles/r4_attn_plans_insitu_class1.jsonl): B=5 6 fused 3.92 ms vs 4 4.10, B=10 3 fused 4.52 vs 4
-            # 4.64, B=16 2 fused 5.25 vs 4 5.28
+            # class: the level-1 reduce) take 6 fused splits -- in situ at ~6k (profiles/
+            # r4_attn_plans_insitu_class1.jsonl; ``batch`` here is the graph's bucket): batch 5 in bucket 8
+            # 3.92 ms per step vs 4.10 with 4 splits, batch 10 in bucket 16 4.52 vs 4.64 (3 splits tie)
             if pages <= 96:
                 splits = min(splits, 12 if hkv <= 2 else 8)
             else:
-                splits = min(splits, 4 if hkv <= 2 else max(1, min(8, N_CU // groups)))
+                splits = min(splits, 4 if hkv <= 2 else 6)
     return splits, fused
 
 

@@ -48,12 +48,11 @@ def test_decode_attn_plan_measured_choices():
     assert not fused and s == 64
 
 
-def test_decode_attn_plan_class1_one_workgroup_per_cu():
-    # the <= 12k context class (level-1 reduce at ~6k): fused splits sized to ~one workgroup per CU, in situ
-    # (profiles/r4_attn_plans_insitu_class1.jsonl): B=5 6, B=10 3, B=16 2 (4 was slower at all three)
-    assert hip.decode_attn_plan(5, 8, 12288) == (6, True)
-    assert hip.decode_attn_plan(10, 8, 12288) == (3, True)
-    assert hip.decode_attn_plan(16, 8, 12288) == (2, True)
+def test_decode_attn_plan_class1_six_fused_splits():
+    # the <= 12k context class (level-1 reduce at ~6k), per graph bucket: 6 fused splits, in situ
+    # (profiles/r4_attn_plans_insitu_class1.jsonl): batch 5 (bucket 8) and batch 10 (bucket 16) faster than 4
+    assert hip.decode_attn_plan(8, 8, 12288) == (6, True)
+    assert hip.decode_attn_plan(16, 8, 12288) == (6, True)
     # the final reduce (B=1, ~13k, <= 32k class) keeps 32 separate splits (best of 16-64 / fused in situ)
     assert hip.decode_attn_plan(1, 8, 32768) == (32, False)
     # TP shards keep their measured cap of 4 in the longer classes
