@@ -10,6 +10,7 @@ Variants (comma separated, ``plan`` = unchanged):
   gate_up:stream_split:WPB:S   split-K gate_up with the SwiGLU in the last arriver
   deferM                       the TP=1 deferred RMSNorm up to M rows (ops.DEFER_NORM_MAX_M)
   fp8resid:N:K:WPB:S           the fp8 deferred-norm producer (stream_fp8, residual epilogue) of one shape
+  buckets:B1+B2+...            decode graph buckets up to the largest given (the rest unchanged)
   env:NAME=VALUE[+NAME=VALUE]  environment overrides read at call time (e.g. env:MRSUM_RESID_SKINNY_O=1,
                                env:MRSUM_TP_PUSH=0)
 
@@ -56,6 +57,8 @@ def main():
     base_fp8r = hip.fp8_resid_cfg
 
     env_set = []
+    import llm_map_reduce_summarizer_amd.engine.engine as engine_mod
+    base_buckets = engine_mod.BUCKETS
 
     def install(v):
         hip.decode_attn_plan, hip.plan = base_attn, base_plan
@@ -67,7 +70,13 @@ def main():
             else:
                 os.environ[name] = old
         env_set.clear()
+        import llm_map_reduce_summarizer_amd.engine.engine as engine_mod
+        engine_mod.BUCKETS = base_buckets
         if v == "plan":
+            return
+        if v.startswith("buckets:"):  # buckets:1+2+4+8+10+16 -- the decode graph buckets below 24
+            low = tuple(int(t) for t in v[len("buckets:"):].split("+"))
+            engine_mod.BUCKETS = low + tuple(b for b in base_buckets if b > max(low))
             return
         if v.startswith("env:"):
             for kv in v[4:].split("+"):
