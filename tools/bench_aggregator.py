@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--max-new-tokens", type=int, default=1000)
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"],
+                    help="KV-cache format; fp8 is a labelled variant (bf16 KV is the credited number)")
     a = ap.parse_args()
     import torch
     from llm_map_reduce_summarizer_amd.config import LLMConfig
@@ -39,7 +41,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     cfg = LLMConfig(MAX_TOKENS=a.max_new_tokens)
     prov = LocalEngineProvider(a.model, cfg, tp=world, dtype=a.dtype, max_model_len=a.context + a.max_new_tokens + 64,
-                               ignore_eos=True, engine_options={"max_num_seqs": 8})
+                               ignore_eos=True, kv_dtype=a.kv_dtype,
+                               engine_options={"max_num_seqs": 8})
     t0 = time.perf_counter()
     eng = prov.engine
     init_s = time.perf_counter() - t0
@@ -76,7 +79,7 @@ def main():
            "prompt_tokens": res.prompt_tokens, "completion_tokens": res.completion_tokens,
            "prefill_s": round(pf_s, 3), "prefill_tok_s": round(res.prompt_tokens / pf_s, 1) if pf_s else None,
            "decode_ms_per_token": round(1000 * dec_s / max(1, dec_steps), 3),
-           "weights_gib": round(eng.model.weight_bytes() / 2 ** 30, 1), "init_s": round(init_s, 1),
+           "kv_dtype": a.kv_dtype, "weights_gib": round(eng.model.weight_bytes() / 2 ** 30, 1), "init_s": round(init_s, 1),
            "hbm_peak_gib": round(torch.cuda.max_memory_allocated() / 2 ** 30, 1),
            "data": "synthetic summaries; random-init weights; generation pinned to max_new_tokens"}
     # the planner's cost model for this pass on an 8-GPU node (TP=8): what a TP prefill forward (RCCL
