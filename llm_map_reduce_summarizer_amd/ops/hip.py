@@ -626,6 +626,9 @@ def gemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, s
         return out
     if kernel is None:
         kernel = GEMM_KERNEL
+    if kernel == "blas" and not swiglu and out.is_contiguous():
+        # plain product on the vendor library (hipBLASLt through torch.mm), for the A/B measurement
+        return torch.mm(x, w.t(), out=out)
     if kernel.startswith("4w"):  # "4w" / "4w5": 4- / 5-step ring; "L": lagged refills
         return gemm4w(x, w, out, swiglu, group_m, ns=(5 if "5" in kernel else 4) | (256 if kernel.endswith("L") else 0))
     return _gemm(_p(x), x.stride(0), _p(w), w.stride(0), out, M, N, K, 0,
@@ -633,7 +636,8 @@ def gemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, s
 
 
 # bf16 prefill GEMM kernel: "8w" = gemm.hip (8 waves, 128 x 64 per wave), "4w" / "4w5" = gemm4w.hip (4 waves,
-# 128 x 128 per wave, 4- / 5-step LDS ring); MRSUM_GEMM_KERNEL overrides for measurements
+# 128 x 128 per wave, 4- / 5-step LDS ring), "blas" = the plain (non-SwiGLU) products on hipBLASLt;
+# MRSUM_GEMM_KERNEL overrides for measurements
 GEMM_KERNEL = os.environ.get("MRSUM_GEMM_KERNEL", "8w")
 
 
