@@ -179,3 +179,19 @@ def test_gemm4w_identity_and_swiglu(kernel):
         torch.cuda.synchronize()
         g, u = x.float() @ wg.float().t(), x.float() @ wu.float().t()
         _check(out, torch.nn.functional.silu(g) * u, tol=3e-2)
+
+
+def test_gemm_blas_knob():
+    """kernel="blas" (the A/B knob, profiles/r4_prefill_plain_gemm_blas_ab.jsonl): the plain product on hipBLASLt
+    matches the fp32 reference; a SwiGLU product stays on gemm.hip, bit-identical to the default kernel."""
+    for M, N, K in ((3000, 4096, 4096), (777, 6144, 4096)):
+        x, w = _rand(M, K, seed=31, scale=0.5), _rand(N, K, seed=32, scale=0.03)
+        out = hip.gemm(x, w, kernel="blas")
+        torch.cuda.synchronize()
+        _check(out, x.float() @ w.float().t(), tol=3e-2)
+    K, F = 4096, 1792
+    x = _rand(500, K, seed=33, scale=0.5)
+    wgu = reference.interleave_gate_up(_rand(F, K, seed=34, scale=0.03), _rand(F, K, seed=35, scale=0.03)).contiguous()
+    a, b = hip.gemm(x, wgu, swiglu=True, kernel="blas"), hip.gemm(x, wgu, swiglu=True, kernel="8w")
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
