@@ -471,7 +471,9 @@ static bool tp_push_ok(const void* ar, int epi, int M, int N) {
 // Split-K last-arriver epilogues take ``counters`` >= N / (16 wpb) ints, zero on the first call (every
 // launch leaves them zero again).  ssq (any epilogue): deferred-RMSNorm input, [M, ssq_tiles] fp32 row
 // sums of squares of x (x = the un-normalised residual rows), ssq_tiles % 32 == 0; the product rows are
-// scaled by rsqrt(sum / K + eps).  N % (16 wpb) == 0, wpb in {4, 5, 6, 7, 8}, M <= 64.
+// scaled by rsqrt(sum / K + eps).  N % (16 wpb) == 0, wpb in {4, 5, 6, 7, 8}, M <= 64 -- or 64 < M <= 128
+// (decode batches of 65-128 sequences: 96- / 128-row x tiles, one pass over the weights instead of one per
+// 64-row chunk) for the bf16 / fp32-slab / SwiGLU epilogues without a deferred norm.
 // Decode weights are streamed with nontemporal loads (each weight row read once per step by one CU:
 // MI355X_MICROARCH.md "nt-weights"; profiles/r1_decode_nt_ab.jsonl).
 MRSUM_API int mrsum_stream_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
@@ -479,9 +481,11 @@ MRSUM_API int mrsum_stream_gemm(const void* x, int ldx, const void* W, int N, in
                                 int ssq_tiles, float eps, void* resid, int ldr, float* ssp, int slab_m, void* ar,
                                 hipStream_t s) {
     if (M <= 0) return 0;
-    if (wpb < 4 || wpb > 8 || M > 64 || K % KBLK || N % (16 * wpb) || splits < 1 || (K / KBLK) % splits ||
+    if (wpb < 4 || wpb > 8 || M > 128 || K % KBLK || N % (16 * wpb) || splits < 1 || (K / KBLK) % splits ||
         epi < EPI_BF16 || epi > EPI_RESID_SPLIT)
         return (int)hipErrorInvalidValue;
+    if (M > 64 && (ssq || (epi != EPI_BF16 && epi != EPI_F32_PARTIAL && epi != EPI_SWIGLU)))
+        return (int)hipErrorInvalidValue;  // tall tiles: no deferred norm, no split-K last-arriver epilogue
     const bool split_epi = epi == EPI_SWIGLU_SPLIT || epi == EPI_RESID_SPLIT;
     if (epi != EPI_F32_PARTIAL && !split_epi && splits != 1) return (int)hipErrorInvalidValue;
     if (split_epi && (!parts || !counters)) return (int)hipErrorInvalidValue;
@@ -515,12 +519,19 @@ MRSUM_API int mrsum_stream_gemm(const void* x, int ldx, const void* W, int N, in
     else if (epi == EPI_SWIGLU) { BY_WPB(MT_, EPI_SWIGLU) }                   \
     else if (epi == EPI_SWIGLU_SPLIT) { BY_WPB(MT_, EPI_SWIGLU_SPLIT) }       \
     else { BY_WPB(MT_, EPI_RESID_SPLIT) }
+#define BY_EPI_TALL(MT_)                                                      \
+    if (epi == EPI_BF16) { BY_WPB(MT_, EPI_BF16) }                            \
+    else if (epi == EPI_F32_PARTIAL) { BY_WPB(MT_, EPI_F32_PARTIAL) }         \
+    else { BY_WPB(MT_, EPI_SWIGLU) }
     switch (mt) {
         case 1: BY_EPI(1); break;
         case 2: BY_EPI(2); break;
         case 3: BY_EPI(3); break;
-        default: BY_EPI(4); break;
+        case 4: BY_EPI(4); break;
+        case 5: case 6: BY_EPI_TALL(6); break;
+        default: BY_EPI_TALL(8); break;
     }
+#undef BY_EPI_TALL
 #undef BY_EPI
 #undef BY_WPB
 #undef L

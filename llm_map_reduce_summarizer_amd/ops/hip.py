@@ -776,21 +776,57 @@ def _stream_gemm(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, no
     M, K = x.shape
     N = w.shape[0]
     if M > SKINNY_MAX_M and epi in (EPI_BF16, EPI_F32_PARTIAL, EPI_SWIGLU) and norm is None:
-        # 64-row chunks: row slices of the bf16 output, or of every fp32 slab (slab row stride = M)
-        for r0 in range(0, M, SKINNY_MAX_M):
-            r1 = min(M, r0 + SKINNY_MAX_M)
-            o = out[:, r0:r1] if epi == EPI_F32_PARTIAL else out[r0:r1]
-            _stream_launch(x[r0:r1], w, o, epi, splits, ldo, wpb, None, None, None, None, None,
-                           M if epi == EPI_F32_PARTIAL else 0)
+        # up to STREAM_TALL_M rows in one pass over the weights (96- / 128-row x tiles, a workgroup width that
+        # keeps a 3-slot ring); above that, row chunks of that height: row slices of the bf16 output, or of
+        # every fp32 slab (slab row stride = M)
+        ch = STREAM_TALL_M if STREAM_TALL_M > SKINNY_MAX_M else SKINNY_MAX_M
+        for r0 in range(0, M, ch):
+            r1 = min(M, r0 + ch)
+            if r1 - r0 > SKINNY_MAX_M:
+                tw = tall_wpb(N, r1 - r0, splits)
+                if tw is not None:
+                    o = out[:, r0:r1] if epi == EPI_F32_PARTIAL else out[r0:r1]
+                    _stream_launch(x[r0:r1], w, o, epi, splits, ldo, tw, None, None, None, None, None,
+                                   M if epi == EPI_F32_PARTIAL else 0)
+                    continue
+            for c0 in range(r0, r1, SKINNY_MAX_M):
+                c1 = min(r1, c0 + SKINNY_MAX_M)
+                o = out[:, c0:c1] if epi == EPI_F32_PARTIAL else out[c0:c1]
+                _stream_launch(x[c0:c1], w, o, epi, splits, ldo, wpb, None, None, None, None, None,
+                               M if epi == EPI_F32_PARTIAL else 0)
         return out
     return _stream_launch(x, w, out, epi, splits, ldo, wpb, parts, counters, norm, resid, ssp, 0, ar)
+
+
+# Decode batches of 65-128 rows run the stream GEMM on 96- / 128-row x tiles in ONE pass over the weights
+# (stream_gemm.hip); before, each 64-row chunk re-streamed every weight byte.  MRSUM_STREAM_TALL_M=64 restores
+# the 64-row chunks (A/B).
+STREAM_TALL_M = int(os.environ.get("MRSUM_STREAM_TALL_M", "128"))
+_TALL_WPB = {6: (4, 5, 6), 8: (4,)}  # widths whose slot (16 wpb W rows + 16 MT x rows) x 256 B leaves a 3-slot ring
+
+
+def tall_wpb(N: int, M: int, splits: int) -> Optional[int]:
+    """Workgroup width (waves) of the tall-tile stream GEMM for M in (64, 128] rows: among the widths that
+    keep a 3-slot LDS ring at that tile height, the one whose grid (N / (16 wpb) x splits) best fills whole
+    rounds of one workgroup per CU; None if no width divides N."""
+    mt = 6 if M <= 96 else 8
+    best, key = None, None
+    for wpb in _TALL_WPB[mt]:
+        if N % (16 * wpb):
+            continue
+        grid = N // (16 * wpb) * splits
+        k = (round(grid / (-(-grid // N_CU) * N_CU), 3), wpb)
+        if key is None or k > key:
+            best, key = wpb, k
+    return best
 
 
 def _stream_launch(x, w, out, epi, splits, ldo, wpb, parts, counters, norm, resid, ssp, slab_m, ar=None):
     M, K = x.shape
     N = w.shape[0]
     _req(w.is_contiguous() and w.shape[1] == K, "stream_gemm: weight must be [N, K] contiguous")
-    _req(1 <= M <= SKINNY_MAX_M and K % 128 == 0 and 4 <= wpb <= 8 and N % (16 * wpb) == 0
+    tall_ok = M <= 128 and epi in (EPI_BF16, EPI_F32_PARTIAL, EPI_SWIGLU) and norm is None
+    _req(1 <= M and (M <= SKINNY_MAX_M or tall_ok) and K % 128 == 0 and 4 <= wpb <= 8 and N % (16 * wpb) == 0
          and (K // 128) % splits == 0, "stream_gemm: unsupported shape M=%d N=%d K=%d S=%d wpb=%d"
          % (M, N, K, splits, wpb))
     if epi in (EPI_SWIGLU_SPLIT, EPI_RESID_SPLIT):

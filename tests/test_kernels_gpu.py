@@ -974,3 +974,26 @@ def test_rmsnorm_fp8_two_term(add):
     out = hip.gemm_fp8(q, sc, wq)
     ref = two @ wq.dequant().t()
     _close(out, ref, 2e-2)
+
+
+@pytest.mark.parametrize("M", [65, 92, 128, 200])
+def test_stream_gemm_tall_tiles_match_row_chunks(M, monkeypatch):
+    """65-128 decode rows run in ONE pass over the weights on 96- / 128-row x tiles (hip.STREAM_TALL_M); every
+    output element accumulates over k in the same order as the 64-row chunks, so the two are bit-identical --
+    bf16 rows, fp32 split-K slabs and SwiGLU, at Llama-3-8B widths."""
+    K = 4096
+    x = _rand(M, K, seed=80)
+    for n, S, epi in ((6144, 4, hip.EPI_F32_PARTIAL), (4096, 1, hip.EPI_BF16), (2048, 1, hip.EPI_SWIGLU)):
+        w = _rand(n, K, scale=0.02, seed=81)
+        wpb = 4 if epi != hip.EPI_F32_PARTIAL else 6
+        shape = (S, M, n) if epi == hip.EPI_F32_PARTIAL else (M, n // 2 if epi == hip.EPI_SWIGLU else n)
+        dt = torch.float32 if epi == hip.EPI_F32_PARTIAL else torch.bfloat16
+        outs = []
+        for tall in (128, 64):
+            monkeypatch.setattr(hip, "STREAM_TALL_M", tall)
+            o = torch.full(shape, float("nan"), dtype=dt, device=DEV)
+            outs.append(hip._stream_gemm(x, w, o, epi, S, n // 2 if epi == hip.EPI_SWIGLU else n, wpb))
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]), (n, S, epi)
+        if epi == hip.EPI_F32_PARTIAL:
+            _close(outs[0].sum(0), x.float() @ w.float().t(), 1e-3, 1e-3)
