@@ -802,6 +802,7 @@ def _stream_gemm(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, no
 # (stream_gemm.hip); before, each 64-row chunk re-streamed every weight byte.  MRSUM_STREAM_TALL_M=64 restores
 # the 64-row chunks (A/B).
 STREAM_TALL_M = int(os.environ.get("MRSUM_STREAM_TALL_M", "128"))
+LINEAR_TALL = os.environ.get("MRSUM_LINEAR_TALL", "1") == "1"  # linear() (the LM head) too; 0 for the A/B
 _TALL_WPB = {6: (4, 5, 6), 8: (4,)}  # widths whose slot (16 wpb W rows + 16 MT x rows) x 256 B leaves a 3-slot ring
 
 
@@ -848,17 +849,22 @@ def linear_takes_norm(M: int, N: int, K: int) -> bool:
 
 def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, norm=None) -> torch.Tensor:
     """x @ w^T, bf16 out: the 256 x 256-tile MFMA GEMM for M > 64 (or shapes the decode kernels do not
-    take), else the LDS-DMA weight-ring stream GEMM when it fills the chip (the LM head), else the
+    take; up to 128 rows of a stream shape take the tall-tile stream GEMM), else the LDS-DMA weight-ring
+    stream GEMM when it fills the chip (the LM head), else the
     register-streaming skinny kernel.  ``norm`` (stream shapes only, see linear_takes_norm): x holds
     un-normalised residual rows, scaled by their deferred RMSNorm factor in the epilogue."""
     M, K = x.shape
     N = w.shape[0]
     _req(norm is None or linear_takes_norm(M, N, K), "linear: a deferred norm needs a stream-GEMM shape")
-    if M > SKINNY_MAX_M or M == 0 or K % 128:
+    tall = (LINEAR_TALL and SKINNY_MAX_M < M <= min(STREAM_TALL_M, 128) and K % 128 == 0 and norm is None
+            and stream_config(N, K, splits=1) is not None and tall_wpb(N, M, 1) is not None)
+    if (M > SKINNY_MAX_M and not tall) or M == 0 or K % 128:
         return gemm(x, w, out=out)
     if out is None:
         out = torch.empty(M, N, dtype=x.dtype, device=x.device)
     _req(out.is_contiguous() and out.shape == (M, N), "linear: bad out")
+    if tall:  # a decode LM head of 65-128 rows: one pass over the weights on the tall-tile stream GEMM
+        return _stream_gemm(x, w, out, EPI_BF16, 1, N, tall_wpb(N, M, 1))
     cfg = stream_config(N, K, splits=1)
     if cfg is not None:
         return _stream_gemm(x, w, out, EPI_BF16, 1, N, cfg[0], norm=norm)

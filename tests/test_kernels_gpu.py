@@ -997,3 +997,14 @@ def test_stream_gemm_tall_tiles_match_row_chunks(M, monkeypatch):
         assert torch.equal(outs[0], outs[1]), (n, S, epi)
         if epi == hip.EPI_F32_PARTIAL:
             _close(outs[0].sum(0), x.float() @ w.float().t(), 1e-3, 1e-3)
+
+
+@pytest.mark.parametrize("M", [65, 96, 128])
+def test_linear_tall_lm_head(M):
+    """linear() of 65-128 rows of a stream shape (the decode LM head of the 24 h map's bucket 96) runs the
+    tall-tile stream GEMM: against fp32, and equal to the 256 x 256-tile GEMM within bf16 rounding."""
+    K, N = 4096, 16 * 4 * 1002  # a vocabulary-like width that the stream kernel tiles (wpb 4)
+    x, w = _rand(M, K, seed=90), _rand(N, K, scale=0.02, seed=91)
+    out = hip.linear(x, w)
+    torch.cuda.synchronize()
+    _close(out, x.float() @ w.float().t(), 2e-2)
