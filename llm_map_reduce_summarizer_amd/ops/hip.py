@@ -779,7 +779,7 @@ def _stream_gemm(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, no
         # up to STREAM_TALL_M rows in one pass over the weights (96- / 128-row x tiles, a workgroup width that
         # keeps a 3-slot ring); above that, row chunks of that height: row slices of the bf16 output, or of
         # every fp32 slab (slab row stride = M)
-        ch = STREAM_TALL_M if STREAM_TALL_M > SKINNY_MAX_M else SKINNY_MAX_M
+        ch = min(STREAM_TALL_M, 128) if STREAM_TALL_M > SKINNY_MAX_M else SKINNY_MAX_M  # kernel: <= 128 rows
         for r0 in range(0, M, ch):
             r1 = min(M, r0 + ch)
             if r1 - r0 > SKINNY_MAX_M:
