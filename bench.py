@@ -183,6 +183,14 @@ def main() -> int:
     work_ok = work["errors"] == 0 and (args.stop_at_eos or work["completion_tokens"] == work["requested_tokens"])
     rep = reports[-1]
     ms = elapsed / max(1, args.steps) * 1000.0
+    # the P2P all-reduce paths of every TP engine this job built (start-up self-test at the model's shapes,
+    # per path) and how many generates fell back to RCCL after a timed-out P2P wait
+    pstats = provider.stats()
+    tp_engs = dict(pstats.get("tp_engines", {}))
+    if "tp_engine" in pstats:
+        tp_engs[str(world)] = pstats["tp_engine"]
+    p2p = {("tp%s" % k): e.get("p2p_selftest") for k, e in sorted(tp_engs.items())}
+    ar_recoveries = sum(int(e.get("custom_ar_recoveries", 0)) for e in tp_engs.values())
     n_chunks = rep["chunks"]
     value = n_chunks / (ms / 1000.0)
     eng = rep.get("engine", {})
@@ -220,17 +228,30 @@ def main() -> int:
         "reduce_plan": rep.get("reduce_plan"),
         "tokens_used": rep.get("tokens_used"),
         "timed_work": dict(work, pinned_ok=work_ok),
+        "p2p_selftest": p2p or None,
+        "ar_recoveries": ar_recoveries,
         "engine_rank0": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in eng.items()},
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
-    pdist.shutdown()
+    rc = 0
     if not work_ok:
         print("bench: timed work is not the pinned work: %d of %d requested tokens generated, %d failed requests"
               % (work["completion_tokens"], work["requested_tokens"], work["errors"]), file=sys.stderr)
-        return 3
-    return 0
+        rc = 3
+    # the measurement is complete and printed: a teardown error must not turn it into a failed run
+    try:
+        pdist.shutdown()
+    except Exception as e:  # noqa: BLE001
+        print("bench: process-group teardown raised after the result was printed: %r" % (e,), file=sys.stderr)
+    return rc
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    code = main()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    # the process groups are already torn down (pdist.shutdown: barrier, subgroups, default group); leave
+    # without the interpreter's finalisation, where the C++ destructors of communication backends that
+    # still hold threads have aborted a finished job (SIGABRT after a good result)
+    os._exit(code)

@@ -23,12 +23,17 @@ __device__ __forceinline__ size_t slab_off(int page, int Hkv, int head) {
     return ((size_t)page * Hkv + head) * SLAB;
 }
 
-// the power of two >= amax / 448 (1 for an all-zero row)
+// the power of two >= amax / 448 (1 for an all-zero row), never below 2^-126: a subnormal scale would make
+// 1 / scale overflow to inf and a zero element of the row 0 * inf = NaN, poisoning every later attention
+// step over the sequence.  Rows with 0 < amax < 448 * 2^-126 quantise against 2^-126 (their elements
+// round towards zero, as bf16 would flush them anyway).
+constexpr int MIN_SCALE_EXP = -126;
 __device__ __forceinline__ float row_scale(float amax) {
     if (!(amax > 0.f)) return 1.f;
     int e;
     const float m = frexpf(amax * (1.f / 448.f), &e);  // amax / 448 = m 2^e, m in [0.5, 1)
-    return ldexpf(1.f, m == 0.5f ? e - 1 : e);
+    e = m == 0.5f ? e - 1 : e;
+    return ldexpf(1.f, e < MIN_SCALE_EXP ? MIN_SCALE_EXP : e);
 }
 
 __device__ __forceinline__ unsigned pack4(float a, float b, float c, float d) {

@@ -753,243 +753,3 @@ MRSUM_API int mrsum_skinny_fp8(const void* x, int ldx, const void* W, const floa
 #undef L
     return (int)hipGetLastError();
 }
-
-
-// ---------------------------------------------------------------------------------------------
-// Fused decode MLP of a tensor-parallel shard (M <= 16 rows): gate_up + SwiGLU and down + residual
-// update (+ the TP push) in ONE launch.  On a TP=8 shard of Llama-3-8B the two launches it replaces
-// stream 29 + 15 MB in 9.2 + 6.7 us (profiles/r3_tp8shard_b1_push_gaps.txt): most of the down launch is
-// its own ramp and drain, not bytes.  Here the down weights never wait for the seam:
-//
-//  * phase A (workgroups < F / 8): skinny_gemm_kernel's SWIGLU tile (16 W rows = 8 gate + 8 up features,
-//    deferred-RMSNorm row scale), its h values published as 8-byte {epoch, 2 x bf16} granules with
-//    agent-scope (sc1) stores -- the data is its own flag (cdna_hip_programming.md Guideline 16, R2);
-//  * every workgroup < H / 16 issues ALL of its down-projection tile's weight loads (K = F <= 2048: <= 4 k
-//    blocks of 128 per wave held in registers) at ENTRY, before its phase-A loads, so the down weights
-//    stream together with gate_up's instead of after a kernel boundary (first measurement: issued after
-//    phase A, the launch lost 1-2.5 us per layer to the two-launch form);
-//  * phase B: each wave reads its h fragments as 16-B sc1 loads and re-reads them (s_sleep between
-//    polls, bounded by ar_common.h's 4 s wall-clock limit -> sticky error word) until every granule
-//    carries this launch's epoch, then the MFMAs and skinny_gemm_kernel's RESID epilogue (TP push,
-//    residual update, per-tile sums of squares for the next consumer).
-//
-// Epoch: workgroup b reads ep[b] + 1 at entry and stores it back at exit; every launch of one grid size
-// advances all its words by one, so they stay equal (lockstep) with no arrival counter, no per-call memset
-// and no launch argument frozen by capture (the workspace is per grid size: ops/hip.py).  Progress:
-// phase-B waves wait only for phase-A tiles, which wait for nothing -- every workgroup must be resident at
-// once (dispatch order is undefined), so the launcher refuses grids above occupancy x CUs.
-namespace {
-constexpr int MLP_MAXB = 4;  // down-projection k blocks per wave in registers: F <= 4 waves x 4 x 128
-
-struct MlpArgs {
-    unsigned long long* h;  // [M][F / 2] granules (epoch << 32 | bf16 pair)
-    unsigned* ep;           // [gridDim.x] per-workgroup epoch words (lockstep, see above)
-    unsigned* error;        // timeout word (the TP group's when pushing)
-    int F, H, na, nb;       // ffn width, hidden, gate_up tiles (F / 8), down tiles (H / 16)
-};
-
-__device__ __forceinline__ bool mlp_spin_done(unsigned long long& t0, unsigned spins, unsigned* error) {
-    if (spins == 0) {
-        t0 = __builtin_amdgcn_s_memrealtime();
-        return __hip_atomic_load(error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-    }
-    if (__builtin_amdgcn_s_memrealtime() - t0 > mrsum_ar::WAIT_TICKS) {
-        atomicOr(error, 1u);
-        return true;
-    }
-    __builtin_amdgcn_s_sleep(1);
-    return false;
-}
-}  // namespace
-
-__global__ __launch_bounds__(256) void mlp_fused_kernel(const bf16* __restrict__ x, int ldx,
-                                                        const bf16* __restrict__ Wgu, const bf16* __restrict__ Wd,
-                                                        int M, const SkinnyNorm e, const MlpArgs a) {
-    __shared__ __attribute__((aligned(16))) float red[4][16][16 + 4];
-    __shared__ float s_part[8 * 16];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, bx = blockIdx.x;
-    const int r = lane & 15, g = lane >> 4;
-    const unsigned prev_epoch = a.ep[bx];
-    const unsigned epoch = prev_epoch + 1 ? prev_epoch + 1 : 1;
-    const bool do_a = bx < a.na, do_b = bx < a.nb;
-    const int nb0 = bx * 16;  // phase B: this workgroup's 16 output columns
-    const unsigned tp_epoch = do_b && e.tp.world > 0 ? e.tp.epochs[nb0 / mrsum_ar::GRAN] + 1 : 0;
-    const int H = a.H, F = a.F, FW = a.F / 2;
-    // phase B's weights first: every k block (w + 4 j) of this wave's down tile, in flight under phase A
-    const int nblk_b = do_b ? (F / KB - w + 3) / 4 : 0;  // <= MLP_MAXB (launcher)
-    AFrag<1> pre[MLP_MAXB];
-#pragma unroll
-    for (int j = 0; j < MLP_MAXB; ++j)
-        if (j < nblk_b) load_a<1>(pre[j], Wd, F, nb0, (w + 4 * j) * KB, lane);
-
-    if (do_a) {  // ---- phase A: gate_up + SwiGLU of features [8 bx, 8 bx + 8)
-        const bool ss_mine = e.ssq && threadIdx.x < 8 * M;
-        SsLoads ssl;
-        if (ss_mine) deferred_issue(e, threadIdx.x >> 3, threadIdx.x & 7, ssl);
-        f32x4 acc[1][1] = {{f32x4{0.f, 0.f, 0.f, 0.f}}};
-        const int n0 = bx * 16;
-        const int kb0 = w * KB;
-        const int nblk = (H - kb0 + 4 * KB - 1) / (4 * KB);
-        AFrag<1> a0, a1;
-        BFrag<1> b;
-        load_a<1>(a0, Wgu, H, n0, kb0, lane);
-        int i = 0;
-        for (; i + 2 < nblk; i += 2) {
-            const int kb = kb0 + i * 4 * KB;
-            load_b<1>(b, x, ldx, M, kb, lane);
-            load_a<1>(a1, Wgu, H, n0, kb + 4 * KB, lane);
-            mma_block<1, 1>(acc, a0, b);
-            load_b<1>(b, x, ldx, M, kb + 4 * KB, lane);
-            load_a<1>(a0, Wgu, H, n0, kb + 8 * KB, lane);
-            mma_block<1, 1>(acc, a1, b);
-        }
-        if (nblk - i == 2) {
-            const int kb = kb0 + i * 4 * KB;
-            load_b<1>(b, x, ldx, M, kb, lane);
-            load_a<1>(a1, Wgu, H, n0, kb + 4 * KB, lane);
-            mma_block<1, 1>(acc, a0, b);
-            load_b<1>(b, x, ldx, M, kb + 4 * KB, lane);
-            mma_block<1, 1>(acc, a1, b);
-        } else if (nblk - i == 1) {
-            load_b<1>(b, x, ldx, M, kb0 + i * 4 * KB, lane);
-            mma_block<1, 1>(acc, a0, b);
-        }
-        const int cn = 4 * g, cm = r;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) red[w][cm][cn + j] = acc[0][0][j];
-        if (ss_mine) s_part[threadIdx.x] = deferred_partial(ssl);
-        __syncthreads();
-        // 32 items = 16 rows x {features 0-3, 4-7}; item (m, n4): two granules at h[m][(8 bx + n4) / 2 ..]
-        if (threadIdx.x < 32) {
-            const int m = threadIdx.x >> 1, n4 = (threadIdx.x & 1) * 4;
-            if (m < M) {
-                const float sc = e.ssq ? deferred_row_scale(e, s_part, m) : 1.f;
-                float rr[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float gv = (red[0][m][n4 + j] + red[1][m][n4 + j] + red[2][m][n4 + j] + red[3][m][n4 + j]) * sc;
-                    const float u = (red[0][m][n4 + 8 + j] + red[1][m][n4 + 8 + j] + red[2][m][n4 + 8 + j] +
-                                     red[3][m][n4 + 8 + j]) * sc;
-                    rr[j] = gv / (1.f + __expf(-gv)) * u;
-                }
-                const unsigned long long tag = (unsigned long long)epoch << 32;
-                unsigned long long* d = a.h + (size_t)m * FW + (8 * bx + n4) / 2;
-                __hip_atomic_store(d, tag | pack2(rr[0], rr[1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(d + 1, tag | pack2(rr[2], rr[3]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        __syncthreads();  // red is reused by phase B
-    }
-
-    if (do_b) {  // ---- phase B: residual[:, nb0 .. nb0 + 16) += h . Wd^T (F = K)
-        const int nblk = nblk_b;
-        const __amdgpu_buffer_rsrc_t hr = sc1_rsrc(a.h);
-        const int hrow = min(r, M - 1);
-        f32x4 acc[1][1] = {{f32x4{0.f, 0.f, 0.f, 0.f}}};
-#pragma unroll
-        for (int j = 0; j < MLP_MAXB; ++j) {
-            if (j >= nblk) break;
-            const int kb = (w + 4 * j) * KB;
-            BFrag<1> b;
-            // lane (r, g) needs h[hrow][kb + 8 g + 32 i .. + 8) = 4 granules = two 16-B loads per i
-            const int off0 = (int)(((size_t)hrow * FW + (kb + 8 * g) / 2) * 8);
-            unsigned long long t0 = 0;
-            for (unsigned spins = 0;; ++spins) {
-                bool ok = true;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const u32x4 p = __builtin_amdgcn_raw_buffer_load_b128(hr, off0 + 128 * i, 0, 16);
-                    const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(hr, off0 + 128 * i + 16, 0, 16);
-                    ok &= p[1] == epoch && p[3] == epoch && q[1] == epoch && q[3] == epoch;
-                    b.v[0][i] = make_uint4(p[0], p[2], q[0], q[2]);
-                }
-                if (__all(ok)) break;
-                if (mlp_spin_done(t0, spins, a.error)) break;
-            }
-            mma_block<1, 1>(acc, pre[j], b);
-        }
-        const int cn = 4 * g, cm = r;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) red[w][cm][cn + j] = acc[0][0][j];
-        __syncthreads();
-        // RESID epilogue (skinny_gemm_kernel EPI_RESID): items = 16 rows x 4 groups of 4 columns
-        if (threadIdx.x < 64) {
-            const int m = threadIdx.x >> 2, n4 = (threadIdx.x & 3) * 4;
-            if (m < M) {
-                float v[4];
-#pragma unroll
-                for (int j = 0; j < 4; ++j) v[j] = red[0][m][n4 + j] + red[1][m][n4 + j] + red[2][m][n4 + j] + red[3][m][n4 + j];
-                uint2* rp = reinterpret_cast<uint2*>(e.resid + (size_t)m * e.ldr + nb0 + n4);
-                const uint2 rv = *rp;
-                float4 s = make_float4(v[0], v[1], v[2], v[3]);
-                if (e.tp.world > 0) {
-                    const long long off = mrsum_ar::tp_item_off(m, H, nb0 + n4);
-                    mrsum_ar::tp_push_item(e.tp, off, tp_epoch, s);
-                    s = mrsum_ar::tp_gather_item(e.tp, off, tp_epoch);
-                }
-                const uint2 hv = make_uint2(pack2(__uint_as_float(rv.x << 16) + s.x, __uint_as_float(rv.x & 0xffff0000u) + s.y),
-                                            pack2(__uint_as_float(rv.y << 16) + s.z, __uint_as_float(rv.y & 0xffff0000u) + s.w));
-                *rp = hv;
-                const float h0 = __uint_as_float(hv.x << 16), h1 = __uint_as_float(hv.x & 0xffff0000u);
-                const float h2 = __uint_as_float(hv.y << 16), h3 = __uint_as_float(hv.y & 0xffff0000u);
-                red[0][m][n4] = (h0 * h0 + h1 * h1) + (h2 * h2 + h3 * h3);
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x < M) {
-            const float* q = red[0][threadIdx.x];
-            e.ssp[(size_t)threadIdx.x * a.nb + bx] = ((q[0] + q[4]) + (q[8] + q[12]));
-        }
-        if (e.tp.world > 0 && threadIdx.x == 0) e.tp.epochs[nb0 / mrsum_ar::GRAN] = tp_epoch;
-    }
-
-    if (threadIdx.x == 0) a.ep[bx] = epoch;  // read by the next launch (kernel boundary orders it)
-}
-
-MRSUM_API int mrsum_mlp_fused_capacity() {
-    static int cap = -1;
-    if (cap < 0) {
-        int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, mlp_fused_kernel, 256, 0) != hipSuccess)
-            return 0;
-        cap = cus * per;
-    }
-    return cap;
-}
-
-// x [M, H] bf16 rows (ldx; the un-normalised residual when ssq is given: deferred RMSNorm, ssq [M][ssq_tiles]),
-// wgu [2F, H] ([8 gate | 8 up] blocks), wd [H, F]; resid [M, H] (ldr) += swiglu(x wgu^T) wd^T, all-reduced over
-// ``ar`` first when given; ssp [M][H / 16] fp32 per-tile row sums of squares of the new residual.  hbuf >= M * F * 4
-// bytes of granules, ep [max(F / 8, H / 16)] and err [1] u32 zeroed once at allocation and used by launches of
-// this grid size only.  M <= 16, H % 128 == 0, F % 128 == 0,
-// F <= 2048, max(F / 8, H / 16) workgroups resident at once.
-MRSUM_API int mrsum_mlp_fused(const void* x, int ldx, const void* wgu, const void* wd, int H, int F, int M,
-                              const float* ssq, int ssq_tiles, float eps, void* resid, int ldr, float* ssp, void* hbuf,
-                              unsigned* ep, unsigned* err, void* ar, hipStream_t s) {
-    using namespace mrsum_ar;
-    if (M <= 0) return 0;
-    if (M > 16 || H % KB || F % KB || F / KB > 4 * MLP_MAXB || !resid || !ssp || !hbuf || !ep || ldr % 4 || ldx % 8)
-        return (int)hipErrorInvalidValue;
-    if (ssq && (ssq_tiles <= 0 || ssq_tiles % 32 || ssq_tiles > 32 * SS_C4)) return (int)hipErrorInvalidValue;
-    const int na = F / 8, nb = H / 16, G = std::max(na, nb);
-    if (G > mrsum_mlp_fused_capacity()) return (int)hipErrorInvalidValue;  // header: progress
-    if (ar) {
-        auto h = (const ArHandle*)ar;
-        if (H / GRAN > MAX_GRAN || (size_t)M * H * 4 > h->max_bytes) return (int)hipErrorInvalidValue;
-        for (int r = 0; r < h->world; ++r)
-            if (!h->peers.base[r]) return (int)hipErrorInvalidValue;
-    } else if (!err) {
-        return (int)hipErrorInvalidValue;
-    }
-    SkinnyNorm e;
-    e.ssq = ssq; e.ssq_tiles = ssq_tiles; e.inv_k = 1.f / (float)H; e.eps = eps;
-    e.resid = (bf16*)resid; e.ldr = ldr; e.ssp = ssp;
-    e.tp = tp_push_of((const ArHandle*)ar);
-    MlpArgs a;
-    a.h = (unsigned long long*)hbuf; a.ep = ep; a.error = ar ? e.tp.error : err;
-    a.F = F; a.H = H; a.na = na; a.nb = nb;
-    mlp_fused_kernel<<<G, 256, 0, s>>>((const bf16*)x, ldx, (const bf16*)wgu, (const bf16*)wd, M, e, a);
-    return (int)hipGetLastError();
-}

@@ -486,6 +486,12 @@ MRSUM_API int mrsum_stream_gemm(const void* x, int ldx, const void* W, int N, in
         return (int)hipErrorInvalidValue;
     if (M > 64 && (ssq || (epi != EPI_BF16 && epi != EPI_F32_PARTIAL && epi != EPI_SWIGLU)))
         return (int)hipErrorInvalidValue;  // tall tiles: no deferred norm, no split-K last-arriver epilogue
+    if (M > 64) {
+        // tall tiles only at widths whose slot (16 wpb W rows + 16 MT x rows, 256 B each) leaves a ring of at
+        // least 3 slots (one being filled, two published); ops/hip.py _TALL_WPB lists the same widths
+        const int slot = (16 * wpb + 16 * (M > 96 ? 8 : 6)) * 256;
+        if (LDS_BUDGET / slot < 3) return (int)hipErrorInvalidValue;
+    }
     const bool split_epi = epi == EPI_SWIGLU_SPLIT || epi == EPI_RESID_SPLIT;
     if (epi != EPI_F32_PARTIAL && !split_epi && splits != 1) return (int)hipErrorInvalidValue;
     if (split_epi && (!parts || !counters)) return (int)hipErrorInvalidValue;

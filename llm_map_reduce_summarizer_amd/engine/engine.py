@@ -506,9 +506,19 @@ class LLMEngine:
             if ar is not None:
                 # every TP rank votes whatever happened locally, so the group's collective sequence stays
                 # aligned: a local exception fails the call on every rank; a timed-out P2P wait anywhere
-                # (the sticky error word) makes every rank re-run the requests on RCCL
-                ar_err, peer_failed = ar.agree_error(failed is not None)
-                if failed is None and peer_failed:
+                # (the sticky error word) makes every rank re-run the requests on RCCL.  Scope: this covers
+                # failures that let the peers reach the vote -- the custom all-reduce's own waits end after
+                # 4 s (sticky error word).  A rank that raises BEFORE an RCCL collective inside _generate (the
+                # sequence-parallel prefill's reduce-scatter / all-gather, an RCCL logits gather) leaves its
+                # peers in that collective until the process-group timeout (MRSUM_DIST_TIMEOUT), which then
+                # fails them too.
+                ar_err, any_failed = ar.agree_error(failed is not None)
+                if any_failed:
+                    # the failing call may have stopped between a push and its wait, leaving epochs / granules
+                    # half-advanced on some ranks: clear the P2P state on the whole group (collective: every
+                    # rank saw the same vote) so the next generate starts clean
+                    ar.reset()
+                if failed is None and any_failed:
                     raise RuntimeError("a tensor-parallel peer failed during this generate")
                 if failed is None and ar_err:
                     out = self._recover_custom_ar(prompts, params, imported or {}, on_prefill, feeder, on_sync)
@@ -993,4 +1003,8 @@ class LLMEngine:
         s["weights_gib"] = self.model.weight_bytes() / 2 ** 30
         if self.device.type == "cuda":
             s["hbm_peak_gib"] = torch.cuda.max_memory_allocated(self.device) / 2 ** 30
+        if self.model.tp_size > 1:
+            ar = self.model.custom_ar
+            s["p2p_selftest"] = ar.selftest_report() if ar is not None else "off (RCCL)"
+            s["custom_ar_recoveries"] = int(self.stats.get("custom_ar_recoveries", 0))
         return s

@@ -41,6 +41,7 @@ import torch
 
 from .. import ops
 from ..ops.reference import Fp8Weight, interleave_gate_up, rope_cos_sin
+from ..parallel.dist import AsyncWorks
 from .config import ModelConfig
 
 
@@ -70,8 +71,8 @@ class _TPReduce:
 
     def fused_ok(self, rows: int, hidden: int) -> bool:
         ar = self.model.custom_ar
-        return self.fused and ar is not None and rows <= ar.MAX_ROWS and hidden % 4 == 0 and hidden <= 8192 and \
-            rows * hidden * 2 <= ar.max_bytes
+        return self.fused and ar is not None and ar.paths["fused_norm"] and rows <= ar.MAX_ROWS and \
+            hidden % 4 == 0 and hidden <= 8192 and rows * hidden * 2 <= ar.max_bytes
 
     def add_rmsnorm(self, parts, residual, ln, eps):
         return self.model.custom_ar.add_rmsnorm(parts, residual, ln, eps)
@@ -84,8 +85,9 @@ class _TPReduce:
     def push_handle(self) -> int:
         return self.model.custom_ar.push_handle()
 
-
-_QUANT_NORM = os.environ.get("MRSUM_QUANT_NORM", "1") == "1"
+    def push_kinds(self) -> set:
+        """TP-push producers that passed the custom all-reduce's start-up self-test."""
+        return self.model.custom_ar.push_kinds()
 
 
 def _page_of(kcache: torch.Tensor, head_dim: int) -> int:
@@ -101,6 +103,11 @@ def _page_of(kcache: torch.Tensor, head_dim: int) -> int:
 # the parity checkpoint; two-term QKV input brings it to ~10 % for ~1.1x the QKV GEMM's cost (the o / gate_up /
 # down inputs stay single-term)  (CPU emulation: profiles/r4_fp8_activation_emulation.txt)
 _QKV_SPLIT = os.environ.get("MRSUM_FP8_QKV_SPLIT", "1") == "1"
+
+
+def _hip():
+    from ..ops import hip
+    return hip
 
 
 def _tp_push_enabled() -> bool:
@@ -187,7 +194,11 @@ class LlamaModel:
         self.custom_ar = None
         if tp_size > 1 and self.device.type == "cuda" and os.environ.get("MRSUM_CUSTOM_AR", "1") == "1":
             from ..parallel.custom_ar import maybe_custom_all_reduce
-            self.custom_ar = maybe_custom_all_reduce(tp_group)
+            # self-tested at THIS model's decode shapes: hidden size, the shard K of the row-parallel
+            # projections (o: the local heads, down: the local ffn), the weight format, decode rows 1-64
+            self.custom_ar = maybe_custom_all_reduce(tp_group, shapes=dict(
+                hidden=cfg.hidden, k={"o": self.hq * self.hd, "down": self.ffn_local},
+                fp8=weight_dtype == "fp8", rows=(1, 16, 64)))
 
     # ------------------------------------------------------------------ weights
     def _init_weights(self, seed: int) -> None:
@@ -314,6 +325,33 @@ class LlamaModel:
         torch.distributed.all_gather_into_tensor(out, shard.contiguous(), group=self.tp_group)
         return out[:T]
 
+    def _prefill_quant(self, T: int):
+        """(o / gate_up input quant, QKV input quant) of an fp8 prefill of T rows, as run_layers picks them:
+        row-wise e4m3 rows made by the norm (single-term for gate_up, two-term for QKV), decided on the FULL
+        row count the consumer GEMMs see (ops._quant_ok: above the decode kernels' rows); (False, False) for
+        bf16 weights."""
+        if self.weight_dtype != "fp8" or not self.device.type == "cuda" or T <= max(_hip().STREAM_MAX_M,
+                                                                                    _hip().STREAM_MAX_M_SWIGLU):
+            return False, False
+        return True, ("split" if _QKV_SPLIT else True)
+
+    def _add_norm_q(self, x: torch.Tensor, residual: torch.Tensor, eps: float, quant):
+        """residual += x; the normed rows -- as ops.QuantRows (fp8 prefill: the norm quantises in the same
+        pass, ``quant`` True / "split") or bf16."""
+        if quant:
+            return ops.QuantRows(*_hip().rmsnorm_fp8(x, ops.unit_gain(residual.shape[1], residual.device), eps,
+                                                     residual=residual, split=quant == "split"))
+        return ops.add_rmsnorm(x, residual, None, eps)
+
+    def _sp_gather_rows(self, x, T: int):
+        """All-gather of this rank's normed row shard (bf16 rows or fp8 QuantRows: e4m3 bytes + fp32 row
+        scales -- the same bytes on the link as the bf16 rows for two-term, half for single-term)."""
+        if isinstance(x, ops.QuantRows):
+            q = self._sp_all_gather(x.q.view(torch.uint8), T).view(torch.float8_e4m3fn)
+            sc = self._sp_all_gather(x.scale.view(-1, 1), T).view(-1)
+            return ops.QuantRows(q.contiguous(), sc.contiguous())
+        return self._sp_all_gather(ops.rows(x), T)
+
     @property
     def tp_sampling(self) -> bool:
         """Sample from the local vocab shard + 8-byte key max instead of gathering the logits."""
@@ -349,7 +387,7 @@ class LlamaModel:
         c = self.cfg
         residual = ops.embed(ids, self.embed)
         # fp8 prefill: the norms feeding the fp8 GEMMs quantise their rows in the same pass (ops.QuantRows)
-        q8 = not decode and self.weight_dtype == "fp8" and _QUANT_NORM
+        q8 = not decode and self.weight_dtype == "fp8"
         q8qkv = ("split" if _QKV_SPLIT else True) if q8 else False  # the QKV projection's input
         x = ops.rmsnorm(residual, None, c.rms_eps, quant=q8qkv)  # gains folded into the consumer weights
         page = _page_of(kcache, self.hd)
@@ -409,9 +447,11 @@ class LlamaModel:
         st = []
         for p in passes:
             res = ops.embed(p.ids, self.embed)
-            x = ops.rmsnorm(res, None, eps)
+            T = int(res.shape[0])
+            q8, q8qkv = self._prefill_quant(T)  # fp8: the norms quantise for the fp8 GEMMs (as run_layers)
+            x = ops.rmsnorm(res, None, eps, quant=q8qkv)
             # SP: the residual is kept as this rank's row shard (see _sp_rows)
-            st.append({"res": self._sp_shard(res) if sp else res, "x": x, "T": int(res.shape[0])})
+            st.append({"res": self._sp_shard(res) if sp else res, "x": x, "T": T, "q": (q8, q8qkv)})
 
         def wait(h):
             if h is not None:
@@ -422,30 +462,37 @@ class LlamaModel:
                 s[key], s["w"] = self._sp_reduce_scatter_async(t)
             else:
                 s[key], s["w"] = t, self._all_reduce_async(t)
+            works.add(s["w"])
 
-        def add_norm(s, key):  # residual += the summed projection; the normed rows for the next GEMM
+        def add_norm(s, key, last=False):  # residual += the summed projection; the normed rows for the next GEMM
             wait(s.pop("w"))
-            x = ops.add_rmsnorm(s.pop(key), s["res"], None, eps)
-            return self._sp_all_gather(ops.rows(x), s["T"]) if sp else x
+            # fp8: the o sum feeds gate_up (single-term rows), the down sum the next QKV (two-term), the last
+            # one the bf16 LM head
+            quant = False if last else s["q"][0 if key == "o" else 1]
+            x = self._add_norm_q(s.pop(key), s["res"], eps, quant)
+            return self._sp_gather_rows(x, s["T"]) if sp else x
 
-        for i, lw in enumerate(self.layers):
-            for p, s in zip(passes, st):
-                if "d" in s:  # previous layer's down-projection sum (overlapped with the other passes' MLPs)
-                    s["x"] = add_norm(s, "d")
-                qkv = ops.qkv_rope(s["x"], lw.wqkv, p.positions, p.seq_idx, block_tables, kcache[i], vcache[i],
-                                   self.cos_sin, self.hq, self.hkv, self.hd, page)
-                kw = {"seqlens": p.seqlens, "items": p.items} if qkv.is_cuda else {}
-                pp = p.paged.layer(kcache[i], vcache[i]) if p.paged is not None else None
-                a = ops.attn_prefill(qkv, p.cu_seqlens, self.hq, self.hkv, self.hd, self.scale, paged=pp, **kw)
-                reduce_async(s, ops.linear(a, lw.wo), "o")
-            for s in st:
-                x = add_norm(s, "o")
-                act = ops.gate_up_swiglu(x, lw.wgu)
-                reduce_async(s, ops.linear(act, lw.wdown), "d")
-        last, s = passes[-1], st[-1]
-        for t in st[:-1]:
-            wait(t.pop("w"))
-        x = add_norm(s, "d")
+        # every async collective started below is waited before this frame is left, also when an op raises
+        # (parallel/dist.py AsyncWorks): no work handle outlives the prefill
+        with AsyncWorks() as works:
+            for i, lw in enumerate(self.layers):
+                for p, s in zip(passes, st):
+                    if "d" in s:  # previous layer's down-projection sum (overlapped with the other passes' MLPs)
+                        s["x"] = add_norm(s, "d")
+                    qkv = ops.qkv_rope(s["x"], lw.wqkv, p.positions, p.seq_idx, block_tables, kcache[i],
+                                       vcache[i], self.cos_sin, self.hq, self.hkv, self.hd, page)
+                    kw = {"seqlens": p.seqlens, "items": p.items} if qkv.is_cuda else {}
+                    pp = p.paged.layer(kcache[i], vcache[i]) if p.paged is not None else None
+                    a = ops.attn_prefill(qkv, p.cu_seqlens, self.hq, self.hkv, self.hd, self.scale, paged=pp, **kw)
+                    reduce_async(s, ops.linear(a, lw.wo), "o")
+                for s in st:
+                    x = add_norm(s, "o")
+                    act = ops.gate_up_swiglu(x, lw.wgu)
+                    reduce_async(s, ops.linear(act, lw.wdown), "d")
+            last, s = passes[-1], st[-1]
+            for t in st[:-1]:
+                wait(t.pop("w"))
+            x = add_norm(s, "d", last=True)
         return self.logits(x.index_select(0, last.last_rows), gather)
 
     def prefill_cp(self, passes, block_tables: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
@@ -465,21 +512,27 @@ class LlamaModel:
         st = []
         for p in passes:
             res = ops.embed(p.ids, self.embed)
-            st.append({"res": res, "x": ops.rmsnorm(res, None, eps)})
-        for i, lw in enumerate(self.layers):
-            qkvs, handles = [], []
-            for k, (p, s) in enumerate(zip(passes, st)):
-                qkvs.append(ops.qkv_rope(s["x"], lw.wqkv, p.positions, p.seq_idx, block_tables, kcache[i], vcache[i],
-                                         self.cos_sin, self.hq, self.hkv, self.hd, page))
-                handles.append(exchange.start(i, k))
-            for p, s, qkv, h in zip(passes, st, qkvs, handles):
-                exchange.finish(h)
-                kw = {"seqlens": p.seqlens, "items": p.items} if qkv.is_cuda else {}
-                a = ops.attn_prefill(qkv, p.cu_seqlens, self.hq, self.hkv, self.hd, self.scale,
-                                     paged=p.paged.layer(kcache[i], vcache[i]), **kw)
-                x = ops.proj_add_rmsnorm(a, lw.wo, s["res"], None, eps, "o", None)
-                act = ops.gate_up_swiglu(x, lw.wgu)
-                s["x"] = ops.proj_add_rmsnorm(act, lw.wdown, s["res"], None, eps, "down", None)
+            q8, q8qkv = self._prefill_quant(int(res.shape[0]))  # fp8 weights: quantising norms (run_layers)
+            st.append({"res": res, "x": ops.rmsnorm(res, None, eps, quant=q8qkv), "q": (q8, q8qkv)})
+        last_layer = len(self.layers) - 1
+        with AsyncWorks() as works:  # every started exchange is waited, also when an op raises
+            for i, lw in enumerate(self.layers):
+                qkvs, handles = [], []
+                for k, (p, s) in enumerate(zip(passes, st)):
+                    qkvs.append(ops.qkv_rope(s["x"], lw.wqkv, p.positions, p.seq_idx, block_tables, kcache[i],
+                                             vcache[i], self.cos_sin, self.hq, self.hkv, self.hd, page))
+                    handles.append(exchange.start(i, k))
+                    works.add(handles[-1][2])
+                for p, s, qkv, h in zip(passes, st, qkvs, handles):
+                    exchange.finish(h)
+                    kw = {"seqlens": p.seqlens, "items": p.items} if qkv.is_cuda else {}
+                    a = ops.attn_prefill(qkv, p.cu_seqlens, self.hq, self.hkv, self.hd, self.scale,
+                                         paged=p.paged.layer(kcache[i], vcache[i]), **kw)
+                    q8, q8qkv = s["q"]
+                    x = ops.proj_add_rmsnorm(a, lw.wo, s["res"], None, eps, "o", None, quant=q8)
+                    act = ops.gate_up_swiglu(x, lw.wgu)
+                    s["x"] = ops.proj_add_rmsnorm(act, lw.wdown, s["res"], None, eps, "down", None,
+                                                  quant=q8qkv if i < last_layer else False)
         if logits_pass is None:
             return None
         p, s = passes[logits_pass], st[logits_pass]

@@ -4,7 +4,7 @@ There is exactly one implementation per device: tensors on a ROCm device go
 to the hand-written gfx950 kernels in ``ops.hip`` (and fail loudly if
 ``libmrsum_kernels.so`` is missing -- no silent fallback), CPU tensors go to
 ``ops.reference`` (the numerics oracle, also what CPU-only tests run).
-``MRSUM_OPS=torch`` forces the reference on the GPU for debugging only.
+There is no switch that sends GPU tensors to the reference.
 
 Every GPU op is a hand-written gfx950 kernel, GEMMs included: decode-shaped
 projections on the weight-streaming MFMA kernels (stream_gemm.hip /
@@ -15,18 +15,13 @@ MFMA GEMM (gemm.hip; bf16 or OCP fp8).  No vendor BLAS on the hot path.
 
 from __future__ import annotations
 
-import os
-
 import torch
 
 from . import reference
 from .reference import Fp8Weight
 
-_FORCE_TORCH = os.environ.get("MRSUM_OPS", "").lower() == "torch"
-
-
 def _use_hip(t) -> bool:
-    return t.is_cuda and not _FORCE_TORCH
+    return t.is_cuda
 
 
 def _impl(t):
@@ -359,37 +354,47 @@ DEFER_NORM_MAX_M = 16
 TP_PUSH_MAX_M = 64
 
 
-def _resid_plan(hip, a, w, role, tp=False):
+RESID_FORCE = {}  # role -> "skinny" | "stream": measurement override of _resid_plan (tools only)
+
+
+def _resid_plan(hip, a, w, role, tp=False, force=None):
     """The deferred-RMSNorm producer of this decode projection: ("stream", wpb, S) (stream kernel, split-K
     last-arriver residual update), ("skinny",) (register-streaming kernel, one tile per workgroup, no
     split-K) or None.  ``tp``: the TP-push producer of a row-parallel shard, which runs whatever the plan
     for its bare GEMM (the all-reduce launch it saves outweighs the kernel choice): on the register-
-    streaming kernel where that is the plan (TP-shard o / down at K <= 2048), else the stream kernel
-    (MRSUM_TP_RESID_KERNEL=skinny|stream forces one, for measurements)."""
+    streaming kernel where that is the plan (TP-shard o / down at K <= 2048), else the stream kernel.
+    ``RESID_FORCE[role]`` ("skinny" / "stream") overrides the choice for in-situ measurements
+    (tools/exp_plans_insitu.py sets it; nothing in the package does); ``force`` likewise, per call (the
+    custom all-reduce's self-test of each producer kind, and the fallback when one kind failed it)."""
     M = a.shape[0]
+    force = force or RESID_FORCE.get(role)
     if M > (TP_PUSH_MAX_M if tp else DEFER_NORM_MAX_M):
         return None
     N, K = w.shape
     if tp and M > 16:  # the register-streaming producer takes one 16-row tile
+        if force == "skinny":
+            return None
         cfg = (hip.fp8_resid_cfg(M, N, K) if isinstance(w, Fp8Weight) else
                (hip.plan(role, M, N, K)[1:] if hip.plan(role, M, N, K)[0] == "stream" else hip.tp_resid_config(N, K)))
         return None if cfg is None or (N // (16 * cfg[0])) % 32 else ("stream",) + tuple(cfg)
     if isinstance(w, Fp8Weight):
+        if force == "skinny":
+            return None
         cfg = hip.fp8_resid_cfg(M, N, K)
     else:
         p = hip.plan(role, M, N, K)
         cfg = p[1:] if p[0] == "stream" else None
-        env = os.environ.get("MRSUM_RESID_SKINNY_" + role.upper())  # measurement override (exp_plans_insitu.py)
-        if not tp and M <= 16 and N % 512 == 0 and (env == "1" or (env is None and role == "o" and K <= 4096)):
+        if not tp and M <= 16 and N % 512 == 0 and (force == "skinny" or (force is None and role == "o" and K <= 4096)):
             # TP=1 o projection on the register-streaming producer (no split-K tail), in situ 4k context
             # (profiles/r3_tp1_resid_skinny_insitu.jsonl): B=1 3.336 vs 3.380 ms per step, B=10 4.078 vs 4.087;
             # down (K 14336) loses (3.50 / 4.32)
             return ("skinny",)
         if tp:
-            force = os.environ.get("MRSUM_TP_RESID_KERNEL", "auto")
-            if (force == "skinny" or (force == "auto" and p[0] == "skinny")) and N % 512 == 0 \
+            if (force == "skinny" or (force is None and p[0] == "skinny")) and N % 512 == 0 \
                     and N // 16 <= hip.skinny_resid_capacity():  # every pushing workgroup resident at once
                 return ("skinny",)
+            if force == "skinny":
+                return None
             if cfg is None or force == "stream":
                 cfg = hip.tp_resid_config(N, K)
     if cfg is None or (N // (16 * cfg[0])) % 32:
@@ -416,6 +421,14 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None, quant=F
             push = all_reduce.push_handle() if ok is not None and ok(a.shape[0], residual.shape[1]) else None
             if all_reduce is None or push is not None:
                 rp = _resid_plan(hip, a, w, role, tp=push is not None)
+                kinds = getattr(all_reduce, "push_kinds", None)
+                if push is not None and rp is not None and kinds is not None and rp[0] not in kinds():
+                    # that producer failed the start-up self-test: the other kind if it takes the shape
+                    # and passed, else the fused all-reduce path below
+                    other = ({"stream", "skinny"} - {rp[0]}) & kinds()
+                    rp = _resid_plan(hip, a, w, role, tp=True, force=other.pop()) if other else None
+                    if rp is not None and rp[0] == "skinny" and w.shape[0] // 16 > hip.skinny_resid_capacity():
+                        rp = None
                 if rp is not None and rp[0] == "skinny":
                     return NormRows(residual, hip.skinny_resid(a, w, residual, tp=push), eps)
                 if rp is not None:
@@ -462,24 +475,12 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None, quant=F
     return reference.add_rmsnorm(o, residual, ln, eps)
 
 
-MLP_FUSED = os.environ.get("MRSUM_MLP_FUSED", "0") == "1"  # measured: see docs/decode_latency.md
-
-
 def mlp(x, wgu, wdown, residual, eps, all_reduce=None, quant=False):
     """The decode/prefill MLP block: residual += swiglu(x wgu^T) wdown^T (TP-all-reduced when
-    ``all_reduce``); returns the next layer's normed input as proj_add_rmsnorm does.
-
-    GPU decode rows of a tensor-parallel shard (bf16, F = ffn / TP <= 2048, M <= 16, ``x`` a NormRows) run
-    the one-launch fused MLP (ops.hip.mlp_fused: gate_up + SwiGLU -> in-launch granule hand-off -> down +
-    residual update + TP push); everything else runs gate_up_swiglu then proj_add_rmsnorm."""
-    if MLP_FUSED and isinstance(x, NormRows) and not quant and not isinstance(wgu, Fp8Weight) and _use_hip(x.h):
-        from . import hip
-        M, H = x.shape
-        F = wdown.shape[1]
-        ok = getattr(all_reduce, "push_ok", None)
-        push = all_reduce.push_handle() if ok is not None and ok(M, H) else None
-        if (all_reduce is None or push is not None) and hip.mlp_fused_ok(M, H, F):
-            return NormRows(residual, hip.mlp_fused(x.h, wgu, wdown, residual, norm=x.norm, tp=push), eps)
+    ``all_reduce``); returns the next layer's normed input as proj_add_rmsnorm does: gate_up_swiglu then
+    proj_add_rmsnorm.  (A one-launch fused MLP of a TP shard was built in round 4, bit-exact and 1-5 %
+    slower per TP=8 shard step -- profiles/r4_mlp_fused_tp8_shard_ab.jsonl, docs/decode_latency.md -- and
+    removed from the library in round 5.)"""
     act = gate_up_swiglu(x, wgu)
     return proj_add_rmsnorm(act, wdown, residual, None, eps, "down", all_reduce, quant=quant)
 

@@ -22,8 +22,8 @@ never run silently.
 
 On a machine with a GPU the kernel library is REQUIRED (``kernels_lib()``
 raises if it is missing) -- there is deliberately no silent PyTorch fallback
-for the hot path.  ``MRSUM_OPS=torch`` selects the pure-PyTorch reference ops
-explicitly (used by CPU tests and as the numerics oracle).
+for the hot path.  The pure-PyTorch reference ops (``ops/reference.py``) run
+only on CPU tensors (CPU tests) and as the numerics oracle of the GPU tests.
 """
 
 from __future__ import annotations

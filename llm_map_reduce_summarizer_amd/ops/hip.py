@@ -42,9 +42,6 @@ _SIGS = {
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int,
                           _c_float, _vp, _c_int, _vp, _vp, _vp],
     "mrsum_skinny_resid_capacity": [],
-    "mrsum_mlp_fused": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_float, _vp, _c_int, _vp, _vp,
-                        _vp, _vp, _vp, _vp],
-    "mrsum_mlp_fused_capacity": [],
     "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_stream_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp,
                           _vp, _c_int, _c_float, _vp, _c_int, _vp, _c_int, _vp, _vp],
@@ -56,7 +53,6 @@ _SIGS = {
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_sample_keys": [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
     "mrsum_sample_finish": [_vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _c_int, _vp],
-    "mrsum_gemm4w": [_vp, _c_int, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_gemm": [_vp, _c_int, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _c_int,
                    _c_int, _vp],
     "mrsum_sample": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_int, _vp, _vp,
@@ -377,10 +373,8 @@ ATTN_SLOTS = 768  # resident decode-attention workgroups (3 per CU, 162 VGPRs; 5
 # fp8 KV cache: a page is half the bytes, so the same split plan keeps half the bytes in flight per CU.  Whole
 # decode steps at 4.4k context with the splits x 1 / 2 / 3 (profiles/r4_kv8_split_sweep.jsonl): B = 10 (80
 # groups) 4.036 / 3.901 / 3.996 ms, B = 20 4.469 / 4.705 / 4.639, B = 39 5.649 / 5.942 / 6.187 -- so twice the
-# splits up to KV8_SPLIT_GROUPS (sequence, kv head) groups, the bf16 plan above them ($MRSUM_KV8_SPLIT_MULT
-# overrides the factor, for measurements)
+# splits up to KV8_SPLIT_GROUPS (sequence, kv head) groups, the bf16 plan above them
 KV8_SPLIT_GROUPS = 96
-_KV8_MULT_ENV = os.environ.get("MRSUM_KV8_SPLIT_MULT")
 
 
 def decode_attn_plan(batch: int, hkv: int, max_ctx: int, kv8: bool = False):
@@ -388,7 +382,7 @@ def decode_attn_plan(batch: int, hkv: int, max_ctx: int, kv8: bool = False):
     (at most one page per split; a fused merge keeps its 16-split cap)."""
     s, fused = decode_attn_plan_bf16(batch, hkv, max_ctx)
     if kv8:
-        mult = float(_KV8_MULT_ENV) if _KV8_MULT_ENV else (2.0 if batch * hkv <= KV8_SPLIT_GROUPS else 1.0)
+        mult = 2.0 if batch * hkv <= KV8_SPLIT_GROUPS else 1.0
         pages = max(1, -(-max_ctx // 64))
         s = max(1, min(int(round(s * mult)), pages, 64, 16 if fused else 64))
     return s, fused
@@ -606,7 +600,7 @@ def _gemm(xp, ldx, wp, ldw, out, M, N, K, fp8, epi, sx, sw, group_m, split=0):
 
 
 def gemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, swiglu: bool = False,
-         group_m: Optional[int] = None, kernel: Optional[str] = None) -> torch.Tensor:
+         group_m: Optional[int] = None) -> torch.Tensor:
     """x [M, K] @ w [N, K]^T in bf16 on the 256 x 256-tile MFMA kernel (csrc/kernels/gemm.hip), any M.
     ``swiglu``: w is the [8 gate | 8 up]-interleaved gate_up weight and the result is silu(gate) * up
     [M, N / 2]."""
@@ -624,33 +618,14 @@ def gemm(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None, s
     _req(out.shape == (M, n_out), "gemm: bad out shape")
     if M == 0:
         return out
-    if kernel is None:
-        kernel = GEMM_KERNEL
-    if kernel == "blas" and not swiglu and out.is_contiguous():
-        # plain product on the vendor library (hipBLASLt through torch.mm), for the A/B measurement
-        return torch.mm(x, w.t(), out=out)
-    if kernel.startswith("4w"):  # "4w" / "4w5": 4- / 5-step ring; "L": lagged refills
-        return gemm4w(x, w, out, swiglu, group_m, ns=(5 if "5" in kernel else 4) | (256 if kernel.endswith("L") else 0))
     return _gemm(_p(x), x.stride(0), _p(w), w.stride(0), out, M, N, K, 0,
                  GEMM_EPI_SWIGLU if swiglu else GEMM_EPI_BF16, None, None, group_m)
 
 
-# bf16 prefill GEMM kernel: "8w" = gemm.hip (8 waves, 128 x 64 per wave), "4w" / "4w5" = gemm4w.hip (4 waves,
-# 128 x 128 per wave, 4- / 5-step LDS ring), "blas" = the plain (non-SwiGLU) products on hipBLASLt;
-# MRSUM_GEMM_KERNEL overrides for measurements
-GEMM_KERNEL = os.environ.get("MRSUM_GEMM_KERNEL", "8w")
-
-
-def gemm4w(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor, swiglu: bool = False,
-           group_m: Optional[int] = None, ns: int = 4) -> torch.Tensor:
-    """The four-wave bf16 GEMM (csrc/kernels/gemm4w.hip); same operands as gemm()."""
-    M, K = x.shape
-    N = w.shape[0]
-    _req(out.stride(1) == 1 and out.stride(0) % 4 == 0 and out.data_ptr() % 8 == 0, "gemm4w: bad out layout")
-    _check(_fn("mrsum_gemm4w")(_p(x), x.stride(0), _p(w), w.stride(0), _p(out), out.stride(0), M, N, K,
-                               GEMM_EPI_SWIGLU if swiglu else GEMM_EPI_BF16,
-                               GEMM_GROUP_M if group_m is None else group_m, ns, _stream()), "gemm4w")
-    return out
+# One backend per op: every bf16 prefill product runs on gemm.hip.  The round-4 experiments that lived here
+# (gemm4w.hip, a four-wave rebuild 20-25 % slower; the plain products on hipBLASLt, +0.25 % end to end) are
+# recorded in profiles/r4_gemm4w_vs_8w_vs_hipblaslt.jsonl and r4_prefill_plain_gemm_blas_ab.jsonl and were
+# removed from the library in round 5.
 
 
 def gemm_fp8(xq: torch.Tensor, xs: torch.Tensor, w, out: Optional[torch.Tensor] = None, swiglu: bool = False,
@@ -779,7 +754,7 @@ def _stream_gemm(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, no
         # up to STREAM_TALL_M rows in one pass over the weights (96- / 128-row x tiles, a workgroup width that
         # keeps a 3-slot ring); above that, row chunks of that height: row slices of the bf16 output, or of
         # every fp32 slab (slab row stride = M)
-        ch = min(STREAM_TALL_M, 128) if STREAM_TALL_M > SKINNY_MAX_M else SKINNY_MAX_M  # kernel: <= 128 rows
+        ch = STREAM_TALL_M  # the kernel's tallest x tile
         for r0 in range(0, M, ch):
             r1 = min(M, r0 + ch)
             if r1 - r0 > SKINNY_MAX_M:
@@ -799,11 +774,11 @@ def _stream_gemm(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, no
 
 
 # Decode batches of 65-128 rows run the stream GEMM on 96- / 128-row x tiles in ONE pass over the weights
-# (stream_gemm.hip); before, each 64-row chunk re-streamed every weight byte.  MRSUM_STREAM_TALL_M=64 restores
-# the 64-row chunks (A/B).
-STREAM_TALL_M = int(os.environ.get("MRSUM_STREAM_TALL_M", "128"))
-LINEAR_TALL = os.environ.get("MRSUM_LINEAR_TALL", "1") == "1"  # linear() (the LM head) too; 0 for the A/B
-_TALL_WPB = {6: (4, 5, 6), 8: (4,)}  # widths whose slot (16 wpb W rows + 16 MT x rows) x 256 B leaves a 3-slot ring
+# (stream_gemm.hip); before, each 64-row chunk re-streamed every weight byte (profiles/r4_stream_tall_tiles_24h_ab.jsonl).
+STREAM_TALL_M = 128
+# widths whose slot (16 wpb W rows + 16 MT x rows) x 256 B leaves a ring of >= 3 slots in the 157 KiB budget
+# (mrsum_stream_gemm refuses the others): MT 6 -> wpb 4-6, MT 8 -> wpb 4-5
+_TALL_WPB = {6: (4, 5, 6), 8: (4, 5)}
 
 
 def tall_wpb(N: int, M: int, splits: int) -> Optional[int]:
@@ -856,7 +831,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None,
     M, K = x.shape
     N = w.shape[0]
     _req(norm is None or linear_takes_norm(M, N, K), "linear: a deferred norm needs a stream-GEMM shape")
-    tall = (LINEAR_TALL and SKINNY_MAX_M < M <= min(STREAM_TALL_M, 128) and K % 128 == 0 and norm is None
+    tall = (SKINNY_MAX_M < M <= STREAM_TALL_M and K % 128 == 0 and norm is None
             and stream_config(N, K, splits=1) is not None and tall_wpb(N, M, 1) is not None)
     if (M > SKINNY_MAX_M and not tall) or M == 0 or K % 128:
         return gemm(x, w, out=out)
@@ -958,76 +933,6 @@ def skinny_resid_capacity() -> int:
     if not _RESID_CAP:
         _RESID_CAP.append(int(_fn("mrsum_skinny_resid_capacity")()))
     return _RESID_CAP[0]
-
-
-_MLP_CAP = []
-_MLP_WS = {}
-MLP_FUSED_MAX_M = 16
-MLP_FUSED_MAX_F = 2048  # skinny_gemm.hip MLP_MAXB: the down tile's k blocks held in registers
-
-
-def mlp_fused_capacity() -> int:
-    """Workgroups of the fused MLP kernel resident at once (its grid of max(F / 8, H / 16) must fit)."""
-    if not _MLP_CAP:
-        _MLP_CAP.append(int(_fn("mrsum_mlp_fused_capacity")()))
-    return _MLP_CAP[0]
-
-
-def mlp_fused_ok(M: int, H: int, F: int) -> bool:
-    """Shapes the one-launch decode MLP takes (a TP shard's: F = ffn / TP <= 2048)."""
-    return (1 <= M <= MLP_FUSED_MAX_M and H % 128 == 0 and F % 128 == 0 and F <= MLP_FUSED_MAX_F
-            and max(F // 8, H // 16) <= min(mlp_fused_capacity(), _MLP_MAX_GRID))
-
-
-_MLP_MAX_GRID = 1024
-
-
-def _mlp_workspace(device, grid: int):
-    """Granule buffer + per-workgroup epoch words of mlp_fused, one set per (device, grid size): the epoch
-    words of one grid size advance in lockstep (skinny_gemm.hip), so launches of another grid size must
-    not share them, nor the granules their tags guard.  Launches sharing a workspace must be ordered (one
-    stream, as the decode graph is): two in flight at once would interleave their epochs.  Zeroed once; word
-    _MLP_MAX_GRID is the timeout word."""
-    key = (str(device), int(grid))
-    ws = _MLP_WS.get(key)
-    if ws is None:
-        h = torch.zeros(MLP_FUSED_MAX_M * MLP_FUSED_MAX_F // 2, dtype=torch.int64, device=device)
-        words = torch.zeros(_MLP_MAX_GRID + 4, dtype=torch.int32, device=device)
-        ws = _MLP_WS[key] = (h, words)
-    return ws
-
-
-def mlp_fused_error(device) -> int:
-    """The fused MLP's sticky timeout words (non-TP launches; a TP launch uses its group's error word)."""
-    return sum(int(w[_MLP_MAX_GRID].item()) for (d, _), (_, w) in _MLP_WS.items() if d == str(device))
-
-
-def mlp_fused(x: torch.Tensor, w_gu: torch.Tensor, w_down: torch.Tensor, residual: torch.Tensor, norm=None,
-              tp=None) -> torch.Tensor:
-    """One-launch decode MLP (skinny_gemm.hip mlp_fused_kernel): residual += swiglu(x w_gu^T) w_down^T --
-    all-reduced over the custom all-reduce group ``tp`` first when given (TP push); ``norm`` (ssq, eps): the
-    deferred RMSNorm of ``x`` (the un-normalised residual rows).  Returns the fp32 [M, H / 16] per-tile row
-    sums of squares of the new residual (the next consumer's deferred norm)."""
-    _bf16_cuda(x, w_gu, w_down, residual)
-    _rows_ok(x)
-    _rows_ok(residual)
-    M, H = x.shape
-    F = w_down.shape[1]
-    _req(w_gu.is_contiguous() and w_down.is_contiguous() and tuple(w_gu.shape) == (2 * F, H)
-         and tuple(w_down.shape) == (H, F) and tuple(residual.shape) == (M, H),
-         "mlp_fused: w_gu [2F, H], w_down [H, F], residual [M, H]")
-    _req(mlp_fused_ok(M, H, F), "mlp_fused: unsupported M=%d H=%d F=%d (capacity %d)"
-         % (M, H, F, mlp_fused_capacity()))
-    sq, tiles, eps = _norm_args(x, norm)
-    h, words = _mlp_workspace(x.device, max(F // 8, H // 16))
-    ssp = torch.empty(M, H // 16, dtype=torch.float32, device=x.device)
-    if tp is not None:
-        STATS["tp_push"] += 1
-    wp = words.data_ptr()
-    _check(_fn("mrsum_mlp_fused")(_p(x), x.stride(0), _p(w_gu), _p(w_down), H, F, M, sq, tiles, eps, _p(residual),
-                                  residual.stride(0), _p(ssp), _p(h), ctypes.c_void_p(wp), ctypes.c_void_p(wp + 4 * _MLP_MAX_GRID),
-                                  tp, _stream()), "mlp_fused")
-    return ssp
 
 
 def skinny_resid(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, tp=None) -> torch.Tensor:

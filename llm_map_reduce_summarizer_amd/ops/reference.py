@@ -74,11 +74,12 @@ def kv8_slab(page: int, d: int) -> int:
 
 def kv8_quant_rows(x: torch.Tensor):
     """Rows [..., d] -> (e4m3fn bytes [..., d] uint8, fp32 scales [...]): scale = the power of two >= max|x| / 448
-    (1 for a zero row), q = RNE e4m3(x / scale) -- kv8.h's row rule."""
+    (1 for a zero row) and at least 2^-126 (a normal number: 1 / scale stays finite), q = RNE e4m3(x / scale) --
+    kv8.h's row rule."""
     xf = x.float()
     amax = xf.abs().amax(-1)
     m, e = torch.frexp(amax / 448.0)
-    e = torch.where(m == 0.5, e - 1, e)
+    e = torch.clamp(torch.where(m == 0.5, e - 1, e), min=-126)
     sc = torch.where(amax > 0, torch.ldexp(torch.ones_like(amax), e), torch.ones_like(amax))
     q = (xf / sc[..., None]).to(torch.float8_e4m3fn).view(torch.uint8)
     return q, sc

@@ -68,6 +68,13 @@ class CustomAllReduce:
     """In-place fp32 sum over ``group`` for tensors of at most ``max_bytes`` (one per process/GPU)."""
 
     MAX_RANKS = 8
+    # the P2P paths the decode uses, each self-tested at the model's shapes (self_test):
+    #   one_shot    -- mrsum_ar_allreduce_f32 (fp32 split-K slabs of the non-fused path)
+    #   fused_norm  -- mrsum_ar_add_rmsnorm (push-mode all-reduce + residual add + RMSNorm)
+    #   push_stream -- the stream GEMM's split-K last arriver pushing its tile (stream_gemm.hip "TP push")
+    #   push_skinny -- the register-streaming producer pushing its tile (every workgroup spins on its peers)
+    #   max_u64     -- the vocab-parallel sampler's 8-byte Gumbel-key max
+    PATHS = ("one_shot", "fused_norm", "push_stream", "push_skinny", "max_u64")
 
     def __init__(self, group=None, max_bytes: int = 4 << 20):
         """``max_bytes`` bounds one message: the one-shot kernel takes at most 1 MiB of it, the fused
@@ -79,6 +86,9 @@ class CustomAllReduce:
         if self.world > self.MAX_RANKS:
             raise ValueError("custom all-reduce supports at most %d ranks" % self.MAX_RANKS)
         self.max_bytes = int(max_bytes)
+        # per-path verdicts of the start-up self-test (self_test): a path that failed on ANY rank is off on
+        # every rank and its callers take the next path (push -> fused add + RMSNorm -> one-shot slabs)
+        self.paths = {p: True for p in self.PATHS}
         self._lib = _lib()
         # every step ends in a collective whatever happened locally, so all ranks agree on the
         # outcome (a rank that raised alone would leave its peers waiting in the next collective)
@@ -100,9 +110,11 @@ class CustomAllReduce:
             self.close()
             raise RuntimeError("custom all-reduce: hipIpcOpenMemHandle failed on some rank (rc %d here)" % rc)
 
+    ONE_SHOT_MAX = 1 << 20  # bytes the one-shot kernel takes per call
+
     def fits(self, t: torch.Tensor) -> bool:
-        return (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() % 4 == 0
-                and t.numel() * 4 <= min(self.max_bytes, 1 << 20))
+        return (self.paths["one_shot"] and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
+                and t.numel() % 4 == 0 and t.numel() * 4 <= min(self.max_bytes, self.ONE_SHOT_MAX))
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         """Sum ``t`` over the group in place (RCCL for tensors the P2P path does not take)."""
@@ -122,7 +134,8 @@ class CustomAllReduce:
         if not (parts.is_cuda and parts.dtype == torch.float32 and parts.is_contiguous() and parts.dim() == 3):
             return False
         _, T, D = parts.shape
-        return T <= self.MAX_ROWS and D % 4 == 0 and D <= 8192 and T * D * 2 <= self.max_bytes
+        return (self.paths["fused_norm"] and T <= self.MAX_ROWS and D % 4 == 0 and D <= 8192
+                and T * D * 2 <= self.max_bytes)
 
     def add_rmsnorm(self, parts: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, eps: float,
                     out: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -149,8 +162,12 @@ class CustomAllReduce:
 
     def push_ok(self, rows: int, hidden: int) -> bool:
         """Can a TP-push GEMM epilogue all-reduce ``rows`` x ``hidden`` over this group?"""
-        return (bool(self._h) and 1 <= rows <= 64 and hidden % 16 == 0 and hidden <= self.PUSH_MAX_HIDDEN
-                and rows * hidden * 4 <= self.max_bytes)
+        return (bool(self._h) and bool(self.push_kinds()) and 1 <= rows <= 64 and hidden % 16 == 0
+                and hidden <= self.PUSH_MAX_HIDDEN and rows * hidden * 4 <= self.max_bytes)
+
+    def push_kinds(self) -> set:
+        """The TP-push producers that passed the self-test: {"stream", "skinny"} or a subset."""
+        return {k for k in ("stream", "skinny") if self.paths["push_" + k]}
 
     def push_handle(self) -> int:
         """The native handle a TP-push GEMM epilogue takes (ops.hip.stream_resid ``tp``)."""
@@ -167,13 +184,81 @@ class CustomAllReduce:
             raise RuntimeError("custom all-reduce (max) launch failed (%d)" % rc)
         return t
 
-    def self_test(self, iters: int = 4, n: int = 65536) -> bool:
-        """Collective check against torch.distributed on every rank: eager and hipGraph-replayed
-        calls with values that change per call (a stale slot or flag shows up as a mismatch).  All
-        ranks return the same verdict."""
-        ok = True
+    def self_test(self, shapes: Optional[dict] = None, iters: int = 3) -> bool:
+        """COLLECTIVE start-up check of every P2P path against torch.distributed, at the MODEL's shapes:
+        ``shapes`` = {"hidden": H, "k": {"o": K_o, "down": K_down} (this rank's shard K of the row-parallel
+        projections), "fp8": bool, "rows": decode row counts (default 1, 16, 64)}; None: Llama-3-8B's
+        hidden 4096 with TP=8 shard K.  Per path (PATHS): eager calls with values that change per call (a
+        stale slot, flag or epoch shows up as a mismatch) and hipGraph replays, compared with RCCL / the fp32
+        reference and across ranks.  Each path's verdict is agreed over the group (a path that failed on one
+        rank is off everywhere; ``self.paths``); the group then resets the P2P state.  Returns whether the
+        handle is usable at all: the one-shot or the fused path (a graph-safe decode all-reduce) AND the key
+        max (the vocab-parallel sampler has no graph-safe fallback)."""
+        sh = dict(hidden=4096, k={"o": 512, "down": 1792}, fp8=False, rows=(1, 16, 64))
+        sh.update(shapes or {})
         dev = torch.device("cuda", torch.cuda.current_device())
-        try:
+        H, rows = int(sh["hidden"]), tuple(int(r) for r in sh["rows"])
+        local = {}
+
+        def run(name, fn):
+            try:
+                local[name] = bool(fn()) and self.error() == 0
+            except Exception as e:  # keep the collective sequence aligned across ranks
+                log.warning("custom all-reduce self-test of %s raised: %s", name, e)
+                local[name] = False
+            if self.error():
+                # a timed-out wait poisons the handle's later calls: clear it (collective) before the next path
+                local[name] = False
+                self.reset()
+
+        run("one_shot", lambda: self._test_one_shot(dev, H, rows, iters))
+        run("fused_norm", lambda: self._test_fused(dev, iters, rows, H))
+        run("max_u64", lambda: self._test_max_u64(dev, rows, iters))
+        exercised = {"one_shot": True, "fused_norm": True, "max_u64": True}
+        for kind in ("stream", "skinny"):
+            def t(kind=kind):
+                tested = False
+                for role, K in sorted(sh["k"].items()):
+                    for M in rows:
+                        if _push_case(self, kind, M, H, int(K), bool(sh["fp8"]), role) is None:
+                            continue
+                        tested = True
+                        graph = M in (rows[0], rows[-1])
+                        if not _test_push(self, dev, iters, group=self.group, M=M, N=H, K=int(K), kind=kind,
+                                          fp8=bool(sh["fp8"]), role=role, graph=graph):
+                            log.warning("custom all-reduce self-test: %s push failed at %s M=%d N=%d K=%d",
+                                        kind, role, M, H, K)
+                            return False
+                exercised["push_" + kind] = tested
+                return True
+            run("push_" + kind, t)
+        votes = [None] * self.world
+        dist.all_gather_object(votes, local, group=self.group)
+        for p in self.PATHS:
+            self.paths[p] = all(v is not None and v.get(p, False) for v in votes)
+        # report: "ok" / "failed" per path, "n/a" where the model's shapes never take that path (e.g. the
+        # register-streaming push under fp8 weights)
+        self.report = {p: ("ok" if self.paths[p] else "failed") if exercised.get(p, True) or not self.paths[p]
+                       else "n/a" for p in self.PATHS}
+        self.report["shapes"] = "hidden %d, shard K %s, rows %s%s" % (H, dict(sh["k"]), list(rows),
+                                                                     ", fp8" if sh["fp8"] else "")
+        # the test's tagged words sit at offsets that later belong to other granules / rows: start the real
+        # traffic from zeroed slots and epoch 1 on every rank, whatever the test's iteration count
+        self.reset()
+        log.info("custom all-reduce self-test (hidden %d, rows %s): %s", H, rows, self.paths)
+        return (self.paths["one_shot"] or self.paths["fused_norm"]) and self.paths["max_u64"]
+
+    def selftest_report(self) -> dict:
+        """Per path "ok" / "failed" / "n/a" of the start-up self-test (+ the shapes it ran at)."""
+        return dict(getattr(self, "report", {p: "untested" for p in self.PATHS}))
+
+    def _test_one_shot(self, dev, H: int, rows, iters: int) -> bool:
+        """mrsum_ar_allreduce_f32 at the decode's message sizes (rows x hidden fp32, capped at the kernel's
+        1 MiB), eager and graph-replayed, bit-equal to RCCL (integer-valued fp32: the sum is exact)."""
+        ok = True
+        for M in rows:
+            n = min(M * H, self.ONE_SHOT_MAX // 4)
+            n -= n % 4
             x = torch.empty(n, device=dev)
             ref = torch.empty(n, device=dev)
             base = torch.arange(n, device=dev, dtype=torch.float32).remainder_(251)
@@ -201,18 +286,53 @@ class CustomAllReduce:
                 dist.all_reduce(ref, group=self.group)
                 torch.cuda.synchronize(dev)
                 ok &= bool(torch.equal(x, ref))
-            ok &= self._test_fused(dev, iters)
-            ok &= _test_push(self, dev, iters, group=self.group)
-            ok &= self.error() == 0
-        except Exception as e:  # keep the collective sequence aligned across ranks
-            log.warning("custom all-reduce self-test raised: %s", e)
-            ok = False
-        votes = [None] * self.world
-        dist.all_gather_object(votes, ok, group=self.group)
-        # the test's tagged words sit at offsets that later belong to other granules / rows: start the real
-        # traffic from zeroed slots and epoch 1 on every rank, whatever the test's iteration count
-        self.reset()
-        return all(votes)
+        return ok
+
+    def _test_max_u64(self, dev, rows, iters: int) -> bool:
+        """max_u64_ over keys with the top bit set and clear (compared UNSIGNED), eager and graph-replayed,
+        against the keys all-gathered over the group and reduced on the host."""
+        import numpy as np
+        ok = True
+        for B in rows:
+            t = torch.empty(B, dtype=torch.int64, device=dev)
+            keep = torch.empty_like(t)
+
+            def fill(i):
+                g = torch.Generator(device="cpu").manual_seed(7919 * i + 31 * self.rank + B)
+                k = torch.randint(-(1 << 62), 1 << 62, (B,), generator=g, dtype=torch.int64) * 2 + (i & 1)
+                t.copy_(k)
+                keep.copy_(k)
+
+            def check():
+                allk = [torch.empty_like(keep) for _ in range(self.world)]
+                if dist.get_backend(self.group) == "nccl":
+                    dist.all_gather(allk, keep, group=self.group)
+                else:
+                    cpu = [torch.empty(B, dtype=torch.int64) for _ in range(self.world)]
+                    dist.all_gather(cpu, keep.cpu(), group=self.group)
+                    allk = cpu
+                want = np.max(np.stack([a.cpu().numpy().view(np.uint64) for a in allk]), axis=0)
+                return bool(np.array_equal(t.cpu().numpy().view(np.uint64), want))
+
+            for i in range(iters):
+                fill(i)
+                self.max_u64_(t)
+                torch.cuda.synchronize(dev)
+                ok &= check()
+            s = torch.cuda.Stream(device=dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(s):
+                self.max_u64_(t)
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                self.max_u64_(t)
+            for i in range(iters):
+                fill(40 + i)
+                g.replay()
+                torch.cuda.synchronize(dev)
+                ok &= check()
+        return ok
 
     def reset(self) -> None:
         """COLLECTIVE: clear the flags, slots, epochs and the sticky error word on every rank of the group
@@ -239,7 +359,15 @@ class CustomAllReduce:
             failed |= bool(f)
         return err, failed
 
-    def _test_fused(self, dev, iters: int, T: int = 5, D: int = 512, S: int = 2) -> bool:
+    def _test_fused(self, dev, iters: int, rows=(5,), D: int = 512, S: int = 2) -> bool:
+        """add_rmsnorm at D = hidden for every decode row count in ``rows``."""
+        ok = True
+        for T in rows:
+            if T * D * 2 <= self.max_bytes and T <= self.MAX_ROWS:
+                ok &= self._test_fused_one(dev, iters, T, D, S)
+        return ok
+
+    def _test_fused_one(self, dev, iters: int, T: int, D: int, S: int) -> bool:
         """add_rmsnorm against (collective sum of the slabs) + the fp32 reference add_rmsnorm, eager
         and graph-replayed; every rank must also produce the bit-identical residual."""
         from ..ops import reference
@@ -356,38 +484,88 @@ class CustomAllReduce:
             pass
 
 
-def _test_push(h, dev, iters: int, group=None, M: int = 3, N: int = 2048, K: int = 512, wpb: int = 4,
-               S: int = 4) -> bool:
-    """The TP-push residual producer (ops.hip.stream_resid with ``tp``) against the collective sum of every
-    rank's x @ w^T on the same residual, eager and graph-replayed (values change per call: a stale slot,
-    flag or epoch shows up); the residual must also be bit-identical across ranks.  ``group`` None with
-    a LocalPush ``h`` (one rank)."""
+def _push_case(h, kind: str, M: int, N: int, K: int, fp8: bool, role: str = "o"):
+    """The producer launch parameters of a TP push of ``kind`` at M x N x K as the decode runs it
+    (ops._resid_plan with tp=True, forced to ``kind``), or None when that producer does not take the shape."""
+    from .. import ops
     from ..ops import hip
+    if M > 64 or K % 128 or N % 16:
+        return None
+    a = torch.empty(M, K, dtype=torch.bfloat16, device="meta")
+    w = _meta_weight(N, K, fp8)
+    try:
+        rp = ops._resid_plan(hip, a, w, role, tp=True, force=kind)
+    except Exception:  # noqa: BLE001 -- a plan the producer cannot take
+        return None
+    if rp is None or rp[0] != kind:
+        return None
+    if kind == "skinny" and (fp8 or N // 16 > hip.skinny_resid_capacity()):
+        return None
+    return rp
+
+
+def _meta_weight(N: int, K: int, fp8: bool):
+    from ..ops.reference import Fp8Weight
+    if fp8:
+        return Fp8Weight(torch.empty(N, K, dtype=torch.float8_e4m3fn, device="meta"),
+                         torch.empty(N, dtype=torch.float32, device="meta"))
+    return torch.empty(N, K, dtype=torch.bfloat16, device="meta")
+
+
+def _test_push(h, dev, iters: int, group=None, M: int = 3, N: int = 2048, K: int = 512, kind: str = "stream",
+               fp8: bool = False, role: str = "o", graph: bool = True, wpb: Optional[int] = None,
+               S: Optional[int] = None) -> bool:
+    """The TP-push residual producer ``kind`` ("stream": ops.hip.stream_resid, bf16 or fp8 weights;
+    "skinny": ops.hip.skinny_resid) at M x N x K with the launch parameters the decode's plan gives that
+    shape (or ``wpb`` / ``S``), against the collective sum of every rank's x @ w^T on the same residual,
+    eager and (``graph``) graph-replayed, values changing per call (a stale slot, flag or epoch shows up);
+    the residual must also be bit-identical across ranks.  ``group`` None with a LocalPush ``h``."""
+    from ..ops import hip
+    from ..ops.reference import Fp8Weight
+    rp = _push_case(h, kind, M, N, K, fp8, role) if (wpb is None or S is None) else ("stream", wpb, S)
+    if rp is None:
+        raise ValueError("no %s push producer for M=%d N=%d K=%d" % (kind, M, N, K))
     ok = True
-    g = torch.Generator(device="cpu").manual_seed(4321)
+    g = torch.Generator(device="cpu").manual_seed(4321 + M)
     res0 = torch.randn(M, N, generator=g).to(torch.bfloat16).to(dev)
     res = res0.clone()
     x = torch.empty(M, K, dtype=torch.bfloat16, device=dev)
-    w = torch.empty(N, K, dtype=torch.bfloat16, device=dev)
+    wb = torch.empty(N, K, dtype=torch.bfloat16, device=dev)
+    w8 = [None]
     ssp = [None]
     rank = h.rank
 
     def fill(i):
-        gi = torch.Generator(device="cpu").manual_seed(1000 * i + 7 * rank)
+        gi = torch.Generator(device="cpu").manual_seed(1000 * i + 7 * rank + M)
         x.copy_((torch.randn(M, K, generator=gi) * 0.5).to(torch.bfloat16))
-        w.copy_((torch.randn(N, K, generator=gi) * 0.05).to(torch.bfloat16))
+        wb.copy_((torch.randn(N, K, generator=gi) * 0.05).to(torch.bfloat16))
+        if fp8:
+            q = Fp8Weight.quantize(wb)
+            if w8[0] is None:
+                w8[0] = q
+            else:  # keep the captured pointers
+                w8[0].q.copy_(q.q)
+                w8[0].scale.copy_(q.scale)
         res.copy_(res0)
 
+    def weight():
+        return w8[0] if fp8 else wb
+
     def run():
-        ssp[0] = hip.stream_resid(x, w, res, wpb, S, tp=h.push_handle())
+        if rp[0] == "skinny":
+            ssp[0] = hip.skinny_resid(x, wb, res, tp=h.push_handle())
+        else:
+            ssp[0] = hip.stream_resid(x, weight(), res, rp[1], rp[2], tp=h.push_handle())
 
     def check():
-        tot = x.float() @ w.float().t()
+        wf = (w8[0].q.float() * w8[0].scale[:, None]) if fp8 else wb.float()
+        tot = x.float() @ wf.t()
         if h.world > 1:
             dist.all_reduce(tot, group=group)
         ref = (res0.float() + tot).to(torch.bfloat16).float()
         good = bool(torch.allclose(res.float(), ref, atol=6e-2, rtol=2e-2))
-        ss = res.float().pow(2).reshape(M, N // (16 * wpb), 16 * wpb).sum(-1)
+        tiles = ssp[0].shape[1]
+        ss = res.float().pow(2).reshape(M, tiles, N // tiles).sum(-1)
         good &= bool(torch.allclose(ssp[0], ss, rtol=1e-3, atol=1e-2))
         if h.world > 1:
             mine = res.float().sum().reshape(1)
@@ -402,21 +580,22 @@ def _test_push(h, dev, iters: int, group=None, M: int = 3, N: int = 2048, K: int
         run()
         torch.cuda.synchronize(dev)
         ok &= check()
-    s = torch.cuda.Stream(device=dev)
-    s.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(s):
-        fill(90)
-        run()
-    torch.cuda.synchronize(dev)
-    ok &= check()
-    gr = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(gr, stream=s):
-        run()
-    for i in range(iters):
-        fill(60 + i)
-        gr.replay()
+    if graph:
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            fill(90)
+            run()
         torch.cuda.synchronize(dev)
         ok &= check()
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, stream=s):
+            run()
+        for i in range(iters):
+            fill(60 + i)
+            gr.replay()
+            torch.cuda.synchronize(dev)
+            ok &= check()
     return ok and h.error() == 0
 
 
@@ -431,12 +610,18 @@ class LocalPush:
 
     def __init__(self, max_bytes: int = 4 << 20):
         self.max_bytes = int(max_bytes)
+        # per-path verdicts of the start-up self-test (self_test): a path that failed on ANY rank is off on
+        # every rank and its callers take the next path (push -> fused add + RMSNorm -> one-shot slabs)
+        self.paths = {p: True for p in self.PATHS}
         self._lib = _lib()
         self._h = self._lib.mrsum_ar_create(0, 1, self.max_bytes)
         if not self._h:
             raise RuntimeError("LocalPush: allocation failed")
 
     MAX_ROWS = CustomAllReduce.MAX_ROWS
+    PATHS = CustomAllReduce.PATHS
+    paths = {p: True for p in CustomAllReduce.PATHS}
+    push_kinds = CustomAllReduce.push_kinds
     push_ok = CustomAllReduce.push_ok
     push_handle = CustomAllReduce.push_handle
     fits_rows = CustomAllReduce.fits_rows
@@ -451,8 +636,11 @@ class LocalPush:
     __del__ = CustomAllReduce.__del__
 
 
-def maybe_custom_all_reduce(group=None, max_bytes: int = 4 << 20) -> Optional[CustomAllReduce]:
-    """A CustomAllReduce for ``group`` when every rank is on a GPU, else None (RCCL/gloo path)."""
+def maybe_custom_all_reduce(group=None, max_bytes: int = 4 << 20, shapes: Optional[dict] = None
+                            ) -> Optional[CustomAllReduce]:
+    """A CustomAllReduce for ``group`` when every rank is on a GPU and its self-test at ``shapes`` (the
+    model's hidden size / shard K, see CustomAllReduce.self_test) leaves a graph-safe path, else None (RCCL /
+    gloo path).  Paths that failed the test are off (``paths``); their callers take the next path."""
     if not (dist.is_initialized() and torch.cuda.is_available()):
         return None
     from .. import IPC_MODE_TOO_LATE
@@ -464,8 +652,8 @@ def maybe_custom_all_reduce(group=None, max_bytes: int = 4 << 20) -> Optional[Cu
                       "(set it in the environment before the first GPU call); dmabuf IPC is unavailable")
         log.warning("custom all-reduce unavailable, using RCCL: %s", e)
         return None
-    if not ar.self_test():
-        log.warning("custom all-reduce failed its self-test on some rank; using RCCL")
+    if not ar.self_test(shapes):
+        log.warning("custom all-reduce failed its self-test on some rank (%s); using RCCL", ar.paths)
         ar.close()
         return None
     return ar

@@ -188,11 +188,68 @@ def all_reduce_max(x: float) -> float:
     return float(t.item())
 
 
+class AsyncWorks:
+    """Scope of asynchronous collectives (``async_op=True`` work handles): every handle registered with
+    ``add`` is waited on leaving the scope, on the normal path AND when an exception unwinds through it, so no
+    work handle outlives the code that started it.  A handle left un-waited holds the backend's pending work
+    until process teardown, where gloo aborts (``terminate called without an active exception``) or RCCL
+    reports an unfinished collective.  Waiting on a finished work is cheap; on the exception path a wait
+    error is swallowed (the original exception propagates), and a peer that never posts its side ends the
+    wait at the process-group timeout."""
+
+    def __init__(self):
+        self._works = []
+
+    def add(self, work):
+        if work is not None:
+            self._works.append(work)
+        return work
+
+    def __enter__(self) -> "AsyncWorks":
+        return self
+
+    def __exit__(self, et, ev, tb) -> bool:
+        works, self._works = self._works, []
+        for w in works:
+            try:
+                w.wait()
+            except Exception:
+                if et is None:
+                    raise
+        return False
+
+
 def shutdown() -> None:
+    """Tear the process groups down in a fixed order on every rank: a barrier (no rank leaves while a peer is
+    still inside a collective), then every subgroup this module created (TP groups), then the default group.
+    Each step runs even if an earlier one raised; the first error is re-raised at the end."""
     global _STATE
-    if is_initialized():
+    if not is_initialized():
+        _STATE = ParallelState()
+        return
+    err = None
+    try:
+        barrier()
+    except Exception as e:  # noqa: BLE001 -- still tear down
+        err = e
+    subgroups = [g for g in list(_TP_GROUPS.values()) + [_STATE.tp_group]
+                 if g is not None and g is not dist.group.WORLD]
+    seen = set()
+    for g in subgroups:
+        if id(g) in seen:
+            continue
+        seen.add(id(g))
         try:
-            barrier()
-        finally:
-            dist.destroy_process_group()
+            dist.destroy_process_group(g)
+        except Exception as e:  # noqa: BLE001
+            err = err or e
+    _TP_GROUPS.clear()
     _STATE = ParallelState()
+    try:
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        err = err or e
+    import gc
+    gc.collect()
+    if err is not None:
+        raise err

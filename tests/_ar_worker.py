@@ -86,7 +86,14 @@ def main():
         torch.cuda.synchronize()
         expect = 1.0 + S * sum(r + 1 + it for r in range(world))
         assert torch.equal(res, torch.full_like(res, expect)), "fused graph replay %d" % it
-    assert ar.self_test()
+    assert ar.self_test(), ar.paths  # Llama-3-8B TP=8 shard shapes (hidden 4096, rows 1 / 16 / 64)
+    assert all(ar.paths.values()) and ar.selftest_report()["push_skinny"] == "ok", ar.selftest_report()
+    # the 70B fp8 shard's shapes: hidden 8192, o / down shard K 1024 / 3584, W8A16 stream producers
+    ar8 = CustomAllReduce(None, max_bytes=4 << 20)
+    assert ar8.self_test(dict(hidden=8192, k={"o": 1024, "down": 3584}, fp8=True)), ar8.paths
+    rep = ar8.selftest_report()
+    assert all(rep[p] in ("ok", "n/a") for p in ar8.PATHS) and rep["push_stream"] == "ok", rep
+    ar8.close()
     lat, per_row = ar.measure_latency(rows=(1, 64), hidden=4096)
     print("rank %d fused all-reduce cost over local add_rmsnorm: %.2f us + %.4f us/row (2 ranks sharing one GPU)"
           % (rank, lat * 1e6, per_row * 1e6), flush=True)

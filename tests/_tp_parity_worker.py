@@ -7,7 +7,13 @@ of the tensor-parallel paths with the independent textbook fp32 forward, with th
      scatter + all-gather), then greedy decode through the TP push (row-parallel GEMM epilogues
      all-reducing their own tiles, bf16 payload) and the vocab-parallel sampler;
   B. CONTEXT-PARALLEL prefill of one prompt over the ranks' full engines (zigzag slices, per-layer K/V
-     exchange) handed to the TP engine (each rank keeps its KV heads), then TP decode."""
+     exchange) handed to the TP engine (each rank keeps its KV heads), then TP decode.
+
+Environment: MODEL (llama3-8b | llama3-70b, 2 layers), WDTYPE (bf16 | fp8).  fp8 weights (the config-5
+aggregator's format: OCP e4m3fn, per-row scales, quantised per TP shard by the loader) are compared with the
+textbook forward of the DEQUANTISED SHARDS every rank holds, rebuilt on rank 0 exactly as the loader slices,
+folds and quantises them (unit gains: nothing to fold), with the TP=1 fp8 bounds; the CP part (B) needs a
+full-weight engine per rank and runs for bf16 only."""
 import os
 import sys
 
@@ -22,6 +28,50 @@ from llm_map_reduce_summarizer_amd.engine import weights as W  # noqa: E402
 from llm_map_reduce_summarizer_amd.engine.config import get_model_config  # noqa: E402
 from llm_map_reduce_summarizer_amd.engine.engine import ImportedPrefill, LLMEngine, SamplingParams  # noqa: E402
 from llm_map_reduce_summarizer_amd.ops import hip  # noqa: E402
+from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight, interleave_gate_up, split_gate_up  # noqa: E402
+
+
+def unit_gain_checkpoint(cfg, seed):
+    """P._checkpoint with every RMSNorm gain 1 (the fp8 comparison needs no gain folding)."""
+    d = P._checkpoint(cfg, seed)
+    for k in d:
+        if k.endswith("norm.weight") or k.endswith("layernorm.weight"):
+            d[k] = torch.ones_like(d[k])
+    return d
+
+
+def fp8_shard_reference(cfg, ckpt, world, dev):
+    """HF-layout fp32 tensors of the model the TP ranks actually run: for every rank, its weight shards sliced
+    as engine/weights.py load_hf slices them, quantised per shard with Fp8Weight.quantize on the device (as the
+    loader does), dequantised and put back in place."""
+    hd, H, F = cfg.head_dim, cfg.hidden, cfg.ffn
+    qs, ks, f = cfg.n_heads * hd // world, cfg.n_kv_heads * hd // world, F // world
+    ref = {"model.embed_tokens.weight": ckpt["model.embed_tokens.weight"],
+           "model.norm.weight": ckpt["model.norm.weight"], "lm_head.weight": ckpt["model.embed_tokens.weight"]}
+
+    def dq(t):
+        return Fp8Weight.quantize(t.to(dev, torch.bfloat16).contiguous()).dequant(torch.float32).cpu()
+
+    for i in range(cfg.n_layers):
+        p = "model.layers.%d." % i
+        wq, wk, wv = (ckpt[p + "self_attn.%s_proj.weight" % n] for n in ("q", "k", "v"))
+        wo, wd = ckpt[p + "self_attn.o_proj.weight"], ckpt[p + "mlp.down_proj.weight"]
+        wg, wu = ckpt[p + "mlp.gate_proj.weight"], ckpt[p + "mlp.up_proj.weight"]
+        q, k, v, o, g, u, d = [], [], [], [], [], [], []
+        for r in range(world):
+            qkv = dq(torch.cat([wq[r * qs:(r + 1) * qs], wk[r * ks:(r + 1) * ks], wv[r * ks:(r + 1) * ks]]))
+            q.append(qkv[:qs]), k.append(qkv[qs:qs + ks]), v.append(qkv[qs + ks:])
+            o.append(dq(wo[:, r * qs:(r + 1) * qs]))
+            gg, uu = split_gate_up(dq(interleave_gate_up(wg[r * f:(r + 1) * f], wu[r * f:(r + 1) * f])).t())
+            g.append(gg.t()), u.append(uu.t())
+            d.append(dq(wd[:, r * f:(r + 1) * f]))
+        ref[p + "self_attn.q_proj.weight"], ref[p + "self_attn.k_proj.weight"] = torch.cat(q), torch.cat(k)
+        ref[p + "self_attn.v_proj.weight"], ref[p + "self_attn.o_proj.weight"] = torch.cat(v), torch.cat(o, 1)
+        ref[p + "mlp.gate_proj.weight"], ref[p + "mlp.up_proj.weight"] = torch.cat(g), torch.cat(u)
+        ref[p + "mlp.down_proj.weight"] = torch.cat(d, 1)
+        ref[p + "input_layernorm.weight"] = ckpt[p + "input_layernorm.weight"]
+        ref[p + "post_attention_layernorm.weight"] = ckpt[p + "post_attention_layernorm.weight"]
+    return ref
 
 
 def spy(eng, rec):
@@ -47,13 +97,21 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     torch.cuda.set_device(0)
     dev = torch.device("cuda:0")
-    cfg = get_model_config("llama3-8b", n_layers=2)
-    ckpt = P._checkpoint(cfg, 11)
+    model, wdt = os.environ.get("MODEL", "llama3-8b"), os.environ.get("WDTYPE", "bf16")
+    cfg = get_model_config(model, n_layers=2)
+    fp8 = wdt == "fp8"
+    ckpt = unit_gain_checkpoint(cfg, 11) if fp8 else P._checkpoint(cfg, 11)
     index = {k: "mem" for k in ckpt}
     W._open_shards = lambda path: (index, {"mem": P._Mem(ckpt)})
     tp = LLMEngine(cfg, device="cuda:0", weights_path="mem", use_graphs=False, max_num_seqs=8, sync_every=64,
-                   max_model_len=4096, kv_pages=256, tp_rank=rank, tp_size=world, tp_group=None)
+                   max_model_len=4096, kv_pages=256, tp_rank=rank, tp_size=world, tp_group=None, weight_dtype=wdt)
     assert tp.model.custom_ar is not None and tp.model.tp_sampling and tp.model.sequence_parallel
+    rep = tp.model.custom_ar.selftest_report()
+    assert all(rep[p] in ("ok", "n/a") for p in tp.model.custom_ar.PATHS), rep  # self-test at these shapes
+    ref_ckpt, tol, min_exact = ckpt, P.BF16_TOL, 0.9
+    if fp8:
+        ref_ckpt = fp8_shard_reference(cfg, ckpt, world, dev) if rank == 0 else None
+        tol, min_exact = P.FP8_TOL, P.FP8_MIN_EXACT
     res = {}
 
     # A: SP prefill + TP-push decode
@@ -77,7 +135,16 @@ def main():
         pre = torch.cat(rows_all[:len(rows_all) - (new - 1)])
         steps = rows_all[len(rows_all) - (new - 1):]
         rows = {i: [pre[slot].to(dev)] + [s[slot].to(dev) for s in steps] for slot, i in enumerate(order)}
-        res["A"] = P._compare(cfg, ckpt, prompts, toks, rows, P.BF16_TOL, dev)
+        res["A"] = P._compare(cfg, ref_ckpt, prompts, toks, rows, tol, dev, min_exact=min_exact)
+    if fp8:
+        if rank == 0:
+            print("tp%d %s fp8 parity: SP prefill (fp8 GEMMs, two-term QKV rows gathered as e4m3) + W8A16 "
+                  "TP-push decode max rel err %.4f top-1 %d/%d (%d pushes); self-test %s"
+                  % ((world, model) + res["A"] + (pushed, rep)), flush=True)
+        dist.barrier()
+        print("rank %d tp parity ok" % rank, flush=True)
+        dist.destroy_process_group()
+        return
 
     # B: context-parallel prefill over the ranks' full engines -> TP decode
     full = LLMEngine(cfg, device="cuda:0", weights_path="mem", use_graphs=False, max_num_seqs=4, sync_every=64,

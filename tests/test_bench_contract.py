@@ -30,7 +30,7 @@ def _run(world: int, *extra: str, self_launch: bool = False):
     else:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
                "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"), *args]
-    env = dict(os.environ, MRSUM_OPS="torch", CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS="2")
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
     p = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=600)

@@ -359,6 +359,16 @@ def test_fp8_kv_cache_cpu():
     deq = q.view(torch.float8_e4m3fn).float() * sc[..., None]
     assert float((deq - x).norm() / x.norm()) < 0.04 and float(deq[3].abs().sum()) == 0.0
     assert float(((x.abs().amax(-1) / sc)[torch.arange(9) != 3]).max()) <= 448.0
+    # rows far below e4m3's range (max|x| < 448 * 2^-126): the scale stays a normal 2^-126, so 1 / scale is
+    # finite and the row quantises to finite bytes (zero elements stay zero) -- never NaN
+    tiny = torch.zeros(3, 128)
+    tiny[0, 5] = 1e-36
+    tiny[1, :] = 3e-37
+    tiny[2, 7] = -2e-37
+    qt, st = R.kv8_quant_rows(tiny)
+    assert torch.all(st == 2.0 ** -126) and torch.all(torch.isfinite(1.0 / st))
+    dq = qt.view(torch.float8_e4m3fn).float()
+    assert torch.all(torch.isfinite(dq)) and float(dq[0, :5].abs().sum()) == 0.0
     b = PagedKVCache.size_pages(1 << 30, 32, 8, 64, 128)
     f = PagedKVCache.size_pages(1 << 30, 32, 8, 64, 128, kv_dtype="fp8")
     assert 1.9 < f / b < 2.0

@@ -139,59 +139,3 @@ def test_gemm_graph_capture():
     g.replay()
     torch.cuda.synchronize()
     _check(out, x.float() @ w.float().t())
-
-
-@pytest.mark.parametrize("kernel", ["4w", "4w5", "4wL", "4w5L"])
-@pytest.mark.parametrize("M,N,K", [(65, 256, 128), (1000, 1280, 4096), (4097, 6144, 4096), (300, 16032, 1024),
-                                   (257, 4096, 14336), (16384 + 13, 4096, 1024)])
-@pytest.mark.parametrize("aligned", [True, False])
-def test_gemm4w_bf16(kernel, M, N, K, aligned):
-    """The four-wave bf16 GEMM (gemm4w.hip: 128 x 128 outputs per wave, one barrier per 32-k step, 4- / 5-step
-    LDS ring) against fp32: ragged M, N tails, K from 2 to 448 steps, both epilogues."""
-    x = _rand(M, K, seed=21, scale=0.5, offset=0.05)
-    w = _rand(N, K, seed=22, scale=0.02, offset=0.001)
-    ref = x.float() @ w.float().t()
-    if aligned:
-        out = hip.gemm(x, w, kernel=kernel)
-    else:
-        big = torch.zeros(M, N + 8, dtype=torch.bfloat16, device=DEV)
-        out = hip.gemm(x, w, out=big[:, 4:4 + N], kernel=kernel)
-        torch.cuda.synchronize()
-        assert float(big[:, :4].abs().max()) == 0.0 and float(big[:, 4 + N:].abs().max()) == 0.0
-    torch.cuda.synchronize()
-    _check(out, ref)
-
-
-@pytest.mark.parametrize("kernel", ["4w", "4w5", "4wL", "4w5L"])
-def test_gemm4w_identity_and_swiglu(kernel):
-    K = 256
-    x = torch.eye(K, dtype=torch.bfloat16, device=DEV)
-    w = (torch.arange(512 * K, device=DEV, dtype=torch.float32).reshape(512, K) % 97 - 48).to(torch.bfloat16)
-    out = hip.gemm(x, w, kernel=kernel)
-    torch.cuda.synchronize()
-    assert torch.equal(out.float(), w.float().t()), "C = I . W^T must equal W^T exactly"
-    for M in (100, 3000):
-        K, F = 4096, 1792
-        x = _rand(M, K, seed=25, scale=0.5)
-        wg, wu = _rand(F, K, seed=26, scale=0.03), _rand(F, K, seed=27, scale=0.03)
-        wgu = reference.interleave_gate_up(wg, wu).contiguous()
-        out = hip.gemm(x, wgu, swiglu=True, kernel=kernel)
-        torch.cuda.synchronize()
-        g, u = x.float() @ wg.float().t(), x.float() @ wu.float().t()
-        _check(out, torch.nn.functional.silu(g) * u, tol=3e-2)
-
-
-def test_gemm_blas_knob():
-    """kernel="blas" (the A/B knob, profiles/r4_prefill_plain_gemm_blas_ab.jsonl): the plain product on hipBLASLt
-    matches the fp32 reference; a SwiGLU product stays on gemm.hip, bit-identical to the default kernel."""
-    for M, N, K in ((3000, 4096, 4096), (777, 6144, 4096)):
-        x, w = _rand(M, K, seed=31, scale=0.5), _rand(N, K, seed=32, scale=0.03)
-        out = hip.gemm(x, w, kernel="blas")
-        torch.cuda.synchronize()
-        _check(out, x.float() @ w.float().t(), tol=3e-2)
-    K, F = 4096, 1792
-    x = _rand(500, K, seed=33, scale=0.5)
-    wgu = reference.interleave_gate_up(_rand(F, K, seed=34, scale=0.03), _rand(F, K, seed=35, scale=0.03)).contiguous()
-    a, b = hip.gemm(x, wgu, swiglu=True, kernel="blas"), hip.gemm(x, wgu, swiglu=True, kernel="8w")
-    torch.cuda.synchronize()
-    assert torch.equal(a, b)
