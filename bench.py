@@ -100,9 +100,9 @@ def main() -> int:
                     help="single-pass reduce over every summary (use a long-context model, e.g. llama3.1-8b)")
     ap.add_argument("--stream-reduce", action="store_true",
                     help="start each level-1 reduce batch as soon as its chunks are summarised (no map barrier)")
-    ap.add_argument("--kv-dtype", choices=["bf16", "fp8"], default="bf16",
-                    help="KV cache format; fp8 (e4m3 rows, power-of-two row scales) is a LABELLED variant: the "
-                         "headline is bf16 KV")
+    ap.add_argument("--kv-dtype", choices=["bf16", "fp8v", "fp8"], default="bf16",
+                    help="KV cache format; fp8v (V rows e4m3 with power-of-two row scales, K bf16) and fp8 (K and V "
+                         "e4m3) are LABELLED variants: the headline is bf16 KV")
     ap.add_argument("--profile", default=None, metavar="DIR", help="torch.profiler trace of the timed steps")
     ap.add_argument("--log-level", default="WARNING")
     args = ap.parse_args()
@@ -201,7 +201,8 @@ def main() -> int:
                      else " [variant: %s, %gh%s%s%s]" % (args.model, args.hours,
                                                          ", single-pass reduce" if args.no_hierarchical else "",
                                                          ", streamed level-1 reduce" if args.stream_reduce else "",
-                                                         ", fp8 KV cache" if args.kv_dtype == "fp8" else "")),
+                                                         {"fp8": ", fp8 KV cache", "fp8v": ", fp8 V cache (bf16 K)"}
+                                                         .get(args.kv_dtype, ""))),
         "value": round(value, 4),
         "unit": "chunks/s",
         "n_gpus": world,

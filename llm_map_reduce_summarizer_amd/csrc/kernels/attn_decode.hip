@@ -286,9 +286,15 @@ __device__ __forceinline__ u32x4 ld_kv(const T* p) {
 // tile per thread) plus each row's scale, and converts every row to bf16 exactly (power-of-two scales)
 // while writing it into the SAME LDS image the bf16 cache fills: QK^T, softmax and PV are unchanged.
 // The fused RoPE writer quantises the new token's rows (kv8 row rule) and patches their DEQUANTISED
-// values into the tile, so this step and later steps see the same K/V.
-template <int G, bool ROPE, bool NT = false, bool KV8 = false>
-__global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
+// values into the tile, so this step and later steps see the same K/V.  KVM is a bitmask: bit 0 = the K
+// cache is fp8 slabs, bit 1 = the V cache is; KVM 2 ("fp8v": bf16 K, fp8 V) stages K with the bf16
+// mapping and V with the slab mapping, each into its own LDS tile.
+// NSET: K/V register sets in flight per thread -- 2 (tiles t+1, t+2 loading while tile t is scored; 3
+// workgroups per CU) or 4 (t+1 .. t+4; one workgroup per CU: grids of at most one workgroup per CU, e.g. B = 1
+// at 8 kv heads x 32 splits, where each workgroup walks ~7 tiles and two loads in flight leave its HBM
+// latency exposed).
+template <int G, bool ROPE, bool NT = false, int KVM = 0, int NSET = 2>
+__global__ __launch_bounds__(256, (NSET == 4 ? 1 : 3)) void attn_decode_mfma_kernel(
     const bf16* __restrict__ q, int q_stride, bf16* __restrict__ kc, bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ positions,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int S, float scale_log2, RopeArgs ra,
@@ -340,7 +346,8 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     const size_t head8 = (size_t)kvr * kv8::SLAB;
     const unsigned char* kc8 = reinterpret_cast<const unsigned char*>(kc);
     const unsigned char* vc8 = reinterpret_cast<const unsigned char*>(vc);
-    float ksc[2], vsc[2], ksc2[2], vsc2[2];  // KV8: row scales of register sets A and B
+    float ksc[2], vsc[2], ksc2[2], vsc2[2];  // fp8 slabs: row scales of register sets A and B
+    constexpr bool K8 = (KVM & 1) != 0, V8 = (KVM & 2) != 0;
     // staging registers are plain named arrays indexed only by unrolled constants (a lambda
     // capturing them by reference put them in scratch), and the prefetch is unconditional (no
     // branch around the loads) so hipcc keeps them in flight.
@@ -350,29 +357,38 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     // loads past the last tile stay unconditional but read the scratch page 0, which every workgroup's
     // overshoot shares and so stays in L2 (re-reading the workgroup's own last tile cost ~9 % extra HBM
     // traffic at B=39, PMC FETCH_SIZE).
-    u32x4 kreg[4], vreg[4], kreg2[4], vreg2[4];
+    u32x4 kreg[4], vreg[4], kreg2[4], vreg2[4], kreg3[4], vreg3[4], kreg4[4], vreg4[4];
+    float ksc3[2], vsc3[2], ksc4[2], vsc4[2];
+    static_assert(NSET == 2 || NSET == 4, "two or four K/V register sets");
 #define KV_ISSUE(KR, VR, KS, VS, TILE)                                                              \
     {                                                                                               \
         const int pg_ = bt[min((TILE), ntiles - 1)];                                                \
-        if constexpr (KV8) {                                                                        \
-            const size_t base_ = (size_t)((TILE) < ntiles ? pg_ : 0) * Hc * kv8::SLAB + head8;      \
+        const int pgx_ = (TILE) < ntiles ? pg_ : 0;                                                 \
+        const size_t base8_ = (size_t)pgx_ * Hc * kv8::SLAB + head8;                                \
+        const size_t base_ = (size_t)pgx_ * Hc * PG * D + head_off;                                 \
+        if constexpr (K8) {                                                                         \
             _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                         \
-                const size_t ro_ = base_ + (size_t)(r8 + 32 * i) * D + 16 * c8;                      \
-                KR[i] = ld_kv<NT>(kc8 + ro_);                                                       \
-                VR[i] = ld_kv<NT>(vc8 + ro_);                                                       \
-                KS[i] = *reinterpret_cast<const float*>(kc8 + base_ + PG * D + 4 * (r8 + 32 * i));  \
-                VS[i] = *reinterpret_cast<const float*>(vc8 + base_ + PG * D + 4 * (r8 + 32 * i));  \
+                KR[i] = ld_kv<NT>(kc8 + base8_ + (size_t)(r8 + 32 * i) * D + 16 * c8);               \
+                KS[i] = *reinterpret_cast<const float*>(kc8 + base8_ + PG * D + 4 * (r8 + 32 * i)); \
             }                                                                                       \
         } else {                                                                                    \
-            const size_t base_ = (size_t)((TILE) < ntiles ? pg_ : 0) * Hc * PG * D + head_off;      \
-            _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                         \
-                KR[i] = ld_kv<NT>(kc + base_ + (size_t)16 * i * D);                                 \
-                VR[i] = ld_kv<NT>(vc + base_ + (size_t)16 * i * D);                                 \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i) KR[i] = ld_kv<NT>(kc + base_ + (size_t)16 * i * D); \
+        }                                                                                           \
+        if constexpr (V8) {                                                                         \
+            _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                         \
+                VR[i] = ld_kv<NT>(vc8 + base8_ + (size_t)(r8 + 32 * i) * D + 16 * c8);               \
+                VS[i] = *reinterpret_cast<const float*>(vc8 + base8_ + PG * D + 4 * (r8 + 32 * i)); \
             }                                                                                       \
+        } else {                                                                                    \
+            _Pragma("unroll") for (int i = 0; i < 4; ++i) VR[i] = ld_kv<NT>(vc + base_ + (size_t)16 * i * D); \
         }                                                                                           \
     }
     KV_ISSUE(kreg, vreg, ksc, vsc, 0)
     KV_ISSUE(kreg2, vreg2, ksc2, vsc2, 1)
+    if constexpr (NSET == 4) {
+        KV_ISSUE(kreg3, vreg3, ksc3, vsc3, 2)
+        KV_ISSUE(kreg4, vreg4, ksc4, vsc4, 3)
+    }
     // ROPE: the q rows of this group (and, for the split holding the new token, its K and V rows)
     // summed over the SP slabs by ALL 256 threads in one round of independent loads into an fp32
     // LDS image (aliasing the K/V tile buffers, which are first written after it is consumed):
@@ -406,9 +422,10 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
                     }
                 }
                 bf16* pdst = lds_new + (isk ? 0 : D) + c;
-                if constexpr (KV8) {
+                if constexpr (KVM != 0) {
                     // quantise the bf16-rounded row, as every other writer does (rope_kv.hip), then the row's 16
-                    // lanes (K: 0-15, V: 16-31) reduce max|x| (kv8.h row rule)
+                    // lanes (K: 0-15, V: 16-31) reduce max|x| (kv8.h row rule) -- all 32 lanes shuffle, a row
+                    // whose cache is bf16 (fp8v: K) then takes the bf16 store below
 #pragma unroll
                     for (int j = 0; j < 8; ++j) kv[j] = (float)(bf16)kv[j];
                     float amax = 0.f;
@@ -416,6 +433,11 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
                     for (int j = 0; j < 8; ++j) amax = fmaxf(amax, fabsf(kv[j]));
 #pragma unroll
                     for (int o = 1; o < 16; o <<= 1) amax = fmaxf(amax, __shfl_xor(amax, o, 64));
+                    if (isk ? !K8 : !V8) {
+                        const uint4 pk = pack8(kv);
+                        *reinterpret_cast<uint4*>((isk ? kc : vc) + dst + c) = pk;
+                        *reinterpret_cast<uint4*>(pdst) = pk;
+                    } else {
                     const float sc = kv8::row_scale(amax), inv = 1.f / sc;
                     const uint2 q = make_uint2(kv8::pack4(kv[0] * inv, kv[1] * inv, kv[2] * inv, kv[3] * inv),
                                                kv8::pack4(kv[4] * inv, kv[5] * inv, kv[6] * inv, kv[7] * inv));
@@ -427,6 +449,7 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
                     u32x4 lo, hi;
                     kv8::dequant16(u32x4{q.x, q.y, 0u, 0u}, sc, lo, hi);
                     *reinterpret_cast<u32x4*>(pdst) = lo;
+                    }
                 } else {
                     const uint4 pk = pack8(kv);
                     *reinterpret_cast<uint4*>((isk ? kc : vc) + dst + c) = pk;
@@ -472,40 +495,54 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     // the new token's row (row pr of tile ptile) is staged from lds_new, not from the page loads
     const int ptile = has_pos ? (ctx - 1 - ks) / PG : -1;
     const int pr = (ctx - 1 - ks) % PG;
-    const bool patcher = has_pos && (KV8 ? r8 == (pr & 31) : st_row == (pr & 15));
+    const bool patcher_k = has_pos && (K8 ? r8 == (pr & 31) : st_row == (pr & 15));
+    const bool patcher_v = has_pos && (V8 ? r8 == (pr & 31) : st_row == (pr & 15));
     if constexpr (ROPE) {
         __syncthreads();  // every lane has its q out of the fp32 image the tiles overwrite
     }
 #define KV_WRITE(KR, VR, KS, VS, TILE)                                                                          \
-    if constexpr (KV8) {                                                                                        \
+    if constexpr (K8) {                                                                                         \
         _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                                         \
-            const bool pt = ROPE && ptile == (TILE) && patcher && i == (pr >> 5);                               \
+            const bool pt = ROPE && ptile == (TILE) && patcher_k && i == (pr >> 5);                             \
             const int row_ = r8 + 32 * i;                                                                       \
-            u32x4 klo, khi, vlo, vhi;                                                                           \
+            u32x4 klo, khi;                                                                                     \
             kv8::dequant16(KR[i], KS[i], klo, khi);                                                             \
-            kv8::dequant16(VR[i], VS[i], vlo, vhi);                                                             \
             if (pt) {                                                                                           \
                 klo = *reinterpret_cast<const u32x4*>(lds_new + 16 * c8);                                       \
                 khi = *reinterpret_cast<const u32x4*>(lds_new + 16 * c8 + 8);                                   \
-                vlo = *reinterpret_cast<const u32x4*>(lds_new + D + 16 * c8);                                   \
-                vhi = *reinterpret_cast<const u32x4*>(lds_new + D + 16 * c8 + 8);                               \
             }                                                                                                   \
             *reinterpret_cast<u32x4*>(ldsK + dk_off(row_, 2 * c8)) = klo;                                      \
             *reinterpret_cast<u32x4*>(ldsK + dk_off(row_, 2 * c8 + 1)) = khi;                                  \
+        }                                                                                                       \
+    } else {                                                                                                    \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                         \
+            const bool pt = ROPE && ptile == (TILE) && patcher_k && i == (pr >> 4);                             \
+            *reinterpret_cast<u32x4*>(ldsK + dk_off(st_row + 16 * i, st_chunk)) =                               \
+                pt ? *reinterpret_cast<const u32x4*>(lds_new + st_chunk * 8) : KR[i];                           \
+        }                                                                                                       \
+    }                                                                                                           \
+    if constexpr (V8) {                                                                                         \
+        _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                                         \
+            const bool pt = ROPE && ptile == (TILE) && patcher_v && i == (pr >> 5);                             \
+            const int row_ = r8 + 32 * i;                                                                       \
+            u32x4 vlo, vhi;                                                                                     \
+            kv8::dequant16(VR[i], VS[i], vlo, vhi);                                                             \
+            if (pt) {                                                                                           \
+                vlo = *reinterpret_cast<const u32x4*>(lds_new + D + 16 * c8);                                   \
+                vhi = *reinterpret_cast<const u32x4*>(lds_new + D + 16 * c8 + 8);                               \
+            }                                                                                                   \
             *reinterpret_cast<u32x4*>(ldsV + dv_off(row_, 2 * c8)) = vlo;                                      \
             *reinterpret_cast<u32x4*>(ldsV + dv_off(row_, 2 * c8 + 1)) = vhi;                                  \
         }                                                                                                       \
     } else {                                                                                                    \
         _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                         \
-            const bool pt = ROPE && ptile == (TILE) && patcher && i == (pr >> 4);                               \
-            *reinterpret_cast<u32x4*>(ldsK + dk_off(st_row + 16 * i, st_chunk)) =                               \
-                pt ? *reinterpret_cast<const u32x4*>(lds_new + st_chunk * 8) : KR[i];                           \
+            const bool pt = ROPE && ptile == (TILE) && patcher_v && i == (pr >> 4);                             \
             *reinterpret_cast<u32x4*>(ldsV + dv_off(st_row + 16 * i, st_chunk)) =                               \
                 pt ? *reinterpret_cast<const u32x4*>(lds_new + D + st_chunk * 8) : VR[i];                       \
         }                                                                                                       \
     }
     KV_WRITE(kreg, vreg, ksc, vsc, 0)
-    KV_ISSUE(kreg, vreg, ksc, vsc, 2)
+    KV_ISSUE(kreg, vreg, ksc, vsc, NSET)
 
     f32x4 o[8];
 #pragma unroll
@@ -549,20 +586,37 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
         }
     };
     // LDS holds tile t; set B carries tile t + 1 and set A tile t + 2 (two tiles in flight while a tile
-    // is scored); unrolled by two so every register array is indexed statically.
-    for (int t = 0; t < ntiles; t += 2) {
+    // is scored; NSET 4: sets B, C, D, A tiles t + 1 .. t + 4); unrolled by NSET so every register array is
+    // indexed statically.
+    for (int t = 0; t < ntiles; t += NSET) {
         compute(t);
         __syncthreads();
         if (t + 1 < ntiles) {
             KV_WRITE(kreg2, vreg2, ksc2, vsc2, t + 1)
-            KV_ISSUE(kreg2, vreg2, ksc2, vsc2, t + 3)
+            KV_ISSUE(kreg2, vreg2, ksc2, vsc2, t + 1 + NSET)
             __syncthreads();
             compute(t + 1);
             __syncthreads();
         }
-        if (t + 2 < ntiles) {
-            KV_WRITE(kreg, vreg, ksc, vsc, t + 2)
-            KV_ISSUE(kreg, vreg, ksc, vsc, t + 4)
+        if constexpr (NSET == 4) {
+            if (t + 2 < ntiles) {
+                KV_WRITE(kreg3, vreg3, ksc3, vsc3, t + 2)
+                KV_ISSUE(kreg3, vreg3, ksc3, vsc3, t + 6)
+                __syncthreads();
+                compute(t + 2);
+                __syncthreads();
+            }
+            if (t + 3 < ntiles) {
+                KV_WRITE(kreg4, vreg4, ksc4, vsc4, t + 3)
+                KV_ISSUE(kreg4, vreg4, ksc4, vsc4, t + 7)
+                __syncthreads();
+                compute(t + 3);
+                __syncthreads();
+            }
+        }
+        if (t + NSET < ntiles) {
+            KV_WRITE(kreg, vreg, ksc, vsc, t + NSET)
+            KV_ISSUE(kreg, vreg, ksc, vsc, t + 2 * NSET)
             __syncthreads();
         }
     }
@@ -609,6 +663,8 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
 // B=39 x 8 kv heads 7.02-7.05 vs 7.18-7.26 ms with the default policy; B <= 10 0.7-1 % slower with nt
 // (profiles/r1_decode_nt_ab.jsonl)
 constexpr int NT_MIN_GROUPS = 64;
+// grids up to this many workgroups run the four-register-set variant (NSET 4, one workgroup per CU)
+constexpr int DEEP_MAX_WGS = 256;
 
 static bool decode_packed(int G) { return G == 1 || G == 2 || G == 4 || G == 8 || G == 16; }
 
@@ -624,7 +680,8 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
                        int B, int Hq, int Hkv, int D, int P, int S, float scale, const RopeArgs* rope, int* counters,
                        int kv8, hipStream_t s) {
     if (B <= 0) return 0;
-    if (D != 128 || P != 64 || Hkv <= 0 || Hq % Hkv || Hq / Hkv > 64 || S < 1 || S > MAX_SPLITS)
+    if (D != 128 || P != 64 || Hkv <= 0 || Hq % Hkv || Hq / Hkv > 64 || S < 1 || S > MAX_SPLITS ||
+        (kv8 != 0 && kv8 != 2 && kv8 != 3))
         return (int)hipErrorInvalidValue;
     const int Hc = Hkv;                          // kv heads of the cache
     const int gq = decode_packed(Hq / Hc) ? 1 : Hq / Hc;
@@ -635,15 +692,23 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
     auto Qp = (const bf16*)q; auto K = (bf16*)kcache; auto V = (bf16*)vcache;
     auto PO = (float*)part_o; auto PM = (float*)part_ml;
     const RopeArgs ra = rope ? *rope : RopeArgs{nullptr, 0, 0, 0, 0, nullptr};
+    // four K/V register sets in flight when the grid is at most one workgroup per CU
+    const bool deep = (long)S * Hkv * B <= DEEP_MAX_WGS;
 #define MFMA_K(G_, R_, NT_, K8_)                                                                                \
-    attn_decode_mfma_kernel<G_, R_, NT_, K8_><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride,  \
+    attn_decode_mfma_kernel<G_, R_, NT_, K8_, 2><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride,  \
                                                                      positions, PO, PM, Hkv, S, sl, ra, counters, \
                                                                      (bf16*)out, out_stride, Hc, gq)
+#define MFMA_DEEP(G_, R_)                                                                                     \
+    attn_decode_mfma_kernel<G_, R_, false, 0, 4><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables,       \
+                                                                         bt_stride, positions, PO, PM, Hkv, S, sl, \
+                                                                         ra, counters, (bf16*)out, out_stride, Hc, gq)
 #define MFMA_L(G_, R_)                                                                                        \
     do {                                                                                                      \
         const bool nt_ = B * Hkv >= NT_MIN_GROUPS;                                                            \
-        if (kv8) { if (nt_) MFMA_K(G_, R_, true, true); else MFMA_K(G_, R_, false, true); }                   \
-        else { if (nt_) MFMA_K(G_, R_, true, false); else MFMA_K(G_, R_, false, false); }                     \
+        if (deep && !nt_ && kv8 == 0) { MFMA_DEEP(G_, R_); break; }                                           \
+        if (kv8 == 3) { if (nt_) MFMA_K(G_, R_, true, 3); else MFMA_K(G_, R_, false, 3); }                    \
+        else if (kv8 == 2) { if (nt_) MFMA_K(G_, R_, true, 2); else MFMA_K(G_, R_, false, 2); }               \
+        else { if (nt_) MFMA_K(G_, R_, true, 0); else MFMA_K(G_, R_, false, 0); }                             \
     } while (0)
 #define MFMA_G(R_)                            \
     switch (G) {                              \
@@ -658,6 +723,7 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
 #undef MFMA_G
 #undef MFMA_L
 #undef MFMA_K
+#undef MFMA_DEEP
     int e = (int)hipGetLastError();
     if (e || counters) return e;
     if (S > 16) {

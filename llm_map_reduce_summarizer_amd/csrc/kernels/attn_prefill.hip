@@ -45,6 +45,8 @@
 // PAGED + KV8 (fp8 KV cache, kv8.h): a 64-key tile is one (page, head) slab of e4m3 rows + row scales;
 // each thread loads one 16-B chunk (16 dims) of one row of K and of V plus the two row scales, and the
 // store converts them exactly to bf16 into the same LDS image (the rest of the kernel is unchanged).
+// KVM is a bitmask (bit 0: the K cache is fp8 slabs, bit 1: the V cache is); KVM 2 ("fp8v") stages K as
+// bf16 rows and V as fp8 slab rows, each into its half of the tile.
 //
 // Numerics: bf16 inputs, fp32 accumulation and softmax, bf16 output.
 #include "kv8.h"
@@ -94,7 +96,7 @@ struct PagedKV {
 // Other GQA ratios (e.g. Llama-3.2-3B: 24 / 8 = 3) run the G = 1 instantiation over Hg = Hq "virtual kv
 // heads", one per query head, each reading the K/V columns of its real kv head h / gq (gq = Hq / Hkv):
 // no K/V reuse across the group inside a workgroup, but any ratio works.  Hg = Hkv and gq = 1 otherwise.
-template <bool PAGED, int G, bool KV8 = false>
+template <bool PAGED, int G, int KVM = 0>
 __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __restrict__ qkv, int row_stride,
                                                               const int* __restrict__ cu_seqlens,
                                                               const int2* __restrict__ items,
@@ -152,19 +154,31 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
     // made hipcc serialise the loop on vmcnt(0).
     const int st_chunk = tid & 15, st_row0 = tid >> 4;
     u32x4 kreg[SIT], vreg[SIT];
-    // KV8: row tid / 8 (0..63) of the slab, 16-B chunk tid % 8; one round per tile
+    // fp8 slab staging: row tid / 8 (0..63) of the slab, 16-B chunk tid % 8; one round per tile
     const int r8 = tid >> 3, c8 = tid & 7;
     float ks8 = 1.f, vs8 = 1.f;
-    static_assert(!KV8 || NTHR / 8 == BN, "KV8 staging: one slab row per 8 threads");
+    constexpr bool K8 = (KVM & 1) != 0, V8 = (KVM & 2) != 0;
+    static_assert(KVM == 0 || NTHR / 8 == BN, "fp8 slab staging: one slab row per 8 threads");
 #define LOAD_TILE(t)                                                                              \
-    if constexpr (PAGED && KV8) {                                                                 \
+    if constexpr (PAGED && KVM != 0) {                                                            \
         const size_t sb = kv8::slab_off(btab[t], Hkv, kvh);                                       \
-        const unsigned char* kb_ = reinterpret_cast<const unsigned char*>(pk.kc) + sb;           \
-        const unsigned char* vb_ = reinterpret_cast<const unsigned char*>(pk.vc) + sb;           \
-        kreg[0] = *reinterpret_cast<const u32x4*>(kb_ + r8 * D + 16 * c8);                        \
-        vreg[0] = *reinterpret_cast<const u32x4*>(vb_ + r8 * D + 16 * c8);                        \
-        ks8 = *reinterpret_cast<const float*>(kb_ + BN * D + 4 * r8);                             \
-        vs8 = *reinterpret_cast<const float*>(vb_ + BN * D + 4 * r8);                             \
+        const size_t pg = (size_t)btab[t] * Hkv * BN * D + head_pg + st_chunk * 8;                \
+        if constexpr (K8) {                                                                       \
+            const unsigned char* kb_ = reinterpret_cast<const unsigned char*>(pk.kc) + sb;       \
+            kreg[0] = *reinterpret_cast<const u32x4*>(kb_ + r8 * D + 16 * c8);                    \
+            ks8 = *reinterpret_cast<const float*>(kb_ + BN * D + 4 * r8);                         \
+        } else {                                                                                  \
+            _Pragma("unroll") for (int i = 0; i < SIT; ++i)                                         \
+                kreg[i] = *reinterpret_cast<const u32x4*>(pk.kc + pg + (size_t)(st_row0 + SROWS * i) * D); \
+        }                                                                                         \
+        if constexpr (V8) {                                                                       \
+            const unsigned char* vb_ = reinterpret_cast<const unsigned char*>(pk.vc) + sb;       \
+            vreg[0] = *reinterpret_cast<const u32x4*>(vb_ + r8 * D + 16 * c8);                    \
+            vs8 = *reinterpret_cast<const float*>(vb_ + BN * D + 4 * r8);                         \
+        } else {                                                                                  \
+            _Pragma("unroll") for (int i = 0; i < SIT; ++i)                                         \
+                vreg[i] = *reinterpret_cast<const u32x4*>(pk.vc + pg + (size_t)(st_row0 + SROWS * i) * D); \
+        }                                                                                         \
     } else if constexpr (PAGED) {                                                                 \
         const size_t pg = (size_t)btab[t] * Hkv * BN * D + head_pg + st_chunk * 8;                \
         _Pragma("unroll") for (int i = 0; i < SIT; ++i) {                                           \
@@ -180,14 +194,24 @@ __global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __res
         }                                                                                         \
     }
 #define STORE_TILE(st)                                                                            \
-    if constexpr (KV8) {                                                                          \
+    if constexpr (KVM != 0) {                                                                     \
         u32x4 lo_, hi_;                                                                           \
-        kv8::dequant16(kreg[0], ks8, lo_, hi_);                                                   \
-        *reinterpret_cast<u32x4*>(lds + (st) + k_off(r8, 2 * c8)) = lo_;                          \
-        *reinterpret_cast<u32x4*>(lds + (st) + k_off(r8, 2 * c8 + 1)) = hi_;                      \
-        kv8::dequant16(vreg[0], vs8, lo_, hi_);                                                   \
-        *reinterpret_cast<u32x4*>(lds + (st) + BN * 256 + v_off(r8, 2 * c8)) = lo_;               \
-        *reinterpret_cast<u32x4*>(lds + (st) + BN * 256 + v_off(r8, 2 * c8 + 1)) = hi_;           \
+        if constexpr (K8) {                                                                       \
+            kv8::dequant16(kreg[0], ks8, lo_, hi_);                                               \
+            *reinterpret_cast<u32x4*>(lds + (st) + k_off(r8, 2 * c8)) = lo_;                      \
+            *reinterpret_cast<u32x4*>(lds + (st) + k_off(r8, 2 * c8 + 1)) = hi_;                  \
+        } else {                                                                                  \
+            _Pragma("unroll") for (int i = 0; i < SIT; ++i)                                         \
+                *reinterpret_cast<u32x4*>(lds + (st) + k_off(st_row0 + SROWS * i, st_chunk)) = kreg[i]; \
+        }                                                                                         \
+        if constexpr (V8) {                                                                       \
+            kv8::dequant16(vreg[0], vs8, lo_, hi_);                                               \
+            *reinterpret_cast<u32x4*>(lds + (st) + BN * 256 + v_off(r8, 2 * c8)) = lo_;           \
+            *reinterpret_cast<u32x4*>(lds + (st) + BN * 256 + v_off(r8, 2 * c8 + 1)) = hi_;       \
+        } else {                                                                                  \
+            _Pragma("unroll") for (int i = 0; i < SIT; ++i)                                         \
+                *reinterpret_cast<u32x4*>(lds + (st) + BN * 256 + v_off(st_row0 + SROWS * i, st_chunk)) = vreg[i]; \
+        }                                                                                         \
     } else                                                                                        \
     _Pragma("unroll") for (int i = 0; i < SIT; ++i) {                                               \
         const int row = st_row0 + SROWS * i;                                                         \
@@ -365,13 +389,17 @@ static void launch_g(dim3 grid, hipStream_t s, const bf16* Q, int row_stride, co
     // kv-head-major order from 8 blocks per CU up (measured crossover: 4096 blocks neutral, 19656 kv-major)
     const int kv_major = grid.x > 8 * 256;
     if constexpr (PAGED) {
-        if (kv8) {
-            attn_prefill_kernel<PAGED, G, true><<<grid, NTHR, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq, Hkv,
-                                                                      Hg, gq, sl, p, kv_major);
+        if (kv8 == 3 || kv8 == 2) {
+            if (kv8 == 3)
+                attn_prefill_kernel<PAGED, G, 3><<<grid, NTHR, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq,
+                                                                       Hkv, Hg, gq, sl, p, kv_major);
+            else
+                attn_prefill_kernel<PAGED, G, 2><<<grid, NTHR, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq,
+                                                                       Hkv, Hg, gq, sl, p, kv_major);
             return;
         }
     }
-    attn_prefill_kernel<PAGED, G, false><<<grid, NTHR, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq, Hkv, Hg,
+    attn_prefill_kernel<PAGED, G, 0><<<grid, NTHR, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq, Hkv, Hg,
                                                                    gq, sl, p, kv_major);
 }
 
@@ -425,7 +453,8 @@ MRSUM_API int mrsum_attn_prefill_paged(const void* qkv, int row_stride, const in
                                        int n_items, int block_m, void* out, int out_stride, int Hq, int Hkv, int Dh,
                                        float scale, const void* kcache, const void* vcache, const int* block_tables,
                                        int bt_stride, const int* seq_slot, const int* prefix, int kv8, hipStream_t s) {
-    if (!kcache || !vcache || !block_tables || !seq_slot || !prefix) return (int)hipErrorInvalidValue;
+    if (!kcache || !vcache || !block_tables || !seq_slot || !prefix || (kv8 != 0 && kv8 != 2 && kv8 != 3))
+        return (int)hipErrorInvalidValue;  // an fp8 K with a bf16 V cache is not a layout the engine makes
     const PagedKV pk{(const bf16*)kcache, (const bf16*)vcache, block_tables, bt_stride, seq_slot, prefix};
     return launch_prefill(qkv, row_stride, cu_seqlens, items, n_items, block_m, out, out_stride, Hq, Hkv, Dh, scale,
                           &pk, kv8, s);

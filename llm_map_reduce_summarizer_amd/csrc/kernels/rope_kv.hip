@@ -20,7 +20,9 @@
 // row r of a (page, head) slab is D OCP e4m3fn bytes at r * D, its fp32 scale at P * D + 4 r.  A
 // row is quantised as a whole (rotated K, raw V): scale = the power of two >= max|x| / 448 (the
 // 8 lanes of the row reduce the max with xor shuffles), q = e4m3(x / scale).  Power-of-two scales
-// make the decode-side dequantisation (cvt_scalef32 to bf16) exact.
+// make the decode-side dequantisation (cvt_scalef32 to bf16) exact.  KVM is a bitmask: bit 0 = the K
+// cache is fp8 slabs, bit 1 = the V cache is (KVM 2, "fp8v": bf16 K, fp8 V -- K rounding is what peaked
+// attention amplifies, profiles/r4_fp8_kv_emulation.txt).
 #include "kv8.h"
 
 // Source of one token row: the bf16 qkv row itself, or (PARTS) the sum of S
@@ -60,7 +62,7 @@ struct RowSrc {
     }
 };
 
-template <int D, bool PARTS, bool KV8>
+template <int D, bool PARTS, int KVM>
 __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ qkv_in, const float* __restrict__ parts,
                                                       int S, int T, bf16* __restrict__ qkv_out, int row_stride,
                                                       const int* __restrict__ positions,
@@ -113,7 +115,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
             bf16* hp = row + h * D;
             *reinterpret_cast<uint4*>(hp + c) = pa;
             *reinterpret_cast<uint4*>(hp + c + HALF) = pb;
-            if constexpr (KV8) {
+            if constexpr ((KVM & 1) != 0) {
                 if (h >= Hq) {  // head-uniform over the row's RI lanes: the shuffles stay inside the row
                     float f[16];
                     unpack8(pa, f);
@@ -145,7 +147,7 @@ __global__ __launch_bounds__(256) void rope_kv_kernel(const bf16* __restrict__ q
                     if (qkv_out != qkv_in) *reinterpret_cast<uint4*>(row + col + 8 * u) = v[u];
                 }
             }
-            if constexpr (KV8) {
+            if constexpr ((KVM & 2) != 0) {
                 float f[16];
                 unpack8(v[0], f);
                 unpack8(v[1], f + 8);
@@ -165,26 +167,25 @@ static int launch_rope(const void* qkv_in, const void* parts, int S, void* qkv_o
                        void* kcache, void* vcache, const void* cos_sin, int Hq, int Hkv, int D, int P,
                        int write_cache, int kv8, hipStream_t s) {
     if (T <= 0) return 0;
-    if (kv8 && D != 128) return (int)hipErrorInvalidValue;
+    if (kv8 < 0 || kv8 > 3 || (kv8 && D != 128)) return (int)hipErrorInvalidValue;
     const int items = (Hq + 2 * Hkv) * (D / 16);
     dim3 g(T, ceil_div(items, 256)), b(256);
     auto QI = (const bf16*)qkv_in; auto PA = (const float*)parts; auto QO = (bf16*)qkv_out;
     auto K = (bf16*)kcache; auto V = (bf16*)vcache; auto CS = (const float2*)cos_sin;
-    if (kv8)
-        rope_kv_kernel<128, PARTS, true><<<g, b, 0, s>>>(QI, PA, S, T, QO, row_stride, positions, seq_idx,
-                                                         block_tables, bt_stride, K, V, CS, Hq, Hkv, P, write_cache);
-    else if (D == 128)
-        rope_kv_kernel<128, PARTS, false><<<g, b, 0, s>>>(QI, PA, S, T, QO, row_stride, positions, seq_idx,
-                                                          block_tables, bt_stride, K, V, CS, Hq, Hkv, P, write_cache);
-    else if (D == 64)
-        rope_kv_kernel<64, PARTS, false><<<g, b, 0, s>>>(QI, PA, S, T, QO, row_stride, positions, seq_idx,
-                                                         block_tables, bt_stride, K, V, CS, Hq, Hkv, P, write_cache);
+#define RK(D_, M_) rope_kv_kernel<D_, PARTS, M_><<<g, b, 0, s>>>(QI, PA, S, T, QO, row_stride, positions, seq_idx, \
+                                                                  block_tables, bt_stride, K, V, CS, Hq, Hkv, P, write_cache)
+    if (kv8 == 3) RK(128, 3);
+    else if (kv8 == 2) RK(128, 2);
+    else if (kv8 == 1) RK(128, 1);
+    else if (D == 128) RK(128, 0);
+    else if (D == 64) RK(64, 0);
     else
         return (int)hipErrorInvalidValue;
+#undef RK
     return (int)hipGetLastError();
 }
 
-// kv8: the cache is the fp8 byte-slab layout (kv8.h), else bf16 [pages, Hkv, P, D]
+// kv8: bit 0 the K cache, bit 1 the V cache is the fp8 byte-slab layout (kv8.h), else bf16 [pages, Hkv, P, D]
 MRSUM_API int mrsum_rope_kv(void* qkv, int T, int row_stride, const int* positions, const int* seq_idx,
                             const int* block_tables, int bt_stride, void* kcache, void* vcache,
                             const void* cos_sin, int Hq, int Hkv, int D, int P, int write_cache, int kv8,

@@ -9,6 +9,10 @@ scratch page: idle decode slots point at it, real sequences never do.
 SLAB = P * hd + 4 * P -- the P rows of e4m3fn bytes then the P fp32 row scales
 of one (page, kv head) (csrc/kernels/kv8.h): 8.25 KiB instead of 16 KiB, so a
 decode step streams half the KV bytes and the cache holds ~1.94x the tokens.
+``kv_dtype="fp8v"``: only ``v`` is fp8 slabs, ``k`` stays bf16 -- the scores'
+K rounding is what peaked attention amplifies (a CPU emulation on the parity
+checkpoint: K+V fp8 20 % logit error, V only 6 %, profiles/r4_fp8_kv_emulation.txt),
+so this keeps 3/4 of the bf16 bytes at a third of the full variant's error.
 
 Allocation is whole-sequence: a request reserves ceil((prompt + max_new) / P)
 pages at admission, so a captured decode graph can run many steps without
@@ -92,40 +96,46 @@ class PageAllocator:
             self._h = None
 
 
+KV_DTYPES = ("bf16", "fp8", "fp8v")
+
+
 class PagedKVCache:
     def __init__(self, n_layers: int, num_pages: int, n_kv_heads: int, page: int, head_dim: int,
                  dtype: torch.dtype, device: torch.device, kv_dtype: str = "bf16"):
         if num_pages < 2:
             raise ValueError("need at least 2 KV pages (page 0 is scratch)")
-        if kv_dtype not in ("bf16", "fp8"):
-            raise ValueError("kv_dtype must be bf16 or fp8")
-        if kv_dtype == "fp8" and (page, head_dim) != (64, 128):
+        if kv_dtype not in KV_DTYPES:
+            raise ValueError("kv_dtype must be one of %s" % (KV_DTYPES,))
+        if kv_dtype != "bf16" and (page, head_dim) != (64, 128):
             raise ValueError("the fp8 KV cache needs page 64 and head dim 128")
         self.page = page
         self.num_pages = num_pages
         self.kv_dtype = kv_dtype
-        shape = (n_layers, num_pages, n_kv_heads, page, head_dim)
-        if kv_dtype == "fp8":
-            from ..ops.reference import kv8_slab
-            shape, dtype = (n_layers, num_pages, n_kv_heads, kv8_slab(page, head_dim)), torch.uint8
+        shape16, dt16 = (n_layers, num_pages, n_kv_heads, page, head_dim), dtype
+        from ..ops.reference import kv8_slab
+        shape8 = (n_layers, num_pages, n_kv_heads, kv8_slab(page, head_dim)) if kv_dtype != "bf16" else None
+        kshape, kdt = (shape8, torch.uint8) if kv_dtype == "fp8" else (shape16, dt16)
+        vshape, vdt = (shape8, torch.uint8) if kv_dtype in ("fp8", "fp8v") else (shape16, dt16)
         # zeroed, not empty: attention kernels read whole pages and mask the scores of rows past a
         # sequence's end (p = 0), and 0 x a stale NaN bit pattern in such a V row would still be NaN
-        self.k = torch.zeros(shape, dtype=dtype, device=device)
-        self.v = torch.zeros(shape, dtype=dtype, device=device)
+        self.k = torch.zeros(kshape, dtype=kdt, device=device)
+        self.v = torch.zeros(vshape, dtype=vdt, device=device)
         self.alloc = PageAllocator(num_pages)
         log.info("KV cache: %d pages x %d tokens (%.1f GiB)", num_pages, page,
-                 2 * self.k.numel() * self.k.element_size() / 2 ** 30)
+                 (self.k.numel() * self.k.element_size() + self.v.numel() * self.v.element_size()) / 2 ** 30)
 
     def pages_for(self, n_tokens: int) -> int:
         return -(-n_tokens // self.page)
 
     @property
     def fp8(self) -> bool:
-        return self.kv_dtype == "fp8"
+        """Any fp8 slab cache (K and V, or V only)."""
+        return self.kv_dtype != "bf16"
 
     @staticmethod
     def size_pages(bytes_budget: int, n_layers: int, n_kv_heads: int, page: int, head_dim: int,
                    dtype_bytes: int = 2, kv_dtype: str = "bf16") -> int:
-        per_head = page * head_dim * dtype_bytes if kv_dtype != "fp8" else page * head_dim + 4 * page
-        per_page = 2 * n_layers * n_kv_heads * per_head
+        bf, f8 = page * head_dim * dtype_bytes, page * head_dim + 4 * page
+        per_head = {"bf16": 2 * bf, "fp8": 2 * f8, "fp8v": bf + f8}[kv_dtype]
+        per_page = n_layers * n_kv_heads * per_head
         return max(2, bytes_budget // per_page)

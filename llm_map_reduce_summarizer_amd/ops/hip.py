@@ -30,6 +30,7 @@ _SIGS = {
                             _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_swiglu": [_vp, _vp, _c_int, _c_int, _vp],
     "mrsum_kv_scatter": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp],
+    "mrsum_kv_prefetch": [_vp, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp],
     "mrsum_embed": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _vp],
     "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_attn_prefill_paged": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float,
@@ -172,18 +173,23 @@ KV8_SLAB = KV8_PAGE * KV8_D + 4 * KV8_PAGE  # csrc/kernels/kv8.h: e4m3 rows then
 
 
 def _cache_kind(kcache: torch.Tensor, vcache: torch.Tensor, hkv: int, page: int, d: int, what: str) -> int:
-    """1 for the fp8 byte-slab cache [pages, hkv, KV8_SLAB] uint8 (kv8.h), 0 for bf16 [pages, hkv, page, d];
-    validates shape / dtype / contiguity either way."""
+    """The kernels' cache-format bitmask: bit 0 = the K cache, bit 1 = the V cache is the fp8 byte-slab layout
+    [pages, hkv, KV8_SLAB] uint8 (kv8.h), else bf16 [pages, hkv, page, d] -- 0 (bf16), 3 (fp8) or 2 (fp8v:
+    bf16 K, fp8 V); validates shape / dtype / contiguity of both (an fp8 K with a bf16 V is refused)."""
     _req(kcache is not None and vcache is not None and kcache.is_cuda and vcache.is_cuda
-         and kcache.is_contiguous() and vcache.is_contiguous() and kcache.shape == vcache.shape
-         and kcache.dtype == vcache.dtype, "%s: K / V caches must be matching contiguous CUDA tensors" % what)
-    if kcache.dtype == torch.uint8:
-        _req(page == KV8_PAGE and d == KV8_D and tuple(kcache.shape[1:]) == (hkv, KV8_SLAB),
-             "%s: fp8 cache must be uint8 [pages, Hkv, %d] (page 64, head dim 128)" % (what, KV8_SLAB))
-        return 1
-    _req(kcache.dtype == torch.bfloat16 and tuple(kcache.shape[1:]) == (hkv, page, d),
-         "%s: cache must be bf16 [pages, Hkv, P, D] (or the fp8 slab layout)" % what)
-    return 0
+         and kcache.is_contiguous() and vcache.is_contiguous() and kcache.shape[0] == vcache.shape[0],
+         "%s: K / V caches must be contiguous CUDA tensors with the same pages" % what)
+    kind = 0
+    for bit, c in ((1, kcache), (2, vcache)):
+        if c.dtype == torch.uint8:
+            _req(page == KV8_PAGE and d == KV8_D and tuple(c.shape[1:]) == (hkv, KV8_SLAB),
+                 "%s: fp8 cache must be uint8 [pages, Hkv, %d] (page 64, head dim 128)" % (what, KV8_SLAB))
+            kind |= bit
+        else:
+            _req(c.dtype == torch.bfloat16 and tuple(c.shape[1:]) == (hkv, page, d),
+                 "%s: cache must be bf16 [pages, Hkv, P, D] (or the fp8 slab layout)" % what)
+    _req(kind != 1, "%s: an fp8 K cache needs an fp8 V cache (formats: bf16, fp8, fp8v)" % what)
+    return kind
 
 
 # ------------------------------------------------------------------ rope + kv
@@ -251,6 +257,28 @@ def kv_scatter(rows: torch.Tensor, page: torch.Tensor, slot: torch.Tensor, kcach
     _req(page.numel() >= n and slot.numel() >= n, "kv_scatter: index")
     _check(_fn("mrsum_kv_scatter")(_p(rows), n, kcache.shape[1], kcache.shape[3], _p(page), _p(slot), _p(kcache),
                                    _p(vcache), kcache.shape[2], _stream()), "kv_scatter")
+
+
+def kv_prefetch(kcache: torch.Tensor, vcache: torch.Tensor, block_tables: torch.Tensor, positions: torch.Tensor,
+                B: int, wps: int = 64, sink: Optional[torch.Tensor] = None) -> None:
+    """Load every cached page of the first B sequences of ONE layer's K / V cache (bf16 or fp8 slabs, any mix)
+    once with the default cache policy, so the decode attention that follows reads them from the Infinity
+    Cache (csrc/kernels/kv_prefetch.hip).  Pages [0, ceil((positions[b] + 1) / 64)) of block-table row b; wps
+    workgroups per sequence.  ``sink`` (test hook): uint32 [>= B * wps * 256] receiving a fold of the bytes."""
+    _req(kcache.is_cuda and vcache.is_cuda and kcache.is_contiguous() and vcache.is_contiguous()
+         and kcache.shape[0] == vcache.shape[0], "kv_prefetch: caches")
+    _i32(block_tables, positions)
+    _req(block_tables.dim() == 2 and block_tables.shape[0] >= B and positions.numel() >= B and B >= 1 and wps >= 1,
+         "kv_prefetch: tables")
+    page = KV8_PAGE if kcache.dtype == torch.uint8 else kcache.shape[2]
+    kpb = kcache[0].numel() * kcache.element_size()
+    vpb = vcache[0].numel() * vcache.element_size()
+    _req(kpb % 16 == 0 and vpb % 16 == 0, "kv_prefetch: page bytes")
+    if sink is not None:
+        _req(sink.is_cuda and sink.dtype == torch.int32 and sink.numel() >= B * wps * 256, "kv_prefetch: sink")
+    _check(_fn("mrsum_kv_prefetch")(_p(kcache), _p(vcache), _p(block_tables), block_tables.stride(0), _p(positions),
+                                    B, page, kpb, vpb, wps, _p(sink), 1 if sink is not None else 0, _stream()),
+           "kv_prefetch")
 
 
 # ------------------------------------------------------------------ activations
@@ -377,11 +405,12 @@ ATTN_SLOTS = 768  # resident decode-attention workgroups (3 per CU, 162 VGPRs; 5
 KV8_SPLIT_GROUPS = 96
 
 
-def decode_attn_plan(batch: int, hkv: int, max_ctx: int, kv8: bool = False):
-    """(splits, fused) of decode_attn_plan_bf16; with ``kv8`` (fp8 KV cache) the measured split multiplier
-    (at most one page per split; a fused merge keeps its 16-split cap)."""
+def decode_attn_plan(batch: int, hkv: int, max_ctx: int, kv8=False):
+    """(splits, fused) of decode_attn_plan_bf16; with ``kv8`` True / "fp8" (fp8 K and V cache) the measured
+    split multiplier (at most one page per split; a fused merge keeps its 16-split cap).  "fp8v" (bf16 K,
+    fp8 V: 3/4 of the bf16 bytes per page) keeps the bf16 plan."""
     s, fused = decode_attn_plan_bf16(batch, hkv, max_ctx)
-    if kv8:
+    if kv8 is True or kv8 == "fp8":
         mult = 2.0 if batch * hkv <= KV8_SPLIT_GROUPS else 1.0
         pages = max(1, -(-max_ctx // 64))
         s = max(1, min(int(round(s * mult)), pages, 64, 16 if fused else 64))

@@ -12,7 +12,7 @@ Layouts shared with the kernels (``csrc/kernels/*.hip``):
   token at position ``p`` of a sequence lives in page
   ``block_tables[row, p // P]`` at offset ``p % P``.
 * ``cos_sin`` [max_pos, D/2, 2] fp32 (cos, sin), HF rotate-half pairing.
-* fp8 KV cache (``--kv-dtype fp8``, csrc/kernels/kv8.h): per layer uint8 [num_pages, Hkv, SLAB],
+* fp8 KV cache (``--kv-dtype fp8``: K and V; ``fp8v``: V only, K stays bf16; csrc/kernels/kv8.h): per layer uint8 [num_pages, Hkv, SLAB],
   SLAB = P * D + 4 * P -- a (page, head) slab holds P rows of D e4m3fn bytes, then P fp32 row scales;
   a row is quantised whole with the power-of-two scale >= max|x| / 448.
 """
@@ -157,7 +157,7 @@ def rope_kv_parts(parts: torch.Tensor, positions, seq_idx, block_tables, kcache,
 def kv_scatter(rows: torch.Tensor, page: torch.Tensor, slot: torch.Tensor, kcache: torch.Tensor,
                vcache: torch.Tensor) -> None:
     """Reference of ops.hip.kv_scatter: cache[page[i], :, slot[i], :] = rows[i, 0 | 1] (page < 0 skipped)."""
-    if kcache.dtype == torch.uint8:
+    if kcache.dtype == torch.uint8 or vcache.dtype == torch.uint8:
         raise ValueError("kv_scatter: the context-parallel K/V exchange takes bf16 caches only")
     keep = page[: rows.shape[0]].long() >= 0
     pg, sl, r = page[: rows.shape[0]].long()[keep], slot[: rows.shape[0]].long()[keep], rows[keep]

@@ -372,9 +372,11 @@ def test_fp8_kv_cache_cpu():
     b = PagedKVCache.size_pages(1 << 30, 32, 8, 64, 128)
     f = PagedKVCache.size_pages(1 << 30, 32, 8, 64, 128, kv_dtype="fp8")
     assert 1.9 < f / b < 2.0
+    fv = PagedKVCache.size_pages(1 << 30, 32, 8, 64, 128, kv_dtype="fp8v")
+    assert 1.3 < fv / b < 1.35  # bf16 K + fp8 V: 24.25 of 32 KiB per (page, head)
     prompts = [[128000] + [(i * 37 + j * 11) % 120000 + 5 for j in range(n)] for i, n in enumerate((300, 129))]
     rec = {}
-    for kvd in ("bf16", "fp8"):
+    for kvd in ("bf16", "fp8", "fp8v"):
         e = LLMEngine(get_model_config("tiny-gqa4", init_std=0.05), device="cpu", max_model_len=1024,
                       max_num_seqs=4, kv_pages=32, kv_dtype=kvd, prefill_chunk=128)
         r = []
@@ -384,3 +386,8 @@ def test_fp8_kv_cache_cpu():
         rec[kvd] = r[-1]
     a, b = rec["bf16"], rec["fp8"]
     assert float((a - b).norm() / a.norm()) < 0.15
+    e = LLMEngine(get_model_config("tiny-gqa4", init_std=0.05), device="cpu", max_model_len=1024,
+                  max_num_seqs=4, kv_pages=32, kv_dtype="fp8v", prefill_chunk=128)
+    assert e.kv.k.dtype == torch.bfloat16 and e.kv.v.dtype == torch.uint8 and e.kv.fp8
+    # V-only rounding: closer to bf16 KV than the K+V variant
+    assert float((a - rec["fp8v"]).norm() / a.norm()) <= float((a - b).norm() / a.norm()) + 1e-6

@@ -109,7 +109,8 @@ def test_attn_prefill(hq, hkv, seqlens):
 
 
 @pytest.mark.parametrize("parts", [False, True])
-def test_rope_kv_fp8_cache(parts):
+@pytest.mark.parametrize("fmt", ["fp8", "fp8v"])
+def test_rope_kv_fp8_cache(parts, fmt):
     """rope_kv / rope_kv_parts writing the fp8 slab cache (kv8.h: e4m3 rows + power-of-two row scales) ==
     the reference quantiser on the same rotated rows; rows of padding tokens (seq_idx < 0) are not written."""
     hq, hkv, d, page, T = 8, 2, 128, 64, 150
@@ -120,6 +121,9 @@ def test_rope_kv_fp8_cache(parts):
     sidx = torch.tensor([0] * 100 + [1] * 49 + [-1], dtype=torch.int32, device=DEV)
     c0 = torch.zeros(48, hkv, reference.kv8_slab(page, d), dtype=torch.uint8, device=DEV)
     k1, v1, k2, v2 = c0.clone(), c0.clone(), c0.clone(), c0.clone()
+    if fmt == "fp8v":  # bf16 K cache beside the fp8 V slabs
+        k1 = torch.zeros(48, hkv, page, d, dtype=torch.bfloat16, device=DEV)
+        k2 = k1.clone()
     if parts:
         pr = (torch.randn(3, T, (hq + 2 * hkv) * d, generator=g) * 0.7).to(DEV)
         q1 = hip.rope_kv_parts(pr, pos, sidx, bt, k1, v1, cs, hq, hkv, d, page)
@@ -130,9 +134,12 @@ def test_rope_kv_fp8_cache(parts):
         hip.rope_kv(q1, pos, sidx, bt, k1, v1, cs, hq, hkv, d, page)
         reference.rope_kv(q2, pos, sidx, bt, k2, v2, cs, hq, hkv, d, page)
     _close(q1, q2, 2e-2)
-    _kv8_close(k1, k2, page, d)
+    if fmt == "fp8":
+        _kv8_close(k1, k2, page, d)
+    else:
+        _close(k1, k2, 2e-2)
     _kv8_close(v1, v2, page, d)
-    assert int(k1[0].sum()) == 0  # page 0 (scratch) untouched
+    assert float(k1[0].float().abs().sum()) == 0 and int(v1[0].sum()) == 0  # page 0 (scratch) untouched
 
 
 def test_rope_kv_fp8_cache_tiny_rows():
@@ -165,7 +172,7 @@ def test_rope_kv_fp8_cache_tiny_rows():
 
 @pytest.mark.parametrize("hq,hkv", [(4, 1), (8, 2), (8, 1), (2, 2), (6, 2)])
 @pytest.mark.parametrize("spans", [[(0, 200)], [(130, 300), (0, 77), (1000, 1129)], [(64, 128), (2047, 2048)]])
-@pytest.mark.parametrize("kv8", [False, True])
+@pytest.mark.parametrize("kv8", ["bf16", "fp8", "fp8v"])
 def test_attn_prefill_paged(hq, hkv, spans, kv8):
     """Chunked-prefill attention: slice rows attend to [0, prefix + slice) of their sequence read from the
     paged cache (random non-contiguous pages, stale rows past the slice end), vs the fp32 reference."""
@@ -175,8 +182,7 @@ def test_attn_prefill_paged(hq, hkv, spans, kv8):
     n_pages, maxp = 160, 40
     kc = (torch.randn(n_pages, hkv, page, d, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
     vc = torch.randn(n_pages, hkv, page, d, generator=g).to(torch.bfloat16).to(DEV)
-    if kv8:
-        kc, vc = reference.kv8_from_bf16(kc.cpu()).to(DEV), reference.kv8_from_bf16(vc.cpu()).to(DEV)
+    kc, vc = _kv_format(kc, vc, kv8)
     nseq = len(spans)
     perm = torch.randperm(n_pages - 1, generator=g)[: nseq * maxp] + 1
     bt = perm.view(nseq, maxp).to(torch.int32).to(DEV)
@@ -213,7 +219,7 @@ def test_attn_prefill_spike(hq):
 @pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (4, 4), (16, 1), (6, 2), (24, 8), (10, 2)])
 @pytest.mark.parametrize("splits", [1, 3, 16, 48])
 @pytest.mark.parametrize("fused", [False, True])
-@pytest.mark.parametrize("kv8", [False, True])
+@pytest.mark.parametrize("kv8", ["bf16", "fp8", "fp8v"])
 def test_attn_decode(hq, hkv, splits, fused, kv8):
     d, page = 128, 64
     ctxs = [1, 65, 700, 129, 64, 1000]
@@ -222,8 +228,7 @@ def test_attn_decode(hq, hkv, splits, fused, kv8):
     g = torch.Generator().manual_seed(13)
     kc = (torch.randn(n_pages, hkv, page, d, generator=g)).to(torch.bfloat16).to(DEV)
     vc = (torch.randn(n_pages, hkv, page, d, generator=g)).to(torch.bfloat16).to(DEV)
-    if kv8:  # the fp8 slab cache (kv8.h); the reference dequantises the same bytes
-        kc, vc = reference.kv8_from_bf16(kc.cpu()).to(DEV), reference.kv8_from_bf16(vc.cpu()).to(DEV)
+    kc, vc = _kv_format(kc, vc, kv8)  # fp8 slab caches (kv8.h); the reference dequantises the same bytes
     perm = torch.randperm(n_pages - 1, generator=g) + 1
     bt = torch.zeros(B, 20, dtype=torch.int32)
     used = 0
@@ -520,7 +525,7 @@ def test_fp8_swiglu_and_quant():
 
 @pytest.mark.parametrize("hq,hkv,S", [(32, 8, 4), (4, 1, 1), (16, 1, 3), (8, 2, 2), (4, 1, 16), (6, 2, 2), (24, 8, 4)])
 @pytest.mark.parametrize("fused_combine", [False, True])
-@pytest.mark.parametrize("kv8", [False, True])
+@pytest.mark.parametrize("kv8", ["bf16", "fp8", "fp8v"])
 def test_attn_decode_rope_fused(hq, hkv, S, fused_combine, kv8):
     """attn_decode_rope (q/k RoPE + new K/V written into the cache + attention, from the QKV GEMM's
     fp32 split-K slabs) == reference rope_kv_parts followed by reference attention."""
@@ -545,8 +550,7 @@ def test_attn_decode_rope_fused(hq, hkv, S, fused_combine, kv8):
     cs = reference.rope_cos_sin(2048, d, 500000.0, DEV)
     sc = 1.0 / math.sqrt(d)
     sidx = torch.arange(B, dtype=torch.int32, device=DEV)
-    if kv8:
-        kc0, vc0 = reference.kv8_from_bf16(kc0), reference.kv8_from_bf16(vc0)
+    kc0, vc0 = _kv_format(kc0, vc0, kv8)
     k2, v2 = kc0.clone().to(DEV), vc0.clone().to(DEV)
     qkv = reference.rope_kv_parts(parts, pos, sidx, bt, k2, v2, cs, hq, hkv, d, page)
     o2 = reference.attn_decode(qkv, k2, v2, bt, pos, hq, hkv, d, page, sc)
@@ -556,20 +560,30 @@ def test_attn_decode_rope_fused(hq, hkv, S, fused_combine, kv8):
     ws.part_o.fill_(float("nan"))  # poisoned workspace: empty splits must publish zero slabs
     for _ in range(3):  # idempotent: later calls rewrite the same K/V row (and re-armed merge tickets)
         o1 = hip.attn_decode_rope(parts, cs, k1, v1, bt, pos, hq, hkv, d, page, sc, workspace=ws)
-        if kv8:  # the kernel rotates the fp32 slab sums, the reference their bf16 rounding: an element of the
-            # new row on an e4m3 rounding boundary may land one step apart, so compare in relative L2
+        if kv8 != "bf16":  # the kernel rotates the fp32 slab sums, the reference their bf16 rounding: an element
+            # of the new row on an e4m3 rounding boundary may land one step apart, so compare in relative L2
             a, b = o1.float().cpu(), o2.float().cpu()
             assert float((a - b).norm() / b.norm()) < 2e-2
         else:
             _close(o1, o2, 2e-2)
     if fused_combine:
         assert int(ws.counters.abs().sum()) == 0
-    if kv8:
-        _kv8_close(k1, k2, page, d)
-        _kv8_close(v1, v2, page, d)
-    else:
-        _close(k1, k2, 3e-2)
-        _close(v1, v2, 3e-2)
+    for c1, c2 in ((k1, k2), (v1, v2)):
+        if c1.dtype == torch.uint8:
+            _kv8_close(c1, c2, page, d)
+        else:
+            _close(c1, c2, 3e-2)
+
+
+def _kv_format(kc, vc, fmt):
+    """bf16 caches [pages, hkv, P, d] in the engine's format ``fmt``: bf16, fp8 (K and V slabs) or fp8v (V
+    slabs, K bf16); same device as the inputs."""
+    dev = kc.device
+    if fmt == "fp8":
+        kc = reference.kv8_from_bf16(kc.cpu()).to(dev)
+    if fmt in ("fp8", "fp8v"):
+        vc = reference.kv8_from_bf16(vc.cpu()).to(dev)
+    return kc, vc
 
 
 def _kv8_close(c1, c2, page, d):

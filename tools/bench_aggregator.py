@@ -25,7 +25,7 @@ def main():
     ap.add_argument("--max-new-tokens", type=int, default=1000)
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"],
+    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8v", "fp8"],
                     help="KV-cache format; fp8 is a labelled variant (bf16 KV is the credited number)")
     a = ap.parse_args()
     import torch

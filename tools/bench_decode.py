@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--batches", default="1,5,10,39")
     ap.add_argument("--ctx", type=int, default=4000)
     ap.add_argument("--new", type=int, default=256)
-    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8v", "fp8"])
     ap.add_argument("--tp-shard", type=int, default=1,
                     help="run ONE rank's shard shapes of TP=K (heads, ffn and vocab / K) on this GPU with no "
                          "all-reduce: the compute + launch floor of a TP=K decode step")
