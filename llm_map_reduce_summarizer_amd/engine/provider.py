@@ -302,11 +302,15 @@ class LocalEngineProvider(Provider):
             if ar is None or self.parallel != "auto":
                 self.hw = plan.with_measurements(hw, tp_ok=ar is not None)
                 return self.hw
-            lat, per_row = ar.measure_latency(rows=(1, 64), hidden=eng.cfg.hidden)
+            m = eng.model
+            # the cross-GPU cost of the decode's own all-reduce: the TP push of the down projection's shard
+            lat, per_row = ar.measure_latency(rows=(1, 64), hidden=eng.cfg.hidden, push_k=m.ffn_local,
+                                              fp8=m.weight_dtype == "fp8")
             bw = _rccl_bandwidth(eng.model.tp_group, eng.cfg.hidden, torch.device(self._device))
             self.hw = plan.with_measurements(hw, ar_lat_s=lat, ar_lat_row_s=per_row, ar_bw=bw, tp_ok=True)
-            log.info("planner constants: all-reduce %.1f us + %.3f us/row (fused, over the local add_rmsnorm), "
-                     "RCCL all-reduce %.1f GB/s", lat * 1e6, per_row * 1e6, bw / 1e9)
+            log.info("planner constants: all-reduce %.1f us + %.3f us/row (%s path, over the same kernel on a "
+                     "group of one), RCCL all-reduce %.1f GB/s", lat * 1e6, per_row * 1e6,
+                     getattr(ar, "latency_path", "fused"), bw / 1e9)
         return self.hw
 
     def _fixed_degree(self, stage: str) -> int:

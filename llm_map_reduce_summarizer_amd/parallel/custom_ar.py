@@ -414,22 +414,39 @@ class CustomAllReduce:
             ok &= check()
         return ok
 
-    def measure_latency(self, rows=(1, 64), hidden: int = 4096, calls: int = 64, reps: int = 3):
-        """(a, b): a fused all-reduce + add_rmsnorm call over this group costs a + b * rows seconds MORE
-        than the same kernel over a group of one rank (LocalPush: the push to its own slot, the wait and
-        the rank-ordered sum, which a TP-shard decode step measured on one GPU already contains) -- the
-        cross-GPU part of a decode all-reduce, the TP push of the GEMM epilogues included (the same
-        remote stores and polls).  Least squares over ``rows``; both timed inside replayed hipGraphs.
-        MAX over the ranks, so every rank plans with the same numbers."""
+    def measure_latency(self, rows=(1, 64), hidden: int = 4096, calls: int = 64, reps: int = 3,
+                        push_k: Optional[int] = None, fp8: bool = False):
+        """(a, b): a decode all-reduce over this group costs a + b * rows seconds MORE than the same kernel
+        over a group of one rank (LocalPush: the push to its own slot, the wait and the rank-ordered sum, which
+        a TP-shard decode step measured on one GPU already contains) -- the cross-GPU part of a decode
+        all-reduce.  Timed on the path the decode runs: with ``push_k`` (the shard K of a row-parallel
+        projection) and a passing push producer, the TP-push residual producer at N = ``hidden``, K = push_k
+        (stream kernel, the plan's launch parameters); else the fused all-reduce + add_rmsnorm.  Least squares
+        over ``rows``; timed inside replayed hipGraphs; MAX over the ranks, so every rank plans with the same
+        numbers."""
+        from ..ops import hip
+        from ..ops.reference import Fp8Weight
         dev = torch.device("cuda", torch.cuda.current_device())
         local = LocalPush(self.max_bytes)
         pts = []
+        use_push = push_k is not None and self.paths["push_stream"]
         for r in rows:
-            r = max(1, min(int(r), self.max_bytes // (hidden * 2), self.MAX_ROWS))
+            r = max(1, min(int(r), self.max_bytes // (hidden * 4), self.MAX_ROWS, 64 if use_push else self.MAX_ROWS))
             parts = torch.zeros(1, r, hidden, device=dev)
             res = torch.zeros(r, hidden, dtype=torch.bfloat16, device=dev)
             w = torch.ones(hidden, dtype=torch.bfloat16, device=dev)
             out = torch.empty_like(res)
+            rp = _push_case(self, "stream", r, hidden, int(push_k), fp8) if use_push else None
+            if rp is not None:
+                x = torch.zeros(r, int(push_k), dtype=torch.bfloat16, device=dev)
+                wm = torch.zeros(hidden, int(push_k), dtype=torch.bfloat16, device=dev)
+                wm = Fp8Weight.quantize(wm) if fp8 else wm
+
+                def fn_of(h):
+                    return lambda: hip.stream_resid(x, wm, res, rp[1], rp[2], tp=h.push_handle())
+            else:
+                def fn_of(h):
+                    return lambda: h.add_rmsnorm(parts, res, w, 1e-5, out)
 
             def timed(fn) -> float:
                 s = torch.cuda.Stream(device=dev)
@@ -454,10 +471,11 @@ class CustomAllReduce:
                     best = min(best, e0.elapsed_time(e1) / 1000.0 / calls)
                 return best
 
-            t_ar = timed(lambda: self.add_rmsnorm(parts, res, w, 1e-5, out))
-            t_local = timed(lambda: local.add_rmsnorm(parts, res, w, 1e-5, out))
+            t_ar = timed(fn_of(self))
+            t_local = timed(fn_of(local))
             pts.append((r, max(0.0, t_ar - t_local)))
         local.close()
+        self.reset()  # the timed pushes advanced the epochs of this handle and of nothing else: start clean
         n = len(pts)
         mx = sum(p[0] for p in pts) / n
         my = sum(p[1] for p in pts) / n
@@ -466,6 +484,7 @@ class CustomAllReduce:
         a = max(0.0, my - b * mx)
         v = torch.tensor([a, b], dtype=torch.float64, device=dev if dist.get_backend(self.group) == "nccl" else "cpu")
         dist.all_reduce(v, op=dist.ReduceOp.MAX, group=self.group)
+        self.latency_path = "push" if use_push else "fused"
         return float(v[0].item()), float(v[1].item())
 
     def error(self) -> int:

@@ -97,6 +97,11 @@ def main():
     lat, per_row = ar.measure_latency(rows=(1, 64), hidden=4096)
     print("rank %d fused all-reduce cost over local add_rmsnorm: %.2f us + %.4f us/row (2 ranks sharing one GPU)"
           % (rank, lat * 1e6, per_row * 1e6), flush=True)
+    # the planner's measurement on the path the decode runs: the TP push of a down-projection shard
+    lat, per_row = ar.measure_latency(rows=(1, 64), hidden=4096, push_k=1792)
+    assert ar.latency_path == "push" and ar.error() == 0
+    print("rank %d TP-push cost over a group of one: %.2f us + %.4f us/row" % (rank, lat * 1e6, per_row * 1e6),
+          flush=True)
     assert ar.error() == 0
     dist.barrier()
     ar.close()

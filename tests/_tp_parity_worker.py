@@ -176,4 +176,10 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except BaseException:  # the launcher's report keeps only the tail of 8 ranks' stderr: say it on stdout
+        import traceback
+        print("RANKFAIL rank %s: %s" % (os.environ.get("RANK"), traceback.format_exc().replace("\n", " | ")),
+              flush=True)
+        raise

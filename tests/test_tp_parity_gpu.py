@@ -33,6 +33,7 @@ def test_tp_paths_match_fp32(world, model, wdtype):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", str(world), "--master-addr",
            "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "tests", "_tp_parity_worker.py")]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=850)
-    assert r.returncode == 0, r.stdout[-4000:] + r.stderr[-4000:]
+    fails = [ln for ln in r.stdout.splitlines() if ln.startswith("RANKFAIL")]
+    assert r.returncode == 0, "\n".join(fails)[:6000] + r.stdout[-2000:] + r.stderr[-2000:]
     assert r.stdout.count("tp parity ok") == world, r.stdout[-2000:]
     print([ln for ln in r.stdout.splitlines() if "parity:" in ln])
