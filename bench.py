@@ -100,9 +100,9 @@ def main() -> int:
                     help="single-pass reduce over every summary (use a long-context model, e.g. llama3.1-8b)")
     ap.add_argument("--stream-reduce", action="store_true",
                     help="start each level-1 reduce batch as soon as its chunks are summarised (no map barrier)")
-    ap.add_argument("--kv-dtype", choices=["bf16", "fp8v", "fp8"], default="bf16",
-                    help="KV cache format; fp8v (V rows e4m3 with power-of-two row scales, K bf16) and fp8 (K and V "
-                         "e4m3) are LABELLED variants: the headline is bf16 KV")
+    ap.add_argument("--kv-dtype", choices=["bf16", "fp8v"], default="bf16",
+                    help="KV cache format; fp8v (V rows e4m3 with power-of-two row scales, K bf16) is a LABELLED "
+                         "variant: the headline is bf16 KV")
     ap.add_argument("--profile", default=None, metavar="DIR", help="torch.profiler trace of the timed steps")
     ap.add_argument("--log-level", default="WARNING")
     args = ap.parse_args()

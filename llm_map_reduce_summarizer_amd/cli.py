@@ -76,10 +76,10 @@ def build_parser() -> argparse.ArgumentParser:
     e.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (ranks per model replica)")
     e.add_argument("--seed", type=int, default=None)
     e.add_argument("--kv-fraction", type=float, default=None, help="fraction of free HBM for the KV cache")
-    e.add_argument("--kv-dtype", choices=["bf16", "fp8v", "fp8"], default=None,
+    e.add_argument("--kv-dtype", choices=["bf16", "fp8v"], default=None,
                    help="KV cache format: bf16 (default, $ENGINE_KV_DTYPE); fp8v = V rows as OCP e4m3fn with "
-                        "power-of-two row scales, K bf16 (3/4 of the KV bytes per decode step); fp8 = K and V rows "
-                        "e4m3fn (half the bytes, ~3x fp8v's logit error); fp8 formats: no context-parallel prefill")
+                        "power-of-two row scales, K bf16 (3/4 of the KV bytes per decode step, 8 %% logit error on "
+                        "the parity checkpoint; no context-parallel prefill)")
     e.add_argument("--no-graphs", action="store_true", help="disable hipGraph capture of decode steps")
     e.add_argument("--max-model-len", type=int, default=None,
                    help="context budget per request (default: 32k for llama3-*, the model window for llama3.1-*); "

@@ -248,7 +248,6 @@ class LLMEngine:
         # decode slot until their last slice has run, so no decode step can touch their pages)
         self.pf_tables = torch.zeros(self.max_num_seqs, self.max_pages, dtype=torch.int32, device=self.device)
         self.interleave = os.environ.get("MRSUM_INTERLEAVE", "1") == "1"
-        self._pf_stream = None  # side stream of the K/V prefetch (_prefetch_plan)
         # test hook (SURVEY §5.3 fault injection): "rank:seconds" -- TP rank ``rank`` sleeps on the host
         # before its first decode window, so its peers' P2P all-reduce waits time out (recovery test)
         spec = os.environ.get("MRSUM_FAULT_AR_DELAY", "")
@@ -401,35 +400,11 @@ class LLMEngine:
         else:
             ops.sample(logits, st_view)
 
-    # K/V prefetch into the Infinity Cache beside the decode chain (model.run_layers, csrc/kernels/
-    # kv_prefetch.hip): for batches whose K/V per layer stays well inside the 256 MiB cache with the weights
-    # streamed in between.  MRSUM_KV_PREFETCH: "off", "qkv" (fork at the layer's QKV GEMM) or "down" (fork at
-    # the previous layer's down projection); MRSUM_KV_PREFETCH_WPS: workgroups per sequence.
-    KV_PREFETCH_BUDGET = 96 << 20
-
-    def _prefetch_plan(self, B: int):
-        mode = os.environ.get("MRSUM_KV_PREFETCH", "off")
-        if mode == "off" or self.device.type != "cuda":
-            return None
-        from ..ops.hip import CTX_CLASSES
-        ctx = min(CTX_CLASSES[self._ctx_cls], self.max_model_len)
-        per_tok = (self.kv.k[0][0].numel() * self.kv.k.element_size()
-                   + self.kv.v[0][0].numel() * self.kv.v.element_size()) / self.page
-        if B * ctx * per_tok > self.KV_PREFETCH_BUDGET:
-            return None
-        if self._pf_stream is None:
-            self._pf_stream = torch.cuda.Stream(self.device)
-        return {"stream": self._pf_stream, "wps": int(os.environ.get("MRSUM_KV_PREFETCH_WPS", "64")), "lead": mode}
-
     def _decode_once(self, B: int) -> None:
         st = self.state
-        self.model.kv_prefetch = self._prefetch_plan(B)
-        try:
-            logits = self.model.decode(st.next_ids[:B], st.positions[:B], st.seq_idx[:B], st.block_tables[:B],
-                                       self.kv.k, self.kv.v, workspace=self._workspace(B),
-                                       gather=not self.model.tp_sampling)
-        finally:
-            self.model.kv_prefetch = None
+        logits = self.model.decode(st.next_ids[:B], st.positions[:B], st.seq_idx[:B], st.block_tables[:B],
+                                   self.kv.k, self.kv.v, workspace=self._workspace(B),
+                                   gather=not self.model.tp_sampling)
         self._sample(logits, st.view(0, B))
 
     def _decode_steps(self, B: int, steps: int) -> None:

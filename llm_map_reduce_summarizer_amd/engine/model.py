@@ -186,9 +186,6 @@ class LlamaModel:
                                     scaling=cfg.rope_scaling)
         self.vocab_offset = tp_rank * self.vocab_local
         self.emulate_tp_reduce = False  # LocalReduce in place of the TP all-reduce (shard measurements)
-        # small-batch decode: {"stream", "wps", "lead"} -- each layer's K/V prefetched into the Infinity Cache on
-        # a side stream beside the chain (run_layers; set per captured graph by the engine), None = off
-        self.kv_prefetch = None
         self._local_push = None
         # TP prefill with sequence parallelism (prefill_passes; MRSUM_SP=0: all-reduces)
         self.sequence_parallel = os.environ.get("MRSUM_SP", "1") == "1"
@@ -396,38 +393,14 @@ class LlamaModel:
         page = _page_of(kcache, self.hd)
         ar = _TPReduce(self) if self.tp_size > 1 else (LocalReduce(self) if self.emulate_tp_reduce else None)
         last = len(self.layers) - 1
-        pf = self.kv_prefetch if decode and ids.is_cuda else None
-        joins = {}
         for i, lw in enumerate(self.layers):
-            if pf is not None and i not in joins:
-                joins[i] = self._prefetch_kv(i, kcache, vcache, block_tables, positions, ids.shape[0])
             qkv = ops.qkv_rope(x, lw.wqkv, positions, seq_idx, block_tables, kcache[i], vcache[i], self.cos_sin,
                                self.hq, self.hkv, self.hd, page, defer=decode)
-            if i in joins:
-                torch.cuda.current_stream().wait_stream(joins.pop(i))
             a = attention(i, qkv)
             x = ops.proj_add_rmsnorm(a, lw.wo, residual, None, c.rms_eps, "o", ar, quant=q8)
-            if pf is not None and pf.get("lead") == "down" and i < last:
-                # start the next layer's K/V prefetch beside this layer's down projection and the next QKV
-                act = ops.gate_up_swiglu(x, lw.wgu)
-                joins[i + 1] = self._prefetch_kv(i + 1, kcache, vcache, block_tables, positions, ids.shape[0])
-                x = ops.proj_add_rmsnorm(act, lw.wdown, residual, None, c.rms_eps, "down", ar, quant=False)
-                continue
             x = ops.mlp(x, lw.wgu, lw.wdown, residual, c.rms_eps, ar,
                         quant=q8qkv if i < last else False)  # the last one feeds the bf16 LM head
         return x
-
-    def _prefetch_kv(self, i: int, kcache, vcache, block_tables, positions, B: int):
-        """Fork: layer i's K/V pages into the Infinity Cache on the side stream (ops.hip.kv_prefetch),
-        concurrent with the main stream's next kernels; returns the stream to join before layer i's
-        attention.  Legal inside a hipGraph capture (the fork / join become graph edges)."""
-        from ..ops import hip
-        main = torch.cuda.current_stream()
-        side = self.kv_prefetch["stream"]
-        side.wait_stream(main)
-        with torch.cuda.stream(side):
-            hip.kv_prefetch(kcache[i], vcache[i], block_tables, positions, B, wps=self.kv_prefetch["wps"])
-        return side
 
     def logits(self, x: torch.Tensor, gather: bool = True) -> torch.Tensor:
         # decode rows: the LDS-DMA weight-ring stream GEMM (the 1 GB head read once); more rows: the

@@ -144,8 +144,10 @@ class LocalEngineProvider(Provider):
         if kv_fraction is not None:
             self._engine_options.setdefault("kv_fraction", kv_fraction)
         kv_dtype = kv_dtype or self.config.ENGINE_KV_DTYPE
-        if kv_dtype not in ("bf16", "fp8", "fp8v"):
-            raise ValueError("kv_dtype must be bf16, fp8 or fp8v, got %s" % kv_dtype)
+        if kv_dtype not in ("bf16", "fp8v"):
+            # fp8 K + V (the engine's "fp8" format) is not offered: 13-22 % logit error on the parity checkpoint
+            # (tests/test_forward_parity_gpu.py), above the 0.15 a variant must meet; fp8v is 8 %
+            raise ValueError("kv_dtype must be bf16 or fp8v, got %s" % kv_dtype)
         self._engine_options.setdefault("kv_dtype", kv_dtype)
         if max_num_seqs is not None:
             self._engine_options.setdefault("max_num_seqs", max_num_seqs)

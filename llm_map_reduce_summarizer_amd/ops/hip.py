@@ -30,7 +30,6 @@ _SIGS = {
                             _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_swiglu": [_vp, _vp, _c_int, _c_int, _vp],
     "mrsum_kv_scatter": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp],
-    "mrsum_kv_prefetch": [_vp, _vp, _vp, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_int, _vp, _c_int, _vp],
     "mrsum_embed": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _vp],
     "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_attn_prefill_paged": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float,
@@ -257,28 +256,6 @@ def kv_scatter(rows: torch.Tensor, page: torch.Tensor, slot: torch.Tensor, kcach
     _req(page.numel() >= n and slot.numel() >= n, "kv_scatter: index")
     _check(_fn("mrsum_kv_scatter")(_p(rows), n, kcache.shape[1], kcache.shape[3], _p(page), _p(slot), _p(kcache),
                                    _p(vcache), kcache.shape[2], _stream()), "kv_scatter")
-
-
-def kv_prefetch(kcache: torch.Tensor, vcache: torch.Tensor, block_tables: torch.Tensor, positions: torch.Tensor,
-                B: int, wps: int = 64, sink: Optional[torch.Tensor] = None) -> None:
-    """Load every cached page of the first B sequences of ONE layer's K / V cache (bf16 or fp8 slabs, any mix)
-    once with the default cache policy, so the decode attention that follows reads them from the Infinity
-    Cache (csrc/kernels/kv_prefetch.hip).  Pages [0, ceil((positions[b] + 1) / 64)) of block-table row b; wps
-    workgroups per sequence.  ``sink`` (test hook): uint32 [>= B * wps * 256] receiving a fold of the bytes."""
-    _req(kcache.is_cuda and vcache.is_cuda and kcache.is_contiguous() and vcache.is_contiguous()
-         and kcache.shape[0] == vcache.shape[0], "kv_prefetch: caches")
-    _i32(block_tables, positions)
-    _req(block_tables.dim() == 2 and block_tables.shape[0] >= B and positions.numel() >= B and B >= 1 and wps >= 1,
-         "kv_prefetch: tables")
-    page = KV8_PAGE if kcache.dtype == torch.uint8 else kcache.shape[2]
-    kpb = kcache[0].numel() * kcache.element_size()
-    vpb = vcache[0].numel() * vcache.element_size()
-    _req(kpb % 16 == 0 and vpb % 16 == 0, "kv_prefetch: page bytes")
-    if sink is not None:
-        _req(sink.is_cuda and sink.dtype == torch.int32 and sink.numel() >= B * wps * 256, "kv_prefetch: sink")
-    _check(_fn("mrsum_kv_prefetch")(_p(kcache), _p(vcache), _p(block_tables), block_tables.stride(0), _p(positions),
-                                    B, page, kpb, vpb, wps, _p(sink), 1 if sink is not None else 0, _stream()),
-           "kv_prefetch")
 
 
 # ------------------------------------------------------------------ activations

@@ -200,16 +200,25 @@ class CustomAllReduce:
         H, rows = int(sh["hidden"]), tuple(int(r) for r in sh["rows"])
         local = {}
 
+        self.why = {}
+
         def run(name, fn):
             try:
-                local[name] = bool(fn()) and self.error() == 0
+                ok = bool(fn())
+                if not ok:
+                    self.why[name] = "mismatch against the reference"
             except Exception as e:  # keep the collective sequence aligned across ranks
                 log.warning("custom all-reduce self-test of %s raised: %s", name, e)
-                local[name] = False
-            if self.error():
-                # a timed-out wait poisons the handle's later calls: clear it (collective) before the next path
-                local[name] = False
+                ok = False
+                self.why[name] = "raised: %s" % (str(e)[:200],)
+            # a timed-out wait (sticky error word, on the waiting rank only) poisons the handle's later
+            # calls: the group agrees on it and clears the P2P state together before the next path
+            err_any, _ = self.agree_error()
+            if err_any:
+                ok = False
+                self.why.setdefault(name, "a wait for a peer timed out (error word %d)" % err_any)
                 self.reset()
+            local[name] = ok
 
         run("one_shot", lambda: self._test_one_shot(dev, H, rows, iters))
         run("fused_norm", lambda: self._test_fused(dev, iters, rows, H))
@@ -242,6 +251,12 @@ class CustomAllReduce:
                        else "n/a" for p in self.PATHS}
         self.report["shapes"] = "hidden %d, shard K %s, rows %s%s" % (H, dict(sh["k"]), list(rows),
                                                                      ", fp8" if sh["fp8"] else "")
+        why = [None] * self.world
+        dist.all_gather_object(why, self.why, group=self.group)
+        reasons = {p: sorted({w[p] for w in why if w and p in w}) for p in self.PATHS if not self.paths[p]}
+        if reasons:
+            self.report["why"] = {p: "; ".join(r) for p, r in reasons.items()}
+            log.warning("custom all-reduce self-test: paths off: %s", self.report["why"])
         # the test's tagged words sit at offsets that later belong to other granules / rows: start the real
         # traffic from zeroed slots and epoch 1 on every rank, whatever the test's iteration count
         self.reset()
@@ -389,13 +404,21 @@ class CustomAllReduce:
             dist.all_reduce(tot, group=self.group)
             ref_res = res0.clone()
             ref_out = reference.add_rmsnorm(tot, ref_res, w, 1e-5)
-            good = torch.allclose(res.float(), ref_res.float(), atol=3e-2, rtol=2e-2)
-            good &= torch.allclose(out.float(), ref_out.float(), atol=6e-2, rtol=3e-2)
+            g1 = bool(torch.allclose(res.float(), ref_res.float(), atol=3e-2, rtol=2e-2))
+            g2 = bool(torch.allclose(out.float(), ref_out.float(), atol=6e-2, rtol=3e-2))
             mine = res.float().sum().reshape(1)
             hi, lo = mine.clone(), mine.clone()
             dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)
             dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=self.group)
-            return bool(good) and bool(torch.equal(hi, lo))
+            g3 = bool(torch.equal(hi, lo))
+            if not (g1 and g2 and g3):
+                self.why.setdefault("fused_norm", "T=%d D=%d: residual %s (max err %.3g), out %s (max err %.3g), "
+                                    "ranks %s" % (T, D, "ok" if g1 else "MISMATCH",
+                                                  float((res.float() - ref_res.float()).abs().max()),
+                                                  "ok" if g2 else "MISMATCH",
+                                                  float((out.float() - ref_out.float()).abs().max()),
+                                                  "agree" if g3 else "DISAGREE"))
+            return g1 and g2 and g3
 
         for i in range(iters):
             fill(i)

@@ -107,6 +107,7 @@ def main():
                    max_model_len=4096, kv_pages=256, tp_rank=rank, tp_size=world, tp_group=None, weight_dtype=wdt)
     assert tp.model.custom_ar is not None and tp.model.tp_sampling and tp.model.sequence_parallel
     rep = tp.model.custom_ar.selftest_report()
+    print("rank %d p2p self-test: %s" % (rank, rep), flush=True)
     assert all(rep[p] in ("ok", "n/a") for p in tp.model.custom_ar.PATHS), rep  # self-test at these shapes
     ref_ckpt, tol, min_exact = ckpt, P.BF16_TOL, 0.9
     if fp8:

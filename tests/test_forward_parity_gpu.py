@@ -247,12 +247,14 @@ def test_llama3_8b_dims_fp8_parity(monkeypatch):
 # over dequantised K/V (the 1300-token prompt makes every prefill pass chunked, through the cache), and the
 # peaked attention of this checkpoint (score std ~6) amplifies the K error like it amplifies fp8 activations
 # (single-term: 24 %): measured 13-22 % on prompts with history, 3.8 % on the one-token prompt, top-1 20/20
-# (profiles/r4_gpu_tests_fp8kv_twoterm.txt).  The bf16-KV headline is unaffected; fp8 KV is a labelled variant.
+# (profiles/r4_gpu_tests_fp8kv_twoterm.txt, r5_parity_bf16_fp8_fp8kv_fp8v.txt).  Above the 0.15 a KV variant
+# must meet, so the CLI / bench offer only fp8v (V fp8, K bf16: 7.95 %) below.
 FP8_KV_TOL = 0.25
 
 
 def test_llama3_8b_dims_fp8_kv_parity(monkeypatch):
-    """--kv-dtype fp8: packed + chunked prefill (slices attend to their prefix through the fp8 cache) and
+    """kv_dtype="fp8" (K and V fp8; an engine format the CLI does not offer, see FP8_KV_TOL): packed + chunked
+    prefill (slices attend to their prefix through the fp8 cache) and
     decode over the fp8 cache, vs the textbook fp32 forward (bf16 weights)."""
     cfg = get_model_config("llama3-8b", n_layers=2)
     ckpt = _checkpoint(cfg, 7)

@@ -11,8 +11,9 @@ Variants (comma separated, ``plan`` = unchanged):
   deferM                       the TP=1 deferred RMSNorm up to M rows (ops.DEFER_NORM_MAX_M)
   fp8resid:N:K:WPB:S           the fp8 deferred-norm producer (stream_fp8, residual epilogue) of one shape
   buckets:B1+B2+...            decode graph buckets up to the largest given (the rest unchanged)
-  env:NAME=VALUE[+NAME=VALUE]  environment overrides read at call time (e.g. env:MRSUM_RESID_SKINNY_O=1,
-                               env:MRSUM_TP_PUSH=0)
+  resid:ROLE=KIND              the deferred-norm / TP-push producer of ROLE (o | down) forced to KIND
+                               (skinny | stream): ops.RESID_FORCE
+  env:NAME=VALUE[+NAME=VALUE]  environment overrides read at call time (e.g. env:MRSUM_TP_PUSH=0)
 
     python tools/exp_plans_insitu.py --tp-shard 8 --batch 1 --variants plan,attnfused32,gate_up:stream_split:4:4
 """
@@ -70,6 +71,7 @@ def main():
             else:
                 os.environ[name] = old
         env_set.clear()
+        ops.RESID_FORCE.clear()
         import llm_map_reduce_summarizer_amd.engine.engine as engine_mod
         engine_mod.BUCKETS = base_buckets
         if v == "plan":
@@ -77,6 +79,10 @@ def main():
         if v.startswith("buckets:"):  # buckets:1+2+4+8+10+16 -- the decode graph buckets below 24
             low = tuple(int(t) for t in v[len("buckets:"):].split("+"))
             engine_mod.BUCKETS = low + tuple(b for b in base_buckets if b > max(low))
+            return
+        if v.startswith("resid:"):
+            role, kind = v[len("resid:"):].split("=")
+            ops.RESID_FORCE[role] = kind
             return
         if v.startswith("env:"):
             for kv in v[4:].split("+"):

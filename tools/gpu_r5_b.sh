@@ -4,8 +4,6 @@
 set -o pipefail
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 300 python -u tools/exp_kv_prefetch.py --batch 1 --ctx 13500 > gpurun_out/r5_kv_prefetch_b1.jsonl 2>gpurun_out/r5_kv_prefetch_b1.err || exit $?
-timeout -k 10 300 python -u tools/exp_kv_prefetch.py --batch 5 --ctx 4400 --configs off,qkv:32,down:32 > gpurun_out/r5_kv_prefetch_b5.jsonl 2>gpurun_out/r5_kv_prefetch_b5.err || exit $?
 for kv in bf16 fp8v fp8; do
   timeout -k 10 300 python -u tools/bench_decode.py --batches 39,10 --ctx 4400 --new 200 --kv-dtype $kv >> gpurun_out/r5_decode_kvfmt.jsonl 2>>gpurun_out/r5_decode_kvfmt.err || exit $?
 done
