@@ -431,6 +431,11 @@ def decode_attn_plan_bf16(batch: int, hkv: int, max_ctx: int):
             # r3_plans_insitu_sc1.jsonl): B=1 64 separate 1.370 ms vs 32 fused 1.39, 16 fused 1.451;
             # B=10 25 separate 1.600 vs 24 fused 1.615, 16 fused 1.623
             return max(1, min(N_CU // groups, pages, 64)), False
+        if not fused and hkv <= 2:
+            # a TP shard's one or two kv heads beyond the 6k class (config 5's 32k final reduce at TP=8): as
+            # many splits as the merge takes -- 64 separate splits for the 70B fp8 TP=8 shard at B=1, 32k: 5.64
+            # ms per step vs 6.22 with the 32 of the TP=1 rule below (in situ, profiles/r5_attn_plans_deep.jsonl)
+            return max(1, min(splits, 64)), False
         if fused and batch == 1 and hkv >= 8 and pages > 32:
             # one sequence x 8 kv heads: 32 splits with the separate merge beat 16 fused in situ (whole decode
             # steps, 4k context: 3.47 vs 3.55 ms; profiles/r2_attn_plans_insitu_b1_b10.jsonl), as in the

@@ -206,7 +206,7 @@ class CustomAllReduce:
             try:
                 ok = bool(fn())
                 if not ok:
-                    self.why[name] = "mismatch against the reference"
+                    self.why.setdefault(name, "mismatch against the reference")
             except Exception as e:  # keep the collective sequence aligned across ranks
                 log.warning("custom all-reduce self-test of %s raised: %s", name, e)
                 ok = False
@@ -400,12 +400,24 @@ class CustomAllReduce:
             res.copy_(res0)
 
         def check():
-            tot = parts.sum(0)
-            dist.all_reduce(tot, group=self.group)
+            # the kernel's arithmetic exactly: each rank's slab sum rounded to the bf16 payload, summed in rank
+            # order in fp32, added to the residual with one bf16 rounding (an fp32 all-reduce as the reference
+            # leaves the payload rounding of `world` ranks in the error: 0.04 worst case at 8 ranks)
+            mine = parts.sum(0).to(torch.bfloat16)
+            allv = [torch.empty_like(mine) for _ in range(self.world)]
+            if dist.get_backend(self.group) == "nccl":
+                dist.all_gather(allv, mine, group=self.group)
+            else:
+                cpu = [torch.empty(mine.shape, dtype=mine.dtype) for _ in range(self.world)]
+                dist.all_gather(cpu, mine.cpu(), group=self.group)
+                allv = [c.to(dev) for c in cpu]
+            tot = torch.zeros(T, D, device=dev)
+            for v in allv:
+                tot += v.float()
             ref_res = res0.clone()
             ref_out = reference.add_rmsnorm(tot, ref_res, w, 1e-5)
-            g1 = bool(torch.allclose(res.float(), ref_res.float(), atol=3e-2, rtol=2e-2))
-            g2 = bool(torch.allclose(out.float(), ref_out.float(), atol=6e-2, rtol=3e-2))
+            g1 = bool(torch.allclose(res.float(), ref_res.float(), atol=1e-3, rtol=1e-2))
+            g2 = bool(torch.allclose(out.float(), ref_out.float(), atol=3e-2, rtol=2e-2))
             mine = res.float().sum().reshape(1)
             hi, lo = mine.clone(), mine.clone()
             dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=self.group)

@@ -55,5 +55,8 @@ def test_decode_attn_plan_class1_six_fused_splits():
     assert hip.decode_attn_plan(16, 8, 12288) == (6, True)
     # the final reduce (B=1, ~13k, <= 32k class) keeps 32 separate splits (best of 16-64 / fused in situ)
     assert hip.decode_attn_plan(1, 8, 32768) == (32, False)
+    # a TP shard's single kv head beyond 6k (config 5's 32k at TP=8): 64 separate splits, in situ
+    # (profiles/r5_attn_plans_deep.jsonl: 5.64 vs 6.22 ms per 70B fp8 shard step at 32 splits)
+    assert hip.decode_attn_plan(1, 1, 32768) == (64, False)
     # TP shards keep their measured cap of 4 in the longer classes
     assert hip.decode_attn_plan(20, 1, 12288)[0] <= 4
