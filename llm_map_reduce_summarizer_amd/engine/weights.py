@@ -63,6 +63,7 @@ def load_hf(model, path: str) -> None:
     v = model.vocab_local
     model.final_norm = put(get("model.norm.weight"))
     model.lm_head = put(fold_gain(lm[r * v:(r + 1) * v], model.final_norm))
+    model._quantize_lm_head()
     for i, lw in enumerate(model.layers):
         p = "model.layers.%d." % i
         lw.ln1 = put(get(p + "input_layernorm.weight"))
@@ -111,7 +112,7 @@ def save_hf(model, path: str) -> None:
     out: Dict[str, torch.Tensor] = {
         "model.embed_tokens.weight": model.embed,
         "model.norm.weight": model.final_norm,
-        "lm_head.weight": unfold_gain(model.lm_head, model.final_norm),
+        "lm_head.weight": unfold_gain(_dense(model.lm_head), model.final_norm),
     }
     for i, lw in enumerate(model.layers):
         p = "model.layers.%d." % i

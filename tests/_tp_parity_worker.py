@@ -46,11 +46,12 @@ def fp8_shard_reference(cfg, ckpt, world, dev):
     loader does), dequantised and put back in place."""
     hd, H, F = cfg.head_dim, cfg.hidden, cfg.ffn
     qs, ks, f = cfg.n_heads * hd // world, cfg.n_kv_heads * hd // world, F // world
-    ref = {"model.embed_tokens.weight": ckpt["model.embed_tokens.weight"],
-           "model.norm.weight": ckpt["model.norm.weight"], "lm_head.weight": ckpt["model.embed_tokens.weight"]}
-
     def dq(t):
         return Fp8Weight.quantize(t.to(dev, torch.bfloat16).contiguous()).dequant(torch.float32).cpu()
+
+    # the LM head is fp8 too (row scales: the vocab shards quantise exactly as the whole matrix does)
+    ref = {"model.embed_tokens.weight": ckpt["model.embed_tokens.weight"],
+           "model.norm.weight": ckpt["model.norm.weight"], "lm_head.weight": dq(ckpt["model.embed_tokens.weight"])}
 
     for i in range(cfg.n_layers):
         p = "model.layers.%d." % i

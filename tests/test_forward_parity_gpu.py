@@ -220,7 +220,7 @@ def test_llama3_8b_dims_fp8_parity(monkeypatch):
     hd, qs, ks = cfg.head_dim, cfg.n_heads * cfg.head_dim, cfg.n_kv_heads * cfg.head_dim
     ones = torch.ones(cfg.hidden, dtype=torch.bfloat16)
     ref = {"model.embed_tokens.weight": ckpt["model.embed_tokens.weight"], "model.norm.weight": ones,
-           "lm_head.weight": model.lm_head.float()}
+           "lm_head.weight": model.lm_head.dequant(torch.float32)}
     from llm_map_reduce_summarizer_amd.ops.reference import split_gate_up
     for i, lw in enumerate(model.layers):
         p = "model.layers.%d." % i
