@@ -24,7 +24,9 @@
 // shape is fixed and the kernel can live inside a captured decode graph.
 #include "kv8.h"
 
-constexpr int MAX_SPLITS = 64;
+// splits of one (sequence, kv head): up to 256 so a TP shard's single kv head at long contexts still fills the
+// chip (70B fp8 TP=8 shard at 32k: 64 splits = 64 workgroups left its 16.8 MB of K/V at ~1.1 TB/s)
+constexpr int MAX_SPLITS = 256;
 
 // partial-result store: agent-scope atomic (global_store sc1, write-through) when a last-arriving
 // workgroup of another XCD will read it in the same launch (combine_if_last<G, true>), else plain
@@ -74,23 +76,31 @@ __device__ __forceinline__ void combine_group(const float* part_o, const float* 
             pre[r][j] = (h < NH && sp < S) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
-    // 2. split weights: one wave per head, one lane per split (S <= MAX_SPLITS = 64)
+    // 2. split weights: one wave per head, lane l holds splits l, l + 64, l + 128, l + 192 (S <= MAX_SPLITS)
+    static_assert(MAX_SPLITS <= 4 * 64, "four splits per lane");
     for (int g = wv; g < G; g += 4) {
-        float ms = -INFINITY, ls = 0.f;
-        {
-            const int sl = min(lane, S - 1);
+        float ms[4], ls[4], mloc = -INFINITY;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int sp = lane + 64 * q;
+            const int sl = min(sp, S - 1);
             float2 v;
             if constexpr (SC1) v = ld_sc1_f2(rm, (g * S + sl) * 8);
             else v = reinterpret_cast<const float2*>(pm0)[g * S + sl];
-            if (lane < S) {
-                ms = v.x;
-                ls = v.y;
-            }
+            ms[q] = sp < S ? v.x : -INFINITY;
+            ls[q] = sp < S ? v.y : 0.f;
+            mloc = fmaxf(mloc, ms[q]);
         }
-        const float M = wave_max(ms);
-        const float w = ms == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms - M);
-        const float den = wave_sum(w * ls);
-        if (lane < S) sw[g * S + lane] = w;
+        const float M = wave_max(mloc);
+        float wl = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int sp = lane + 64 * q;
+            const float w = ms[q] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms[q] - M);
+            wl += w * ls[q];
+            if (sp < S) sw[g * S + sp] = w;
+        }
+        const float den = wave_sum(wl);
         if (lane == 0) sden[g] = den;
     }
     __syncthreads();
@@ -654,7 +664,7 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
                        int kv8, hipStream_t s) {
     if (B <= 0) return 0;
     if (D != 128 || P != 64 || Hkv <= 0 || Hq % Hkv || Hq / Hkv > 64 || S < 1 || S > MAX_SPLITS ||
-        (kv8 != 0 && kv8 != 2 && kv8 != 3))
+        (kv8 != 0 && kv8 != 2 && kv8 != 3) || (counters && !out))
         return (int)hipErrorInvalidValue;
     const int Hc = Hkv;                          // kv heads of the cache
     const int gq = decode_packed(Hq / Hc) ? 1 : Hq / Hc;
@@ -690,7 +700,7 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
 #undef MFMA_L
 #undef MFMA_K
     int e = (int)hipGetLastError();
-    if (e || counters) return e;
+    if (e || counters || !out) return e;  // no out: partials only, merged by the consumer (skinny_gemm.hip MERGE)
     if (S > 16) {
         // many splits (long contexts): one merge workgroup per query head instead of per kv-head group,
         // G x more workgroups with G x fewer partial loads each (B=1, 11k context, S=48: 8 workgroups
@@ -705,6 +715,16 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
         case 8: attn_decode_combine_kernel<8><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
         case 16: attn_decode_combine_kernel<16><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
     }
+    return (int)hipGetLastError();
+}
+
+// The split merge alone (partials of an attention launch made without ``out``): out [B, Hq * D] bf16.
+MRSUM_API int mrsum_attn_decode_merge(const void* part_o, const void* part_ml, void* out, int out_stride, int B,
+                                      int Hq, int S, hipStream_t s) {
+    if (B <= 0) return 0;
+    if (!part_o || !part_ml || !out || Hq <= 0 || S < 1 || S > MAX_SPLITS) return (int)hipErrorInvalidValue;
+    attn_decode_combine_kernel<1><<<B * Hq, 256, 0, s>>>((const float*)part_o, (const float*)part_ml, (bf16*)out,
+                                                        out_stride, Hq, Hq, S);
     return (int)hipGetLastError();
 }
 

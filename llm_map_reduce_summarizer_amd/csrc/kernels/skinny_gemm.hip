@@ -49,7 +49,89 @@ struct SkinnyNorm {
     int ldr;
     float* ssp;        // RESID producer: [M][gridDim.x] row sums of squares of the new residual per tile
     mrsum_ar::TPPush tp;
+    // MERGE (RESID, one row): x is not read -- it is the decode attention's split merge of part_o
+    // [1][Hq][mS][128] / part_ml [1][Hq][mS][2] (attn_decode.hip), done by every workgroup into LDS
+    const float* mo;
+    const float* mml;
+    int mS;
 };
+
+// Consumer-side split merge (attn_decode.hip combine_group, re-cut for one row and a 64 NW-thread
+// workgroup): x[h * 128 + d] = sum_s 2^(m_s - M) o_s[d] / sum_s 2^(m_s - M) l_s for the Hq = K / 128 heads,
+// written as bf16 into the LDS row ``xm``.  Every workgroup repeats it (the partials are L2-resident after
+// the first reader of each XCD); it runs after the workgroup's first weight loads are issued, under their
+// HBM latency, and the separate merge launch disappears.  Needs Hq * 32 <= 64 NW, S <= MERGE_MAX_S.
+constexpr int MERGE_MAX_S = 256, MERGE_MAX_HQ = 16, MERGE_PRE = 8;
+template <int NW>
+__device__ __forceinline__ void merge_row_to_lds(const SkinnyNorm& e, int K, bf16* xm, float* sw, float* sden,
+                                                 float4* scratch) {
+    constexpr int NTH = 64 * NW, D = 128;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int Hq = K / D, S = e.mS;
+    const int NV = Hq * (D / 4), NH = NTH / NV;  // float4 items, split subsets per item
+    const int item = tid % NV, hs = tid / NV, head = item / (D / 4), d4 = item % (D / 4);
+    const float4* po = reinterpret_cast<const float4*>(e.mo) + (size_t)head * S * (D / 4) + d4;
+    // 1. the first MERGE_PRE slabs of this thread's subset, issued before the split weights are known
+    float4 pre[MERGE_PRE];
+#pragma unroll
+    for (int j = 0; j < MERGE_PRE; ++j) {
+        const int sp = hs + j * NH;
+        const float4 v = po[(size_t)min(sp, S - 1) * (D / 4)];  // unconditional (clamped) load
+        pre[j] = (hs < NH && sp < S) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    // 2. split weights: one wave per head, lane l holds splits l + 64 q
+    for (int g = wv; g < Hq; g += NW) {
+        float ms[4], ls[4], mloc = -INFINITY;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int sp = lane + 64 * q;
+            const float2 v = reinterpret_cast<const float2*>(e.mml)[g * S + min(sp, S - 1)];
+            ms[q] = sp < S ? v.x : -INFINITY;
+            ls[q] = sp < S ? v.y : 0.f;
+            mloc = fmaxf(mloc, ms[q]);
+        }
+        const float M = wave_max(mloc);
+        float wl = 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int sp = lane + 64 * q;
+            const float w = ms[q] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms[q] - M);
+            wl += w * ls[q];
+            if (sp < S) sw[g * S + sp] = w;
+        }
+        const float den = wave_sum(wl);
+        if (lane == 0) sden[g] = den;
+    }
+    __syncthreads();
+    // 3. weighted sums, subsets merged through LDS, bf16 into the row
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (hs < NH) {
+        const float* w = sw + head * S;
+#pragma unroll
+        for (int j = 0; j < MERGE_PRE; ++j) {
+            const int sp = hs + j * NH;
+            const float ws = sp < S ? w[sp] : 0.f;
+            acc.x += ws * pre[j].x; acc.y += ws * pre[j].y; acc.z += ws * pre[j].z; acc.w += ws * pre[j].w;
+        }
+        for (int sp = hs + MERGE_PRE * NH; sp < S; sp += NH) {
+            const float4 v = po[(size_t)sp * (D / 4)];
+            const float ws = w[sp];
+            acc.x += ws * v.x; acc.y += ws * v.y; acc.z += ws * v.z; acc.w += ws * v.w;
+        }
+    }
+    scratch[tid] = acc;
+    __syncthreads();
+    if (hs == 0) {
+        for (int j = 1; j < NH; ++j) {
+            const float4 v = scratch[j * NV + item];
+            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        }
+        const float den = sden[head];
+        const float inv = den > 0.f ? 1.f / den : 0.f;
+        *reinterpret_cast<uint2*>(xm + head * D + 4 * d4) =
+            make_uint2(pack2(acc.x * inv, acc.y * inv), pack2(acc.z * inv, acc.w * inv));
+    }
+}
 
 // Deferred norm of row m, in stream_gemm.hip's order: partial p (< 8) of ssq_tiles / 8 consecutive tiles
 // summed in float4 steps (thread 8 m + p; its loads issued in the kernel prologue, into registers, so they
@@ -120,6 +202,14 @@ __device__ __forceinline__ void load_b(BFrag<MT>& b, const bf16* __restrict__ x,
     }
 }
 
+// the per-wave partial sums of one output, waves in order (pairwise for 8, the 4-wave order unchanged)
+template <int NW, typename R>
+__device__ __forceinline__ float wsum(const R& red, int m, int n) {
+    const float s4 = red[0][m][n] + red[1][m][n] + red[2][m][n] + red[3][m][n];
+    if constexpr (NW == 8) return s4 + (red[4][m][n] + red[5][m][n] + red[6][m][n] + red[7][m][n]);
+    return s4;
+}
+
 template <int NT, int MT>
 __device__ __forceinline__ void mma_block(f32x4 (&acc)[NT][MT], const AFrag<NT>& a, const BFrag<MT>& b) {
 #pragma unroll
@@ -134,14 +224,24 @@ __device__ __forceinline__ void mma_block(f32x4 (&acc)[NT][MT], const AFrag<NT>&
 }
 }  // namespace
 
-template <int NT, int MT, int EPI>
-__global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16* __restrict__ x, int ldx,
-                                                          const bf16* __restrict__ W, int K, int M,
-                                                          void* __restrict__ out, int ldo, int kper,
-                                                          const SkinnyNorm e) {
+// NW = waves per workgroup (4 or 8), interleaved over the k blocks: a grid of about one workgroup per CU
+// (a TP shard's N / 16 tiles) keeps only NW x two blocks of W in flight per CU, so the 8-wave form doubles the
+// bytes in flight where the grid cannot (Little's law: ~32 KiB per CU in flight is ~3 TB/s at decode latency).
+template <int NT, int MT, int EPI, int NW = 4, bool MERGE = false>
+__global__ __launch_bounds__(64 * NW) void skinny_gemm_kernel(const bf16* __restrict__ x, int ldx,
+                                                              const bf16* __restrict__ W, int K, int M,
+                                                              void* __restrict__ out, int ldo, int kper,
+                                                              const SkinnyNorm e) {
     constexpr int BN = 16 * NT, BM = 16 * MT;
     static_assert(EPI != EPI_RESID || (NT == 1 && MT == 1), "RESID: one 16-row tile, M <= 16");
-    __shared__ __attribute__((aligned(16))) float red[4][BM][BN + 4];
+    static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+    static_assert(!MERGE || (EPI == EPI_RESID && MT == 1), "MERGE: the residual producer of one row");
+    __shared__ __attribute__((aligned(16))) float red[NW][BM][BN + 4];
+    // MERGE: the merged x row (bf16, K <= 2048), split weights, per-head denominators, subset partials
+    __shared__ __attribute__((aligned(16))) bf16 xm[MERGE ? MERGE_MAX_HQ * 128 : 1];
+    __shared__ float msw[MERGE ? MERGE_MAX_HQ * MERGE_MAX_S : 1];
+    __shared__ float msden[MERGE ? MERGE_MAX_HQ : 1];
+    __shared__ float4 mscr[MERGE ? 64 * NW : 1];
     __shared__ float s_part[EPI == EPI_SWIGLU ? 8 * BM : 1];  // deferred-norm partials [m][8]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int n0 = blockIdx.x * BN;
@@ -160,7 +260,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16* __restrict
 #pragma unroll
         for (int m = 0; m < MT; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // wave w takes k blocks ks + (w + 4j) * KB.  Issue order per block: x fragments of THIS block,
+    // wave w takes k blocks ks + (w + NW j) * KB.  Issue order per block: x fragments of THIS block,
     // then W of the NEXT block, then the MFMAs -- vmcnt retires loads in issue order, so waiting
     // for x must not also wait for the prefetched W (which would serialise the stream).  The steady
     // loop issues every next-block load unconditionally and the last one or two blocks run in
@@ -169,30 +269,45 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16* __restrict
     // MFMA of the block, one exposed memory round trip per block.  Same-box A/B: TP=8 shard B=10 -1.4 %,
     // 70B fp8 B=1 -0.5 %, TP=1 B=1/10 unchanged -- the many resident waves had hidden most of it
     // (profiles/r3_skinny_prefetch_fix_ab.jsonl).
+    constexpr int STEP = NW * KB;
     const int kb0 = ks + w * KB;
-    const int nb = kb0 < ke ? (ke - kb0 + 4 * KB - 1) / (4 * KB) : 0;  // this wave's k blocks
+    const int nb = kb0 < ke ? (ke - kb0 + STEP - 1) / STEP : 0;  // this wave's k blocks
     AFrag<NT> a0, a1;
     BFrag<MT> b;
     if (nb > 0) load_a<NT>(a0, W, K, n0, kb0, lane);
+    if constexpr (MERGE) {
+        merge_row_to_lds<NW>(e, K, xm, msw, msden, mscr);  // under the first weight block's latency
+        __syncthreads();
+    }
+    // x fragments of k block kb: global rows, or (MERGE) the merged row in LDS
+    auto ldb = [&](int kb) {
+        if constexpr (MERGE) {
+            const bf16* p = xm + kb + 8 * (lane >> 4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b.v[0][q] = *reinterpret_cast<const uint4*>(p + 32 * q);
+        } else {
+            load_b<MT>(b, x, ldx, M, kb, lane);
+        }
+    };
     int i = 0;
     for (; i + 2 < nb; i += 2) {  // blocks i and i + 1, each with a successor
-        const int kb = kb0 + i * 4 * KB;
-        load_b<MT>(b, x, ldx, M, kb, lane);
-        load_a<NT>(a1, W, K, n0, kb + 4 * KB, lane);
+        const int kb = kb0 + i * STEP;
+        ldb(kb);
+        load_a<NT>(a1, W, K, n0, kb + STEP, lane);
         mma_block<NT, MT>(acc, a0, b);
-        load_b<MT>(b, x, ldx, M, kb + 4 * KB, lane);
-        load_a<NT>(a0, W, K, n0, kb + 8 * KB, lane);
+        ldb(kb + STEP);
+        load_a<NT>(a0, W, K, n0, kb + 2 * STEP, lane);
         mma_block<NT, MT>(acc, a1, b);
     }
     if (nb - i == 2) {
-        const int kb = kb0 + i * 4 * KB;
-        load_b<MT>(b, x, ldx, M, kb, lane);
-        load_a<NT>(a1, W, K, n0, kb + 4 * KB, lane);
+        const int kb = kb0 + i * STEP;
+        ldb(kb);
+        load_a<NT>(a1, W, K, n0, kb + STEP, lane);
         mma_block<NT, MT>(acc, a0, b);
-        load_b<MT>(b, x, ldx, M, kb + 4 * KB, lane);
+        ldb(kb + STEP);
         mma_block<NT, MT>(acc, a1, b);
     } else if (nb - i == 1) {
-        load_b<MT>(b, x, ldx, M, kb0 + i * 4 * KB, lane);
+        ldb(kb0 + i * STEP);
         mma_block<NT, MT>(acc, a0, b);
     }
 
@@ -211,12 +326,12 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16* __restrict
 
     // each item = 4 consecutive n of one m
     constexpr int ITEMS = BM * (BN / 4);
-    for (int it = threadIdx.x; it < ITEMS; it += 256) {
+    for (int it = threadIdx.x; it < ITEMS; it += 64 * NW) {
         const int m = it / (BN / 4), n4 = (it % (BN / 4)) * 4;
         if (m >= M) continue;
         float v[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = red[0][m][n4 + j] + red[1][m][n4 + j] + red[2][m][n4 + j] + red[3][m][n4 + j];
+        for (int j = 0; j < 4; ++j) v[j] = wsum<NW>(red, m, n4 + j);
         if constexpr (EPI == EPI_BF16) {
             uint2 o;
             o.x = pack2(v[0], v[1]);
@@ -249,8 +364,7 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16* __restrict
                 float r[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const float u = (red[0][m][n4 + H + j] + red[1][m][n4 + H + j] + red[2][m][n4 + H + j] +
-                                     red[3][m][n4 + H + j]) * sc;
+                    const float u = wsum<NW>(red, m, n4 + H + j) * sc;
                     const float g = v[j] * sc;
                     r[j] = g / (1.f + __expf(-g)) * u;
                 }
@@ -271,47 +385,60 @@ __global__ __launch_bounds__(256) void skinny_gemm_kernel(const bf16* __restrict
     }
 }
 
-template <int NT, int EPI>
+template <int NT, int EPI, int NW>
 static int launch_mt(int mt, dim3 grid, hipStream_t s, const bf16* x, int ldx, const bf16* W, int K, int M,
                      void* out, int ldo, int kper, const SkinnyNorm& e) {
+    const dim3 block(64 * NW);
     switch (mt) {
-        case 1: skinny_gemm_kernel<NT, 1, EPI><<<grid, 256, 0, s>>>(x, ldx, W, K, M, out, ldo, kper, e); break;
-        case 2: skinny_gemm_kernel<NT, 2, EPI><<<grid, 256, 0, s>>>(x, ldx, W, K, M, out, ldo, kper, e); break;
-        case 3: skinny_gemm_kernel<NT, 3, EPI><<<grid, 256, 0, s>>>(x, ldx, W, K, M, out, ldo, kper, e); break;
-        case 4: skinny_gemm_kernel<NT, 4, EPI><<<grid, 256, 0, s>>>(x, ldx, W, K, M, out, ldo, kper, e); break;
+        case 1: skinny_gemm_kernel<NT, 1, EPI, NW><<<grid, block, 0, s>>>(x, ldx, W, K, M, out, ldo, kper, e); break;
+        case 2: skinny_gemm_kernel<NT, 2, EPI, NW><<<grid, block, 0, s>>>(x, ldx, W, K, M, out, ldo, kper, e); break;
+        case 3: skinny_gemm_kernel<NT, 3, EPI, NW><<<grid, block, 0, s>>>(x, ldx, W, K, M, out, ldo, kper, e); break;
+        case 4: skinny_gemm_kernel<NT, 4, EPI, NW><<<grid, block, 0, s>>>(x, ldx, W, K, M, out, ldo, kper, e); break;
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
 }
 
-// Workgroups of the residual-update (TP push) instantiation that can be resident on this device at once:
-// occupancy per CU x CUs (header: a TP-push grid must fit, every workgroup spins on its peers).
-MRSUM_API int mrsum_skinny_resid_capacity() {
-    static int cap = -1;
-    if (cap < 0) {
+// Workgroups of the residual-update (TP push) instantiation with ``waves`` waves that can be resident on this
+// device at once: occupancy per CU x CUs (header: a TP-push grid must fit, every workgroup spins on its peers).
+MRSUM_API int mrsum_skinny_resid_capacity_w(int waves) {
+    static int cap[2] = {-1, -1};
+    const int i = waves == 8 ? 1 : 0;
+    if (cap[i] < 0) {
         int dev = 0, cus = 0, per = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, skinny_gemm_kernel<1, 1, EPI_RESID>, 256, 0) !=
-                hipSuccess)
-            return 0;
-        cap = cus * per;
+        hipError_t st = hipGetDevice(&dev);
+        if (st == hipSuccess) st = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        // the smaller of the plain and the split-merging (MERGE, more LDS) instantiation
+        int pm = 0;
+        if (st == hipSuccess)
+            st = i ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, skinny_gemm_kernel<1, 1, EPI_RESID, 8>, 512, 0)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, skinny_gemm_kernel<1, 1, EPI_RESID, 4>, 256, 0);
+        if (st == hipSuccess)
+            st = i ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&pm, skinny_gemm_kernel<1, 1, EPI_RESID, 8, true>, 512, 0)
+                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&pm, skinny_gemm_kernel<1, 1, EPI_RESID, 4, true>, 256, 0);
+        if (st != hipSuccess) return 0;
+        cap[i] = cus * std::min(per, pm);
     }
-    return cap;
+    return cap[i];
 }
+
+MRSUM_API int mrsum_skinny_resid_capacity() { return mrsum_skinny_resid_capacity_w(4); }
 
 // epi: 0 bf16 [M, ldo], 1 fp32 partial [S, M, ldo], 2 swiglu bf16 [M, ldo] (ldo >= N/2), 3 residual update
 // (resid [M, ldr] bf16 += x W^T, ssp fp32 [M, N / 16] per-tile row sums of squares of the new residual;
 // nt 1, splits 1, M <= 16; ``ar`` non-null: all-reduced over that custom all-reduce group first (TP push,
 // M * N * 4 <= its slot bytes)).  nt: 16-row W tiles per workgroup (1 or 2; swiglu needs 1); splits: S (K/S
 // multiple of 128).  ssq (swiglu only): deferred-RMSNorm input [M, ssq_tiles] fp32, ssq_tiles % 32 == 0.
+// waves: 4 or 8 per workgroup (kernel header).
+// mo / mml / mS (epi 3, M = 1, K <= 2048): x is the split merge of decode-attention partials (kernel MERGE).
 MRSUM_API int mrsum_skinny_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
                                 int epi, int nt, int splits, const float* ssq, int ssq_tiles, float eps, void* resid,
-                                int ldr, float* ssp, void* ar, hipStream_t s) {
+                                int ldr, float* ssp, void* ar, const float* mo, const float* mml, int mS, int waves,
+                                hipStream_t s) {
     using namespace mrsum_ar;
     if (M <= 0) return 0;
     if (M > 64 || K % KB || splits < 1 || (K / KB) % splits || (nt != 1 && nt != 2) || N % (16 * nt) ||
-        epi < EPI_BF16 || epi > EPI_RESID)
+        epi < EPI_BF16 || epi > EPI_RESID || (waves != 4 && waves != 8))
         return (int)hipErrorInvalidValue;
     if (epi != EPI_F32_PARTIAL && splits != 1) return (int)hipErrorInvalidValue;
     if (epi == EPI_SWIGLU && nt != 1) return (int)hipErrorInvalidValue;  // weight blocks of [8 gate | 8 up]
@@ -324,25 +451,41 @@ MRSUM_API int mrsum_skinny_gemm(const void* x, int ldx, const void* W, int N, in
         for (int r = 0; r < h->world; ++r)
             if (!h->peers.base[r]) return (int)hipErrorInvalidValue;
     }
-    if (ar && N / 16 > mrsum_skinny_resid_capacity()) return (int)hipErrorInvalidValue;  // header: progress
+    if (ar && N / 16 > mrsum_skinny_resid_capacity_w(waves)) return (int)hipErrorInvalidValue;  // header: progress
+    const bool merge = mo != nullptr;
+    if (merge && (epi != EPI_RESID || M != 1 || !mml || mS < 1 || mS > MERGE_MAX_S || K % 128 ||
+                  K / 128 > MERGE_MAX_HQ || (K / 128) * 32 > 64 * waves))
+        return (int)hipErrorInvalidValue;
     SkinnyNorm e;
     e.ssq = ssq; e.ssq_tiles = ssq_tiles; e.inv_k = 1.f / (float)K; e.eps = eps;
     e.resid = (bf16*)resid; e.ldr = ldr; e.ssp = ssp;
     e.tp = tp_push_of((const ArHandle*)ar);
+    e.mo = mo; e.mml = mml; e.mS = mS;
     const int kper = K / splits;
     const int mt = (M + 15) / 16;
     dim3 grid(N / (16 * nt), splits);
     auto X = (const bf16*)x; auto Wp = (const bf16*)W;
+#define BY_W(NT_, EPI_)                                                                       \
+    return waves == 8 ? launch_mt<NT_, EPI_, 8>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper, e) \
+                      : launch_mt<NT_, EPI_, 4>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper, e)
     if (nt == 1) {
-        if (epi == EPI_BF16) return launch_mt<1, EPI_BF16>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper, e);
-        if (epi == EPI_F32_PARTIAL) return launch_mt<1, EPI_F32_PARTIAL>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper, e);
-        if (epi == EPI_SWIGLU) return launch_mt<1, EPI_SWIGLU>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper, e);
-        skinny_gemm_kernel<1, 1, EPI_RESID><<<grid, 256, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, e);
+        if (epi == EPI_BF16) BY_W(1, EPI_BF16);
+        if (epi == EPI_F32_PARTIAL) BY_W(1, EPI_F32_PARTIAL);
+        if (epi == EPI_SWIGLU) BY_W(1, EPI_SWIGLU);
+        if (merge) {
+            if (waves == 8) skinny_gemm_kernel<1, 1, EPI_RESID, 8, true><<<grid, 512, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, e);
+            else skinny_gemm_kernel<1, 1, EPI_RESID, 4, true><<<grid, 256, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, e);
+        } else if (waves == 8) {
+            skinny_gemm_kernel<1, 1, EPI_RESID, 8><<<grid, 512, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, e);
+        } else {
+            skinny_gemm_kernel<1, 1, EPI_RESID, 4><<<grid, 256, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, e);
+        }
         return (int)hipGetLastError();
     } else {
-        if (epi == EPI_BF16) return launch_mt<2, EPI_BF16>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper, e);
-        if (epi == EPI_F32_PARTIAL) return launch_mt<2, EPI_F32_PARTIAL>(mt, grid, s, X, ldx, Wp, K, M, out, ldo, kper, e);
+        if (epi == EPI_BF16) BY_W(2, EPI_BF16);
+        if (epi == EPI_F32_PARTIAL) BY_W(2, EPI_F32_PARTIAL);
     }
+#undef BY_W
     return (int)hipErrorInvalidValue;
 }
 
@@ -586,15 +729,16 @@ __device__ __forceinline__ void mma_block8(f32x4 (&acc)[NT][MT], const A8Frag<NT
 // XL also takes a deferred-RMSNorm input (stream_gemm.hip header): x = the un-normalised residual row,
 // ``ssq`` [1][ssq_tiles] its producer's per-tile sums of squares, reduced in the stream consumer's fixed
 // order (8 partials of ssq_tiles / 8 tiles, float4 steps) so both consumers scale by the same factor.
-template <int NT, int MT, int EPI, bool XL>
-__global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict__ x, int ldx,
-                                                         const uint8_t* __restrict__ W,
-                                                         const float* __restrict__ wscale, int K, int M,
-                                                         void* __restrict__ out, int ldo, int kper,
-                                                         const float* __restrict__ ssq, int ssq_tiles, float eps) {
+// NW = 4 or 8 waves per workgroup (skinny_gemm_kernel header: bytes in flight per CU on small grids).
+template <int NT, int MT, int EPI, bool XL, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void skinny_fp8_kernel(const bf16* __restrict__ x, int ldx,
+                                                             const uint8_t* __restrict__ W,
+                                                             const float* __restrict__ wscale, int K, int M,
+                                                             void* __restrict__ out, int ldo, int kper,
+                                                             const float* __restrict__ ssq, int ssq_tiles, float eps) {
     constexpr int BN = 16 * NT, BM = 16 * MT;
     static_assert(!XL || MT == 1, "the LDS x slice holds one row");
-    __shared__ __attribute__((aligned(16))) float red[4][BM][BN + 4];
+    __shared__ __attribute__((aligned(16))) float red[NW][BM][BN + 4];
     __shared__ float s_ss[8];
     extern __shared__ __attribute__((aligned(16))) char xs[];  // XL: kper bf16 of x row 0
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -602,7 +746,7 @@ __global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict_
     const int ks = blockIdx.y * kper, ke = min(K, ks + kper);
     if constexpr (XL) {
         const uint4* src = reinterpret_cast<const uint4*>(x + ks);
-        for (int i = threadIdx.x; i < kper / 8; i += 256) reinterpret_cast<uint4*>(xs)[i] = src[i];
+        for (int i = threadIdx.x; i < kper / 8; i += 64 * NW) reinterpret_cast<uint4*>(xs)[i] = src[i];
         if (ssq && threadIdx.x < 8) {
             const int C = ssq_tiles / 8;
             const float4* sp = reinterpret_cast<const float4*>(ssq + threadIdx.x * C);
@@ -632,30 +776,31 @@ __global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict_
         for (int m = 0; m < MT; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // unconditional next-block loads in the steady loop, straight-line tails (as skinny_gemm_kernel)
+    constexpr int STEP = NW * KB;
     const int kb0 = ks + w * KB;
-    const int nb = kb0 < ke ? (ke - kb0 + 4 * KB - 1) / (4 * KB) : 0;
+    const int nb = kb0 < ke ? (ke - kb0 + STEP - 1) / STEP : 0;
     A8Frag<NT> a0, a1;
     BFrag<MT> b;
     if (nb > 0) load_a8<NT>(a0, W, K, n0, kb0, lane);
     int i = 0;
     for (; i + 2 < nb; i += 2) {
-        const int kb = kb0 + i * 4 * KB;
+        const int kb = kb0 + i * STEP;
         load_b(b, kb);
-        load_a8<NT>(a1, W, K, n0, kb + 4 * KB, lane);
+        load_a8<NT>(a1, W, K, n0, kb + STEP, lane);
         mma_block8<NT, MT>(acc, a0, b);
-        load_b(b, kb + 4 * KB);
-        load_a8<NT>(a0, W, K, n0, kb + 8 * KB, lane);
+        load_b(b, kb + STEP);
+        load_a8<NT>(a0, W, K, n0, kb + 2 * STEP, lane);
         mma_block8<NT, MT>(acc, a1, b);
     }
     if (nb - i == 2) {
-        const int kb = kb0 + i * 4 * KB;
+        const int kb = kb0 + i * STEP;
         load_b(b, kb);
-        load_a8<NT>(a1, W, K, n0, kb + 4 * KB, lane);
+        load_a8<NT>(a1, W, K, n0, kb + STEP, lane);
         mma_block8<NT, MT>(acc, a0, b);
-        load_b(b, kb + 4 * KB);
+        load_b(b, kb + STEP);
         mma_block8<NT, MT>(acc, a1, b);
     } else if (nb - i == 1) {
-        load_b(b, kb0 + i * 4 * KB);
+        load_b(b, kb0 + i * STEP);
         mma_block8<NT, MT>(acc, a0, b);
     }
 
@@ -676,14 +821,13 @@ __global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict_
     }
 
     constexpr int ITEMS = BM * (BN / 4);
-    for (int it = threadIdx.x; it < ITEMS; it += 256) {
+    for (int it = threadIdx.x; it < ITEMS; it += 64 * NW) {
         const int m = it / (BN / 4), n4 = (it % (BN / 4)) * 4;
         if (m >= M) continue;
         float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-            v[j] = (red[0][m][n4 + j] + red[1][m][n4 + j] + red[2][m][n4 + j] + red[3][m][n4 + j]) *
-                   wscale[n0 + n4 + j] * rs;
+            v[j] = wsum<NW>(red, m, n4 + j) * wscale[n0 + n4 + j] * rs;
         if constexpr (EPI == EPI_BF16) {
             uint2 o;
             o.x = pack2(v[0], v[1]);
@@ -698,8 +842,7 @@ __global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict_
                 float rr[4];
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const float u = (red[0][m][n4 + H + j] + red[1][m][n4 + H + j] + red[2][m][n4 + H + j] +
-                                     red[3][m][n4 + H + j]) * wscale[n0 + n4 + H + j] * rs;
+                    const float u = wsum<NW>(red, m, n4 + H + j) * wscale[n0 + n4 + H + j] * rs;
                     rr[j] = v[j] / (1.f + __expf(-v[j])) * u;
                 }
                 uint2 o;
@@ -712,12 +855,13 @@ __global__ __launch_bounds__(256) void skinny_fp8_kernel(const bf16* __restrict_
 }
 
 // ssq (deferred-RMSNorm input, M = 1 with the x slice in LDS only): [1][ssq_tiles] fp32 row sums of squares
-// of x per producer tile, ssq_tiles % 32 == 0; the product is scaled by rsqrt(sum / K + eps).
+// of x per producer tile, ssq_tiles % 32 == 0; the product is scaled by rsqrt(sum / K + eps).  waves: 4 or 8.
 MRSUM_API int mrsum_skinny_fp8(const void* x, int ldx, const void* W, const float* wscale, int N, int K, int M,
                                void* out, int ldo, int epi, int nt, int splits, const float* ssq, int ssq_tiles,
-                               float eps, hipStream_t s) {
+                               float eps, int waves, hipStream_t s) {
     if (M <= 0) return 0;
-    if (M > 64 || K % KB || splits < 1 || (K / KB) % splits || (nt != 1 && nt != 2) || N % (16 * nt))
+    if (M > 64 || K % KB || splits < 1 || (K / KB) % splits || (nt != 1 && nt != 2) || N % (16 * nt) ||
+        (waves != 4 && waves != 8))
         return (int)hipErrorInvalidValue;
     if (epi != EPI_F32_PARTIAL && splits != 1) return (int)hipErrorInvalidValue;
     if (epi == EPI_SWIGLU && nt != 1) return (int)hipErrorInvalidValue;
@@ -727,27 +871,31 @@ MRSUM_API int mrsum_skinny_fp8(const void* x, int ldx, const void* W, const floa
     auto X = (const bf16*)x; auto Wp = (const uint8_t*)W;
     const bool xl = M == 1 && kper * 2 <= 56 * 1024;  // x slice in (default-limit) dynamic LDS
     if (ssq && (!xl || ssq_tiles <= 0 || ssq_tiles % 32)) return (int)hipErrorInvalidValue;
-#define L(NT_, MT_, EPI_)                                                                                        \
-    skinny_fp8_kernel<NT_, MT_, EPI_, false><<<grid, 256, 0, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper, nullptr, 0, 0.f)
-#define L1(NT_, EPI_)                                                                                            \
-    if (xl) skinny_fp8_kernel<NT_, 1, EPI_, true><<<grid, 256, kper * 2, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper, \
-                                                                             ssq, ssq_tiles, eps);             \
-    else L(NT_, 1, EPI_)
-#define BY_MT(NT_, EPI_)                        \
+#define L(NT_, MT_, EPI_, NW_)                                                                                  \
+    skinny_fp8_kernel<NT_, MT_, EPI_, false, NW_><<<grid, 64 * NW_, 0, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper, \
+                                                                          nullptr, 0, 0.f)
+#define L1(NT_, EPI_, NW_)                                                                                      \
+    if (xl) skinny_fp8_kernel<NT_, 1, EPI_, true, NW_><<<grid, 64 * NW_, kper * 2, s>>>(X, ldx, Wp, wscale, K, M, out, \
+                                                                                      ldo, kper, ssq, ssq_tiles, eps); \
+    else L(NT_, 1, EPI_, NW_)
+#define BY_MT(NT_, EPI_, NW_)                   \
     switch (mt) {                               \
-        case 1: L1(NT_, EPI_); break;           \
-        case 2: L(NT_, 2, EPI_); break;         \
-        case 3: L(NT_, 3, EPI_); break;         \
-        default: L(NT_, 4, EPI_); break;        \
+        case 1: L1(NT_, EPI_, NW_); break;      \
+        case 2: L(NT_, 2, EPI_, NW_); break;    \
+        case 3: L(NT_, 3, EPI_, NW_); break;    \
+        default: L(NT_, 4, EPI_, NW_); break;   \
     }
-    if (nt == 1) {
-        if (epi == EPI_BF16) { BY_MT(1, EPI_BF16) }
-        else if (epi == EPI_F32_PARTIAL) { BY_MT(1, EPI_F32_PARTIAL) }
-        else { BY_MT(1, EPI_SWIGLU) }
-    } else {
-        if (epi == EPI_BF16) { BY_MT(2, EPI_BF16) }
-        else { BY_MT(2, EPI_F32_PARTIAL) }
+#define BY_EPI(NW_)                                                           \
+    if (nt == 1) {                                                            \
+        if (epi == EPI_BF16) { BY_MT(1, EPI_BF16, NW_) }                      \
+        else if (epi == EPI_F32_PARTIAL) { BY_MT(1, EPI_F32_PARTIAL, NW_) }   \
+        else { BY_MT(1, EPI_SWIGLU, NW_) }                                    \
+    } else {                                                                  \
+        if (epi == EPI_BF16) { BY_MT(2, EPI_BF16, NW_) }                      \
+        else { BY_MT(2, EPI_F32_PARTIAL, NW_) }                               \
     }
+    if (waves == 8) { BY_EPI(8) } else { BY_EPI(4) }
+#undef BY_EPI
 #undef BY_MT
 #undef L1
 #undef L

@@ -391,7 +391,7 @@ def _resid_plan(hip, a, w, role, tp=False, force=None):
             return ("skinny",)
         if tp:
             if (force == "skinny" or (force is None and p[0] == "skinny")) and N % 512 == 0 \
-                    and N // 16 <= hip.skinny_resid_capacity():  # every pushing workgroup resident at once
+                    and N // 16 <= hip.skinny_resid_capacity(N):  # every pushing workgroup resident at once
                 return ("skinny",)
             if force == "skinny":
                 return None
@@ -412,9 +412,15 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None, quant=F
     all-reduces its tile over the group first (TP push), so no all-reduce kernel runs either.  ``all_reduce`` is a callable summing a tensor over
     the TP group in place; when it also offers ``add_rmsnorm``/``fused_ok`` (the model's P2P
     all-reduce) the decode path runs the projection's split-K slabs straight into one fused
-    all-reduce + residual add + RMSNorm kernel."""
+    all-reduce + residual add + RMSNorm kernel.
+
+    ``a`` may be the decode attention's split partials (ops.hip.AttnParts, one row): the register-streaming
+    residual producer merges them itself; every other path merges them first (the merge kernel)."""
+    merge = None
     if _use_hip(a):
         from . import hip
+        if isinstance(a, hip.AttnParts):
+            merge, a = a, a.out
         if ln is None and a.shape[0] <= hip.SKINNY_MAX_M:
             # TP: the producer all-reduces its own tiles (TP push) when the group's buffers take the rows
             ok = getattr(all_reduce, "push_ok", None)
@@ -427,12 +433,16 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None, quant=F
                     # and passed, else the fused all-reduce path below
                     other = ({"stream", "skinny"} - {rp[0]}) & kinds()
                     rp = _resid_plan(hip, a, w, role, tp=True, force=other.pop()) if other else None
-                    if rp is not None and rp[0] == "skinny" and w.shape[0] // 16 > hip.skinny_resid_capacity():
+                    if rp is not None and rp[0] == "skinny" and w.shape[0] // 16 > hip.skinny_resid_capacity(w.shape[0]):
                         rp = None
                 if rp is not None and rp[0] == "skinny":
-                    return NormRows(residual, hip.skinny_resid(a, w, residual, tp=push), eps)
+                    return NormRows(residual, hip.skinny_resid(merge or a, w, residual, tp=push), eps)
                 if rp is not None:
+                    if merge is not None:
+                        merge.merged()  # fills a
                     return NormRows(residual, hip.stream_resid(a, w, residual, rp[1], rp[2], tp=push), eps)
+        if merge is not None:
+            merge.merged()  # fills a
     if ln is None:
         ln = unit_gain(residual.shape[1], residual.device)
     if _use_hip(a) and isinstance(w, Fp8Weight):

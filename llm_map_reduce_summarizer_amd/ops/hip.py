@@ -40,15 +40,16 @@ _SIGS = {
     "mrsum_attn_decode_rope": [_vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int,
                                _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _c_int, _vp],
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int,
-                          _c_float, _vp, _c_int, _vp, _vp, _vp],
-    "mrsum_skinny_resid_capacity": [],
+                          _c_float, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp],
+    "mrsum_skinny_resid_capacity_w": [_c_int],
+    "mrsum_attn_decode_merge": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_stream_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp,
                           _vp, _c_int, _c_float, _vp, _c_int, _vp, _c_int, _vp, _vp],
     "mrsum_stream_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp,
                          _vp, _c_int, _c_float, _vp, _c_int, _vp, _vp, _vp],
     "mrsum_skinny_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp,
-                         _c_int, _c_float, _vp],
+                         _c_int, _c_float, _c_int, _vp],
     "mrsum_quant_fp8_rows": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_sample_keys": [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
@@ -358,6 +359,7 @@ def decode_splits(batch: int, hkv: int, max_ctx: int, target_wgs: int = 1024, ma
     return s
 
 
+MAX_SPLITS = 256  # attn_decode.hip MAX_SPLITS: splits of one (sequence, kv head) the merge takes
 ATTN_PAGES_PER_SPLIT = 2  # at least 2 pages per split (1 measured slower at B=1: r1_attn_splits_ab.jsonl)
 
 
@@ -432,10 +434,11 @@ def decode_attn_plan_bf16(batch: int, hkv: int, max_ctx: int):
             # B=10 25 separate 1.600 vs 24 fused 1.615, 16 fused 1.623
             return max(1, min(N_CU // groups, pages, 64)), False
         if not fused and hkv <= 2:
-            # a TP shard's one or two kv heads beyond the 6k class (config 5's 32k final reduce at TP=8): as
-            # many splits as the merge takes -- 64 separate splits for the 70B fp8 TP=8 shard at B=1, 32k: 5.64
-            # ms per step vs 6.22 with the 32 of the TP=1 rule below (in situ, profiles/r5_attn_plans_deep.jsonl)
-            return max(1, min(splits, 64)), False
+            # a TP shard's one or two kv heads beyond the 6k class (config 5's 32k final reduce at TP=8): the
+            # TP=1 rule below leaves B=1 at 32 workgroups.  Up to ATTN_SLOTS workgroups of >= 2 pages, at most
+            # MAX_SPLITS (attn_decode.hip) separate splits: 70B fp8 TP=8 shard at B=1, 32k -- 64 splits 5.11-5.12
+            # ms per step vs 5.66 at 32 (in situ, profiles/r5_attn_plans.jsonl)
+            return max(1, min(ATTN_SLOTS // groups, -(-pages // ATTN_PAGES_PER_SPLIT), MAX_SPLITS)), False
         if fused and batch == 1 and hkv >= 8 and pages > 32:
             # one sequence x 8 kv heads: 32 splits with the separate merge beat 16 fused in situ (whole decode
             # steps, 4k context: 3.47 vs 3.55 ms; profiles/r2_attn_plans_insitu_b1_b10.jsonl), as in the
@@ -474,10 +477,14 @@ def decode_groups(hq: int, hkv: int) -> int:
 
 class DecodeWorkspace:
     """Split-K partial buffers + per-(seq, kv head) arrival counters for attn_decode
-    (allocated once per batch bucket; counters start at 0 and every launch re-arms them)."""
+    (allocated once per batch bucket; counters start at 0 and every launch re-arms them).
+    ``consumer_merge``: the attention launch writes only the split partials and returns them as AttnParts;
+    the o projection merges them itself (skinny_gemm.hip MERGE) or, on any other path, AttnParts.merged()
+    runs the merge kernel first."""
 
     def __init__(self, batch: int, hq: int, d: int, splits: int, device, hkv: Optional[int] = None,
-                 fused_combine: bool = False):
+                 fused_combine: bool = False, consumer_merge: bool = False):
+        self.consumer_merge = consumer_merge and not fused_combine
         # fused_combine (last-arriver merge inside the split kernel) measured SLOWER than the separate
         # merge kernel at every B >= 8 (the per-workgroup drain + agent release costs more than the
         # launch boundary it saves: B=39 238 vs 189 us), so the separate kernel is the default.
@@ -488,6 +495,44 @@ class DecodeWorkspace:
                          if fused_combine else None)
 
 
+# The o projection merges the attention splits (consumer_merge) when one decode row's partials are at most
+# this many bytes: every o workgroup re-reads them from L2, so the merge must stay short next to the weight
+# stream it hides under (TP=8 shard of Llama-3-8B at 4k: 4 heads x 63 splits x 512 B = 126 KiB).
+CONSUMER_MERGE_MAX_BYTES = 160 << 10
+MERGE_MAX_HQ = 16  # skinny_gemm.hip MERGE_MAX_HQ
+
+
+def consumer_merge_ok(batch: int, hq: int, splits: int, fused: bool) -> bool:
+    """Whether a decode bucket's attention leaves its split merge to the o projection (hip.DecodeWorkspace):
+    one row, a separate merge, at most MERGE_MAX_HQ query heads (a TP shard) and CONSUMER_MERGE_MAX_BYTES of
+    partials."""
+    return (batch == 1 and not fused and hq <= MERGE_MAX_HQ and splits <= MAX_SPLITS
+            and hq * splits * 128 * 4 <= CONSUMER_MERGE_MAX_BYTES)
+
+
+def merge_fits(merge: "AttnParts", N: int) -> bool:
+    """Can the N-column register-streaming residual producer merge these partials (skinny_gemm.hip MERGE)?"""
+    return (merge.B == 1 and merge.d == 128 and merge.hq <= MERGE_MAX_HQ and merge.ws.splits <= MAX_SPLITS
+            and merge.hq * 32 <= 64 * skinny_waves(N, 1, 1))
+
+
+class AttnParts:
+    """Decode attention output left as its split partials (DecodeWorkspace.consumer_merge): ``part_o``
+    [B, hq, S, d] / ``part_ml`` [B, hq, S, 2] fp32.  ``out`` is the [B, hq d] bf16 buffer the merge fills
+    when a consumer needs the rows (merged())."""
+
+    def __init__(self, ws: "DecodeWorkspace", B: int, hq: int, d: int, out: torch.Tensor):
+        self.ws, self.B, self.hq, self.d, self.out = ws, B, hq, d, out
+        self.shape = out.shape
+        self.device = out.device
+        self.dtype = out.dtype
+        self.is_cuda = out.is_cuda
+
+    def merged(self) -> torch.Tensor:
+        _check(_fn("mrsum_attn_decode_merge")(_p(self.ws.part_o), _p(self.ws.part_ml), _p(self.out),
+                                              self.out.stride(0), self.B, self.hq, self.ws.splits, _stream()),
+               "attn_decode_merge")
+        return self.out
 
 
 def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
@@ -516,12 +561,13 @@ def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.T
     if out is None:
         out = torch.empty(B, hq * d, dtype=torch.bfloat16, device=parts.device)
     _rows_ok(out)
+    cm = getattr(workspace, "consumer_merge", False)
     _check(_fn("mrsum_attn_decode_rope")(_p(parts), SP, _p(cos_sin), _p(kcache), _p(vcache), _p(block_tables),
                                          block_tables.stride(0), _p(positions), _p(workspace.part_o),
-                                         _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
-                                         workspace.splits, scale, _p(workspace.counters), kv8, _stream()),
+                                         _p(workspace.part_ml), None if cm else _p(out), out.stride(0), B, hq, hkv,
+                                         d, page, workspace.splits, scale, _p(workspace.counters), kv8, _stream()),
            "attn_decode_rope")
-    return out
+    return AttnParts(workspace, B, hq, d, out) if cm else out
 
 
 def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, block_tables: torch.Tensor,
@@ -546,12 +592,13 @@ def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, blo
     if out is None:
         out = torch.empty(B, hq * d, dtype=q.dtype, device=q.device)
     _rows_ok(out)
+    cm = getattr(workspace, "consumer_merge", False)
     _check(_fn("mrsum_attn_decode_mfma")(_p(q), q.stride(0), _p(kcache), _p(vcache), _p(block_tables),
                                          block_tables.stride(0), _p(positions), _p(workspace.part_o),
-                                         _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
-                                         workspace.splits, scale, _p(workspace.counters), kv8, _stream()),
+                                         _p(workspace.part_ml), None if cm else _p(out), out.stride(0), B, hq, hkv,
+                                         d, page, workspace.splits, scale, _p(workspace.counters), kv8, _stream()),
            "attn_decode_mfma")
-    return out
+    return AttnParts(workspace, B, hq, d, out) if cm else out
 
 
 # ------------------------------------------------------------------ sampler
@@ -693,9 +740,25 @@ def choose_splits(N: int, K: int, nt: int, target_wgs: int = 512, max_splits: in
     return best
 
 
-def _skinny(x, w, out, epi, nt, splits, ldo, norm=None, resid=None, ssp=None, ar=None):
+# Register-streaming kernels (skinny_gemm.hip) run 8-wave workgroups when the grid is at most
+# SKINNY_WAVES8_MAX_WGS workgroups (about one per CU or less: a TP shard's N / 16 tiles), so twice the weight
+# bytes are in flight per CU; larger grids already hold several 4-wave workgroups per CU.
+# ``SKINNY_WAVES_FORCE`` (4 / 8) overrides the choice for in-situ A/Bs (tools/exp_plans_insitu.py "waves:W").
+SKINNY_WAVES8_MAX_WGS = 2 * 256
+SKINNY_WAVES_FORCE = None
+
+
+def skinny_waves(N: int, nt: int, splits: int) -> int:
+    """Waves per workgroup (4 or 8) of a register-streaming launch of N / (16 nt) x splits workgroups."""
+    if SKINNY_WAVES_FORCE in (4, 8):
+        return SKINNY_WAVES_FORCE
+    return 8 if (N // (16 * nt)) * splits <= SKINNY_WAVES8_MAX_WGS else 4
+
+
+def _skinny(x, w, out, epi, nt, splits, ldo, norm=None, resid=None, ssp=None, ar=None, merge=None):
     """Register-streaming decode GEMM (skinny_gemm.hip).  ``norm``: deferred-RMSNorm input of the SwiGLU
-    epilogue; EPI_SKINNY_RESID: residual += x @ w^T (TP push over ``ar`` when given), ``ssp`` [M, N / 16]."""
+    epilogue; EPI_SKINNY_RESID: residual += x @ w^T (TP push over ``ar`` when given), ``ssp`` [M, N / 16];
+    ``merge`` (AttnParts, one row): x is that attention's split merge, done by the kernel itself."""
     _bf16_cuda(x, w)
     _rows_ok(x)
     M, K = x.shape
@@ -712,8 +775,17 @@ def _skinny(x, w, out, epi, nt, splits, ldo, norm=None, resid=None, ssp=None, ar
         _req(resid.shape == (M, N) and ssp is not None and ssp.dtype == torch.float32 and ssp.is_contiguous()
              and ssp.shape == (M, N // 16), "skinny resid: residual [M, N] bf16 and ssp fp32 [M, N / 16]")
         rp, ldr, sp = _p(resid), resid.stride(0), _p(ssp)
+    mo = mml = None
+    mS = 0
+    if merge is not None:
+        waves = skinny_waves(N, nt, splits)
+        _req(epi == EPI_SKINNY_RESID and M == 1 and merge.B == 1 and merge.hq * merge.d == K and merge.d == 128
+             and merge.hq <= MERGE_MAX_HQ and merge.hq * 32 <= 64 * waves and merge.ws.splits <= MAX_SPLITS,
+             "skinny resid: merge needs one row of hq <= %d heads" % MERGE_MAX_HQ)
+        mo, mml, mS = _p(merge.ws.part_o), _p(merge.ws.part_ml), merge.ws.splits
     _check(_fn("mrsum_skinny_gemm")(_p(x), x.stride(0), _p(w), N, K, M, _p(out), ldo, epi, nt, splits, sq, tiles, eps,
-                                    rp, ldr, sp, ar, _stream()), "skinny_gemm")
+                                    rp, ldr, sp, ar, mo, mml, mS, skinny_waves(N, nt, splits), _stream()),
+           "skinny_gemm")
     return out
 
 
@@ -935,29 +1007,40 @@ def stream_resid(x: torch.Tensor, w, residual: torch.Tensor, wpb: int, splits: i
     return ssp
 
 
-_RESID_CAP = []
+_RESID_CAP = {}
 
 
-def skinny_resid_capacity() -> int:
+def skinny_resid_capacity(N: Optional[int] = None) -> int:
     """Workgroups of the register-streaming residual producer resident at once on this device (a TP-push
-    grid of N / 16 workgroups must fit: every one spins on its peers' copies of its tile)."""
-    if not _RESID_CAP:
-        _RESID_CAP.append(int(_fn("mrsum_skinny_resid_capacity")()))
-    return _RESID_CAP[0]
+    grid of N / 16 workgroups must fit: every one spins on its peers' copies of its tile) -- for the
+    workgroup width that an N-column launch runs (skinny_waves), the 4-wave form without N."""
+    waves = skinny_waves(N, 1, 1) if N is not None else 4
+    if waves not in _RESID_CAP:
+        _RESID_CAP[waves] = int(_fn("mrsum_skinny_resid_capacity_w")(waves))
+    return _RESID_CAP[waves]
 
 
-def skinny_resid(x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, tp=None) -> torch.Tensor:
+def skinny_resid(x, w: torch.Tensor, residual: torch.Tensor, tp=None) -> torch.Tensor:
     """Deferred-RMSNorm producer on the register-streaming kernel (one 16-row tile per workgroup, no
     split-K, M <= 16): residual += x @ w^T -- all-reduced over the custom all-reduce group ``tp`` first
-    (TP push) when given; returns the fp32 [M, N / 16] per-tile row sums of squares of the new residual."""
-    M = x.shape[0]
+    (TP push) when given; returns the fp32 [M, N / 16] per-tile row sums of squares of the new residual.
+    ``x`` may be AttnParts (one decode row): the kernel merges the attention's splits itself."""
+    merge = x if isinstance(x, AttnParts) else None
     N = w.shape[0]
+    if merge is not None:
+        x = merge.out  # shape / pointer only: the kernel merges the partials instead of reading it
+        if merge_fits(merge, N):
+            STATS["consumer_merge"] += 1
+        else:
+            merge.merged()
+            merge = None
+    M = x.shape[0]
     ssp = torch.empty(M, N // 16, dtype=torch.float32, device=x.device)
     if tp is not None:
-        _req(N // 16 <= skinny_resid_capacity(), "skinny_resid: TP-push grid of %d workgroups is not fully "
-             "resident (capacity %d)" % (N // 16, skinny_resid_capacity()))
+        _req(N // 16 <= skinny_resid_capacity(N), "skinny_resid: TP-push grid of %d workgroups is not fully "
+             "resident (capacity %d)" % (N // 16, skinny_resid_capacity(N)))
         STATS["tp_push"] += 1
-    _skinny(x, w, None, EPI_SKINNY_RESID, 1, 1, 0, resid=residual, ssp=ssp, ar=tp)
+    _skinny(x, w, None, EPI_SKINNY_RESID, 1, 1, 0, resid=residual, ssp=ssp, ar=tp, merge=merge)
     return ssp
 
 
@@ -1011,7 +1094,7 @@ def add_rmsnorm_parts(parts: torch.Tensor, residual: torch.Tensor, w: torch.Tens
 # Streaming floor (probe): qkv 9.5, o 7.6, down 20.1, gate_up 39.1.
 # Plan = ("stream", wpb, S) | ("skinny", nt, S) | ("lds", S) | ("gemm",) (the 256 x 256-tile kernel)
 N_CU = 256
-STATS = {"tp_push": 0}  # host-side launch counts of selected paths (tests check which path ran)
+STATS = {"tp_push": 0, "consumer_merge": 0}  # host-side launch counts of selected paths (tests check which path ran)
 
 
 def stream_config(N: int, K: int, swiglu: bool = False, splits: Optional[int] = None, max_splits: int = 16):
@@ -1166,7 +1249,7 @@ def _skinny_fp8(x, w, out, epi, nt, splits, ldo, norm=None):
     _req(norm is None or skinny_fp8_takes_norm(M, K, splits), "skinny_fp8: a deferred norm needs M = 1")
     sq, tiles, eps = _norm_args(x, norm)
     _check(_fn("mrsum_skinny_fp8")(_p(x), x.stride(0), _p(w.q), _p(w.scale), N, K, M, _p(out), ldo, epi, nt, splits,
-                                   sq, tiles, eps, _stream()), "skinny_fp8")
+                                   sq, tiles, eps, skinny_waves(N, nt, splits), _stream()), "skinny_fp8")
     return out
 
 

@@ -553,7 +553,7 @@ def _push_case(h, kind: str, M: int, N: int, K: int, fp8: bool, role: str = "o")
         return None
     if rp is None or rp[0] != kind:
         return None
-    if kind == "skinny" and (fp8 or N // 16 > hip.skinny_resid_capacity()):
+    if kind == "skinny" and (fp8 or N // 16 > hip.skinny_resid_capacity(N)):
         return None
     return rp
 

@@ -55,8 +55,37 @@ def test_decode_attn_plan_class1_six_fused_splits():
     assert hip.decode_attn_plan(16, 8, 12288) == (6, True)
     # the final reduce (B=1, ~13k, <= 32k class) keeps 32 separate splits (best of 16-64 / fused in situ)
     assert hip.decode_attn_plan(1, 8, 32768) == (32, False)
-    # a TP shard's single kv head beyond 6k (config 5's 32k at TP=8): 64 separate splits, in situ
-    # (profiles/r5_attn_plans_deep.jsonl: 5.64 vs 6.22 ms per 70B fp8 shard step at 32 splits)
-    assert hip.decode_attn_plan(1, 1, 32768) == (64, False)
+    # a TP shard's single kv head beyond 6k (config 5's 32k at TP=8): one workgroup per 2 pages, up to the
+    # merge's 256 splits (64 splits measured 5.11 vs 5.66 ms per 70B fp8 shard step at 32, r5_attn_plans.jsonl)
+    assert hip.decode_attn_plan(1, 1, 32768) == (256, False)
+    assert hip.decode_attn_plan(16, 1, 32768) == (48, False)
+    assert all(hip.decode_attn_plan(b, h, c)[0] <= hip.MAX_SPLITS for b in (1, 2, 16, 64) for h in (1, 2, 8)
+               for c in (4096, 12288, 32768, 131072))
     # TP shards keep their measured cap of 4 in the longer classes
     assert hip.decode_attn_plan(20, 1, 12288)[0] <= 4
+
+
+def test_consumer_merge_only_for_one_row_of_a_tp_shard():
+    # the o projection merges the attention splits for one decode row of a TP shard when the partials every
+    # o workgroup re-reads stay small (8B TP=8 at 4k: 4 heads x 63 splits = 126 KiB)
+    assert hip.consumer_merge_ok(1, 4, 63, False)
+    assert not hip.consumer_merge_ok(1, 4, 63, True)     # the fused (in-launch) merge has no partials left
+    assert not hip.consumer_merge_ok(2, 4, 63, False)    # two rows
+    assert not hip.consumer_merge_ok(1, 32, 32, False)   # TP=1: 512 KiB per workgroup
+    assert not hip.consumer_merge_ok(1, 8, 256, False)   # 70B TP=8 at 32k: 1 MiB
+    assert not hip.consumer_merge_ok(1, 32, 2, False)    # more heads than the kernel's LDS row holds
+    old = hip.CONSUMER_MERGE_MAX_BYTES
+    try:
+        hip.CONSUMER_MERGE_MAX_BYTES = 0  # off (tools/exp_plans_insitu.py "cmerge:0")
+        assert not hip.consumer_merge_ok(1, 4, 63, False)
+    finally:
+        hip.CONSUMER_MERGE_MAX_BYTES = old
+
+
+def test_skinny_waves_rule():
+    # 8-wave workgroups where the grid is about one workgroup per CU or less (TP-shard N / 16 tiles)
+    assert hip.skinny_waves(3584, 1, 1) == 8      # 8B TP=8 gate_up: 224 workgroups
+    assert hip.skinny_waves(4096, 1, 1) == 8      # o / down producers: 256
+    assert hip.skinny_waves(7168, 1, 1) == 8      # 70B TP=8 gate_up: 448
+    assert hip.skinny_waves(57344, 1, 1) == 4     # 70B TP=1 gate_up: 3584
+    assert hip.skinny_waves(4096, 1, 4) == 4      # split-K slabs: 1024

@@ -217,7 +217,7 @@ def test_attn_prefill_spike(hq):
 
 
 @pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (4, 4), (16, 1), (6, 2), (24, 8), (10, 2)])
-@pytest.mark.parametrize("splits", [1, 3, 16, 48])
+@pytest.mark.parametrize("splits", [1, 3, 16, 48, 100])  # 100 > 64: the merge's lanes hold several splits
 @pytest.mark.parametrize("fused", [False, True])
 @pytest.mark.parametrize("kv8", ["bf16", "fp8", "fp8v"])
 def test_attn_decode(hq, hkv, splits, fused, kv8):
@@ -251,6 +251,70 @@ def test_attn_decode(hq, hkv, splits, fused, kv8):
         _close(o1, o2, 2e-2)
     if fused:
         assert int(ws.counters.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("splits,fused", [(64, False), (160, False), (256, False), (256, True)])
+def test_attn_decode_many_splits_one_kv_head(splits, fused):
+    """A TP shard's single kv head at a long context split up to the merge's 256 ways (decode_attn_plan's
+    TP-shard rule; the merge's lanes hold four splits each) -- vs the fp32 reference, replayed."""
+    hq, hkv, d, page, ctx = 8, 1, 128, 64, 20000
+    npg = -(-ctx // page)
+    g = torch.Generator().manual_seed(91)
+    kc = torch.randn(npg + 1, hkv, page, d, generator=g).to(torch.bfloat16).to(DEV)
+    vc = torch.randn(npg + 1, hkv, page, d, generator=g).to(torch.bfloat16).to(DEV)
+    bt = (torch.randperm(npg, generator=g).to(torch.int32) + 1).view(1, npg).to(DEV)
+    pos = torch.tensor([ctx - 1], dtype=torch.int32, device=DEV)
+    q = _rand(1, (hq + 2 * hkv) * d, seed=92)
+    sc = 1.0 / math.sqrt(d)
+    ws = hip.DecodeWorkspace(1, hq, d, splits, DEV, hip.decode_groups(hq, hkv), fused_combine=fused)
+    ws.part_o.fill_(float("nan"))
+    o2 = reference.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc)
+    for _ in range(2):
+        o1 = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws)
+        _close(o1, o2, 2e-2)
+
+
+@pytest.mark.parametrize("hq,splits,tp", [(4, 63, False), (4, 63, True), (8, 17, False), (16, 5, True), (2, 256, False)])
+def test_attn_consumer_merge_in_o_projection(hq, splits, tp):
+    """Decode attention that leaves its split merge to the o projection (DecodeWorkspace.consumer_merge ->
+    AttnParts; skinny_gemm.hip MERGE): the residual update and per-tile sums of squares equal the separate
+    merge + register-streaming producer's, and AttnParts.merged() equals the fp32 attention reference."""
+    from llm_map_reduce_summarizer_amd.parallel.custom_ar import LocalPush
+    hkv, d, page, ctx, N = 1, 128, 64, 17000, 4096  # 266 pages: every split holds keys
+    npg = -(-ctx // page)
+    g = torch.Generator().manual_seed(95)
+    kc = torch.randn(npg + 1, hkv, page, d, generator=g).to(torch.bfloat16).to(DEV)
+    vc = torch.randn(npg + 1, hkv, page, d, generator=g).to(torch.bfloat16).to(DEV)
+    bt = (torch.randperm(npg, generator=g).to(torch.int32) + 1).view(1, npg).to(DEV)
+    pos = torch.tensor([ctx - 1], dtype=torch.int32, device=DEV)
+    q = _rand(1, (hq + 2 * hkv) * d, seed=96)
+    sc = 1.0 / math.sqrt(d)
+    w = _rand(N, hq * d, scale=0.05, seed=97)
+    res0 = _rand(1, N, seed=98)
+    h = LocalPush(max_bytes=1 << 20) if tp else None
+    try:
+        push = h.push_handle() if tp else None
+        ws = hip.DecodeWorkspace(1, hq, d, splits, DEV, hkv, consumer_merge=True)
+        ws_ref = hip.DecodeWorkspace(1, hq, d, splits, DEV, hkv)
+        a_ref = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws_ref)
+        _close(a_ref, reference.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc), 2e-2)
+        r_ref = res0.clone()
+        ss_ref = hip.skinny_resid(a_ref, w, r_ref, tp=push)
+        n0 = hip.STATS["consumer_merge"]
+        for _ in range(2):  # replayed: partials overwritten, the merge re-done
+            parts = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws)
+            assert isinstance(parts, hip.AttnParts)
+            r = res0.clone()
+            ss = hip.skinny_resid(parts, w, r, tp=push)
+            _close(r, r_ref, 1e-2, 1e-2)
+            _close(ss, ss_ref, 1e-2, 1e-3)
+        assert hip.STATS["consumer_merge"] == n0 + 2
+        _close(parts.merged(), a_ref, 1e-2)
+        if tp:
+            assert h.error() == 0
+    finally:
+        if h is not None:
+            h.close()
 
 
 class _St:
@@ -906,6 +970,48 @@ def test_skinny_resid_producer(M, tp):
     finally:
         if h is not None:
             h.close()
+
+
+@pytest.mark.parametrize("waves", [4, 8])
+@pytest.mark.parametrize("M", [1, 7, 16, 40])
+def test_skinny_waves_every_epilogue(waves, M):
+    """Register-streaming kernels (bf16 and fp8 weights) with 4- and 8-wave workgroups (hip.skinny_waves):
+    bf16 out, split-K fp32 slabs (k blocks not a multiple of the wave count), SwiGLU with and without the
+    deferred norm, the residual producer -- against fp32 references."""
+    from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight, interleave_gate_up
+    old = hip.SKINNY_WAVES_FORCE
+    hip.SKINNY_WAVES_FORCE = waves
+    try:
+        N, K = 512, 1792  # 14 k blocks: 8 waves -> waves 6, 7 take one block fewer
+        x = _rand(M, K, seed=90)
+        w = _rand(N, K, scale=0.05, seed=91)
+        ref = x.float() @ w.float().t()
+        for nt in (1, 2):
+            out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+            _close(hip._skinny(x, w, out, hip.EPI_BF16, nt, 1, N), ref, 2e-2)
+        parts = torch.empty(7, M, N, dtype=torch.float32, device=DEV)
+        _close(hip._skinny(x, w, parts, hip.EPI_F32_PARTIAL, 1, 7, N).sum(0), ref, 2e-3, 2e-3)
+        wgu = interleave_gate_up(_rand(N, K, scale=0.05, seed=92), _rand(N, K, scale=0.05, seed=93)).contiguous()
+        g, u = (x.float() @ wgu.float().t()).reshape(M, -1, 2, 8).unbind(2)
+        act = hip.linear_swiglu(x, wgu, kernel="skinny")
+        _close(act, (g * torch.sigmoid(g) * u).reshape(M, N), 2e-2, 3e-2)
+        if M <= 16:
+            res0 = _rand(M, N, seed=94)
+            res = res0.clone()
+            ssp = hip.skinny_resid(x, w, res)
+            _close(res, (res0.float() + ref).to(torch.bfloat16), 3e-2, 2e-2)
+            _close(ssp, res.float().pow(2).reshape(M, N // 16, 16).sum(-1), 1e-2, 1e-3)
+            y = hip.linear_swiglu(res, wgu[:, :N].contiguous(), kernel="skinny", norm=(ssp, 1e-5))
+            xn = reference.rmsnorm(res, torch.ones(N, dtype=torch.bfloat16, device=DEV), 1e-5)
+            _close(y, hip.linear_swiglu(xn, wgu[:, :N].contiguous(), kernel="skinny"), 2e-2, 3e-2)
+        w8 = Fp8Weight.quantize(w)
+        ref8 = x.float() @ w8.dequant().t()
+        out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+        _close(hip._skinny_fp8(x, w8, out, hip.EPI_BF16, 1, 1, N), ref8, 2e-2)
+        parts = torch.empty(7, M, N, dtype=torch.float32, device=DEV)
+        _close(hip._skinny_fp8(x, w8, parts, hip.EPI_F32_PARTIAL, 2, 7, N).sum(0), ref8, 2e-3, 2e-3)
+    finally:
+        hip.SKINNY_WAVES_FORCE = old
 
 
 @pytest.mark.parametrize("add", [False, True])
