@@ -664,7 +664,7 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
                        int kv8, hipStream_t s) {
     if (B <= 0) return 0;
     if (D != 128 || P != 64 || Hkv <= 0 || Hq % Hkv || Hq / Hkv > 64 || S < 1 || S > MAX_SPLITS ||
-        (kv8 != 0 && kv8 != 2 && kv8 != 3) || (counters && !out))
+        (kv8 != 0 && kv8 != 2 && kv8 != 3) || !out)
         return (int)hipErrorInvalidValue;
     const int Hc = Hkv;                          // kv heads of the cache
     const int gq = decode_packed(Hq / Hc) ? 1 : Hq / Hc;
@@ -700,7 +700,7 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
 #undef MFMA_L
 #undef MFMA_K
     int e = (int)hipGetLastError();
-    if (e || counters || !out) return e;  // no out: partials only, merged by the consumer (skinny_gemm.hip MERGE)
+    if (e || counters) return e;
     if (S > 16) {
         // many splits (long contexts): one merge workgroup per query head instead of per kv-head group,
         // G x more workgroups with G x fewer partial loads each (B=1, 11k context, S=48: 8 workgroups
@@ -715,16 +715,6 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
         case 8: attn_decode_combine_kernel<8><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
         case 16: attn_decode_combine_kernel<16><<<B * Hkv, 256, 0, s>>>(PO, PM, (bf16*)out, out_stride, Hq, Hkv, S); break;
     }
-    return (int)hipGetLastError();
-}
-
-// The split merge alone (partials of an attention launch made without ``out``): out [B, Hq * D] bf16.
-MRSUM_API int mrsum_attn_decode_merge(const void* part_o, const void* part_ml, void* out, int out_stride, int B,
-                                      int Hq, int S, hipStream_t s) {
-    if (B <= 0) return 0;
-    if (!part_o || !part_ml || !out || Hq <= 0 || S < 1 || S > MAX_SPLITS) return (int)hipErrorInvalidValue;
-    attn_decode_combine_kernel<1><<<B * Hq, 256, 0, s>>>((const float*)part_o, (const float*)part_ml, (bf16*)out,
-                                                        out_stride, Hq, Hq, S);
     return (int)hipGetLastError();
 }
 

@@ -49,89 +49,7 @@ struct SkinnyNorm {
     int ldr;
     float* ssp;        // RESID producer: [M][gridDim.x] row sums of squares of the new residual per tile
     mrsum_ar::TPPush tp;
-    // MERGE (RESID, one row): x is not read -- it is the decode attention's split merge of part_o
-    // [1][Hq][mS][128] / part_ml [1][Hq][mS][2] (attn_decode.hip), done by every workgroup into LDS
-    const float* mo;
-    const float* mml;
-    int mS;
 };
-
-// Consumer-side split merge (attn_decode.hip combine_group, re-cut for one row and a 64 NW-thread
-// workgroup): x[h * 128 + d] = sum_s 2^(m_s - M) o_s[d] / sum_s 2^(m_s - M) l_s for the Hq = K / 128 heads,
-// written as bf16 into the LDS row ``xm``.  Every workgroup repeats it (the partials are L2-resident after
-// the first reader of each XCD); it runs after the workgroup's first weight loads are issued, under their
-// HBM latency, and the separate merge launch disappears.  Needs Hq * 32 <= 64 NW, S <= MERGE_MAX_S.
-constexpr int MERGE_MAX_S = 256, MERGE_MAX_HQ = 16, MERGE_PRE = 8;
-template <int NW>
-__device__ __forceinline__ void merge_row_to_lds(const SkinnyNorm& e, int K, bf16* xm, float* sw, float* sden,
-                                                 float4* scratch) {
-    constexpr int NTH = 64 * NW, D = 128;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int Hq = K / D, S = e.mS;
-    const int NV = Hq * (D / 4), NH = NTH / NV;  // float4 items, split subsets per item
-    const int item = tid % NV, hs = tid / NV, head = item / (D / 4), d4 = item % (D / 4);
-    const float4* po = reinterpret_cast<const float4*>(e.mo) + (size_t)head * S * (D / 4) + d4;
-    // 1. the first MERGE_PRE slabs of this thread's subset, issued before the split weights are known
-    float4 pre[MERGE_PRE];
-#pragma unroll
-    for (int j = 0; j < MERGE_PRE; ++j) {
-        const int sp = hs + j * NH;
-        const float4 v = po[(size_t)min(sp, S - 1) * (D / 4)];  // unconditional (clamped) load
-        pre[j] = (hs < NH && sp < S) ? v : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    // 2. split weights: one wave per head, lane l holds splits l + 64 q
-    for (int g = wv; g < Hq; g += NW) {
-        float ms[4], ls[4], mloc = -INFINITY;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int sp = lane + 64 * q;
-            const float2 v = reinterpret_cast<const float2*>(e.mml)[g * S + min(sp, S - 1)];
-            ms[q] = sp < S ? v.x : -INFINITY;
-            ls[q] = sp < S ? v.y : 0.f;
-            mloc = fmaxf(mloc, ms[q]);
-        }
-        const float M = wave_max(mloc);
-        float wl = 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int sp = lane + 64 * q;
-            const float w = ms[q] == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(ms[q] - M);
-            wl += w * ls[q];
-            if (sp < S) sw[g * S + sp] = w;
-        }
-        const float den = wave_sum(wl);
-        if (lane == 0) sden[g] = den;
-    }
-    __syncthreads();
-    // 3. weighted sums, subsets merged through LDS, bf16 into the row
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (hs < NH) {
-        const float* w = sw + head * S;
-#pragma unroll
-        for (int j = 0; j < MERGE_PRE; ++j) {
-            const int sp = hs + j * NH;
-            const float ws = sp < S ? w[sp] : 0.f;
-            acc.x += ws * pre[j].x; acc.y += ws * pre[j].y; acc.z += ws * pre[j].z; acc.w += ws * pre[j].w;
-        }
-        for (int sp = hs + MERGE_PRE * NH; sp < S; sp += NH) {
-            const float4 v = po[(size_t)sp * (D / 4)];
-            const float ws = w[sp];
-            acc.x += ws * v.x; acc.y += ws * v.y; acc.z += ws * v.z; acc.w += ws * v.w;
-        }
-    }
-    scratch[tid] = acc;
-    __syncthreads();
-    if (hs == 0) {
-        for (int j = 1; j < NH; ++j) {
-            const float4 v = scratch[j * NV + item];
-            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
-        }
-        const float den = sden[head];
-        const float inv = den > 0.f ? 1.f / den : 0.f;
-        *reinterpret_cast<uint2*>(xm + head * D + 4 * d4) =
-            make_uint2(pack2(acc.x * inv, acc.y * inv), pack2(acc.z * inv, acc.w * inv));
-    }
-}
 
 // Deferred norm of row m, in stream_gemm.hip's order: partial p (< 8) of ssq_tiles / 8 consecutive tiles
 // summed in float4 steps (thread 8 m + p; its loads issued in the kernel prologue, into registers, so they
@@ -224,10 +142,42 @@ __device__ __forceinline__ void mma_block(f32x4 (&acc)[NT][MT], const AFrag<NT>&
 }
 }  // namespace
 
+// RESID epilogue of one item (4 consecutive columns c .. c+3 of row m, product v): h = bf16(residual + v) (+
+// the TP group's copies of the item, rank order, when e.tp.world > 0); returns the item's sum of h^2.
+__device__ __forceinline__ float resid_item(const SkinnyNorm& e, int m, int c, int width, unsigned tp_epoch,
+                                            const float (&v)[4]) {
+    uint2* rp = reinterpret_cast<uint2*>(e.resid + (size_t)m * e.ldr + c);
+    const uint2 rv = *rp;
+    float4 a = make_float4(v[0], v[1], v[2], v[3]);
+    if (e.tp.world > 0) {
+        const long long off = mrsum_ar::tp_item_off(m, width, c);
+        mrsum_ar::tp_push_item(e.tp, off, tp_epoch, a);
+        a = mrsum_ar::tp_gather_item(e.tp, off, tp_epoch);
+    }
+    const uint2 hv = make_uint2(pack2(__uint_as_float(rv.x << 16) + a.x, __uint_as_float(rv.x & 0xffff0000u) + a.y),
+                                pack2(__uint_as_float(rv.y << 16) + a.z, __uint_as_float(rv.y & 0xffff0000u) + a.w));
+    *rp = hv;
+    const float h0 = __uint_as_float(hv.x << 16), h1 = __uint_as_float(hv.x & 0xffff0000u);
+    const float h2 = __uint_as_float(hv.y << 16), h3 = __uint_as_float(hv.y & 0xffff0000u);
+    return (h0 * h0 + h1 * h1) + (h2 * h2 + h3 * h3);
+}
+
+// RESID tail: the 16-column tile's row sums of h^2 (the 4 items' sums in ``rows[m][0, 4, 8, 12]``) to
+// ssp[m][tile], then the TP push epoch of the tile's granule.
+template <typename Rows>
+__device__ __forceinline__ void resid_tail(const SkinnyNorm& e, const Rows& rows, int M, int n0, unsigned tp_epoch) {
+    __syncthreads();
+    if (threadIdx.x < M) {
+        const float* q = rows[threadIdx.x];
+        e.ssp[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = ((q[0] + q[4]) + (q[8] + q[12]));
+    }
+    if (e.tp.world > 0 && threadIdx.x == 0) e.tp.epochs[n0 / mrsum_ar::GRAN] = tp_epoch;
+}
+
 // NW = waves per workgroup (4 or 8), interleaved over the k blocks: a grid of about one workgroup per CU
 // (a TP shard's N / 16 tiles) keeps only NW x two blocks of W in flight per CU, so the 8-wave form doubles the
 // bytes in flight where the grid cannot (Little's law: ~32 KiB per CU in flight is ~3 TB/s at decode latency).
-template <int NT, int MT, int EPI, int NW = 4, bool MERGE = false>
+template <int NT, int MT, int EPI, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void skinny_gemm_kernel(const bf16* __restrict__ x, int ldx,
                                                               const bf16* __restrict__ W, int K, int M,
                                                               void* __restrict__ out, int ldo, int kper,
@@ -235,13 +185,7 @@ __global__ __launch_bounds__(64 * NW) void skinny_gemm_kernel(const bf16* __rest
     constexpr int BN = 16 * NT, BM = 16 * MT;
     static_assert(EPI != EPI_RESID || (NT == 1 && MT == 1), "RESID: one 16-row tile, M <= 16");
     static_assert(NW == 4 || NW == 8, "4 or 8 waves");
-    static_assert(!MERGE || (EPI == EPI_RESID && MT == 1), "MERGE: the residual producer of one row");
     __shared__ __attribute__((aligned(16))) float red[NW][BM][BN + 4];
-    // MERGE: the merged x row (bf16, K <= 2048), split weights, per-head denominators, subset partials
-    __shared__ __attribute__((aligned(16))) bf16 xm[MERGE ? MERGE_MAX_HQ * 128 : 1];
-    __shared__ float msw[MERGE ? MERGE_MAX_HQ * MERGE_MAX_S : 1];
-    __shared__ float msden[MERGE ? MERGE_MAX_HQ : 1];
-    __shared__ float4 mscr[MERGE ? 64 * NW : 1];
     __shared__ float s_part[EPI == EPI_SWIGLU ? 8 * BM : 1];  // deferred-norm partials [m][8]
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int n0 = blockIdx.x * BN;
@@ -275,20 +219,7 @@ __global__ __launch_bounds__(64 * NW) void skinny_gemm_kernel(const bf16* __rest
     AFrag<NT> a0, a1;
     BFrag<MT> b;
     if (nb > 0) load_a<NT>(a0, W, K, n0, kb0, lane);
-    if constexpr (MERGE) {
-        merge_row_to_lds<NW>(e, K, xm, msw, msden, mscr);  // under the first weight block's latency
-        __syncthreads();
-    }
-    // x fragments of k block kb: global rows, or (MERGE) the merged row in LDS
-    auto ldb = [&](int kb) {
-        if constexpr (MERGE) {
-            const bf16* p = xm + kb + 8 * (lane >> 4);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) b.v[0][q] = *reinterpret_cast<const uint4*>(p + 32 * q);
-        } else {
-            load_b<MT>(b, x, ldx, M, kb, lane);
-        }
-    };
+    auto ldb = [&](int kb) { load_b<MT>(b, x, ldx, M, kb, lane); };
     int i = 0;
     for (; i + 2 < nb; i += 2) {  // blocks i and i + 1, each with a successor
         const int kb = kb0 + i * STEP;
@@ -341,22 +272,7 @@ __global__ __launch_bounds__(64 * NW) void skinny_gemm_kernel(const bf16* __rest
             float* o = reinterpret_cast<float*>(out) + ((size_t)blockIdx.y * M + m) * ldo + n0 + n4;
             *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
         } else if constexpr (EPI == EPI_RESID) {
-            // h = bf16(residual + tile) (+ the TP group's tiles, rank order); the tile's row sum of h^2
-            // over its 4 items (lanes 4m .. 4m+3 of wave 0) to ssp[m][tile]
-            uint2* rp = reinterpret_cast<uint2*>(e.resid + (size_t)m * e.ldr + n0 + n4);
-            const uint2 rv = *rp;
-            float4 a = make_float4(v[0], v[1], v[2], v[3]);
-            if (e.tp.world > 0) {
-                const long long off = mrsum_ar::tp_item_off(m, gridDim.x * BN, n0 + n4);
-                mrsum_ar::tp_push_item(e.tp, off, tp_epoch, a);
-                a = mrsum_ar::tp_gather_item(e.tp, off, tp_epoch);
-            }
-            const uint2 hv = make_uint2(pack2(__uint_as_float(rv.x << 16) + a.x, __uint_as_float(rv.x & 0xffff0000u) + a.y),
-                                        pack2(__uint_as_float(rv.y << 16) + a.z, __uint_as_float(rv.y & 0xffff0000u) + a.w));
-            *rp = hv;
-            const float h0 = __uint_as_float(hv.x << 16), h1 = __uint_as_float(hv.x & 0xffff0000u);
-            const float h2 = __uint_as_float(hv.y << 16), h3 = __uint_as_float(hv.y & 0xffff0000u);
-            red[0][m][n4] = (h0 * h0 + h1 * h1) + (h2 * h2 + h3 * h3);  // own slot: every red read is done
+            red[0][m][n4] = resid_item(e, m, n0 + n4, gridDim.x * BN, tp_epoch, v);  // own slot: reads are done
         } else {  // SWIGLU: tile rows [0, BN/2) gate, [BN/2, BN) up of features [blockIdx.x*BN/2, +BN/2)
             constexpr int H = BN / 2;
             if (n4 < H) {
@@ -375,14 +291,7 @@ __global__ __launch_bounds__(64 * NW) void skinny_gemm_kernel(const bf16* __rest
             }
         }
     }
-    if constexpr (EPI == EPI_RESID) {
-        __syncthreads();
-        if (threadIdx.x < M) {
-            const float* q = red[0][threadIdx.x];
-            e.ssp[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = ((q[0] + q[4]) + (q[8] + q[12]));
-        }
-        if (e.tp.world > 0 && threadIdx.x == 0) e.tp.epochs[n0 / mrsum_ar::GRAN] = tp_epoch;
-    }
+    if constexpr (EPI == EPI_RESID) resid_tail(e, red[0], M, n0, tp_epoch);
 }
 
 template <int NT, int EPI, int NW>
@@ -408,16 +317,11 @@ MRSUM_API int mrsum_skinny_resid_capacity_w(int waves) {
         int dev = 0, cus = 0, per = 0;
         hipError_t st = hipGetDevice(&dev);
         if (st == hipSuccess) st = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        // the smaller of the plain and the split-merging (MERGE, more LDS) instantiation
-        int pm = 0;
         if (st == hipSuccess)
             st = i ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, skinny_gemm_kernel<1, 1, EPI_RESID, 8>, 512, 0)
                    : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, skinny_gemm_kernel<1, 1, EPI_RESID, 4>, 256, 0);
-        if (st == hipSuccess)
-            st = i ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&pm, skinny_gemm_kernel<1, 1, EPI_RESID, 8, true>, 512, 0)
-                   : hipOccupancyMaxActiveBlocksPerMultiprocessor(&pm, skinny_gemm_kernel<1, 1, EPI_RESID, 4, true>, 256, 0);
         if (st != hipSuccess) return 0;
-        cap[i] = cus * std::min(per, pm);
+        cap[i] = cus * per;
     }
     return cap[i];
 }
@@ -430,11 +334,9 @@ MRSUM_API int mrsum_skinny_resid_capacity() { return mrsum_skinny_resid_capacity
 // M * N * 4 <= its slot bytes)).  nt: 16-row W tiles per workgroup (1 or 2; swiglu needs 1); splits: S (K/S
 // multiple of 128).  ssq (swiglu only): deferred-RMSNorm input [M, ssq_tiles] fp32, ssq_tiles % 32 == 0.
 // waves: 4 or 8 per workgroup (kernel header).
-// mo / mml / mS (epi 3, M = 1, K <= 2048): x is the split merge of decode-attention partials (kernel MERGE).
 MRSUM_API int mrsum_skinny_gemm(const void* x, int ldx, const void* W, int N, int K, int M, void* out, int ldo,
                                 int epi, int nt, int splits, const float* ssq, int ssq_tiles, float eps, void* resid,
-                                int ldr, float* ssp, void* ar, const float* mo, const float* mml, int mS, int waves,
-                                hipStream_t s) {
+                                int ldr, float* ssp, void* ar, int waves, hipStream_t s) {
     using namespace mrsum_ar;
     if (M <= 0) return 0;
     if (M > 64 || K % KB || splits < 1 || (K / KB) % splits || (nt != 1 && nt != 2) || N % (16 * nt) ||
@@ -452,15 +354,10 @@ MRSUM_API int mrsum_skinny_gemm(const void* x, int ldx, const void* W, int N, in
             if (!h->peers.base[r]) return (int)hipErrorInvalidValue;
     }
     if (ar && N / 16 > mrsum_skinny_resid_capacity_w(waves)) return (int)hipErrorInvalidValue;  // header: progress
-    const bool merge = mo != nullptr;
-    if (merge && (epi != EPI_RESID || M != 1 || !mml || mS < 1 || mS > MERGE_MAX_S || K % 128 ||
-                  K / 128 > MERGE_MAX_HQ || (K / 128) * 32 > 64 * waves))
-        return (int)hipErrorInvalidValue;
     SkinnyNorm e;
     e.ssq = ssq; e.ssq_tiles = ssq_tiles; e.inv_k = 1.f / (float)K; e.eps = eps;
     e.resid = (bf16*)resid; e.ldr = ldr; e.ssp = ssp;
     e.tp = tp_push_of((const ArHandle*)ar);
-    e.mo = mo; e.mml = mml; e.mS = mS;
     const int kper = K / splits;
     const int mt = (M + 15) / 16;
     dim3 grid(N / (16 * nt), splits);
@@ -472,10 +369,7 @@ MRSUM_API int mrsum_skinny_gemm(const void* x, int ldx, const void* W, int N, in
         if (epi == EPI_BF16) BY_W(1, EPI_BF16);
         if (epi == EPI_F32_PARTIAL) BY_W(1, EPI_F32_PARTIAL);
         if (epi == EPI_SWIGLU) BY_W(1, EPI_SWIGLU);
-        if (merge) {
-            if (waves == 8) skinny_gemm_kernel<1, 1, EPI_RESID, 8, true><<<grid, 512, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, e);
-            else skinny_gemm_kernel<1, 1, EPI_RESID, 4, true><<<grid, 256, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, e);
-        } else if (waves == 8) {
+        if (waves == 8) {
             skinny_gemm_kernel<1, 1, EPI_RESID, 8><<<grid, 512, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, e);
         } else {
             skinny_gemm_kernel<1, 1, EPI_RESID, 4><<<grid, 256, 0, s>>>(X, ldx, Wp, K, M, out, ldo, kper, e);
@@ -730,20 +624,25 @@ __device__ __forceinline__ void mma_block8(f32x4 (&acc)[NT][MT], const A8Frag<NT
 // ``ssq`` [1][ssq_tiles] its producer's per-tile sums of squares, reduced in the stream consumer's fixed
 // order (8 partials of ssq_tiles / 8 tiles, float4 steps) so both consumers scale by the same factor.
 // NW = 4 or 8 waves per workgroup (skinny_gemm_kernel header: bytes in flight per CU on small grids).
+// EPI_RESID (one 16-row tile, M <= 16): the residual producer of skinny_gemm_kernel with fp8 weights --
+// residual += x W^T (after the TP push when e.tp.world > 0), per-tile row sums of squares to e.ssp.
 template <int NT, int MT, int EPI, bool XL, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void skinny_fp8_kernel(const bf16* __restrict__ x, int ldx,
                                                              const uint8_t* __restrict__ W,
                                                              const float* __restrict__ wscale, int K, int M,
                                                              void* __restrict__ out, int ldo, int kper,
-                                                             const float* __restrict__ ssq, int ssq_tiles, float eps) {
+                                                             const float* __restrict__ ssq, int ssq_tiles, float eps,
+                                                             const SkinnyNorm e) {
     constexpr int BN = 16 * NT, BM = 16 * MT;
     static_assert(!XL || MT == 1, "the LDS x slice holds one row");
+    static_assert(EPI != EPI_RESID || (NT == 1 && MT == 1), "RESID: one 16-row tile, M <= 16");
     __shared__ __attribute__((aligned(16))) float red[NW][BM][BN + 4];
     __shared__ float s_ss[8];
     extern __shared__ __attribute__((aligned(16))) char xs[];  // XL: kper bf16 of x row 0
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int n0 = blockIdx.x * BN;
     const int ks = blockIdx.y * kper, ke = min(K, ks + kper);
+    const unsigned tp_epoch = EPI == EPI_RESID && e.tp.world > 0 ? e.tp.epochs[n0 / mrsum_ar::GRAN] + 1 : 0;
     if constexpr (XL) {
         const uint4* src = reinterpret_cast<const uint4*>(x + ks);
         for (int i = threadIdx.x; i < kper / 8; i += 64 * NW) reinterpret_cast<uint4*>(xs)[i] = src[i];
@@ -836,6 +735,8 @@ __global__ __launch_bounds__(64 * NW) void skinny_fp8_kernel(const bf16* __restr
         } else if constexpr (EPI == EPI_F32_PARTIAL) {
             float* o = reinterpret_cast<float*>(out) + ((size_t)blockIdx.y * M + m) * ldo + n0 + n4;
             *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+        } else if constexpr (EPI == EPI_RESID) {
+            red[0][m][n4] = resid_item(e, m, n0 + n4, gridDim.x * BN, tp_epoch, v);  // own slot: reads are done
         } else {  // SWIGLU, nt == 1: rows [0, 8) gate, [8, 16) up
             constexpr int H = BN / 2;
             if (n4 < H) {
@@ -852,19 +753,36 @@ __global__ __launch_bounds__(64 * NW) void skinny_fp8_kernel(const bf16* __restr
             }
         }
     }
+    if constexpr (EPI == EPI_RESID) resid_tail(e, red[0], M, n0, tp_epoch);
 }
+
+MRSUM_API int mrsum_skinny_fp8_resid_capacity();
 
 // ssq (deferred-RMSNorm input, M = 1 with the x slice in LDS only): [1][ssq_tiles] fp32 row sums of squares
 // of x per producer tile, ssq_tiles % 32 == 0; the product is scaled by rsqrt(sum / K + eps).  waves: 4 or 8.
+// epi 3 (residual update, mrsum_skinny_gemm's contract): resid [M, ldr] bf16 += x W^T, ssp [M, N / 16]; nt 1,
+// splits 1, M <= 16; ``ar``: TP push over that custom all-reduce group.
 MRSUM_API int mrsum_skinny_fp8(const void* x, int ldx, const void* W, const float* wscale, int N, int K, int M,
                                void* out, int ldo, int epi, int nt, int splits, const float* ssq, int ssq_tiles,
-                               float eps, int waves, hipStream_t s) {
+                               float eps, void* resid, int ldr, float* ssp, void* ar, int waves, hipStream_t s) {
+    using namespace mrsum_ar;
     if (M <= 0) return 0;
     if (M > 64 || K % KB || splits < 1 || (K / KB) % splits || (nt != 1 && nt != 2) || N % (16 * nt) ||
-        (waves != 4 && waves != 8))
+        (waves != 4 && waves != 8) || epi < EPI_BF16 || epi > EPI_RESID)
         return (int)hipErrorInvalidValue;
     if (epi != EPI_F32_PARTIAL && splits != 1) return (int)hipErrorInvalidValue;
     if (epi == EPI_SWIGLU && nt != 1) return (int)hipErrorInvalidValue;
+    if (epi == EPI_RESID && (nt != 1 || M > 16 || !resid || !ssp || ldr % 4 || ssq)) return (int)hipErrorInvalidValue;
+    if (ar) {
+        auto h = (const ArHandle*)ar;
+        if (epi != EPI_RESID || N / GRAN > MAX_GRAN || (size_t)M * N * 4 > h->max_bytes) return (int)hipErrorInvalidValue;
+        for (int r = 0; r < h->world; ++r)
+            if (!h->peers.base[r]) return (int)hipErrorInvalidValue;
+        if (N / 16 > mrsum_skinny_fp8_resid_capacity()) return (int)hipErrorInvalidValue;  // every pusher resident
+    }
+    SkinnyNorm e{};
+    e.resid = (bf16*)resid; e.ldr = ldr; e.ssp = ssp;
+    e.tp = tp_push_of((const ArHandle*)ar);
     const int kper = K / splits;
     const int mt = (M + 15) / 16;
     dim3 grid(N / (16 * nt), splits);
@@ -873,10 +791,10 @@ MRSUM_API int mrsum_skinny_fp8(const void* x, int ldx, const void* W, const floa
     if (ssq && (!xl || ssq_tiles <= 0 || ssq_tiles % 32)) return (int)hipErrorInvalidValue;
 #define L(NT_, MT_, EPI_, NW_)                                                                                  \
     skinny_fp8_kernel<NT_, MT_, EPI_, false, NW_><<<grid, 64 * NW_, 0, s>>>(X, ldx, Wp, wscale, K, M, out, ldo, kper, \
-                                                                          nullptr, 0, 0.f)
+                                                                          nullptr, 0, 0.f, e)
 #define L1(NT_, EPI_, NW_)                                                                                      \
     if (xl) skinny_fp8_kernel<NT_, 1, EPI_, true, NW_><<<grid, 64 * NW_, kper * 2, s>>>(X, ldx, Wp, wscale, K, M, out, \
-                                                                                      ldo, kper, ssq, ssq_tiles, eps); \
+                                                                                      ldo, kper, ssq, ssq_tiles, eps, e); \
     else L(NT_, 1, EPI_, NW_)
 #define BY_MT(NT_, EPI_, NW_)                   \
     switch (mt) {                               \
@@ -889,7 +807,8 @@ MRSUM_API int mrsum_skinny_fp8(const void* x, int ldx, const void* W, const floa
     if (nt == 1) {                                                            \
         if (epi == EPI_BF16) { BY_MT(1, EPI_BF16, NW_) }                      \
         else if (epi == EPI_F32_PARTIAL) { BY_MT(1, EPI_F32_PARTIAL, NW_) }   \
-        else { BY_MT(1, EPI_SWIGLU, NW_) }                                    \
+        else if (epi == EPI_SWIGLU) { BY_MT(1, EPI_SWIGLU, NW_) }             \
+        else { L1(1, EPI_RESID, NW_); }                                       \
     } else {                                                                  \
         if (epi == EPI_BF16) { BY_MT(2, EPI_BF16, NW_) }                      \
         else { BY_MT(2, EPI_F32_PARTIAL, NW_) }                               \
@@ -900,4 +819,32 @@ MRSUM_API int mrsum_skinny_fp8(const void* x, int ldx, const void* W, const floa
 #undef L1
 #undef L
     return (int)hipGetLastError();
+}
+
+// Workgroups of the fp8 residual producer resident at once (the smaller of the 4- / 8-wave, LDS-x / global-x
+// forms; a TP-push grid of N / 16 workgroups must fit, as for mrsum_skinny_resid_capacity_w).
+MRSUM_API int mrsum_skinny_fp8_resid_capacity() {
+    static int cap = -1;
+    if (cap < 0) {
+        int dev = 0, cus = 0, lo = 1 << 30;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 0;
+        int per = 0;
+        // the LDS-x form is sized for the largest x slice it takes (56 KiB)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, skinny_fp8_kernel<1, 1, EPI_RESID, true, 4>, 256,
+                                                         56 * 1024) != hipSuccess) return 0;
+        lo = std::min(lo, per);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, skinny_fp8_kernel<1, 1, EPI_RESID, true, 8>, 512,
+                                                         56 * 1024) != hipSuccess) return 0;
+        lo = std::min(lo, per);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, skinny_fp8_kernel<1, 1, EPI_RESID, false, 4>, 256, 0)
+            != hipSuccess) return 0;
+        lo = std::min(lo, per);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, skinny_fp8_kernel<1, 1, EPI_RESID, false, 8>, 512, 0)
+            != hipSuccess) return 0;
+        lo = std::min(lo, per);
+        cap = cus * lo;
+    }
+    return cap;
 }

@@ -285,13 +285,11 @@ class LLMEngine:
         key = (B, self._ctx_cls)
         ws = self._workspaces.get(key)
         if ws is None:
-            from ..ops.hip import CTX_CLASSES, DecodeWorkspace, consumer_merge_ok, decode_attn_plan, decode_groups
+            from ..ops.hip import CTX_CLASSES, DecodeWorkspace, decode_attn_plan, decode_groups
             ng = decode_groups(self.model.hq, self.model.hkv)  # kv heads, or query heads for odd GQA ratios
             s, fused = decode_attn_plan(B, ng, min(CTX_CLASSES[self._ctx_cls], self.max_model_len),
                                         kv8=self.kv.kv_dtype if self.kv.fp8 else False)
-            # one row of a TP shard: the o projection merges the attention splits (no merge launch)
-            ws = DecodeWorkspace(B, self.model.hq, self.cfg.head_dim, s, self.device, ng, fused_combine=fused,
-                                 consumer_merge=consumer_merge_ok(B, self.model.hq, s, fused))
+            ws = DecodeWorkspace(B, self.model.hq, self.cfg.head_dim, s, self.device, ng, fused_combine=fused)
             self._workspaces[key] = ws
         return ws
 

@@ -352,6 +352,13 @@ DEFER_NORM_MAX_M = 16
 # on a TP=8 shard: profiles/r3_tp8shard_b20_gaps.txt), so the TP push runs at every decode batch the
 # stream kernel takes.
 TP_PUSH_MAX_M = 64
+# fp8 weights: the TP-push producer of a row-parallel shard projection runs on the fp8 register-streaming
+# kernel (skinny_gemm.hip skinny_fp8_kernel EPI_RESID, no split-K tail) instead of the split-K stream kernel
+# for K <= FP8_SKINNY_PUSH_MAX_K, and at one row for K <= FP8_SKINNY_PUSH_MAX_K_M1.  In situ, Llama-3-70B fp8
+# TP=8 shard (profiles/r5_fp8_skinny_push_ab.jsonl): B=1 at 32k 4.77 ms -> o 4.64, down 4.62; B=10 at 4k
+# 5.74 -> o 5.58, but down (K 3584) 5.87
+FP8_SKINNY_PUSH_MAX_K = 1024
+FP8_SKINNY_PUSH_MAX_K_M1 = 4096
 
 
 RESID_FORCE = {}  # role -> "skinny" | "stream": measurement override of _resid_plan (tools only)
@@ -378,8 +385,12 @@ def _resid_plan(hip, a, w, role, tp=False, force=None):
                (hip.plan(role, M, N, K)[1:] if hip.plan(role, M, N, K)[0] == "stream" else hip.tp_resid_config(N, K)))
         return None if cfg is None or (N // (16 * cfg[0])) % 32 else ("stream",) + tuple(cfg)
     if isinstance(w, Fp8Weight):
-        if force == "skinny":
-            return None
+        if force == "skinny" or (force is None and tp and (K <= FP8_SKINNY_PUSH_MAX_K or
+                                                           (M == 1 and K <= FP8_SKINNY_PUSH_MAX_K_M1))):
+            # the fp8 register-streaming producer (one 16-row tile per workgroup, no split-K tail)
+            ok = M <= 16 and N % 512 == 0 and N // 16 <= hip.skinny_fp8_resid_capacity()
+            if ok or force == "skinny":
+                return ("skinny",) if ok else None
         cfg = hip.fp8_resid_cfg(M, N, K)
     else:
         p = hip.plan(role, M, N, K)
@@ -412,15 +423,9 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None, quant=F
     all-reduces its tile over the group first (TP push), so no all-reduce kernel runs either.  ``all_reduce`` is a callable summing a tensor over
     the TP group in place; when it also offers ``add_rmsnorm``/``fused_ok`` (the model's P2P
     all-reduce) the decode path runs the projection's split-K slabs straight into one fused
-    all-reduce + residual add + RMSNorm kernel.
-
-    ``a`` may be the decode attention's split partials (ops.hip.AttnParts, one row): the register-streaming
-    residual producer merges them itself; every other path merges them first (the merge kernel)."""
-    merge = None
+    all-reduce + residual add + RMSNorm kernel."""
     if _use_hip(a):
         from . import hip
-        if isinstance(a, hip.AttnParts):
-            merge, a = a, a.out
         if ln is None and a.shape[0] <= hip.SKINNY_MAX_M:
             # TP: the producer all-reduces its own tiles (TP push) when the group's buffers take the rows
             ok = getattr(all_reduce, "push_ok", None)
@@ -436,13 +441,9 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None, quant=F
                     if rp is not None and rp[0] == "skinny" and w.shape[0] // 16 > hip.skinny_resid_capacity(w.shape[0]):
                         rp = None
                 if rp is not None and rp[0] == "skinny":
-                    return NormRows(residual, hip.skinny_resid(merge or a, w, residual, tp=push), eps)
+                    return NormRows(residual, hip.skinny_resid(a, w, residual, tp=push), eps)
                 if rp is not None:
-                    if merge is not None:
-                        merge.merged()  # fills a
                     return NormRows(residual, hip.stream_resid(a, w, residual, rp[1], rp[2], tp=push), eps)
-        if merge is not None:
-            merge.merged()  # fills a
     if ln is None:
         ln = unit_gain(residual.shape[1], residual.device)
     if _use_hip(a) and isinstance(w, Fp8Weight):

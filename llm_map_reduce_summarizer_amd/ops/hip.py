@@ -31,25 +31,26 @@ _SIGS = {
     "mrsum_swiglu": [_vp, _vp, _c_int, _c_int, _vp],
     "mrsum_kv_scatter": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp],
     "mrsum_embed": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _vp],
-    "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
+    "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int,
+                           _vp],
     "mrsum_attn_prefill_paged": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float,
                                  _vp,
-                                 _vp, _vp, _c_int, _vp, _vp, _c_int, _vp],
+                                 _vp, _vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "mrsum_attn_decode_mfma": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int,
                                _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _c_int, _vp],
     "mrsum_attn_decode_rope": [_vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int,
                                _c_int, _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _c_int, _vp],
     "mrsum_skinny_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _c_int,
-                          _c_float, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _vp],
+                          _c_float, _vp, _c_int, _vp, _vp, _c_int, _vp],
     "mrsum_skinny_resid_capacity_w": [_c_int],
-    "mrsum_attn_decode_merge": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_skinny_lds": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp],
     "mrsum_stream_gemm": [_vp, _c_int, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp,
                           _vp, _c_int, _c_float, _vp, _c_int, _vp, _c_int, _vp, _vp],
     "mrsum_stream_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp,
                          _vp, _c_int, _c_float, _vp, _c_int, _vp, _vp, _vp],
     "mrsum_skinny_fp8": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _vp,
-                         _c_int, _c_float, _c_int, _vp],
+                         _c_int, _c_float, _vp, _c_int, _vp, _vp, _c_int, _vp],
+    "mrsum_skinny_fp8_resid_capacity": [],
     "mrsum_quant_fp8_rows": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
     "mrsum_add_rmsnorm_parts": [_vp, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_sample_keys": [_vp, _c_int, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _vp],
@@ -305,6 +306,11 @@ def prefill_items(seqlens, group: int) -> torch.Tensor:
     return torch.tensor([(s, qb) for qb, s in items], dtype=torch.int32).reshape(-1, 2)
 
 
+# 32-row query blocks per wave of the prefill attention (attn_prefill.hip QB): 1 = 8 waves x 32 rows, 2 = 4 waves
+# x 64 rows (each K / V fragment read from LDS feeds two MFMAs; bf16 K/V only)
+ATTN_PREFILL_QB = 1
+
+
 def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int, d: int, scale: float,
                  out: Optional[torch.Tensor] = None, items: Optional[torch.Tensor] = None,
                  seqlens=None, paged=None) -> torch.Tensor:
@@ -342,11 +348,12 @@ def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int,
                  "attn_prefill: slice [%d, %d) beyond block table" % (pre, pre + n))
         _check(_fn("mrsum_attn_prefill_paged")(_p(qkv), qkv.stride(0), _p(cu_seqlens), _p(items), items.shape[0],
                                                block_m, _p(out), out.stride(0), hq, hkv, d, scale, _p(kc), _p(vc), _p(bt),
-                                               bt.stride(0), _p(paged.seq_slot), _p(paged.prefix), kv8, _stream()),
+                                               bt.stride(0), _p(paged.seq_slot), _p(paged.prefix), kv8,
+                                               ATTN_PREFILL_QB if kv8 == 0 else 1, _stream()),
                "attn_prefill_paged")
         return out
     _check(_fn("mrsum_attn_prefill")(_p(qkv), qkv.stride(0), _p(cu_seqlens), _p(items), items.shape[0], block_m, _p(out),
-                                     out.stride(0), hq, hkv, d, scale, _stream()), "attn_prefill")
+                                     out.stride(0), hq, hkv, d, scale, ATTN_PREFILL_QB, _stream()), "attn_prefill")
     return out
 
 
@@ -360,6 +367,7 @@ def decode_splits(batch: int, hkv: int, max_ctx: int, target_wgs: int = 1024, ma
 
 
 MAX_SPLITS = 256  # attn_decode.hip MAX_SPLITS: splits of one (sequence, kv head) the merge takes
+TP_SHARD_MAX_SPLITS = 128  # decode_attn_plan_bf16: a TP shard's kv head beyond 6k (measured, see there)
 ATTN_PAGES_PER_SPLIT = 2  # at least 2 pages per split (1 measured slower at B=1: r1_attn_splits_ab.jsonl)
 
 
@@ -436,9 +444,11 @@ def decode_attn_plan_bf16(batch: int, hkv: int, max_ctx: int):
         if not fused and hkv <= 2:
             # a TP shard's one or two kv heads beyond the 6k class (config 5's 32k final reduce at TP=8): the
             # TP=1 rule below leaves B=1 at 32 workgroups.  Up to ATTN_SLOTS workgroups of >= 2 pages, at most
-            # MAX_SPLITS (attn_decode.hip) separate splits: 70B fp8 TP=8 shard at B=1, 32k -- 64 splits 5.11-5.12
-            # ms per step vs 5.66 at 32 (in situ, profiles/r5_attn_plans.jsonl)
-            return max(1, min(ATTN_SLOTS // groups, -(-pages // ATTN_PAGES_PER_SPLIT), MAX_SPLITS)), False
+            # TP_SHARD_MAX_SPLITS separate splits.  In situ, whole steps (profiles/r5_attn_plans*.jsonl): 70B fp8
+            # TP=8 shard at B=1, 32k -- 32 / 64 / 128 / 250 splits 5.66 / 5.07 / 4.80 / 5.10 ms (the merge of
+            # 250 splits costs more than the wider attention gains); 8B TP=8 shard at 13.5k -- 106 splits
+            # 1.24 ms vs 64 1.28, 32 1.29
+            return max(1, min(ATTN_SLOTS // groups, -(-pages // ATTN_PAGES_PER_SPLIT), TP_SHARD_MAX_SPLITS)), False
         if fused and batch == 1 and hkv >= 8 and pages > 32:
             # one sequence x 8 kv heads: 32 splits with the separate merge beat 16 fused in situ (whole decode
             # steps, 4k context: 3.47 vs 3.55 ms; profiles/r2_attn_plans_insitu_b1_b10.jsonl), as in the
@@ -478,13 +488,12 @@ def decode_groups(hq: int, hkv: int) -> int:
 class DecodeWorkspace:
     """Split-K partial buffers + per-(seq, kv head) arrival counters for attn_decode
     (allocated once per batch bucket; counters start at 0 and every launch re-arms them).
-    ``consumer_merge``: the attention launch writes only the split partials and returns them as AttnParts;
-    the o projection merges them itself (skinny_gemm.hip MERGE) or, on any other path, AttnParts.merged()
-    runs the merge kernel first."""
+    (A third merge placement -- every workgroup of the o projection merging one row's splits into LDS under
+    its weight loads -- measured equal at a TP=8 shard's 4k and 8 % slower at 13.5k, the partials re-read
+    by every workgroup costing what the merge launch did: profiles/r5_consumer_merge_ab.jsonl.  Removed.)"""
 
     def __init__(self, batch: int, hq: int, d: int, splits: int, device, hkv: Optional[int] = None,
-                 fused_combine: bool = False, consumer_merge: bool = False):
-        self.consumer_merge = consumer_merge and not fused_combine
+                 fused_combine: bool = False):
         # fused_combine (last-arriver merge inside the split kernel) measured SLOWER than the separate
         # merge kernel at every B >= 8 (the per-workgroup drain + agent release costs more than the
         # launch boundary it saves: B=39 238 vs 189 us), so the separate kernel is the default.
@@ -494,45 +503,6 @@ class DecodeWorkspace:
         self.counters = (torch.zeros(batch * (hkv or hq), dtype=torch.int32, device=device)
                          if fused_combine else None)
 
-
-# The o projection merges the attention splits (consumer_merge) when one decode row's partials are at most
-# this many bytes: every o workgroup re-reads them from L2, so the merge must stay short next to the weight
-# stream it hides under (TP=8 shard of Llama-3-8B at 4k: 4 heads x 63 splits x 512 B = 126 KiB).
-CONSUMER_MERGE_MAX_BYTES = 160 << 10
-MERGE_MAX_HQ = 16  # skinny_gemm.hip MERGE_MAX_HQ
-
-
-def consumer_merge_ok(batch: int, hq: int, splits: int, fused: bool) -> bool:
-    """Whether a decode bucket's attention leaves its split merge to the o projection (hip.DecodeWorkspace):
-    one row, a separate merge, at most MERGE_MAX_HQ query heads (a TP shard) and CONSUMER_MERGE_MAX_BYTES of
-    partials."""
-    return (batch == 1 and not fused and hq <= MERGE_MAX_HQ and splits <= MAX_SPLITS
-            and hq * splits * 128 * 4 <= CONSUMER_MERGE_MAX_BYTES)
-
-
-def merge_fits(merge: "AttnParts", N: int) -> bool:
-    """Can the N-column register-streaming residual producer merge these partials (skinny_gemm.hip MERGE)?"""
-    return (merge.B == 1 and merge.d == 128 and merge.hq <= MERGE_MAX_HQ and merge.ws.splits <= MAX_SPLITS
-            and merge.hq * 32 <= 64 * skinny_waves(N, 1, 1))
-
-
-class AttnParts:
-    """Decode attention output left as its split partials (DecodeWorkspace.consumer_merge): ``part_o``
-    [B, hq, S, d] / ``part_ml`` [B, hq, S, 2] fp32.  ``out`` is the [B, hq d] bf16 buffer the merge fills
-    when a consumer needs the rows (merged())."""
-
-    def __init__(self, ws: "DecodeWorkspace", B: int, hq: int, d: int, out: torch.Tensor):
-        self.ws, self.B, self.hq, self.d, self.out = ws, B, hq, d, out
-        self.shape = out.shape
-        self.device = out.device
-        self.dtype = out.dtype
-        self.is_cuda = out.is_cuda
-
-    def merged(self) -> torch.Tensor:
-        _check(_fn("mrsum_attn_decode_merge")(_p(self.ws.part_o), _p(self.ws.part_ml), _p(self.out),
-                                              self.out.stride(0), self.B, self.hq, self.ws.splits, _stream()),
-               "attn_decode_merge")
-        return self.out
 
 
 def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
@@ -561,13 +531,12 @@ def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.T
     if out is None:
         out = torch.empty(B, hq * d, dtype=torch.bfloat16, device=parts.device)
     _rows_ok(out)
-    cm = getattr(workspace, "consumer_merge", False)
     _check(_fn("mrsum_attn_decode_rope")(_p(parts), SP, _p(cos_sin), _p(kcache), _p(vcache), _p(block_tables),
                                          block_tables.stride(0), _p(positions), _p(workspace.part_o),
-                                         _p(workspace.part_ml), None if cm else _p(out), out.stride(0), B, hq, hkv,
-                                         d, page, workspace.splits, scale, _p(workspace.counters), kv8, _stream()),
+                                         _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
+                                         workspace.splits, scale, _p(workspace.counters), kv8, _stream()),
            "attn_decode_rope")
-    return AttnParts(workspace, B, hq, d, out) if cm else out
+    return out
 
 
 def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, block_tables: torch.Tensor,
@@ -592,13 +561,12 @@ def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, blo
     if out is None:
         out = torch.empty(B, hq * d, dtype=q.dtype, device=q.device)
     _rows_ok(out)
-    cm = getattr(workspace, "consumer_merge", False)
     _check(_fn("mrsum_attn_decode_mfma")(_p(q), q.stride(0), _p(kcache), _p(vcache), _p(block_tables),
                                          block_tables.stride(0), _p(positions), _p(workspace.part_o),
-                                         _p(workspace.part_ml), None if cm else _p(out), out.stride(0), B, hq, hkv,
-                                         d, page, workspace.splits, scale, _p(workspace.counters), kv8, _stream()),
+                                         _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
+                                         workspace.splits, scale, _p(workspace.counters), kv8, _stream()),
            "attn_decode_mfma")
-    return AttnParts(workspace, B, hq, d, out) if cm else out
+    return out
 
 
 # ------------------------------------------------------------------ sampler
@@ -740,25 +708,29 @@ def choose_splits(N: int, K: int, nt: int, target_wgs: int = 512, max_splits: in
     return best
 
 
-# Register-streaming kernels (skinny_gemm.hip) run 8-wave workgroups when the grid is at most
-# SKINNY_WAVES8_MAX_WGS workgroups (about one per CU or less: a TP shard's N / 16 tiles), so twice the weight
-# bytes are in flight per CU; larger grids already hold several 4-wave workgroups per CU.
+# Register-streaming kernels (skinny_gemm.hip) run 8-wave workgroups for one decode row when the grid is at
+# most SKINNY_WAVES8_MAX_WGS workgroups (about one per CU or less: a TP shard's N / 16 tiles), so twice the
+# weight bytes are in flight per CU; larger grids already hold several 4-wave workgroups per CU.  In situ,
+# whole decode steps (profiles/r5_skinny_waves_insitu.jsonl): Llama-3-8B TP=8 shard B=1 at 4k 1.374 -> 1.219
+# ms, TP=1 B=1 at 13.5k 3.539 -> 3.522, 70B fp8 TP=8 shard B=1 at 32k 5.122 -> 5.105; at B=10 8 waves lose
+# 0.3-1 % (TP=8 shard 1.449 vs 1.465, TP=1 4.527 vs 4.541), so more rows keep 4.
 # ``SKINNY_WAVES_FORCE`` (4 / 8) overrides the choice for in-situ A/Bs (tools/exp_plans_insitu.py "waves:W").
 SKINNY_WAVES8_MAX_WGS = 2 * 256
+SKINNY_WAVES8_MAX_M = 1
 SKINNY_WAVES_FORCE = None
 
 
-def skinny_waves(N: int, nt: int, splits: int) -> int:
-    """Waves per workgroup (4 or 8) of a register-streaming launch of N / (16 nt) x splits workgroups."""
+def skinny_waves(N: int, nt: int, splits: int, M: int = 1) -> int:
+    """Waves per workgroup (4 or 8) of a register-streaming launch of N / (16 nt) x splits workgroups over M
+    rows."""
     if SKINNY_WAVES_FORCE in (4, 8):
         return SKINNY_WAVES_FORCE
-    return 8 if (N // (16 * nt)) * splits <= SKINNY_WAVES8_MAX_WGS else 4
+    return 8 if M <= SKINNY_WAVES8_MAX_M and (N // (16 * nt)) * splits <= SKINNY_WAVES8_MAX_WGS else 4
 
 
-def _skinny(x, w, out, epi, nt, splits, ldo, norm=None, resid=None, ssp=None, ar=None, merge=None):
+def _skinny(x, w, out, epi, nt, splits, ldo, norm=None, resid=None, ssp=None, ar=None):
     """Register-streaming decode GEMM (skinny_gemm.hip).  ``norm``: deferred-RMSNorm input of the SwiGLU
-    epilogue; EPI_SKINNY_RESID: residual += x @ w^T (TP push over ``ar`` when given), ``ssp`` [M, N / 16];
-    ``merge`` (AttnParts, one row): x is that attention's split merge, done by the kernel itself."""
+    epilogue; EPI_SKINNY_RESID: residual += x @ w^T (TP push over ``ar`` when given), ``ssp`` [M, N / 16]."""
     _bf16_cuda(x, w)
     _rows_ok(x)
     M, K = x.shape
@@ -775,17 +747,8 @@ def _skinny(x, w, out, epi, nt, splits, ldo, norm=None, resid=None, ssp=None, ar
         _req(resid.shape == (M, N) and ssp is not None and ssp.dtype == torch.float32 and ssp.is_contiguous()
              and ssp.shape == (M, N // 16), "skinny resid: residual [M, N] bf16 and ssp fp32 [M, N / 16]")
         rp, ldr, sp = _p(resid), resid.stride(0), _p(ssp)
-    mo = mml = None
-    mS = 0
-    if merge is not None:
-        waves = skinny_waves(N, nt, splits)
-        _req(epi == EPI_SKINNY_RESID and M == 1 and merge.B == 1 and merge.hq * merge.d == K and merge.d == 128
-             and merge.hq <= MERGE_MAX_HQ and merge.hq * 32 <= 64 * waves and merge.ws.splits <= MAX_SPLITS,
-             "skinny resid: merge needs one row of hq <= %d heads" % MERGE_MAX_HQ)
-        mo, mml, mS = _p(merge.ws.part_o), _p(merge.ws.part_ml), merge.ws.splits
     _check(_fn("mrsum_skinny_gemm")(_p(x), x.stride(0), _p(w), N, K, M, _p(out), ldo, epi, nt, splits, sq, tiles, eps,
-                                    rp, ldr, sp, ar, mo, mml, mS, skinny_waves(N, nt, splits), _stream()),
-           "skinny_gemm")
+                                    rp, ldr, sp, ar, skinny_waves(N, nt, splits, M), _stream()), "skinny_gemm")
     return out
 
 
@@ -1012,36 +975,41 @@ _RESID_CAP = {}
 
 def skinny_resid_capacity(N: Optional[int] = None) -> int:
     """Workgroups of the register-streaming residual producer resident at once on this device (a TP-push
-    grid of N / 16 workgroups must fit: every one spins on its peers' copies of its tile) -- for the
-    workgroup width that an N-column launch runs (skinny_waves), the 4-wave form without N."""
-    waves = skinny_waves(N, 1, 1) if N is not None else 4
-    if waves not in _RESID_CAP:
-        _RESID_CAP[waves] = int(_fn("mrsum_skinny_resid_capacity_w")(waves))
-    return _RESID_CAP[waves]
+    grid of N / 16 workgroups must fit: every one spins on its peers' copies of its tile) -- the smaller
+    of the 4- and 8-wave forms (skinny_waves picks either by the row count).  ``N`` is accepted for the
+    callers' readability; the bound does not depend on it."""
+    for waves in (4, 8):
+        if waves not in _RESID_CAP:
+            _RESID_CAP[waves] = int(_fn("mrsum_skinny_resid_capacity_w")(waves))
+    return min(_RESID_CAP[4], _RESID_CAP[8])
 
 
-def skinny_resid(x, w: torch.Tensor, residual: torch.Tensor, tp=None) -> torch.Tensor:
+def skinny_resid(x: torch.Tensor, w, residual: torch.Tensor, tp=None) -> torch.Tensor:
     """Deferred-RMSNorm producer on the register-streaming kernel (one 16-row tile per workgroup, no
-    split-K, M <= 16): residual += x @ w^T -- all-reduced over the custom all-reduce group ``tp`` first
-    (TP push) when given; returns the fp32 [M, N / 16] per-tile row sums of squares of the new residual.
-    ``x`` may be AttnParts (one decode row): the kernel merges the attention's splits itself."""
-    merge = x if isinstance(x, AttnParts) else None
+    split-K, M <= 16): residual += x @ w^T (bf16 or Fp8Weight ``w``) -- all-reduced over the custom
+    all-reduce group ``tp`` first (TP push) when given; returns the fp32 [M, N / 16] per-tile row sums of
+    squares of the new residual."""
     N = w.shape[0]
-    if merge is not None:
-        x = merge.out  # shape / pointer only: the kernel merges the partials instead of reading it
-        if merge_fits(merge, N):
-            STATS["consumer_merge"] += 1
-        else:
-            merge.merged()
-            merge = None
+    fp8 = isinstance(w, Fp8Weight)
     M = x.shape[0]
     ssp = torch.empty(M, N // 16, dtype=torch.float32, device=x.device)
     if tp is not None:
-        _req(N // 16 <= skinny_resid_capacity(N), "skinny_resid: TP-push grid of %d workgroups is not fully "
-             "resident (capacity %d)" % (N // 16, skinny_resid_capacity(N)))
+        cap = skinny_fp8_resid_capacity() if fp8 else skinny_resid_capacity(N)
+        _req(N // 16 <= cap, "skinny_resid: TP-push grid of %d workgroups is not fully resident (capacity %d)"
+             % (N // 16, cap))
         STATS["tp_push"] += 1
-    _skinny(x, w, None, EPI_SKINNY_RESID, 1, 1, 0, resid=residual, ssp=ssp, ar=tp, merge=merge)
+    if fp8:
+        _skinny_fp8(x, w, None, EPI_SKINNY_RESID, 1, 1, 0, resid=residual, ssp=ssp, ar=tp)
+    else:
+        _skinny(x, w, None, EPI_SKINNY_RESID, 1, 1, 0, resid=residual, ssp=ssp, ar=tp)
     return ssp
+
+
+def skinny_fp8_resid_capacity() -> int:
+    """skinny_resid_capacity of the fp8-weight residual producer."""
+    if "fp8" not in _RESID_CAP:
+        _RESID_CAP["fp8"] = int(_fn("mrsum_skinny_fp8_resid_capacity")())
+    return _RESID_CAP["fp8"]
 
 
 def linear_swiglu(x: torch.Tensor, w_gu: torch.Tensor, out: Optional[torch.Tensor] = None,
@@ -1094,7 +1062,7 @@ def add_rmsnorm_parts(parts: torch.Tensor, residual: torch.Tensor, w: torch.Tens
 # Streaming floor (probe): qkv 9.5, o 7.6, down 20.1, gate_up 39.1.
 # Plan = ("stream", wpb, S) | ("skinny", nt, S) | ("lds", S) | ("gemm",) (the 256 x 256-tile kernel)
 N_CU = 256
-STATS = {"tp_push": 0, "consumer_merge": 0}  # host-side launch counts of selected paths (tests check which path ran)
+STATS = {"tp_push": 0}  # host-side launch counts of selected paths (tests check which path ran)
 
 
 def stream_config(N: int, K: int, swiglu: bool = False, splits: Optional[int] = None, max_splits: int = 16):
@@ -1236,7 +1204,7 @@ def skinny_fp8_takes_norm(M: int, K: int, splits: int = 1) -> bool:
     return M == 1 and K % 128 == 0 and (K // 128) % splits == 0 and (K // splits) * 2 <= 56 * 1024
 
 
-def _skinny_fp8(x, w, out, epi, nt, splits, ldo, norm=None):
+def _skinny_fp8(x, w, out, epi, nt, splits, ldo, norm=None, resid=None, ssp=None, ar=None):
     _bf16_cuda(x)
     _rows_ok(x)
     M, K = x.shape
@@ -1248,8 +1216,17 @@ def _skinny_fp8(x, w, out, epi, nt, splits, ldo, norm=None):
          "skinny_fp8: unsupported shape M=%d N=%d K=%d nt=%d S=%d" % (M, N, K, nt, splits))
     _req(norm is None or skinny_fp8_takes_norm(M, K, splits), "skinny_fp8: a deferred norm needs M = 1")
     sq, tiles, eps = _norm_args(x, norm)
+    rp, ldr, sp = None, 0, None
+    if epi == EPI_SKINNY_RESID:
+        _req(nt == 1 and splits == 1 and M <= 16 and norm is None, "skinny_fp8 resid: one 16-row tile, M <= 16")
+        _bf16_cuda(resid)
+        _rows_ok(resid)
+        _req(resid.shape == (M, N) and ssp is not None and ssp.dtype == torch.float32 and ssp.is_contiguous()
+             and ssp.shape == (M, N // 16), "skinny_fp8 resid: residual [M, N] bf16 and ssp fp32 [M, N / 16]")
+        rp, ldr, sp = _p(resid), resid.stride(0), _p(ssp)
     _check(_fn("mrsum_skinny_fp8")(_p(x), x.stride(0), _p(w.q), _p(w.scale), N, K, M, _p(out), ldo, epi, nt, splits,
-                                   sq, tiles, eps, skinny_waves(N, nt, splits), _stream()), "skinny_fp8")
+                                   sq, tiles, eps, rp, ldr, sp, ar, skinny_waves(N, nt, splits, M), _stream()),
+           "skinny_fp8")
     return out
 
 

@@ -553,7 +553,7 @@ def _push_case(h, kind: str, M: int, N: int, K: int, fp8: bool, role: str = "o")
         return None
     if rp is None or rp[0] != kind:
         return None
-    if kind == "skinny" and (fp8 or N // 16 > hip.skinny_resid_capacity(N)):
+    if kind == "skinny" and N // 16 > (hip.skinny_fp8_resid_capacity() if fp8 else hip.skinny_resid_capacity(N)):
         return None
     return rp
 
@@ -607,7 +607,7 @@ def _test_push(h, dev, iters: int, group=None, M: int = 3, N: int = 2048, K: int
 
     def run():
         if rp[0] == "skinny":
-            ssp[0] = hip.skinny_resid(x, wb, res, tp=h.push_handle())
+            ssp[0] = hip.skinny_resid(x, weight(), res, tp=h.push_handle())
         else:
             ssp[0] = hip.stream_resid(x, weight(), res, rp[1], rp[2], tp=h.push_handle())
 

@@ -55,31 +55,15 @@ def test_decode_attn_plan_class1_six_fused_splits():
     assert hip.decode_attn_plan(16, 8, 12288) == (6, True)
     # the final reduce (B=1, ~13k, <= 32k class) keeps 32 separate splits (best of 16-64 / fused in situ)
     assert hip.decode_attn_plan(1, 8, 32768) == (32, False)
-    # a TP shard's single kv head beyond 6k (config 5's 32k at TP=8): one workgroup per 2 pages, up to the
-    # merge's 256 splits (64 splits measured 5.11 vs 5.66 ms per 70B fp8 shard step at 32, r5_attn_plans.jsonl)
-    assert hip.decode_attn_plan(1, 1, 32768) == (256, False)
+    # a TP shard's single kv head beyond 6k (config 5's 32k at TP=8): one workgroup per 2 pages, up to 128
+    # splits (70B fp8 shard step at 32k: 128 splits 4.80 ms vs 64 5.07, 250 5.10, 32 5.66; r5_attn_plans*.jsonl)
+    assert hip.decode_attn_plan(1, 1, 32768) == (128, False)
+    assert hip.decode_attn_plan(1, 1, 12288) == (96, False)
     assert hip.decode_attn_plan(16, 1, 32768) == (48, False)
     assert all(hip.decode_attn_plan(b, h, c)[0] <= hip.MAX_SPLITS for b in (1, 2, 16, 64) for h in (1, 2, 8)
                for c in (4096, 12288, 32768, 131072))
     # TP shards keep their measured cap of 4 in the longer classes
     assert hip.decode_attn_plan(20, 1, 12288)[0] <= 4
-
-
-def test_consumer_merge_only_for_one_row_of_a_tp_shard():
-    # the o projection merges the attention splits for one decode row of a TP shard when the partials every
-    # o workgroup re-reads stay small (8B TP=8 at 4k: 4 heads x 63 splits = 126 KiB)
-    assert hip.consumer_merge_ok(1, 4, 63, False)
-    assert not hip.consumer_merge_ok(1, 4, 63, True)     # the fused (in-launch) merge has no partials left
-    assert not hip.consumer_merge_ok(2, 4, 63, False)    # two rows
-    assert not hip.consumer_merge_ok(1, 32, 32, False)   # TP=1: 512 KiB per workgroup
-    assert not hip.consumer_merge_ok(1, 8, 256, False)   # 70B TP=8 at 32k: 1 MiB
-    assert not hip.consumer_merge_ok(1, 32, 2, False)    # more heads than the kernel's LDS row holds
-    old = hip.CONSUMER_MERGE_MAX_BYTES
-    try:
-        hip.CONSUMER_MERGE_MAX_BYTES = 0  # off (tools/exp_plans_insitu.py "cmerge:0")
-        assert not hip.consumer_merge_ok(1, 4, 63, False)
-    finally:
-        hip.CONSUMER_MERGE_MAX_BYTES = old
 
 
 def test_skinny_waves_rule():
@@ -89,3 +73,28 @@ def test_skinny_waves_rule():
     assert hip.skinny_waves(7168, 1, 1) == 8      # 70B TP=8 gate_up: 448
     assert hip.skinny_waves(57344, 1, 1) == 4     # 70B TP=1 gate_up: 3584
     assert hip.skinny_waves(4096, 1, 4) == 4      # split-K slabs: 1024
+    assert hip.skinny_waves(4096, 1, 1, M=10) == 4  # more than one row: 4 waves (measured 0.3-1 % faster)
+
+
+def test_fp8_tp_push_producer_rule(monkeypatch):
+    # 70B fp8 TP=8 shard: o (K 1024) on the fp8 register-streaming producer at every decode row count up to
+    # 16, down (K 3584) only at one row (in situ, profiles/r5_fp8_skinny_push_ab.jsonl); TP=1 keeps the stream
+    # producer
+    import torch
+    from llm_map_reduce_summarizer_amd import ops
+    from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight
+    monkeypatch.setattr(hip, "skinny_fp8_resid_capacity", lambda: 1024)
+
+    def w(N, K):
+        return Fp8Weight(torch.empty(N, K, dtype=torch.float8_e4m3fn, device="meta"),
+                         torch.empty(N, dtype=torch.float32, device="meta"))
+
+    def a(M, K):
+        return torch.empty(M, K, dtype=torch.bfloat16, device="meta")
+
+    assert ops._resid_plan(hip, a(1, 1024), w(8192, 1024), "o", tp=True) == ("skinny",)
+    assert ops._resid_plan(hip, a(10, 1024), w(8192, 1024), "o", tp=True) == ("skinny",)
+    assert ops._resid_plan(hip, a(1, 3584), w(8192, 3584), "down", tp=True) == ("skinny",)
+    assert ops._resid_plan(hip, a(10, 3584), w(8192, 3584), "down", tp=True)[0] == "stream"
+    assert ops._resid_plan(hip, a(1, 8192), w(8192, 8192), "o", tp=False)[0] == "stream"
+    assert ops._resid_plan(hip, a(1, 1024), w(8192, 1024), "o", tp=True, force="stream")[0] == "stream"

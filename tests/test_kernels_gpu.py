@@ -97,13 +97,19 @@ def test_swiglu_embed():
 # (6, 2) / (24, 8) / (10, 2): GQA ratios 3 and 5 (Llama-3.2-3B is 24 / 8) take the per-query-head fallback
 @pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (2, 2), (6, 2), (24, 8), (10, 2)])
 @pytest.mark.parametrize("seqlens", [[1, 37, 130, 300], [64], [129, 256], [1000, 33, 2100]])
-def test_attn_prefill(hq, hkv, seqlens):
+@pytest.mark.parametrize("qb", [1, 2])
+def test_attn_prefill(hq, hkv, seqlens, qb):
+    """Causal varlen prefill attention vs fp32; qb = 32-row query blocks per wave (attn_prefill.hip QB)."""
     d = 128
     T = sum(seqlens)
     qkv = _rand(T, (hq + 2 * hkv) * d, seed=11)
     cu = torch.tensor([0] + list(torch.tensor(seqlens).cumsum(0)), dtype=torch.int32, device=DEV)
     sc = 1.0 / math.sqrt(d)
-    o1 = hip.attn_prefill(qkv, cu, hq, hkv, d, sc)
+    old, hip.ATTN_PREFILL_QB = hip.ATTN_PREFILL_QB, qb
+    try:
+        o1 = hip.attn_prefill(qkv, cu, hq, hkv, d, sc)
+    finally:
+        hip.ATTN_PREFILL_QB = old
     o2 = reference.attn_prefill(qkv, cu, hq, hkv, d, sc)
     _close(o1, o2, 2e-2)
 
@@ -172,7 +178,7 @@ def test_rope_kv_fp8_cache_tiny_rows():
 
 @pytest.mark.parametrize("hq,hkv", [(4, 1), (8, 2), (8, 1), (2, 2), (6, 2)])
 @pytest.mark.parametrize("spans", [[(0, 200)], [(130, 300), (0, 77), (1000, 1129)], [(64, 128), (2047, 2048)]])
-@pytest.mark.parametrize("kv8", ["bf16", "fp8", "fp8v"])
+@pytest.mark.parametrize("kv8", ["bf16", "fp8", "fp8v", "bf16-qb2"])
 def test_attn_prefill_paged(hq, hkv, spans, kv8):
     """Chunked-prefill attention: slice rows attend to [0, prefix + slice) of their sequence read from the
     paged cache (random non-contiguous pages, stale rows past the slice end), vs the fp32 reference."""
@@ -182,6 +188,8 @@ def test_attn_prefill_paged(hq, hkv, spans, kv8):
     n_pages, maxp = 160, 40
     kc = (torch.randn(n_pages, hkv, page, d, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
     vc = torch.randn(n_pages, hkv, page, d, generator=g).to(torch.bfloat16).to(DEV)
+    qb = 2 if kv8.endswith("-qb2") else 1  # 4 waves x two 32-row query blocks (bf16 caches only)
+    kv8 = kv8.split("-")[0]
     kc, vc = _kv_format(kc, vc, kv8)
     nseq = len(spans)
     perm = torch.randperm(n_pages - 1, generator=g)[: nseq * maxp] + 1
@@ -196,7 +204,11 @@ def test_attn_prefill_paged(hq, hkv, spans, kv8):
     i32 = lambda x: torch.tensor(x, dtype=torch.int32, device=DEV)  # noqa: E731
     pp = PagedPrefill(bt, i32(slots), i32(pre), slots, pre, kc, vc)
     sc = 1.0 / math.sqrt(d)
-    o1 = hip.attn_prefill(qkv, cu, hq, hkv, d, sc, paged=pp)
+    old, hip.ATTN_PREFILL_QB = hip.ATTN_PREFILL_QB, qb
+    try:
+        o1 = hip.attn_prefill(qkv, cu, hq, hkv, d, sc, paged=pp)
+    finally:
+        hip.ATTN_PREFILL_QB = old
     o2 = reference.attn_prefill_paged(qkv, cu, hq, hkv, d, sc, pp)
     _close(o1, o2, 2e-2)
 
@@ -272,49 +284,6 @@ def test_attn_decode_many_splits_one_kv_head(splits, fused):
     for _ in range(2):
         o1 = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws)
         _close(o1, o2, 2e-2)
-
-
-@pytest.mark.parametrize("hq,splits,tp", [(4, 63, False), (4, 63, True), (8, 17, False), (16, 5, True), (2, 256, False)])
-def test_attn_consumer_merge_in_o_projection(hq, splits, tp):
-    """Decode attention that leaves its split merge to the o projection (DecodeWorkspace.consumer_merge ->
-    AttnParts; skinny_gemm.hip MERGE): the residual update and per-tile sums of squares equal the separate
-    merge + register-streaming producer's, and AttnParts.merged() equals the fp32 attention reference."""
-    from llm_map_reduce_summarizer_amd.parallel.custom_ar import LocalPush
-    hkv, d, page, ctx, N = 1, 128, 64, 17000, 4096  # 266 pages: every split holds keys
-    npg = -(-ctx // page)
-    g = torch.Generator().manual_seed(95)
-    kc = torch.randn(npg + 1, hkv, page, d, generator=g).to(torch.bfloat16).to(DEV)
-    vc = torch.randn(npg + 1, hkv, page, d, generator=g).to(torch.bfloat16).to(DEV)
-    bt = (torch.randperm(npg, generator=g).to(torch.int32) + 1).view(1, npg).to(DEV)
-    pos = torch.tensor([ctx - 1], dtype=torch.int32, device=DEV)
-    q = _rand(1, (hq + 2 * hkv) * d, seed=96)
-    sc = 1.0 / math.sqrt(d)
-    w = _rand(N, hq * d, scale=0.05, seed=97)
-    res0 = _rand(1, N, seed=98)
-    h = LocalPush(max_bytes=1 << 20) if tp else None
-    try:
-        push = h.push_handle() if tp else None
-        ws = hip.DecodeWorkspace(1, hq, d, splits, DEV, hkv, consumer_merge=True)
-        ws_ref = hip.DecodeWorkspace(1, hq, d, splits, DEV, hkv)
-        a_ref = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws_ref)
-        _close(a_ref, reference.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc), 2e-2)
-        r_ref = res0.clone()
-        ss_ref = hip.skinny_resid(a_ref, w, r_ref, tp=push)
-        n0 = hip.STATS["consumer_merge"]
-        for _ in range(2):  # replayed: partials overwritten, the merge re-done
-            parts = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws)
-            assert isinstance(parts, hip.AttnParts)
-            r = res0.clone()
-            ss = hip.skinny_resid(parts, w, r, tp=push)
-            _close(r, r_ref, 1e-2, 1e-2)
-            _close(ss, ss_ref, 1e-2, 1e-3)
-        assert hip.STATS["consumer_merge"] == n0 + 2
-        _close(parts.merged(), a_ref, 1e-2)
-        if tp:
-            assert h.error() == 0
-    finally:
-        if h is not None:
-            h.close()
 
 
 class _St:
@@ -937,6 +906,35 @@ def test_stream_resid_tp_push_group_of_one(fp8, M):
         assert h.error() == 0
     finally:
         h.close()
+
+
+@pytest.mark.parametrize("M", [1, 5, 16])
+@pytest.mark.parametrize("tp", [False, True])
+@pytest.mark.parametrize("K", [1024, 3584])
+def test_skinny_fp8_resid_producer(M, tp, K):
+    """fp8-weight register-streaming residual producer (skinny_fp8_kernel EPI_RESID; 70B TP=8 shard o / down
+    shapes): residual += x @ dequant(w)^T through the TP push over a group of one when ``tp``, per-tile row
+    sums of squares -- against fp32, repeated calls (push epochs advance)."""
+    from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight
+    from llm_map_reduce_summarizer_amd.parallel.custom_ar import LocalPush
+    h = LocalPush(max_bytes=1 << 20) if tp else None
+    try:
+        N = 8192
+        x = _rand(M, K, scale=0.5, seed=31)
+        w = Fp8Weight.quantize(_rand(N, K, scale=0.05, seed=32))
+        res0 = _rand(M, N, seed=33)
+        res = res0.clone()
+        for _ in range(3):
+            res.copy_(res0)
+            ssp = hip.skinny_resid(x, w, res, tp=h.push_handle() if tp else None)
+        ref = (res0.float() + x.float() @ w.dequant().t()).to(torch.bfloat16)
+        _close(res, ref, 3e-2, 2e-2)
+        _close(ssp, res.float().pow(2).reshape(M, N // 16, 16).sum(-1), 1e-2, 1e-3)
+        if tp:
+            assert h.error() == 0
+    finally:
+        if h is not None:
+            h.close()
 
 
 @pytest.mark.parametrize("M", [1, 5, 16])

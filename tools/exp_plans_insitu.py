@@ -10,7 +10,6 @@ Variants (comma separated, ``plan`` = unchanged):
   gate_up:stream_split:WPB:S   split-K gate_up with the SwiGLU in the last arriver
   deferM                       the TP=1 deferred RMSNorm up to M rows (ops.DEFER_NORM_MAX_M)
   waves:W                      register-streaming kernels with W (4 | 8) waves per workgroup at every grid
-  cmerge:BYTES                 the o projection merges the attention splits up to BYTES of partials (0: off)
   fp8resid:N:K:WPB:S           the fp8 deferred-norm producer (stream_fp8, residual epilogue) of one shape
   buckets:B1+B2+...            decode graph buckets up to the largest given (the rest unchanged)
   resid:ROLE=KIND              the deferred-norm / TP-push producer of ROLE (o | down) forced to KIND
@@ -58,7 +57,6 @@ def main():
     from llm_map_reduce_summarizer_amd import ops
     base_defer = ops.DEFER_NORM_MAX_M
     base_fp8r = hip.fp8_resid_cfg
-    base_cmerge = hip.CONSUMER_MERGE_MAX_BYTES
 
     env_set = []
     import llm_map_reduce_summarizer_amd.engine.engine as engine_mod
@@ -69,7 +67,6 @@ def main():
         ops.DEFER_NORM_MAX_M = base_defer
         hip.fp8_resid_cfg = base_fp8r
         hip.SKINNY_WAVES_FORCE = None
-        hip.CONSUMER_MERGE_MAX_BYTES = base_cmerge
         for name, old in env_set:
             if old is None:
                 os.environ.pop(name, None)
@@ -98,9 +95,6 @@ def main():
         if v.startswith("fp8resid:"):  # fp8resid:N:K:wpb:S -- the fp8 deferred-norm producer of one shape
             N0, K0, wpb, S = (int(t) for t in v.split(":")[1:])
             hip.fp8_resid_cfg = lambda M, N, K: (wpb, S) if (N, K) == (N0, K0) else base_fp8r(M, N, K)
-            return
-        if v.startswith("cmerge:"):
-            hip.CONSUMER_MERGE_MAX_BYTES = int(v[len("cmerge:"):])
             return
         if v.startswith("waves:"):
             hip.SKINNY_WAVES_FORCE = int(v[len("waves:"):])
