@@ -96,23 +96,14 @@ struct PagedKV {
 // Other GQA ratios (e.g. Llama-3.2-3B: 24 / 8 = 3) run the G = 1 instantiation over Hg = Hq "virtual kv
 // heads", one per query head, each reading the K/V columns of its real kv head h / gq (gq = Hq / Hkv):
 // no K/V reuse across the group inside a workgroup, but any ratio works.  Hg = Hkv and gq = 1 otherwise.
-// QB = 32-row query blocks per wave: 1 (8 waves) or 2 (4 waves, one per SIMD, each wave running two of the
-// 8 blocks): every K / V fragment read from LDS then feeds two MFMAs, halving the LDS read traffic per MFMA
-// (with 8 waves x 32 rows the LDS reads of K and V take as many cycles as the MFMAs they feed), at twice the
-// registers per wave (one wave per SIMD).  Virtual block j = QB w + qb plays the role of wave j of QB = 1.
-template <bool PAGED, int G, int KVM = 0, int QB = 1>
-__global__ __launch_bounds__(NTHR / QB, 1) void attn_prefill_kernel(const bf16* __restrict__ qkv, int row_stride,
+template <bool PAGED, int G, int KVM = 0>
+__global__ __launch_bounds__(NTHR, 1) void attn_prefill_kernel(const bf16* __restrict__ qkv, int row_stride,
                                                               const int* __restrict__ cu_seqlens,
                                                               const int2* __restrict__ items,
                                                               bf16* __restrict__ out, int out_stride, int Hq,
                                                               int Hkv, int Hg, int gq, float scale_log2, PagedKV pk,
                                                               int kv_major) {
     constexpr int BMP = 32 * (NW / G);  // query positions per workgroup
-    constexpr int NT_ = NTHR / QB;      // threads
-    constexpr int SR_ = NT_ / 16;       // tile rows staged per load round
-    constexpr int SI_ = BN / SR_;       // load rounds per 64-row tile
-    static_assert(QB == 1 || QB == 2, "one or two query blocks per wave");
-    static_assert(QB == 1 || KVM == 0, "fp8 slab staging assumes 512 threads");
     // two-stage ring of [K tile | V tile]: tile t+1 is written into the other stage while tile t is
     // consumed, one barrier per tile
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
@@ -130,6 +121,7 @@ __global__ __launch_bounds__(NTHR / QB, 1) void attn_prefill_kernel(const bf16* 
     const int kvh = G == 1 ? kvg / gq : kvg;                             // its real kv head
     const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5, r32 = lane & 31;
     const int w = tid >> 6;
+    const int h = G == 1 ? kvg : kvh * G + w % G, rb = w / G;
     const int s0 = cu_seqlens[seq], len = cu_seqlens[seq + 1] - s0;
     const bf16* base = qkv + (size_t)s0 * row_stride;
     const int kcol = (Hq + kvh) * D, vcol = (Hq + Hkv + kvh) * D;
@@ -138,23 +130,18 @@ __global__ __launch_bounds__(NTHR / QB, 1) void attn_prefill_kernel(const bf16* 
     const int* btab = PAGED ? pk.block_tables + (size_t)pk.seq_slot[seq] * pk.bt_stride : nullptr;
     const size_t head_pg = (size_t)kvh * BN * D;  // this kv head's 64-row slab inside a page
 
-    // Q^T fragments: lane holds Q[row r32][dims 16ks + 8half .. +8] for ks = 0..7, per query block qb:
-    // virtual wave j = QB w + qb runs head kvh*G + j%G over rows qblock + 32(j/G) .. +32
-    int hq_[QB], q0_[QB], qi_[QB];
-    bf16x8 qf[QB][8];
-#pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-        const int j = QB * w + qb;
-        hq_[qb] = G == 1 ? kvg : kvh * G + j % G;
-        q0_[qb] = qblock + 32 * (j / G);  // the block's first query row
-        qi_[qb] = q0_[qb] + r32;
-        const bool ok = qi_[qb] < len;
-        const bf16* qp = base + (size_t)(ok ? qi_[qb] : 0) * row_stride + hq_[qb] * D + 8 * half;
+    // Q^T fragments: lane holds Q[row r32][dims 16ks + 8half .. +8] for ks = 0..7
+    const int q0 = qblock + 32 * rb;  // the wave's first query row
+    const int qi = q0 + r32;
+    bf16x8 qf[8];
+    {
+        const bool ok = qi < len;
+        const bf16* qp = base + (size_t)(ok ? qi : 0) * row_stride + h * D + 8 * half;
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) {
             uint4 v = *reinterpret_cast<const uint4*>(qp + 16 * ks);
             if (!ok) v = make_uint4(0, 0, 0, 0);
-            qf[qb][ks] = as_bf16x8(v);
+            qf[ks] = as_bf16x8(v);
         }
     }
 
@@ -166,12 +153,12 @@ __global__ __launch_bounds__(NTHR / QB, 1) void attn_prefill_kernel(const bf16* 
     // sequence; such rows are masked out of the scores and V rows stay finite) -- a conditional prefetch
     // made hipcc serialise the loop on vmcnt(0).
     const int st_chunk = tid & 15, st_row0 = tid >> 4;
-    u32x4 kreg[SI_], vreg[SI_];
+    u32x4 kreg[SIT], vreg[SIT];
     // fp8 slab staging: row tid / 8 (0..63) of the slab, 16-B chunk tid % 8; one round per tile
     const int r8 = tid >> 3, c8 = tid & 7;
     float ks8 = 1.f, vs8 = 1.f;
     constexpr bool K8 = (KVM & 1) != 0, V8 = (KVM & 2) != 0;
-    static_assert(KVM == 0 || NT_ / 8 == BN, "fp8 slab staging: one slab row per 8 threads");
+    static_assert(KVM == 0 || NTHR / 8 == BN, "fp8 slab staging: one slab row per 8 threads");
 #define LOAD_TILE(t)                                                                              \
     if constexpr (PAGED && KVM != 0) {                                                            \
         const size_t sb = kv8::slab_off(btab[t], Hkv, kvh);                                       \
@@ -181,26 +168,26 @@ __global__ __launch_bounds__(NTHR / QB, 1) void attn_prefill_kernel(const bf16* 
             kreg[0] = *reinterpret_cast<const u32x4*>(kb_ + r8 * D + 16 * c8);                    \
             ks8 = *reinterpret_cast<const float*>(kb_ + BN * D + 4 * r8);                         \
         } else {                                                                                  \
-            _Pragma("unroll") for (int i = 0; i < SI_; ++i)                                         \
-                kreg[i] = *reinterpret_cast<const u32x4*>(pk.kc + pg + (size_t)(st_row0 + SR_ * i) * D); \
+            _Pragma("unroll") for (int i = 0; i < SIT; ++i)                                         \
+                kreg[i] = *reinterpret_cast<const u32x4*>(pk.kc + pg + (size_t)(st_row0 + SROWS * i) * D); \
         }                                                                                         \
         if constexpr (V8) {                                                                       \
             const unsigned char* vb_ = reinterpret_cast<const unsigned char*>(pk.vc) + sb;       \
             vreg[0] = *reinterpret_cast<const u32x4*>(vb_ + r8 * D + 16 * c8);                    \
             vs8 = *reinterpret_cast<const float*>(vb_ + BN * D + 4 * r8);                         \
         } else {                                                                                  \
-            _Pragma("unroll") for (int i = 0; i < SI_; ++i)                                         \
-                vreg[i] = *reinterpret_cast<const u32x4*>(pk.vc + pg + (size_t)(st_row0 + SR_ * i) * D); \
+            _Pragma("unroll") for (int i = 0; i < SIT; ++i)                                         \
+                vreg[i] = *reinterpret_cast<const u32x4*>(pk.vc + pg + (size_t)(st_row0 + SROWS * i) * D); \
         }                                                                                         \
     } else if constexpr (PAGED) {                                                                 \
         const size_t pg = (size_t)btab[t] * Hkv * BN * D + head_pg + st_chunk * 8;                \
-        _Pragma("unroll") for (int i = 0; i < SI_; ++i) {                                           \
-            kreg[i] = *reinterpret_cast<const u32x4*>(pk.kc + pg + (size_t)(st_row0 + SR_ * i) * D); \
-            vreg[i] = *reinterpret_cast<const u32x4*>(pk.vc + pg + (size_t)(st_row0 + SR_ * i) * D); \
+        _Pragma("unroll") for (int i = 0; i < SIT; ++i) {                                           \
+            kreg[i] = *reinterpret_cast<const u32x4*>(pk.kc + pg + (size_t)(st_row0 + SROWS * i) * D); \
+            vreg[i] = *reinterpret_cast<const u32x4*>(pk.vc + pg + (size_t)(st_row0 + SROWS * i) * D); \
         }                                                                                         \
     } else {                                                                                      \
-        _Pragma("unroll") for (int i = 0; i < SI_; ++i) {                                           \
-            const int key = min((t) * BN + st_row0 + SR_ * i, len - 1);                           \
+        _Pragma("unroll") for (int i = 0; i < SIT; ++i) {                                           \
+            const int key = min((t) * BN + st_row0 + SROWS * i, len - 1);                           \
             const bf16* p = base + (size_t)key * row_stride + st_chunk * 8;                      \
             kreg[i] = *reinterpret_cast<const u32x4*>(p + kcol);                                 \
             vreg[i] = *reinterpret_cast<const u32x4*>(p + vcol);                                 \
@@ -214,41 +201,34 @@ __global__ __launch_bounds__(NTHR / QB, 1) void attn_prefill_kernel(const bf16* 
             *reinterpret_cast<u32x4*>(lds + (st) + k_off(r8, 2 * c8)) = lo_;                      \
             *reinterpret_cast<u32x4*>(lds + (st) + k_off(r8, 2 * c8 + 1)) = hi_;                  \
         } else {                                                                                  \
-            _Pragma("unroll") for (int i = 0; i < SI_; ++i)                                         \
-                *reinterpret_cast<u32x4*>(lds + (st) + k_off(st_row0 + SR_ * i, st_chunk)) = kreg[i]; \
+            _Pragma("unroll") for (int i = 0; i < SIT; ++i)                                         \
+                *reinterpret_cast<u32x4*>(lds + (st) + k_off(st_row0 + SROWS * i, st_chunk)) = kreg[i]; \
         }                                                                                         \
         if constexpr (V8) {                                                                       \
             kv8::dequant16(vreg[0], vs8, lo_, hi_);                                               \
             *reinterpret_cast<u32x4*>(lds + (st) + BN * 256 + v_off(r8, 2 * c8)) = lo_;           \
             *reinterpret_cast<u32x4*>(lds + (st) + BN * 256 + v_off(r8, 2 * c8 + 1)) = hi_;       \
         } else {                                                                                  \
-            _Pragma("unroll") for (int i = 0; i < SI_; ++i)                                         \
-                *reinterpret_cast<u32x4*>(lds + (st) + BN * 256 + v_off(st_row0 + SR_ * i, st_chunk)) = vreg[i]; \
+            _Pragma("unroll") for (int i = 0; i < SIT; ++i)                                         \
+                *reinterpret_cast<u32x4*>(lds + (st) + BN * 256 + v_off(st_row0 + SROWS * i, st_chunk)) = vreg[i]; \
         }                                                                                         \
     } else                                                                                        \
-    _Pragma("unroll") for (int i = 0; i < SI_; ++i) {                                               \
-        const int row = st_row0 + SR_ * i;                                                         \
+    _Pragma("unroll") for (int i = 0; i < SIT; ++i) {                                               \
+        const int row = st_row0 + SROWS * i;                                                         \
         *reinterpret_cast<u32x4*>(lds + (st) + k_off(row, st_chunk)) = kreg[i];                    \
         *reinterpret_cast<u32x4*>(lds + (st) + BN * 256 + v_off(row, st_chunk)) = vreg[i];         \
     }
 
-    f32x16 o[QB][4];
-    float m[QB], l[QB];
+    f32x16 o[4];
 #pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) o[qb][dt] = f32x16{};
-        m[qb] = -INFINITY;
-        l[qb] = 0.f;
-    }
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x16{};
+    float m = -INFINITY, l = 0.f;
 
     LOAD_TILE(0);
     STORE_TILE(0);
     LOAD_TILE(min(1, ntiles - 1));
 
-    int wave_last_q = pre + q0_[0] + 31;  // absolute position of the wave's last row
-#pragma unroll
-    for (int qb = 1; qb < QB; ++qb) wave_last_q = max(wave_last_q, pre + q0_[qb] + 31);
+    const int wave_last_q = pre + q0 + 31;  // absolute position of the wave's last row
     // PV operand addressing (loop-invariant parts): lane (g, q4, p4) reads V rows 4(g>>1) + q4 (+8) of each
     // 16-key slab at columns dt*32 + 16(g&1) + 4p4
     const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
@@ -271,102 +251,77 @@ __global__ __launch_bounds__(NTHR / QB, 1) void attn_prefill_kernel(const bf16* 
         const char* ldsV = ldsK + BN * 256;
         if (!act) continue;
         // S^T = K Q^T: all 16 K fragments read up front (64 VGPRs, dead after the QK^T MFMAs), so the
-        // ds_reads run ahead of the MFMA chain instead of one exposed LDS round trip per MFMA; with QB = 2
-        // every fragment feeds both query blocks
-        f32x16 sacc[QB][2];
-        if constexpr (QB == 1) {
-            uint4 kf[2][8];
+        // ds_reads run ahead of the MFMA chain instead of one exposed LDS round trip per MFMA
+        uint4 kf[2][8];
+        f32x16 sacc[2];
 #pragma unroll
-            for (int kt = 0; kt < 2; ++kt)
+        for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-                for (int ks = 0; ks < 8; ++ks)
-                    kf[kt][ks] = *reinterpret_cast<const uint4*>(ldsK + k_off(kt * 32 + r32, 2 * ks + half));
+            for (int ks = 0; ks < 8; ++ks)
+                kf[kt][ks] = *reinterpret_cast<const uint4*>(ldsK + k_off(kt * 32 + r32, 2 * ks + half));
 #pragma unroll
-            for (int kt = 0; kt < 2; ++kt) {
-                sacc[0][kt] = f32x16{};
+        for (int kt = 0; kt < 2; ++kt) {
+            sacc[kt] = f32x16{};
 #pragma unroll
-                for (int ks = 0; ks < 8; ++ks)
-                    sacc[0][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[kt][ks]), qf[0][ks],
-                                                                          sacc[0][kt], 0, 0, 0);
-            }
-            // schedule (cdna_hip_programming.md T19): 8 reads ahead, then one read per MFMA gap -- without it
-            // the machine scheduler sinks every read next to its MFMA and waits lgkmcnt(0) before each one
-            __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
-        } else {
-            // two query blocks: the 8 K fragments of one 32-key half at a time (32 VGPRs), each feeding both
-            // blocks' MFMAs -- the register budget of a 4-wave workgroup holds O, Q of two blocks
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt) {
-                uint4 kf[8];
-#pragma unroll
-                for (int ks = 0; ks < 8; ++ks)
-                    kf[ks] = *reinterpret_cast<const uint4*>(ldsK + k_off(kt * 32 + r32, 2 * ks + half));
-#pragma unroll
-                for (int qb = 0; qb < QB; ++qb) sacc[qb][kt] = f32x16{};
-#pragma unroll
-                for (int ks = 0; ks < 8; ++ks)
-#pragma unroll
-                    for (int qb = 0; qb < QB; ++qb)
-                        sacc[qb][kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[ks]), qf[qb][ks],
-                                                                               sacc[qb][kt], 0, 0, 0);
-            }
+            for (int ks = 0; ks < 8; ++ks)
+                sacc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(as_bf16x8(kf[kt][ks]), qf[ks], sacc[kt], 0, 0, 0);
         }
-        bf16x8 pf[QB][2][2];
+        // schedule (cdna_hip_programming.md T19): 8 reads ahead, then one read per MFMA gap -- without it the
+        // machine scheduler sinks every read next to its MFMA and waits lgkmcnt(0) before each one
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
-        for (int qb = 0; qb < QB; ++qb) {
-            // mask + row max (key index of reg i: kt*32 + (i&3) + 8(i>>2) + 4half).  The causal/length mask is
-            // only needed on tiles that reach past the block's first query row or the sequence end (wave-uniform
-            // test); scores stay unscaled until the exponent, which is one FMA: p = 2^(s * scale_log2 - m), with
-            // the raw v_exp_f32.
-            const int kmax = pre + min(qi_[qb], len - 1) - kv0 - 4 * half;  // last valid key offset for row qi
-            if (kv0 + BN - 1 > pre + q0_[qb] || kv0 + BN > pre + len) {
-#pragma unroll
-                for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-                    for (int i = 0; i < 16; ++i) {
-                        const int koff = kt * 32 + (i & 3) + 8 * (i >> 2);  // key - kv0 - 4*half
-                        sacc[qb][kt][i] = koff <= kmax ? sacc[qb][kt][i] : -INFINITY;
-                    }
-            }
-            float mt = -INFINITY;
+        for (int i = 0; i < 8; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+        // mask + row max (key index of reg i: kt*32 + (i&3) + 8(i>>2) + 4half).  The causal/length mask is
+        // only needed on tiles that reach past the wave's first query row or the sequence end (wave-uniform
+        // test); scores stay unscaled until the exponent, which is one FMA: p = 2^(s * scale_log2 - m), with
+        // the raw v_exp_f32.
+        const int kmax = pre + min(qi, len - 1) - kv0 - 4 * half;  // last valid key offset for row qi
+        if (kv0 + BN - 1 > pre + q0 || kv0 + BN > pre + len) {
 #pragma unroll
             for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sacc[qb][kt][i]);
-            mt = halves_max(mt);
-            // deferred rescale (cdna_hip_programming.md T13): the running max m only moves (and o, l are
-            // rescaled) when some row's max grew by more than RESCALE_LOG2 -- until then p <= 2^RESCALE_LOG2,
-            // harmless in fp32 and in the bf16 P operand.  The previous tile's P.V is complete (program order)
-            // and this tile's P is exponentiated after the decision.  Key 0 is valid for every row, so m is
-            // finite after tile 0 (a block whose rows all lie above this tile's keys gets p = 0 here).
-            const float mc = mt * scale_log2;
-            if (__ballot(mc > m[qb] + RESCALE_LOG2)) {
-                const float mn = fmaxf(m[qb], mc);
-                const float alpha = __builtin_amdgcn_exp2f(m[qb] - mn);  // m = -inf before tile 0 -> 0
-                m[qb] = mn;
-                l[qb] *= alpha;
-#pragma unroll
-                for (int dt = 0; dt < 4; ++dt) o[qb][dt] *= alpha;
-            }
-            float ls = 0.f;
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    const float p = __builtin_amdgcn_exp2f(fmaf(sacc[qb][kt][i], scale_log2, -m[qb]));
-                    ls += p;
-                    pf[qb][kt][i >> 3][i & 7] = (bf16)p;
+                    const int koff = kt * 32 + (i & 3) + 8 * (i >> 2);  // key - kv0 - 4*half
+                    sacc[kt][i] = koff <= kmax ? sacc[kt][i] : -INFINITY;
                 }
-            }
-            l[qb] += ls;
         }
-        // O^T[d][q] += V^T[d][key] P^T[key][q]: per 32-dim block dt, its 8 transposed reads, then 4 QB MFMAs
+        float mt = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) mt = fmaxf(mt, sacc[kt][i]);
+        mt = halves_max(mt);
+        // deferred rescale (cdna_hip_programming.md T13): the running max m only moves (and o, l are
+        // rescaled) when some row's max grew by more than RESCALE_LOG2 -- until then p <= 2^RESCALE_LOG2,
+        // harmless in fp32 and in the bf16 P operand.  The previous tile's P.V is complete (program order)
+        // and this tile's P is exponentiated after the decision.  Key 0 is valid for every row, so m is
+        // finite after tile 0.
+        const float mc = mt * scale_log2;
+        if (__ballot(mc > m + RESCALE_LOG2)) {
+            const float mn = fmaxf(m, mc);
+            const float alpha = __builtin_amdgcn_exp2f(m - mn);  // m = -inf before tile 0 -> 0
+            m = mn;
+            l *= alpha;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) o[dt] *= alpha;
+        }
+        float ls = 0.f;
+        bf16x8 pf[2][2];
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float p = __builtin_amdgcn_exp2f(fmaf(sacc[kt][i], scale_log2, -m));
+                ls += p;
+                pf[kt][i >> 3][i & 7] = (bf16)p;
+            }
+        }
+        l += ls;
+        // O^T[d][q] += V^T[d][key] P^T[key][q]: per 32-dim block dt, its 8 transposed reads, then 4 MFMAs
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt) {
             const int col = dt * 32 + 16 * (g & 1) + 4 * p4;  // this lane's address column
@@ -385,21 +340,17 @@ __global__ __launch_bounds__(NTHR / QB, 1) void attn_prefill_kernel(const bf16* 
             for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
                 for (int s = 0; s < 2; ++s)
-#pragma unroll
-                    for (int qb = 0; qb < QB; ++qb)
-                        o[qb][dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va[kt][s]),
-                                                                            pf[qb][kt][s], o[qb][dt], 0, 0, 0);
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va[kt][s]), pf[kt][s],
+                                                                    o[dt], 0, 0, 0);
         }
-        if constexpr (QB == 1) {
-            // 8 transposed reads ahead, two per MFMA gap after that
-            __builtin_amdgcn_sched_group_barrier(0x100, 8, 1);
+        // 8 transposed reads ahead, two per MFMA gap after that
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 1);
 #pragma unroll
-            for (int i = 0; i < 12; ++i) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-                __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);
+        for (int i = 0; i < 12; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+            __builtin_amdgcn_sched_group_barrier(0x100, 2, 1);
         }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 1);
     }
 #undef LOAD_TILE
 #undef STORE_TILE
@@ -407,37 +358,34 @@ __global__ __launch_bounds__(NTHR / QB, 1) void attn_prefill_kernel(const bf16* 
     // normalise and store.  Reg i of tile dt holds d = dt*32 + (i&3) + 8(i>>2) + 4half for query qi; one
     // v_permlane32_swap per dword pair regroups two 4-dim groups so every lane stores 16 contiguous bytes
     // (cdna_hip_programming.md T21): lane < 32 dims 16j..16j+7, lane >= 32 dims 16j+8..16j+15 of row qi.
+    const float lt = halves_sum(l);
+    const float inv = 1.f / lt;
+    uint4 ov[4][2];
 #pragma unroll
-    for (int qb = 0; qb < QB; ++qb) {
-        const float lt = halves_sum(l[qb]);
-        const float inv = 1.f / lt;
-        uint4 ov[4][2];
+    for (int dt = 0; dt < 4; ++dt) {
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {  // groups g4 = 2j, 2j+1 of this 32-dim block
-                const uint32_t a0 = pack2(o[qb][dt][8 * j + 0] * inv, o[qb][dt][8 * j + 1] * inv);
-                const uint32_t a1 = pack2(o[qb][dt][8 * j + 2] * inv, o[qb][dt][8 * j + 3] * inv);
-                const uint32_t b0 = pack2(o[qb][dt][8 * j + 4] * inv, o[qb][dt][8 * j + 5] * inv);
-                const uint32_t b1 = pack2(o[qb][dt][8 * j + 6] * inv, o[qb][dt][8 * j + 7] * inv);
-                const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
-                const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
-                ov[dt][j] = make_uint4(r0[0], r1[0], r0[1], r1[1]);
-            }
+        for (int j = 0; j < 2; ++j) {  // groups g4 = 2j, 2j+1 of this 32-dim block
+            const uint32_t a0 = pack2(o[dt][8 * j + 0] * inv, o[dt][8 * j + 1] * inv);
+            const uint32_t a1 = pack2(o[dt][8 * j + 2] * inv, o[dt][8 * j + 3] * inv);
+            const uint32_t b0 = pack2(o[dt][8 * j + 4] * inv, o[dt][8 * j + 5] * inv);
+            const uint32_t b1 = pack2(o[dt][8 * j + 6] * inv, o[dt][8 * j + 7] * inv);
+            const auto r0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+            const auto r1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+            ov[dt][j] = make_uint4(r0[0], r1[0], r0[1], r1[1]);
         }
-        if (qi_[qb] < len) {
-            bf16* op = out + (size_t)(s0 + qi_[qb]) * out_stride + hq_[qb] * D + 8 * half;
+    }
+    if (qi < len) {
+        bf16* op = out + (size_t)(s0 + qi) * out_stride + h * D + 8 * half;
 #pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
+        for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
-                for (int j = 0; j < 2; ++j) *reinterpret_cast<uint4*>(op + dt * 32 + 16 * j) = ov[dt][j];
-        }
+            for (int j = 0; j < 2; ++j) *reinterpret_cast<uint4*>(op + dt * 32 + 16 * j) = ov[dt][j];
     }
 }
 
 template <bool PAGED, int G>
 static void launch_g(dim3 grid, hipStream_t s, const bf16* Q, int row_stride, const int* cu, const int2* it, bf16* out,
-                     int out_stride, int Hq, int Hkv, int Hg, int gq, float sl, const PagedKV& p, int kv8, int qb) {
+                     int out_stride, int Hq, int Hkv, int Hg, int gq, float sl, const PagedKV& p, int kv8) {
     // kv-head-major order from 8 blocks per CU up (measured crossover: 4096 blocks neutral, 19656 kv-major)
     const int kv_major = grid.x > 8 * 256;
     if constexpr (PAGED) {
@@ -451,12 +399,8 @@ static void launch_g(dim3 grid, hipStream_t s, const bf16* Q, int row_stride, co
             return;
         }
     }
-    if (qb == 2)
-        attn_prefill_kernel<PAGED, G, 0, 2><<<grid, NTHR / 2, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq, Hkv,
-                                                                       Hg, gq, sl, p, kv_major);
-    else
-        attn_prefill_kernel<PAGED, G, 0><<<grid, NTHR, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq, Hkv, Hg,
-                                                               gq, sl, p, kv_major);
+    attn_prefill_kernel<PAGED, G, 0><<<grid, NTHR, 0, s>>>(Q, row_stride, cu, it, out, out_stride, Hq, Hkv, Hg,
+                                                                   gq, sl, p, kv_major);
 }
 
 static bool packed_ratio(int G) { return G == 1 || G == 2 || G == 4 || G == 8; }
@@ -471,10 +415,9 @@ MRSUM_API int mrsum_attn_prefill_block_m(int Hq, int Hkv) {
 
 static int launch_prefill(const void* qkv, int row_stride, const int* cu_seqlens, const int* items, int n_items,
                           int block_m, void* out, int out_stride, int Hq, int Hkv, int Dh, float scale,
-                          const PagedKV* pk, int kv8, int qb, hipStream_t s) {
+                          const PagedKV* pk, int kv8, hipStream_t s) {
     if (n_items <= 0) return 0;
-    if (Dh != D || mrsum_attn_prefill_block_m(Hq, Hkv) != block_m || (qb != 1 && qb != 2))
-        return (int)hipErrorInvalidValue;
+    if (Dh != D || mrsum_attn_prefill_block_m(Hq, Hkv) != block_m) return (int)hipErrorInvalidValue;
     const int G = Hq / Hkv;
     const int Hg = packed_ratio(G) ? Hkv : Hq;  // head groups per work item (see the kernel's header)
     const int gq = packed_ratio(G) ? 1 : G;
@@ -486,10 +429,10 @@ static int launch_prefill(const void* qkv, int row_stride, const int* cu_seqlens
     const PagedKV p = pk ? *pk : PagedKV{nullptr, nullptr, nullptr, 0, nullptr, nullptr};
 #define DISPATCH(PG)                                                                                                 \
     switch (packed_ratio(G) ? G : 1) {                                                                               \
-        case 1: launch_g<PG, 1>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p, kv8, qb); break; \
-        case 2: launch_g<PG, 2>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p, kv8, qb); break; \
-        case 4: launch_g<PG, 4>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p, kv8, qb); break; \
-        default: launch_g<PG, 8>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p, kv8, qb); break; \
+        case 1: launch_g<PG, 1>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p, kv8); break; \
+        case 2: launch_g<PG, 2>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p, kv8); break; \
+        case 4: launch_g<PG, 4>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p, kv8); break; \
+        default: launch_g<PG, 8>(grid, s, Q, row_stride, cu_seqlens, IT, O, out_stride, Hq, Hkv, Hg, gq, sl, p, kv8); break; \
     }
     if (pk) { DISPATCH(true) } else { DISPATCH(false) }
 #undef DISPATCH
@@ -497,12 +440,11 @@ static int launch_prefill(const void* qkv, int row_stride, const int* cu_seqlens
 }
 
 // items: (sequence, first query row) pairs of block_m = mrsum_attn_prefill_block_m(Hq, Hkv) rows each.
-// qb: 32-row query blocks per wave (1: 8 waves; 2: 4 waves, bf16 K/V only -- the kernel header).
 MRSUM_API int mrsum_attn_prefill(const void* qkv, int row_stride, const int* cu_seqlens, const int* items,
                                  int n_items, int block_m, void* out, int out_stride, int Hq, int Hkv, int Dh,
-                                 float scale, int qb, hipStream_t s) {
+                                 float scale, hipStream_t s) {
     return launch_prefill(qkv, row_stride, cu_seqlens, items, n_items, block_m, out, out_stride, Hq, Hkv, Dh, scale,
-                          nullptr, 0, qb, s);
+                          nullptr, 0, s);
 }
 
 // Chunked-prefill attention: q rows of the packed slices (qkv, cu_seqlens), keys / values from the paged
@@ -510,12 +452,10 @@ MRSUM_API int mrsum_attn_prefill(const void* qkv, int row_stride, const int* cu_
 MRSUM_API int mrsum_attn_prefill_paged(const void* qkv, int row_stride, const int* cu_seqlens, const int* items,
                                        int n_items, int block_m, void* out, int out_stride, int Hq, int Hkv, int Dh,
                                        float scale, const void* kcache, const void* vcache, const int* block_tables,
-                                       int bt_stride, const int* seq_slot, const int* prefix, int kv8, int qb,
-                                       hipStream_t s) {
-    if (!kcache || !vcache || !block_tables || !seq_slot || !prefix || (kv8 != 0 && kv8 != 2 && kv8 != 3) ||
-        (kv8 != 0 && qb != 1))
+                                       int bt_stride, const int* seq_slot, const int* prefix, int kv8, hipStream_t s) {
+    if (!kcache || !vcache || !block_tables || !seq_slot || !prefix || (kv8 != 0 && kv8 != 2 && kv8 != 3))
         return (int)hipErrorInvalidValue;  // an fp8 K with a bf16 V cache is not a layout the engine makes
     const PagedKV pk{(const bf16*)kcache, (const bf16*)vcache, block_tables, bt_stride, seq_slot, prefix};
     return launch_prefill(qkv, row_stride, cu_seqlens, items, n_items, block_m, out, out_stride, Hq, Hkv, Dh, scale,
-                          &pk, kv8, qb, s);
+                          &pk, kv8, s);
 }

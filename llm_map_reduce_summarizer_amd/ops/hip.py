@@ -31,11 +31,10 @@ _SIGS = {
     "mrsum_swiglu": [_vp, _vp, _c_int, _c_int, _vp],
     "mrsum_kv_scatter": [_vp, _c_int, _c_int, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp],
     "mrsum_embed": [_vp, _vp, _vp, _c_int, _c_int, _c_int, _vp],
-    "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _c_int,
-                           _vp],
+    "mrsum_attn_prefill": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float, _vp],
     "mrsum_attn_prefill_paged": [_vp, _c_int, _vp, _vp, _c_int, _c_int, _vp, _c_int, _c_int, _c_int, _c_int, _c_float,
                                  _vp,
-                                 _vp, _vp, _c_int, _vp, _vp, _c_int, _c_int, _vp],
+                                 _vp, _vp, _c_int, _vp, _vp, _c_int, _vp],
     "mrsum_attn_decode_mfma": [_vp, _c_int, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int, _c_int,
                                _c_int, _c_int, _c_int, _c_int, _c_float, _vp, _c_int, _vp],
     "mrsum_attn_decode_rope": [_vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _c_int, _c_int,
@@ -306,11 +305,6 @@ def prefill_items(seqlens, group: int) -> torch.Tensor:
     return torch.tensor([(s, qb) for qb, s in items], dtype=torch.int32).reshape(-1, 2)
 
 
-# 32-row query blocks per wave of the prefill attention (attn_prefill.hip QB): 1 = 8 waves x 32 rows, 2 = 4 waves
-# x 64 rows (each K / V fragment read from LDS feeds two MFMAs; bf16 K/V only)
-ATTN_PREFILL_QB = 1
-
-
 def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int, d: int, scale: float,
                  out: Optional[torch.Tensor] = None, items: Optional[torch.Tensor] = None,
                  seqlens=None, paged=None) -> torch.Tensor:
@@ -348,12 +342,11 @@ def attn_prefill(qkv: torch.Tensor, cu_seqlens: torch.Tensor, hq: int, hkv: int,
                  "attn_prefill: slice [%d, %d) beyond block table" % (pre, pre + n))
         _check(_fn("mrsum_attn_prefill_paged")(_p(qkv), qkv.stride(0), _p(cu_seqlens), _p(items), items.shape[0],
                                                block_m, _p(out), out.stride(0), hq, hkv, d, scale, _p(kc), _p(vc), _p(bt),
-                                               bt.stride(0), _p(paged.seq_slot), _p(paged.prefix), kv8,
-                                               ATTN_PREFILL_QB if kv8 == 0 else 1, _stream()),
+                                               bt.stride(0), _p(paged.seq_slot), _p(paged.prefix), kv8, _stream()),
                "attn_prefill_paged")
         return out
     _check(_fn("mrsum_attn_prefill")(_p(qkv), qkv.stride(0), _p(cu_seqlens), _p(items), items.shape[0], block_m, _p(out),
-                                     out.stride(0), hq, hkv, d, scale, ATTN_PREFILL_QB, _stream()), "attn_prefill")
+                                     out.stride(0), hq, hkv, d, scale, _stream()), "attn_prefill")
     return out
 
 

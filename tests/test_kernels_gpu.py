@@ -97,19 +97,14 @@ def test_swiglu_embed():
 # (6, 2) / (24, 8) / (10, 2): GQA ratios 3 and 5 (Llama-3.2-3B is 24 / 8) take the per-query-head fallback
 @pytest.mark.parametrize("hq,hkv", [(4, 2), (8, 2), (8, 1), (2, 2), (6, 2), (24, 8), (10, 2)])
 @pytest.mark.parametrize("seqlens", [[1, 37, 130, 300], [64], [129, 256], [1000, 33, 2100]])
-@pytest.mark.parametrize("qb", [1, 2])
-def test_attn_prefill(hq, hkv, seqlens, qb):
-    """Causal varlen prefill attention vs fp32; qb = 32-row query blocks per wave (attn_prefill.hip QB)."""
+def test_attn_prefill(hq, hkv, seqlens):
+    """Causal varlen prefill attention vs fp32."""
     d = 128
     T = sum(seqlens)
     qkv = _rand(T, (hq + 2 * hkv) * d, seed=11)
     cu = torch.tensor([0] + list(torch.tensor(seqlens).cumsum(0)), dtype=torch.int32, device=DEV)
     sc = 1.0 / math.sqrt(d)
-    old, hip.ATTN_PREFILL_QB = hip.ATTN_PREFILL_QB, qb
-    try:
-        o1 = hip.attn_prefill(qkv, cu, hq, hkv, d, sc)
-    finally:
-        hip.ATTN_PREFILL_QB = old
+    o1 = hip.attn_prefill(qkv, cu, hq, hkv, d, sc)
     o2 = reference.attn_prefill(qkv, cu, hq, hkv, d, sc)
     _close(o1, o2, 2e-2)
 
@@ -178,7 +173,7 @@ def test_rope_kv_fp8_cache_tiny_rows():
 
 @pytest.mark.parametrize("hq,hkv", [(4, 1), (8, 2), (8, 1), (2, 2), (6, 2)])
 @pytest.mark.parametrize("spans", [[(0, 200)], [(130, 300), (0, 77), (1000, 1129)], [(64, 128), (2047, 2048)]])
-@pytest.mark.parametrize("kv8", ["bf16", "fp8", "fp8v", "bf16-qb2"])
+@pytest.mark.parametrize("kv8", ["bf16", "fp8", "fp8v"])
 def test_attn_prefill_paged(hq, hkv, spans, kv8):
     """Chunked-prefill attention: slice rows attend to [0, prefix + slice) of their sequence read from the
     paged cache (random non-contiguous pages, stale rows past the slice end), vs the fp32 reference."""
@@ -188,8 +183,6 @@ def test_attn_prefill_paged(hq, hkv, spans, kv8):
     n_pages, maxp = 160, 40
     kc = (torch.randn(n_pages, hkv, page, d, generator=g) * 0.5).to(torch.bfloat16).to(DEV)
     vc = torch.randn(n_pages, hkv, page, d, generator=g).to(torch.bfloat16).to(DEV)
-    qb = 2 if kv8.endswith("-qb2") else 1  # 4 waves x two 32-row query blocks (bf16 caches only)
-    kv8 = kv8.split("-")[0]
     kc, vc = _kv_format(kc, vc, kv8)
     nseq = len(spans)
     perm = torch.randperm(n_pages - 1, generator=g)[: nseq * maxp] + 1
@@ -204,11 +197,7 @@ def test_attn_prefill_paged(hq, hkv, spans, kv8):
     i32 = lambda x: torch.tensor(x, dtype=torch.int32, device=DEV)  # noqa: E731
     pp = PagedPrefill(bt, i32(slots), i32(pre), slots, pre, kc, vc)
     sc = 1.0 / math.sqrt(d)
-    old, hip.ATTN_PREFILL_QB = hip.ATTN_PREFILL_QB, qb
-    try:
-        o1 = hip.attn_prefill(qkv, cu, hq, hkv, d, sc, paged=pp)
-    finally:
-        hip.ATTN_PREFILL_QB = old
+    o1 = hip.attn_prefill(qkv, cu, hq, hkv, d, sc, paged=pp)
     o2 = reference.attn_prefill_paged(qkv, cu, hq, hkv, d, sc, pp)
     _close(o1, o2, 2e-2)
 

@@ -37,18 +37,7 @@ def main():
     ap.add_argument("--hq", type=int, default=32)
     ap.add_argument("--hkv", type=int, default=8)
     ap.add_argument("--prefix", type=int, default=0, help="paged case: cached tokens before each slice")
-    ap.add_argument("--qb", default="", help="query blocks per wave to compare, e.g. 1,2 (attn_prefill.hip QB)")
     a = ap.parse_args()
-    if a.qb:
-        for qb in a.qb.split(","):
-            hip.ATTN_PREFILL_QB = int(qb)
-            a.tag = "qb%s" % qb
-            run(a)
-        return
-    run(a)
-
-
-def run(a):
     dev, hq, hkv, d = "cuda:0", a.hq, a.hkv, 128
     torch.manual_seed(0)
     for case in a.cases.split(","):
