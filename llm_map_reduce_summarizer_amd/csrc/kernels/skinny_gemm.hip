@@ -643,9 +643,30 @@ __global__ __launch_bounds__(64 * NW) void skinny_fp8_kernel(const bf16* __restr
     const int n0 = blockIdx.x * BN;
     const int ks = blockIdx.y * kper, ke = min(K, ks + kper);
     const unsigned tp_epoch = EPI == EPI_RESID && e.tp.world > 0 ? e.tp.epochs[n0 / mrsum_ar::GRAN] + 1 : 0;
+    constexpr int STEP = NW * KB;
+    const int kb0 = ks + w * KB;
+    const int nb = kb0 < ke ? (ke - kb0 + STEP - 1) / STEP : 0;
+    A8Frag<NT> a0, a1;
+    // XL: the x slice's loads first, then the first weight block's, and only then the LDS writes of the
+    // slice -- waiting for x (the older loads: vmcnt retires in order) never waits for W, so the weight
+    // stream starts under the slice's round trip instead of after the barrier
+    constexpr int XPRE = 4;  // 16-B x chunks per thread held in registers across the first weight loads
+    const uint4* xsrc = reinterpret_cast<const uint4*>(x + ks);
+    const int nx = kper / 8;
+    uint4 xr[XL ? XPRE : 1];
     if constexpr (XL) {
-        const uint4* src = reinterpret_cast<const uint4*>(x + ks);
-        for (int i = threadIdx.x; i < kper / 8; i += 64 * NW) reinterpret_cast<uint4*>(xs)[i] = src[i];
+#pragma unroll
+        for (int j = 0; j < XPRE; ++j) xr[j] = xsrc[min((int)threadIdx.x + j * 64 * NW, nx - 1)];  // clamped
+    }
+    if (nb > 0) load_a8<NT>(a0, W, K, n0, kb0, lane);
+    if constexpr (XL) {
+#pragma unroll
+        for (int j = 0; j < XPRE; ++j) {
+            const int i = threadIdx.x + j * 64 * NW;
+            if (i < nx) reinterpret_cast<uint4*>(xs)[i] = xr[j];
+        }
+        for (int i = threadIdx.x + XPRE * 64 * NW; i < nx; i += 64 * NW)  // slices beyond 4 chunks per thread
+            reinterpret_cast<uint4*>(xs)[i] = xsrc[i];
         if (ssq && threadIdx.x < 8) {
             const int C = ssq_tiles / 8;
             const float4* sp = reinterpret_cast<const float4*>(ssq + threadIdx.x * C);
@@ -656,7 +677,10 @@ __global__ __launch_bounds__(64 * NW) void skinny_fp8_kernel(const bf16* __restr
             }
             s_ss[threadIdx.x] = (a.x + a.y) + (a.z + a.w);
         }
-        __syncthreads();
+        // LDS writes visible to the workgroup; no vmcnt(0) here (the weight loads stay in flight)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
     }
     auto load_b = [&](BFrag<MT>& b, int kb) {
         if constexpr (XL) {
@@ -675,12 +699,7 @@ __global__ __launch_bounds__(64 * NW) void skinny_fp8_kernel(const bf16* __restr
         for (int m = 0; m < MT; ++m) acc[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // unconditional next-block loads in the steady loop, straight-line tails (as skinny_gemm_kernel)
-    constexpr int STEP = NW * KB;
-    const int kb0 = ks + w * KB;
-    const int nb = kb0 < ke ? (ke - kb0 + STEP - 1) / STEP : 0;
-    A8Frag<NT> a0, a1;
     BFrag<MT> b;
-    if (nb > 0) load_a8<NT>(a0, W, K, n0, kb0, lane);
     int i = 0;
     for (; i + 2 < nb; i += 2) {
         const int kb = kb0 + i * STEP;

@@ -10,6 +10,7 @@ Variants (comma separated, ``plan`` = unchanged):
   gate_up:stream_split:WPB:S   split-K gate_up with the SwiGLU in the last arriver
   deferM                       the TP=1 deferred RMSNorm up to M rows (ops.DEFER_NORM_MAX_M)
   waves:W                      register-streaming kernels with W (4 | 8) waves per workgroup at every grid
+  w8max:N                      8-wave register-streaming workgroups for one row up to N workgroups
   fp8resid:N:K:WPB:S           the fp8 deferred-norm producer (stream_fp8, residual epilogue) of one shape
   buckets:B1+B2+...            decode graph buckets up to the largest given (the rest unchanged)
   resid:ROLE=KIND              the deferred-norm / TP-push producer of ROLE (o | down) forced to KIND
@@ -57,6 +58,7 @@ def main():
     from llm_map_reduce_summarizer_amd import ops
     base_defer = ops.DEFER_NORM_MAX_M
     base_fp8r = hip.fp8_resid_cfg
+    base_w8max = hip.SKINNY_WAVES8_MAX_WGS
 
     env_set = []
     import llm_map_reduce_summarizer_amd.engine.engine as engine_mod
@@ -67,6 +69,7 @@ def main():
         ops.DEFER_NORM_MAX_M = base_defer
         hip.fp8_resid_cfg = base_fp8r
         hip.SKINNY_WAVES_FORCE = None
+        hip.SKINNY_WAVES8_MAX_WGS = base_w8max
         for name, old in env_set:
             if old is None:
                 os.environ.pop(name, None)
@@ -95,6 +98,9 @@ def main():
         if v.startswith("fp8resid:"):  # fp8resid:N:K:wpb:S -- the fp8 deferred-norm producer of one shape
             N0, K0, wpb, S = (int(t) for t in v.split(":")[1:])
             hip.fp8_resid_cfg = lambda M, N, K: (wpb, S) if (N, K) == (N0, K0) else base_fp8r(M, N, K)
+            return
+        if v.startswith("w8max:"):
+            hip.SKINNY_WAVES8_MAX_WGS = int(v[len("w8max:"):])
             return
         if v.startswith("waves:"):
             hip.SKINNY_WAVES_FORCE = int(v[len("waves:"):])
