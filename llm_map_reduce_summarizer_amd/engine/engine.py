@@ -199,15 +199,18 @@ class LLMEngine:
                  kv_pages: Optional[int] = None, kv_fraction: float = 0.6, page_size: int = 64,
                  max_prefill_tokens: int = 16384, use_graphs: bool = True, sync_every: int = 16,
                  eos_ids: Sequence[int] = (128001, 128009), tp_rank: int = 0, tp_size: int = 1, tp_group=None,
-                 weight_dtype: str = "bf16", weights_path: Optional[str] = None, prefill_chunk: int = 4096,
+                 weight_dtype: str = "bf16", weights_path: Optional[str] = None, prefill_chunk: int = 8192,
                  kv_dtype: Optional[str] = None):
         """``kv_dtype``: "bf16" (default, $MRSUM_KV_DTYPE), "fp8v" (V rows fp8, K bf16) or "fp8" -- e4m3fn K/V rows with power-of-two
         row scales (engine/kv_cache.py): half the KV bytes per decode step; no context-parallel prefill.
 
         ``prefill_chunk``: cut prompts longer than this many tokens into slices prefilled one pass
         after the other through the paged cache (chunked prefill; 0 = one pass per prompt).  At 32k
-        tokens on Llama-3-8B 4096-token slices took 0.669 s vs 0.701 s in one pass; 70B fp8 8192-token
-        slices 3.53 vs 3.52 s (profiles/r2_chunked_prefill_32k_ab.jsonl)."""
+        tokens on Llama-3-8B 4096-token slices took 0.669 s vs 0.701 s in one pass (profiles/
+        r2_chunked_prefill_32k_ab.jsonl); 8192-token slices keep every GEMM's 256-row tile grid whole waves on
+        256 CUs (4096 rows left the QKV projections at 1.5 / 2.5 waves): Llama-3-70B fp8 at 32k 3.21 s vs
+        3.27 with 4096 and 3.23 with 16384, Llama-3-8B at 13.5k / 32k 0.203 / 0.607 s vs 0.207 / 0.610
+        (profiles/r5_prefill_chunk_{70b,8b}_ab.jsonl)."""
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
