@@ -13,4 +13,12 @@ MRSUM_DIST_BACKEND=gloo timeout -k 10 900 python -m torch.distributed.run --nnod
 rc=$?
 grep "^{" gpurun_out/r5_rehearsal_8rank.log > gpurun_out/r5_rehearsal_8rank.json
 echo "rc=$rc"
+[ $rc -eq 0 ] || exit $rc
+# the same with round 4's 4-wave register-streaming kernels (their fp32 summation order)
+MRSUM_SKINNY_WAVES=4 MRSUM_DIST_BACKEND=gloo timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+  --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 8 --hours 1 --steps 1 --warmup 0 \
+  --max-new-tokens 32 --parallel map:tp2,reduce_final:tp8 --log-level INFO > gpurun_out/r5_rehearsal_8rank_w4.log 2>&1
+rc=$?
+grep "^{" gpurun_out/r5_rehearsal_8rank_w4.log > gpurun_out/r5_rehearsal_8rank_w4.json
+echo "rc=$rc"
 exit $rc
