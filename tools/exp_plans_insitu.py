@@ -10,6 +10,7 @@ Variants (comma separated, ``plan`` = unchanged):
   gate_up:stream_split:WPB:S   split-K gate_up with the SwiGLU in the last arriver
   deferM                       the TP=1 deferred RMSNorm up to M rows (ops.DEFER_NORM_MAX_M)
   waves:W                      register-streaming kernels with W (4 | 8) waves per workgroup at every grid
+  fp8stream:N:K:WPB:S          the fp8 weight of shape N x K on the LDS-DMA stream kernel with (wpb, S) (S 1 for SwiGLU)
   w8max:N                      8-wave register-streaming workgroups for one row up to N workgroups
   fp8resid:N:K:WPB:S           the fp8 deferred-norm producer (stream_fp8, residual epilogue) of one shape
   buckets:B1+B2+...            decode graph buckets up to the largest given (the rest unchanged)
@@ -58,6 +59,7 @@ def main():
     from llm_map_reduce_summarizer_amd import ops
     base_defer = ops.DEFER_NORM_MAX_M
     base_fp8r = hip.fp8_resid_cfg
+    base_scf8 = hip.stream_config_fp8
     base_w8max = hip.SKINNY_WAVES8_MAX_WGS
 
     env_set = []
@@ -68,6 +70,7 @@ def main():
         hip.decode_attn_plan, hip.plan = base_attn, base_plan
         ops.DEFER_NORM_MAX_M = base_defer
         hip.fp8_resid_cfg = base_fp8r
+        hip.stream_config_fp8 = base_scf8
         hip.SKINNY_WAVES_FORCE = None
         hip.SKINNY_WAVES8_MAX_WGS = base_w8max
         for name, old in env_set:
@@ -94,6 +97,15 @@ def main():
                 name, val = kv.split("=", 1)
                 env_set.append((name, os.environ.get(name)))
                 os.environ[name] = val
+            return
+        if v.startswith("fp8stream:"):  # fp8stream:N:K:wpb:S -- one fp8 shape on the stream kernel
+            N0, K0, wpb, S = (int(t) for t in v.split(":")[1:])
+
+            def scf8(N, K, swiglu=False, splits=None, M=1):
+                if (N, K) == (N0, K0):
+                    return (wpb, splits or S)
+                return base_scf8(N, K, swiglu=swiglu, splits=splits, M=M)
+            hip.stream_config_fp8 = scf8
             return
         if v.startswith("fp8resid:"):  # fp8resid:N:K:wpb:S -- the fp8 deferred-norm producer of one shape
             N0, K0, wpb, S = (int(t) for t in v.split(":")[1:])
