@@ -22,7 +22,6 @@ every chunk of a rank is in flight at once, bounded only by HBM.
 from __future__ import annotations
 
 import logging
-import math
 import os
 import time
 from dataclasses import dataclass, field
