@@ -391,3 +391,34 @@ def test_fp8_kv_cache_cpu():
     assert e.kv.k.dtype == torch.bfloat16 and e.kv.v.dtype == torch.uint8 and e.kv.fp8
     # V-only rounding: closer to bf16 KV than the K+V variant
     assert float((a - rec["fp8v"]).norm() / a.norm()) <= float((a - b).norm() / a.norm()) + 1e-6
+
+
+def test_pinned_windows_run_to_the_first_length_stop():
+    """ignore_eos: no row can stop before its max_new_tokens, so the host syncs only when the first row runs
+    out of steps (LLMEngine._window), not every sync_every steps -- with identical tokens."""
+    cfg = get_model_config("tiny", init_std=0.05)
+    ps = [SamplingParams(5 + 4 * i, 0.3, 20 + i) for i in range(4)]
+    outs, wins = [], []
+    for se in (2, 64):
+        e = LLMEngine(cfg, device="cpu", max_model_len=512, max_num_seqs=8, kv_pages=64, sync_every=se)
+        outs.append([o.token_ids for o in e.generate(_prompts(4), ps, ignore_eos=True)])
+        wins.append(e.stats["decode_windows"])
+        assert e.state.eos_ids  # re-armed after the pinned call
+        armed = e.generate(_prompts(4), ps)  # EOS armed: sync_every windows again
+        assert [len(o.token_ids) for o in armed] <= [p.max_new_tokens for p in ps]
+    assert outs[0] == outs[1]
+    assert [len(t) for t in outs[0]] == [p.max_new_tokens for p in ps]
+    # max_new 5 / 9 / 13 / 17 (first token sampled at prefill): windows of 4, 4, 4, 4 steps at most
+    assert wins[0] == wins[1] == 4
+
+
+def test_window_rule():
+    e = LLMEngine(get_model_config("tiny"), device="cpu", max_model_len=256, max_num_seqs=4, kv_pages=16,
+                  sync_every=16)
+    assert e._window([], False) == 0 and e._window([0, 0], False) == 0
+    assert e._window([40, 7], False) == 16  # EOS armed: sync_every, bounded by the longest row
+    assert e._window([5, 3], False) == 5
+    e.state.set_eos([])
+    assert e._window([40, 7], False) == 7  # pinned: until the first row runs out
+    assert e._window([4000, 3000], False) == 256  # at most MAX_WINDOW
+    assert e._window([40, 7], True) == 16  # a feeder / stream hook / interleaved prefill wants sync points
