@@ -254,5 +254,9 @@ if __name__ == "__main__":
     sys.stderr.flush()
     # the process groups are already torn down (pdist.shutdown: barrier, subgroups, default group); leave
     # without the interpreter's finalisation, where the C++ destructors of communication backends that
-    # still hold threads have aborted a finished job (SIGABRT after a good result)
-    os._exit(code)
+    # still hold threads have aborted a finished job (SIGABRT after a good result).  A single process that
+    # never formed a group exits normally: its atexit work includes a profiler's flush (rocprofv3 writes
+    # its traces there; os._exit would drop them).
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or os.environ.get("MRSUM_FORCE_DIST") == "1":
+        os._exit(code)
+    sys.exit(code)
