@@ -270,3 +270,20 @@ def test_fp8_kv_cache_engine(kvd):
     agree = sum(e.generate([p + o.token_ids[:-1]], [SamplingParams(1, 0.0, 0)])[0].token_ids[0] == o.token_ids[-1]
                 for p, o in zip(prompts, outs))
     assert agree >= len(prompts) - 1
+
+
+def test_pinned_windows_match_short_windows(eng, monkeypatch):
+    """ignore_eos: one window of up to MAX_WINDOW graph replays per batch (LLMEngine._window) gives the same
+    tokens as 2-step windows with a host sync between them (equal max_new: same batch composition)."""
+    prompts = _prompts()
+    ps = [SamplingParams(40, 0.3, 7 + i) for i in range(len(prompts))]
+    w0 = eng.stats.get("decode_windows", 0)
+    long_w = eng.generate(prompts, ps, ignore_eos=True)
+    n_long = eng.stats["decode_windows"] - w0
+    monkeypatch.setattr(LLMEngine, "_window", lambda self, left, hooked: min(2, max([0] + left)))
+    w1 = eng.stats["decode_windows"]
+    short_w = eng.generate(prompts, ps, ignore_eos=True)
+    n_short = eng.stats["decode_windows"] - w1
+    assert [o.token_ids for o in long_w] == [o.token_ids for o in short_w]
+    assert all(len(o.token_ids) == 40 for o in long_w)
+    assert n_long == 1 and n_short == 20  # 39 steps after the prefill's token: one window vs twenty
