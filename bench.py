@@ -158,6 +158,7 @@ def main() -> int:
         torch.cuda.synchronize()
     from llm_map_reduce_summarizer_amd.utils.profiling import maybe_profile
     work0 = dict(provider.work)
+    stages0 = {k: dict(v) for k, v in provider.stage_seconds.items()}
     t0 = time.perf_counter()
     reports = []
     with maybe_profile(args.profile, rank):
@@ -193,6 +194,18 @@ def main() -> int:
     ar_recoveries = sum(int(e.get("custom_ar_recoveries", 0)) for e in tp_engs.values())
     n_chunks = rep["chunks"]
     value = n_chunks / (ms / 1000.0)
+    # per stage and timed step: the planner's prediction at the layout the stage ran next to its measured wall
+    # time (parallel/plan.py stage_seconds vs the provider's generate calls; rank 0's clock), and the measured
+    # cross-GPU cost of one decode all-reduce per path and TP degree -- what a first multi-GPU run needs to
+    # tell which stage missed its model and whether the xGMI push latency is the reason
+    stages = {}
+    for st, r in provider.stage_seconds.items():
+        r0 = stages0.get(st, {"calls": 0, "predicted_s": 0.0, "measured_s": 0.0})
+        n = max(1, args.steps)
+        pred = None if r.get("predicted_s") is None or r0.get("predicted_s") is None else \
+            round((r["predicted_s"] - r0["predicted_s"]) / n, 6)
+        stages[st] = {"tp": r["tp"], "calls_per_step": (r["calls"] - r0["calls"]) / n, "predicted_s": pred,
+                      "measured_s": round((r["measured_s"] - r0["measured_s"]) / n, 4)}
     eng = rep.get("engine", {})
     out = {
         "metric": "chunks/sec (whole node) + end-to-end wall-clock, 10h transcript, Llama-3-8B"
@@ -230,6 +243,9 @@ def main() -> int:
         "tokens_used": rep.get("tokens_used"),
         "timed_work": dict(work, pinned_ok=work_ok),
         "p2p_selftest": p2p or None,
+        "stages": stages,
+        "p2p_latency_us": pstats.get("p2p_latency") or None,
+        "planner_hw": pstats.get("planner_hw"),
         "ar_recoveries": ar_recoveries,
         "engine_rank0": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in eng.items()},
     }
@@ -249,14 +265,8 @@ def main() -> int:
 
 
 if __name__ == "__main__":
+    # one exit path with the CLI: flush, then os._exit for a rank of a multi-process job (no backend C++
+    # destructors after the printed result), sys.exit otherwise (parallel/dist.py exit_process)
     code = main()
-    sys.stdout.flush()
-    sys.stderr.flush()
-    # the process groups are already torn down (pdist.shutdown: barrier, subgroups, default group); leave
-    # without the interpreter's finalisation, where the C++ destructors of communication backends that
-    # still hold threads have aborted a finished job (SIGABRT after a good result).  A single process that
-    # never formed a group exits normally: its atexit work includes a profiler's flush (rocprofv3 writes
-    # its traces there; os._exit would drop them).
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or os.environ.get("MRSUM_FORCE_DIST") == "1":
-        os._exit(code)
-    sys.exit(code)
+    from llm_map_reduce_summarizer_amd.parallel import dist as _pdist
+    _pdist.exit_process(code)

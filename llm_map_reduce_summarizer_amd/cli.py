@@ -220,4 +220,5 @@ def main(argv: Optional[List[str]] = None) -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    from .parallel.dist import exit_process
+    exit_process(main())

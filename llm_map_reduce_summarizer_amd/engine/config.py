@@ -14,6 +14,11 @@ from __future__ import annotations
 from dataclasses import dataclass, replace
 from typing import Optional, Tuple
 
+# The engine's default chunked-prefill slice length (tokens; engine/engine.py LLMEngine ``prefill_chunk``).
+# Defined here, next to the model presets, so the planner (parallel/plan.py) prices the slice length the
+# engine actually runs without importing the engine; tests/test_plan.py fails if the two drift.
+PREFILL_CHUNK = 8192
+
 
 @dataclass(frozen=True)
 class ModelConfig:

@@ -32,7 +32,7 @@ import numpy as np
 import torch
 
 from .. import ops
-from .config import ModelConfig
+from .config import PREFILL_CHUNK, ModelConfig
 from .kv_cache import PagedKVCache
 from .model import LlamaModel
 
@@ -183,10 +183,14 @@ class _CPExchange:
             work = dist.all_gather(out, mine.cpu(), group=self.group, async_op=True)
         return (layer, k, work, out, mine)
 
-    def finish(self, h) -> None:
-        """Wait for a started exchange and scatter the other ranks' rows into the paged cache."""
+    def finish(self, h, works=None) -> None:
+        """Wait for a started exchange and scatter the other ranks' rows into the paged cache; ``works``
+        (parallel/dist.py AsyncWorks) stops tracking the handle once waited, so its buffers can go."""
         layer, k, work, out, _mine = h
-        work.wait()
+        if works is not None:
+            works.wait(work)
+        else:
+            work.wait()
         e = self.eng
         rows = out if self.nccl else torch.stack(out).to(e.device)
         page_d, slot_d = self.dst[k]
@@ -200,7 +204,7 @@ class LLMEngine:
                  kv_pages: Optional[int] = None, kv_fraction: float = 0.6, page_size: int = 64,
                  max_prefill_tokens: int = 16384, use_graphs: bool = True, sync_every: int = 16,
                  eos_ids: Sequence[int] = (128001, 128009), tp_rank: int = 0, tp_size: int = 1, tp_group=None,
-                 weight_dtype: str = "bf16", weights_path: Optional[str] = None, prefill_chunk: int = 8192,
+                 weight_dtype: str = "bf16", weights_path: Optional[str] = None, prefill_chunk: int = PREFILL_CHUNK,
                  kv_dtype: Optional[str] = None):
         """``kv_dtype``: "bf16" (default, $MRSUM_KV_DTYPE), "fp8v" (V rows fp8, K bf16) or "fp8" -- e4m3fn K/V rows with power-of-two
         row scales (engine/kv_cache.py): half the KV bytes per decode step; no context-parallel prefill.

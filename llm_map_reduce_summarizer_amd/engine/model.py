@@ -461,9 +461,8 @@ class LlamaModel:
             # SP: the residual is kept as this rank's row shard (see _sp_rows)
             st.append({"res": self._sp_shard(res) if sp else res, "x": x, "T": T, "q": (q8, q8qkv)})
 
-        def wait(h):
-            if h is not None:
-                h.wait()
+        def wait(h):  # a waited handle is dropped from the scope at once (AsyncWorks.wait)
+            works.wait(h)
 
         def reduce_async(s, t, key):  # the TP sum of a projection's partial rows
             if sp:
@@ -532,7 +531,7 @@ class LlamaModel:
                     handles.append(exchange.start(i, k))
                     works.add(handles[-1][2])
                 for p, s, qkv, h in zip(passes, st, qkvs, handles):
-                    exchange.finish(h)
+                    exchange.finish(h, works)
                     kw = {"seqlens": p.seqlens, "items": p.items} if qkv.is_cuda else {}
                     a = ops.attn_prefill(qkv, p.cu_seqlens, self.hq, self.hkv, self.hd, self.scale,
                                          paged=p.paged.layer(kcache[i], vcache[i]), **kw)

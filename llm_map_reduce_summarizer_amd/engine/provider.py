@@ -183,6 +183,12 @@ class LocalEngineProvider(Provider):
         if self.handoff:
             self._dp_needed = True
         self.stage_plan: Dict[str, Any] = {}
+        # per stage: the planner's predicted seconds (parallel/plan.py stage_seconds at the layout the stage
+        # ran) next to the measured wall time of its generate calls -- the record that makes the first real
+        # multi-GPU run diagnosable (which stage missed its model, by how much)
+        self.stage_seconds: Dict[str, Dict[str, Any]] = {}
+        # TP degree -> the cross-GPU cost of one decode all-reduce per path, measured when its engine is built
+        self.p2p_latency: Dict[str, Dict[str, float]] = {}
         self.owner_maps: Dict[str, List[List[int]]] = {}  # stage -> replica of every request, per call
         if self.use_tp_engine:
             self._engine_options.setdefault("kv_fraction", float(os.environ.get("MRSUM_DP_KV_FRACTION", "0.5")))
@@ -272,7 +278,59 @@ class LocalEngineProvider(Provider):
                     self.parallel, self.use_tp_engine, self._dp_needed = "dp", False, True
                 return None
             self._tp_engines[k] = eng
+            self._measure_p2p(k, eng)
         return eng
+
+    def _measure_p2p(self, k: int, eng) -> None:
+        """COLLECTIVE within the TP=k group (every rank builds the engine at the same point): the cross-GPU
+        cost of one decode all-reduce on each path the decode can take -- the TP push of the down projection's
+        shard (the path it runs) and the fused all-reduce + add + RMSNorm (its fallback) -- as a + b x rows
+        over the same kernel on a group of one (CustomAllReduce.measure_latency).  Recorded per degree for the
+        bench JSON; MRSUM_P2P_LATENCY=0 skips it."""
+        ar = eng.model.custom_ar
+        if ar is None or os.environ.get("MRSUM_P2P_LATENCY", "1") != "1":
+            return
+        m = eng.model
+        rec: Dict[str, float] = {}
+        try:
+            for path, push_k in (("push", m.ffn_local), ("fused", None)):
+                if path == "push" and not ar.paths.get("push_stream"):
+                    continue
+                lat, per_row = ar.measure_latency(rows=(1, 64), hidden=eng.cfg.hidden, push_k=push_k,
+                                                  fp8=m.weight_dtype == "fp8")
+                rec[path + "_us"] = round(lat * 1e6, 2)
+                rec[path + "_us_per_row"] = round(per_row * 1e6, 4)
+        except Exception as e:  # noqa: BLE001 -- a diagnostic: never fail the job on it
+            log.warning("P2P latency probe of the TP=%d engine failed: %s", k, e)
+            rec["error"] = str(e)[:200]
+        self.p2p_latency["tp%d" % k] = rec
+        log.info("TP=%d decode all-reduce, cross-GPU part: %s", k, rec)
+
+    def _predict_stage(self, prompts, reqs, tp: int, handoff: bool) -> Optional[float]:
+        """The planner's estimate (seconds) of this generate at TP degree ``tp`` over this job's ranks."""
+        try:
+            from ..parallel import plan
+            d = plan.ModelDims.of(self.model_config(),
+                                  1.0 if self._engine_options.get("weight_dtype") == "fp8" else 2.0)
+            hw = self.hw or plan.HWModel()
+            world = max(1, self.par.world)
+            if self.par.tp > 1:  # DP replicas of a TP engine
+                tp = self.par.tp
+            return plan.stage_seconds(d, hw, [len(p) for p in prompts], [r.max_tokens for r in reqs], tp, world,
+                                      handoff)
+        except Exception as e:  # noqa: BLE001 -- a diagnostic
+            log.debug("stage prediction failed: %s", e)
+            return None
+
+    def _record_stage(self, stage: str, tp: int, predicted: Optional[float], measured: float) -> None:
+        rec = self.stage_seconds.setdefault(stage, {"tp": tp, "calls": 0, "predicted_s": 0.0, "measured_s": 0.0})
+        rec["calls"] += 1
+        rec["tp"] = tp
+        rec["measured_s"] = round(rec["measured_s"] + measured, 6)
+        if predicted is None or rec["predicted_s"] is None:
+            rec["predicted_s"] = None
+        else:
+            rec["predicted_s"] = round(rec["predicted_s"] + predicted, 7)
 
     def warm(self, capture_batch: Optional[int] = None) -> None:
         """Build the engines (and measure the planner's constants) outside any timed region; with
@@ -306,8 +364,14 @@ class LocalEngineProvider(Provider):
                 return self.hw
             m = eng.model
             # the cross-GPU cost of the decode's own all-reduce: the TP push of the down projection's shard
-            lat, per_row = ar.measure_latency(rows=(1, 64), hidden=eng.cfg.hidden, push_k=m.ffn_local,
-                                              fp8=m.weight_dtype == "fp8")
+            # (measured when the engine was built, _measure_p2p; again here if that probe was skipped)
+            rec = self.p2p_latency.get("tp%d" % self.par.world, {})
+            key = "push" if "push_us" in rec else ("fused" if "fused_us" in rec else None)
+            if key is not None:
+                lat, per_row = rec[key + "_us"] * 1e-6, rec[key + "_us_per_row"] * 1e-6
+            else:
+                lat, per_row = ar.measure_latency(rows=(1, 64), hidden=eng.cfg.hidden, push_k=m.ffn_local,
+                                                  fp8=m.weight_dtype == "fp8")
             bw = _rccl_bandwidth(eng.model.tp_group, eng.cfg.hidden, torch.device(self._device))
             self.hw = plan.with_measurements(hw, ar_lat_s=lat, ar_lat_row_s=per_row, ar_bw=bw, tp_ok=True)
             log.info("planner constants: all-reduce %.1f us + %.3f us/row (%s path, over the same kernel on a "
@@ -549,10 +613,12 @@ class LocalEngineProvider(Provider):
         stage = reqs[0].stage if reqs else "map"
         tp, handoff = self._stage_tp(stage, prompts, reqs) if self.par.world > 1 and self.tp == 1 else (1, False)
         self.stage_plan.setdefault(stage, {"tp": tp, "handoff": handoff})
+        predicted = self._predict_stage(prompts, reqs, tp, handoff)
         if tp > 1:
             # TP=tp groups (tp = world: every rank runs every request); the TP ranks sample identically
             res = self._generate_tp(prompts, reqs, handoff, tp, stage)
             self.timings["generate_s"] += time.perf_counter() - t0
+            self._record_stage(stage, tp, predicted, time.perf_counter() - t0)
             self._tally(res, [r.max_tokens for r in reqs])
             return res
         dp, dp_rank = self.par.dp, self.par.dp_rank
@@ -602,6 +668,7 @@ class LocalEngineProvider(Provider):
         else:
             merged = {r["i"]: r for r in local}
         self.timings["allgather_s"] += time.perf_counter() - t1
+        self._record_stage(stage, self.par.tp, predicted, time.perf_counter() - t0)
         res = [_result(merged[i]) if i in merged else GenResult("", error="request %d produced no result" % i)
                for i in range(len(reqs))]
         self._tally(res, [r.max_tokens for r in reqs])
@@ -701,6 +768,10 @@ class LocalEngineProvider(Provider):
                              **self.timings}
         if self.stage_plan:
             s["stage_plan"] = dict(self.stage_plan)
+        if self.stage_seconds:
+            s["stage_seconds"] = {k: dict(v) for k, v in self.stage_seconds.items()}
+        if self.p2p_latency:
+            s["p2p_latency"] = {k: dict(v) for k, v in self.p2p_latency.items()}
         if self.hw is not None:
             s["planner_hw"] = {"ar_lat_us": round(self.hw.ar_lat_s * 1e6, 2),
                                "ar_us_per_row": round(self.hw.ar_lat_row_s * 1e6, 4),

@@ -437,9 +437,9 @@ def proj_add_rmsnorm(a, w, residual, ln, eps, role="o", all_reduce=None, quant=F
                     # that producer failed the start-up self-test: the other kind if it takes the shape
                     # and passed, else the fused all-reduce path below
                     other = ({"stream", "skinny"} - {rp[0]}) & kinds()
+                    # (_resid_plan's forced "skinny" checks the capacity of the kernel the weight runs on:
+                    # skinny_fp8_resid_capacity for an Fp8Weight, skinny_resid_capacity for bf16)
                     rp = _resid_plan(hip, a, w, role, tp=True, force=other.pop()) if other else None
-                    if rp is not None and rp[0] == "skinny" and w.shape[0] // 16 > hip.skinny_resid_capacity(w.shape[0]):
-                        rp = None
                 if rp is not None and rp[0] == "skinny":
                     return NormRows(residual, hip.skinny_resid(a, w, residual, tp=push), eps)
                 if rp is not None:

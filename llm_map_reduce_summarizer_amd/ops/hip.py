@@ -709,7 +709,7 @@ def choose_splits(N: int, K: int, nt: int, target_wgs: int = 512, max_splits: in
 # 0.3-1 % (TP=8 shard 1.449 vs 1.465, TP=1 4.527 vs 4.541), so more rows keep 4.
 # ``SKINNY_WAVES_FORCE`` (4 / 8) overrides the choice for in-situ A/Bs (tools/exp_plans_insitu.py "waves:W");
 # $MRSUM_SKINNY_WAVES sets it at import (multi-process rehearsals: the 4-wave summation order reproduces round
-# 4's token streams bit for bit, tools/gpu_r5_q.sh).
+# 4's token streams bit for bit, git show 96648c3:tools/gpu_r5_q.sh).
 SKINNY_WAVES8_MAX_WGS = 2 * 256
 SKINNY_WAVES8_MAX_M = 1
 SKINNY_WAVES_FORCE = int(os.environ["MRSUM_SKINNY_WAVES"]) if os.environ.get("MRSUM_SKINNY_WAVES") else None

@@ -192,8 +192,9 @@ class CustomAllReduce:
         stale slot, flag or epoch shows up as a mismatch) and hipGraph replays, compared with RCCL / the fp32
         reference and across ranks.  Each path's verdict is agreed over the group (a path that failed on one
         rank is off everywhere; ``self.paths``); the group then resets the P2P state.  Returns whether the
-        handle is usable at all: the one-shot or the fused path (a graph-safe decode all-reduce) AND the key
-        max (the vocab-parallel sampler has no graph-safe fallback)."""
+        handle is usable at all (graph_safe): a graph-safe decode reduction for every decode bucket -- the
+        fused path, or the one-shot path where one fp32 slab of the largest bucket fits it -- AND the key max
+        (the vocab-parallel sampler has no graph-safe fallback)."""
         sh = dict(hidden=4096, k={"o": 512, "down": 1792}, fp8=False, rows=(1, 16, 64))
         sh.update(shapes or {})
         dev = torch.device("cuda", torch.cuda.current_device())
@@ -226,20 +227,35 @@ class CustomAllReduce:
         exercised = {"one_shot": True, "fused_norm": True, "max_u64": True}
         for kind in ("stream", "skinny"):
             def t(kind=kind):
-                tested = False
+                # every (role, M) case runs on every rank, whatever an earlier case gave on any rank, and the
+                # group agrees on each case's outcome before the next one starts: a case that failed or raised
+                # on one rank only must not leave that rank in a different collective (or a push kernel
+                # waiting on a peer that has moved on) than its peers
+                tested, ok = False, True
                 for role, K in sorted(sh["k"].items()):
                     for M in rows:
                         if _push_case(self, kind, M, H, int(K), bool(sh["fp8"]), role) is None:
                             continue
                         tested = True
                         graph = M in (rows[0], rows[-1])
-                        if not _test_push(self, dev, iters, group=self.group, M=M, N=H, K=int(K), kind=kind,
-                                          fp8=bool(sh["fp8"]), role=role, graph=graph):
+                        try:
+                            case = _test_push(self, dev, iters, group=self.group, M=M, N=H, K=int(K), kind=kind,
+                                              fp8=bool(sh["fp8"]), role=role, graph=graph)
+                        except Exception as e:
+                            log.warning("custom all-reduce self-test: %s push raised at %s M=%d: %s", kind, role,
+                                        M, e)
+                            self.why.setdefault("push_" + kind, "raised at %s M=%d: %s" % (role, M, str(e)[:160]))
+                            case = False
+                        err_any, failed_any = self.agree_error(local_failed=not case)
+                        if err_any:
+                            self.reset()
+                        if not case or err_any or failed_any:
                             log.warning("custom all-reduce self-test: %s push failed at %s M=%d N=%d K=%d",
                                         kind, role, M, H, K)
-                            return False
+                            self.why.setdefault("push_" + kind, "mismatch at %s M=%d on some rank" % (role, M))
+                            ok = False
                 exercised["push_" + kind] = tested
-                return True
+                return ok
             run("push_" + kind, t)
         votes = [None] * self.world
         dist.all_gather_object(votes, local, group=self.group)
@@ -261,7 +277,11 @@ class CustomAllReduce:
         # traffic from zeroed slots and epoch 1 on every rank, whatever the test's iteration count
         self.reset()
         log.info("custom all-reduce self-test (hidden %d, rows %s): %s", H, rows, self.paths)
-        return (self.paths["one_shot"] or self.paths["fused_norm"]) and self.paths["max_u64"]
+        usable = graph_safe(self.paths, H, self.ONE_SHOT_MAX, self.MAX_ROWS)
+        if not usable:
+            self.report["unusable"] = ("the passing paths leave decode batches up to %d rows at hidden %d "
+                                       "without a graph-safe all-reduce" % (self.MAX_ROWS, H))
+        return usable
 
     def selftest_report(self) -> dict:
         """Per path "ok" / "failed" / "n/a" of the start-up self-test (+ the shapes it ran at)."""
@@ -688,6 +708,21 @@ class LocalPush:
         if rc:
             raise RuntimeError("LocalPush: reset failed (%d)" % rc)
     __del__ = CustomAllReduce.__del__
+
+
+def graph_safe(paths: dict, hidden: int, one_shot_max: int, max_rows: int) -> bool:
+    """Whether the self-tested ``paths`` leave a graph-safe TP reduction for EVERY decode batch up to
+    ``max_rows`` rows (the engine's largest graph bucket) at ``hidden``: the fused all-reduce + add + RMSNorm
+    takes any of them; without it the decode falls back to the one-shot kernel over one fp32 slab [M, hidden],
+    which must then fit ``one_shot_max`` bytes at ``max_rows`` rows -- otherwise a captured large-batch step
+    would reach the RCCL path inside the capture (model._all_reduce refuses that).  The vocab-parallel
+    sampler's key max has no graph-safe fallback.  A False verdict drops the handle: the engine then runs
+    RCCL and no decode graphs."""
+    if not paths.get("max_u64"):
+        return False
+    if paths.get("fused_norm"):
+        return True
+    return bool(paths.get("one_shot")) and max_rows * hidden * 4 <= one_shot_max
 
 
 def maybe_custom_all_reduce(group=None, max_bytes: int = 4 << 20, shapes: Optional[dict] = None

@@ -32,6 +32,7 @@ import datetime
 import json
 import logging
 import os
+import sys
 from dataclasses import dataclass
 from typing import Any, List, Optional
 
@@ -195,7 +196,12 @@ class AsyncWorks:
     until process teardown, where gloo aborts (``terminate called without an active exception``) or RCCL
     reports an unfinished collective.  Waiting on a finished work is cheap; on the exception path a wait
     error is swallowed (the original exception propagates), and a peer that never posts its side ends the
-    wait at the process-group timeout."""
+    wait at the process-group timeout.
+
+    Only PENDING handles are kept: ``wait(work)`` waits and drops the handle at once.  A finished RCCL
+    WorkNCCL still pins its output tensors while it lives, so a scope that kept every handle of a layer-major
+    prefill would hold every layer's reduce-scatter / all-reduce output (and every CP K/V gather buffer)
+    until the prefill ends -- O(layers x pass activations) of extra HBM."""
 
     def __init__(self):
         self._works = []
@@ -204,6 +210,19 @@ class AsyncWorks:
         if work is not None:
             self._works.append(work)
         return work
+
+    def wait(self, work) -> None:
+        """Wait on ``work`` (a handle from ``add``, or None) and stop tracking it."""
+        if work is None:
+            return
+        for i, w in enumerate(self._works):
+            if w is work:
+                del self._works[i]
+                break
+        work.wait()
+
+    def __len__(self) -> int:
+        return len(self._works)
 
     def __enter__(self) -> "AsyncWorks":
         return self
@@ -217,6 +236,28 @@ class AsyncWorks:
                 if et is None:
                     raise
         return False
+
+
+def exit_process(code: int) -> None:
+    """Leave the process with ``code`` once its work is done and the groups are torn down (``shutdown``):
+    the one exit path of bench.py and the CLI (``python -m llm_map_reduce_summarizer_amd``).
+
+    A rank of a multi-process job leaves through ``os._exit`` after flushing stdout / stderr: interpreter
+    finalisation would run the C++ destructors of the communication backends, which in round 4 aborted a
+    finished world-8 job once (SIGABRT after a good result; gloo's ``terminate called without an active
+    exception``); the round-5 AsyncWorks scope waits every async work before its frame ends and ``shutdown``
+    destroys the groups in a fixed order, after which the abort did not recur, but no destructor is left to
+    chance after the result is out.  A single process that never formed a group exits normally: its atexit
+    work includes a profiler's flush (rocprofv3 writes its traces there; ``os._exit`` would drop them)."""
+    try:
+        sys.stdout.flush()
+        sys.stderr.flush()
+    except Exception:  # noqa: BLE001 -- closed streams must not change the exit code
+        pass
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 or os.environ.get("MRSUM_FORCE_DIST") == "1":
+        logging.shutdown()
+        os._exit(int(code))
+    sys.exit(int(code))
 
 
 def shutdown() -> None:

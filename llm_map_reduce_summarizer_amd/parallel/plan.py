@@ -86,7 +86,7 @@ def decode_step_s(d: ModelDims, hw: HWModel, batch: int, ctx: float, tp: int) ->
     return stream + floor + comm
 
 
-PREFILL_CHUNK = 4096  # engine default slice length of chunked prefill (engine/engine.py)
+from ..engine.config import PREFILL_CHUNK  # noqa: E402 -- the engine's default slice (engine/engine.py)
 
 
 def prefill_s(d: ModelDims, hw: HWModel, tokens: int, tp: int, longest: int = 0,

@@ -94,6 +94,15 @@ def main():
     rep = ar8.selftest_report()
     assert all(rep[p] in ("ok", "n/a") for p in ar8.PATHS) and rep["push_stream"] == "ok", rep
     ar8.close()
+    # the fused all-reduce + norm path failing its test (forced here on every rank): the one-shot path alone
+    # does not take a 256-row bucket's fp32 slab at hidden 4096, so the handle must be reported unusable
+    # (the engine then runs RCCL without decode graphs instead of raising inside a large-batch capture)
+    ar3 = CustomAllReduce(None, max_bytes=4 << 20)
+    ar3._test_fused = lambda *a, **k: False
+    assert not ar3.self_test(), ar3.paths
+    assert ar3.paths["one_shot"] and not ar3.paths["fused_norm"], ar3.paths
+    assert "unusable" in ar3.selftest_report(), ar3.selftest_report()
+    ar3.close()
     lat, per_row = ar.measure_latency(rows=(1, 64), hidden=4096)
     print("rank %d fused all-reduce cost over local add_rmsnorm: %.2f us + %.4f us/row (2 ranks sharing one GPU)"
           % (rank, lat * 1e6, per_row * 1e6), flush=True)

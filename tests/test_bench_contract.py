@@ -59,6 +59,16 @@ def test_bench_prints_one_json_line(world, extra):
     tw = out["timed_work"]
     assert tw["pinned_ok"] and tw["errors"] == 0 and tw["requests"] > 0
     assert tw["completion_tokens"] == tw["requested_tokens"] > 0
+    # diagnostics of a first multi-GPU run (VERDICT r5 #2b): per stage the planner's predicted seconds next
+    # to the measured seconds of one timed step, and the P2P latency per TP degree (None without GPUs)
+    assert "p2p_latency_us" in out and "planner_hw" in out
+    st = out["stages"]
+    assert "map" in st and "reduce_final" in st, st
+    for name, r in st.items():
+        assert {"tp", "calls_per_step", "predicted_s", "measured_s"} <= set(r), (name, r)
+        assert r["calls_per_step"] >= 1 and r["measured_s"] > 0
+        assert r["predicted_s"] is not None and r["predicted_s"] > 0
+        assert r["tp"] == (2 if extra == ("--parallel", "tp") else 1)
 
 
 def test_bench_self_launches_ranks():
@@ -69,3 +79,29 @@ def test_bench_self_launches_ranks():
     assert own["n_gpus"] == 2 and own["ranks_seen"] == 2 and own["backend"] == "gloo"
     assert own["summary_sha16"] == ref["summary_sha16"]
     assert own["config"]["global_batch"] == ref["config"]["global_batch"]
+
+
+def test_cli_torchrun_world4_exits_zero(tmp_path):
+    """the user-facing multi-rank entry point (``torchrun ... -m llm_map_reduce_summarizer_amd
+    --provider local``) leaves through the bench's exit path (parallel/dist.py exit_process) and exits 0 on
+    every rank, data-parallel and with a TP=4 reduce, on gloo / CPU ranks with a tiny model."""
+    sys.path.insert(0, ROOT)
+    from llm_map_reduce_summarizer_amd.utils.synth import synthetic_transcript
+    tr = tmp_path / "t.json"
+    tr.write_text(json.dumps(synthetic_transcript(0.3, seed=3)))
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", OMP_NUM_THREADS="1", MAX_TOKENS="6",
+               PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    for par in ("dp", "map:tp1,reduce_l1:tp4,reduce_final:tp4"):
+        out = tmp_path / ("s_%s.txt" % par.split(":")[0])
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+               "--master-addr", "127.0.0.1", "--master-port", str(_port()), "-m", "llm_map_reduce_summarizer_amd",
+               "-i", str(tr), "--provider", "local", "--model", "tiny-kv8", "--max-tokens-per-chunk", "1000",
+               "--parallel", par, "-q", "-o", str(out), "--report"]
+        p = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=600)
+        assert p.returncode == 0, (par, p.stderr[-3000:])
+        assert "terminate called" not in p.stderr and "Abort" not in p.stderr, p.stderr[-3000:]
+        assert out.read_text(encoding="utf-8").strip()
+        rep = json.loads(out.with_suffix(".report.json").read_text(encoding="utf-8"))
+        assert rep["chunks"] >= 1 and rep["summary"]
