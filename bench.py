@@ -103,6 +103,10 @@ def main() -> int:
     ap.add_argument("--kv-dtype", choices=["bf16", "fp8v"], default="bf16",
                     help="KV cache format; fp8v (V rows e4m3 with power-of-two row scales, K bf16) is a LABELLED "
                          "variant: the headline is bf16 KV")
+    ap.add_argument("--reduce-batch-tokens", type=int, default=None,
+                    help="rehearsal knob: the aggregator's token budget per reduce call (default 6000, with 1000 "
+                         "reserved); a small value forces a multi-level reduce with short pinned summaries "
+                         "(labelled variant, never the headline)")
     ap.add_argument("--profile", default=None, metavar="DIR", help="torch.profiler trace of the timed steps")
     ap.add_argument("--log-level", default="WARNING")
     args = ap.parse_args()
@@ -135,9 +139,11 @@ def main() -> int:
     provider = LocalEngineProvider(args.model, cfg, use_graphs=not args.no_graphs, ignore_eos=not args.stop_at_eos,
                                    parallel=args.parallel, kv_dtype=args.kv_dtype)
     executor = LLMExecutor(config=cfg, provider_obj=provider)
+    agg_opts = ({"max_tokens_per_batch": args.reduce_batch_tokens, "reserved_tokens": 0}
+                if args.reduce_batch_tokens else None)
     summarizer = TranscriptSummarizer(executor=executor, max_tokens_per_chunk=args.chunk_tokens,
                                       hierarchical_aggregation=not args.no_hierarchical,
-                                      stream_reduce=args.stream_reduce)
+                                      stream_reduce=args.stream_reduce, aggregator_options=agg_opts)
     transcript = synthetic_transcript(args.hours, seed=0)
     # weight init, KV allocation, planner measurements and the decode graphs of every batch bucket a
     # stage of this transcript can use: engine start-up, outside the timed region
@@ -210,10 +216,12 @@ def main() -> int:
     out = {
         "metric": "chunks/sec (whole node) + end-to-end wall-clock, 10h transcript, Llama-3-8B"
                   + ("" if args.model == "llama3-8b" and args.hours == 10.0 and not args.no_hierarchical
-                     and not args.stream_reduce and args.kv_dtype == "bf16"
-                     else " [variant: %s, %gh%s%s%s]" % (args.model, args.hours,
+                     and not args.stream_reduce and args.kv_dtype == "bf16" and not args.reduce_batch_tokens
+                     else " [variant: %s, %gh%s%s%s%s]" % (args.model, args.hours,
                                                          ", single-pass reduce" if args.no_hierarchical else "",
                                                          ", streamed level-1 reduce" if args.stream_reduce else "",
+                                                         (", reduce batches of %d tokens" % args.reduce_batch_tokens)
+                                                         if args.reduce_batch_tokens else "",
                                                          {"fp8": ", fp8 KV cache", "fp8v": ", fp8 V cache (bf16 K)"}
                                                          .get(args.kv_dtype, ""))),
         "value": round(value, 4),

@@ -15,12 +15,12 @@ latency.  Prefill is compute-bound: DP divides it by N for free, TP adds RCCL al
 activations.  Which is faster depends on the batch, the context and the all-reduce latency of the
 node, so the choice is a cost model whose hardware constants are *measured*:
 
-* ``hbm_bw``, ``step_floor_s``, ``tp_floor_s``, ``tp_row_s``: one least-squares fit (tools/fit_hwmodel.py)
-  over the round-3 decode steps of TP=1 and of one rank's TP=2/4/8 shard with the TP kernel sequence over
-  a group of one rank (TP push in the row-parallel GEMM epilogues; profiles/r3_decode_steps_push.jsonl,
-  B=1/5/10/20/39 at 4k context):
-  t = (W + B ctx kv) / TP / 5.82 TB/s + 0.70 ms + [TP > 1] 0.25 ms + 6.9 us x B x log2(TP), every point
-  within 8.3 % (few-kv-head attention and the per-kernel latency of small shards are what stay);
+* ``hbm_bw``, ``step_floor_s``, ``tp_row_s``, ``tp_shard_s``, ``fp8_row_s``, ``fp8_floor_s``: one MINIMAX fit
+  (tools/fit_hwmodel.py) over the round-6 decode steps of TP=1 and of one rank's TP=2/4/8 shard with the TP
+  kernel sequence over a group of one rank (TP push in the row-parallel GEMM epilogues), Llama-3-8B bf16 at
+  B=1/10/39 x 4k and Llama-3-70B fp8 at TP=1 / TP=8 (profiles/r6_decode_steps.jsonl):
+  t = (W + B ctx kv) / TP / 6.02 TB/s + L/32 x (0.862 ms + 7.58 us x B log2(TP) + [TP > 1] 0.438 ms / TP
+  + [fp8] (55.7 us + 46.4 us x B)), every point within 4.3 % (tests/test_plan.py pins that);
 * ``prefill_flops``: the engine's prefill rate in the 10 h bench (~76k tok/s of Llama-3-8B);
 * ``ar_lat_s`` / ``ar_lat_row_s`` and ``ar_bw``: timed at start-up on the job's own GPUs (the fused
   all-reduce inside a replayed hipGraph at 1 and 64 rows against the same kernel over a group of one
@@ -48,10 +48,12 @@ from typing import Dict, List, Sequence
 
 @dataclass(frozen=True)
 class HWModel:
-    hbm_bw: float = 5.82e12         # bytes/s streamed by the decode GEMM + attention kernels
-    step_floor_s: float = 0.70e-3   # fixed per-step cost of the decode graph (kernel latencies), 32 layers
-    tp_floor_s: float = 0.25e-3     # extra fixed cost of a TP shard's decode graph (32 layers) ...
-    tp_row_s: float = 6.9e-6        # ... plus this per decode row per log2(TP) (few-kv-head attention is latency-bound)
+    hbm_bw: float = 6.02e12         # bytes/s streamed by the decode GEMM + attention kernels
+    step_floor_s: float = 0.862e-3  # fixed per-step cost of the decode graph (kernel latencies), per 32 layers
+    tp_shard_s: float = 0.438e-3    # a TP shard's extra fixed cost per 32 layers, divided by TP ...
+    tp_row_s: float = 7.58e-6       # ... plus this per decode row per log2(TP) (few-kv-head attention is latency-bound)
+    fp8_floor_s: float = 55.7e-6    # W8A16 decode kernels: extra fixed cost per 32 layers ...
+    fp8_row_s: float = 46.4e-6      # ... and per decode row (the e4m3 -> bf16 conversion grows with the rows)
     prefill_flops: float = 1.1e15   # effective prefill FLOP/s (MFMA GEMMs + flash attention)
     ar_lat_s: float = 20e-6         # one decode all-reduce (custom P2P kernel), measured at start-up ...
     ar_lat_row_s: float = 0.0       # ... plus this per decode row (the push sends every row to every peer)
@@ -66,13 +68,15 @@ class ModelDims:
     flops_per_token: float
     n_layers: int
     hidden: int
+    fp8: bool = False  # W8A16 decode kernels (1-byte weights)
 
     @classmethod
     def of(cls, cfg, weight_bytes_per_param: float = 2.0) -> "ModelDims":
         n = cfg.n_params()
         emb = cfg.vocab_size * cfg.hidden  # the embedding table is gathered, not streamed
         return cls(weight_bytes=(n - emb) * weight_bytes_per_param, kv_bytes_per_token=cfg.kv_bytes_per_token(),
-                   flops_per_token=2.0 * (n - 2 * emb), n_layers=cfg.n_layers, hidden=cfg.hidden)
+                   flops_per_token=2.0 * (n - 2 * emb), n_layers=cfg.n_layers, hidden=cfg.hidden,
+                   fp8=weight_bytes_per_param < 2.0)
 
 
 def decode_step_s(d: ModelDims, hw: HWModel, batch: int, ctx: float, tp: int) -> float:
@@ -80,8 +84,8 @@ def decode_step_s(d: ModelDims, hw: HWModel, batch: int, ctx: float, tp: int) ->
     if batch <= 0:
         return 0.0
     stream = (d.weight_bytes + batch * ctx * d.kv_bytes_per_token) / tp / hw.hbm_bw
-    floor = (hw.step_floor_s + (hw.tp_floor_s if tp > 1 else 0.0) + hw.tp_row_s * batch * math.log2(tp)) \
-        * d.n_layers / 32.0
+    floor = (hw.step_floor_s + (hw.tp_shard_s / tp if tp > 1 else 0.0) + hw.tp_row_s * batch * math.log2(tp)
+             + ((hw.fp8_floor_s + hw.fp8_row_s * batch) if d.fp8 else 0.0)) * d.n_layers / 32.0
     comm = (2 * d.n_layers + 1) * (hw.ar_lat_s + hw.ar_lat_row_s * batch) if tp > 1 else 0.0
     return stream + floor + comm
 
