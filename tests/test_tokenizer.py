@@ -58,3 +58,21 @@ def test_count_close_to_cl100k_scale(example_transcript):
     segs = preprocess_transcript(example_transcript["segments"])
     n = sum(tok.count("[%s] %s: %s" % (format_timestamp(s["start"]), s["speaker"], s["text"])) for s in segs)
     assert 90000 < n < 115000
+
+
+def test_ascii_presplit_matches_the_unicode_pattern():
+    """The stdlib-``re`` ASCII fast path of the cl100k pre-split gives the same pieces as the ``regex`` pattern on
+    ASCII text, control characters included (engine/tokenizer.py _CL100K_ASCII)."""
+    import random
+
+    import regex
+
+    from llm_map_reduce_summarizer_amd.engine.tokenizer import _CL100K_ASCII, CL100K_PATTERN
+    full = regex.compile(CL100K_PATTERN)
+    rng = random.Random(0)
+    alpha = "ab AB zZ09'sStTrRvVmMlLdD.,!?-\t\n\r\x0b\x0c\x1c\x1d\x1e\x1f\x00\x7f'   :;[]()\"#"
+    for _ in range(5000):
+        s = "".join(rng.choice(alpha) for _ in range(rng.randint(0, 48)))
+        assert _CL100K_ASCII.findall(s) == full.findall(s), repr(s)
+    text = "[00:14] SPEAKER_00: We'll see--it's 3.14159 o'clock!\n\n  Tabs\tand\r\nlines   end  "
+    assert _CL100K_ASCII.findall(text) == full.findall(text)
