@@ -478,7 +478,7 @@ class LocalEngineProvider(Provider):
         numel = [math.prod(s) for s in shapes]
         recv_sizes = [sum(numel[i] for i in range(len(prompts)) if owner[i] == s) for s in range(world)]
         nccl = dist.get_backend() == "nccl"
-        err = None
+        err, oom = None, False
         try:
             self._maybe_fault()
             firsts, packs = self.engine.prefill_export([prompts[i] for i in mine], [sp[i] for i in mine], world,
@@ -486,6 +486,7 @@ class LocalEngineProvider(Provider):
             send = torch.cat(packs) if packs else torch.empty(0, dtype=self.engine.kv.k.dtype)
             send_sizes = [p.numel() for p in packs]
         except Exception as e:  # noqa: BLE001 -- still enter the all-to-all with the sizes the peers expect
+            oom = isinstance(e, MemoryError)
             err = "rank %d prefill: %s: %s" % (self.par.rank, type(e).__name__, e)
             log.error("%s", err)
             firsts = [0] * len(mine)
@@ -496,12 +497,21 @@ class LocalEngineProvider(Provider):
         send = send.to(dev)
         recv = torch.empty(sum(recv_sizes), dtype=send.dtype, device=dev)
         dist.all_to_all_single(recv, send, recv_sizes, send_sizes, group=group)
-        tok, errs = {}, []
-        for part in pdist.all_gather_json({"tok": {str(i): int(t) for i, t in zip(mine, firsts)}, "err": err},
-                                          group):
+        tok, errs, ooms = {}, [], []
+        for part in pdist.all_gather_json({"tok": {str(i): int(t) for i, t in zip(mine, firsts)}, "err": err,
+                                           "oom": oom}, group):
             tok.update({int(k): v for k, v in part["tok"].items()})
             if part["err"]:
                 errs.append(part["err"])
+                ooms.append(bool(part.get("oom")))
+        if errs and all(ooms):
+            # only KV-pool exhaustion on the DP engines (their pools are sized for the DP stages, not for a TP
+            # group's whole share): every rank of the group saw the same verdicts, so all fall back alike to the
+            # TP engine's own prefill -- the hand-off's speed is lost, not the requests
+            log.warning("disaggregated prefill does not fit the DP engines' KV pools (%s): the TP=%d engine "
+                        "prefills the prompts", "; ".join(errs), world)
+            self.timings["handoff_fallbacks"] = self.timings.get("handoff_fallbacks", 0) + 1
+            return None
         if errs:  # every rank raises the same error: the stage fails as a whole, consistently
             raise RuntimeError("; ".join(errs))
         out, off = {}, 0
