@@ -17,6 +17,7 @@ Variants (comma separated, ``plan`` = unchanged):
   resid:ROLE=KIND              the deferred-norm / TP-push producer of ROLE (o | down) forced to KIND
                                (skinny | stream): ops.RESID_FORCE
   env:NAME=VALUE[+NAME=VALUE]  environment overrides read at call time (e.g. env:MRSUM_TP_PUSH=0)
+  A&B&...                      several of the above at once (e.g. buckets:1+2+4+8+10+16&attnfused3)
 
     python tools/exp_plans_insitu.py --tp-shard 8 --batch 1 --variants plan,attnfused32,gate_up:stream_split:4:4
 """
@@ -67,6 +68,11 @@ def main():
     base_buckets = engine_mod.BUCKETS
 
     def install(v):
+        reset()
+        for part in v.split("&"):  # a variant may combine specs: buckets:1+2+4+8+10+16&attnfused3
+            apply(part)
+
+    def reset():
         hip.decode_attn_plan, hip.plan = base_attn, base_plan
         ops.DEFER_NORM_MAX_M = base_defer
         hip.fp8_resid_cfg = base_fp8r
@@ -82,6 +88,9 @@ def main():
         ops.RESID_FORCE.clear()
         import llm_map_reduce_summarizer_amd.engine.engine as engine_mod
         engine_mod.BUCKETS = base_buckets
+
+    def apply(v):
+        import llm_map_reduce_summarizer_amd.engine.engine as engine_mod
         if v == "plan":
             return
         if v.startswith("buckets:"):  # buckets:1+2+4+8+10+16 -- the decode graph buckets below 24
@@ -123,7 +132,7 @@ def main():
         if v.startswith("attn"):
             fused = v.startswith("attnfused")
             S = int(v[len("attnfused"):] if fused else v[len("attnsep"):])
-            hip.decode_attn_plan = lambda B, hkv, ctx, **kw: (S, fused) if B == bucket else base_attn(B, hkv, ctx, **kw)
+            hip.decode_attn_plan = lambda B, hkv, ctx, **kw: (S, fused) if B == eng._bucket(a.batch) else base_attn(B, hkv, ctx, **kw)
             return
         role, kind, p1, p2 = v.split(":")
         p = (kind, int(p1), int(p2))
