@@ -299,14 +299,8 @@ __device__ __forceinline__ u32x4 ld_kv(const T* p) {
 // values into the tile, so this step and later steps see the same K/V.  KVM is a bitmask: bit 0 = the K
 // cache is fp8 slabs, bit 1 = the V cache is; KVM 2 ("fp8v": bf16 K, fp8 V) stages K with the bf16
 // mapping and V with the slab mapping, each into its own LDS tile.
-// NSET: K/V register sets in flight per thread -- 2 (tiles t+1, t+2 loading while tile t is scored; 3 workgroups
-// per CU) or 4 (t+1 .. t+4; one workgroup per CU): LONG splits on grids of at most one workgroup per CU (the
-// level-1 reduce's B=10 x 8 kv heads x 3 splits of ~25 pages), where a workgroup's two loads in flight leave its
-// HBM latency exposed at every tile barrier (PMC: ~36 % of wave cycles at barriers with one workgroup per CU).
-// Short splits keep NSET 2: their overshoot loads past the last tile outweighed the deeper queue in round 5
-// (B=1 at 13.5k, 6-7 pages per split, and TP shards: r5_attn_deep_ab.jsonl).
-template <int G, bool ROPE, bool NT = false, int KVM = 0, int NSET = 2>
-__global__ __launch_bounds__(256, (NSET == 4 ? 1 : 3)) void attn_decode_mfma_kernel(
+template <int G, bool ROPE, bool NT = false, int KVM = 0>
+__global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     const bf16* __restrict__ q, int q_stride, bf16* __restrict__ kc, bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ positions,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int S, float scale_log2, RopeArgs ra,
@@ -369,9 +363,7 @@ __global__ __launch_bounds__(256, (NSET == 4 ? 1 : 3)) void attn_decode_mfma_ker
     // loads past the last tile stay unconditional but read the scratch page 0, which every workgroup's
     // overshoot shares and so stays in L2 (re-reading the workgroup's own last tile cost ~9 % extra HBM
     // traffic at B=39, PMC FETCH_SIZE).
-    u32x4 kreg[4], vreg[4], kreg2[4], vreg2[4], kreg3[4], vreg3[4], kreg4[4], vreg4[4];
-    float ksc3[2], vsc3[2], ksc4[2], vsc4[2];
-    static_assert(NSET == 2 || NSET == 4, "two or four K/V register sets");
+    u32x4 kreg[4], vreg[4], kreg2[4], vreg2[4];
 #define KV_ISSUE(KR, VR, KS, VS, TILE)                                                              \
     {                                                                                               \
         const int pg_ = bt[min((TILE), ntiles - 1)];                                                \
@@ -397,10 +389,6 @@ __global__ __launch_bounds__(256, (NSET == 4 ? 1 : 3)) void attn_decode_mfma_ker
     }
     KV_ISSUE(kreg, vreg, ksc, vsc, 0)
     KV_ISSUE(kreg2, vreg2, ksc2, vsc2, 1)
-    if constexpr (NSET == 4) {
-        KV_ISSUE(kreg3, vreg3, ksc3, vsc3, 2)
-        KV_ISSUE(kreg4, vreg4, ksc4, vsc4, 3)
-    }
     // ROPE: the q rows of this group (and, for the split holding the new token, its K and V rows)
     // summed over the SP slabs by ALL 256 threads in one round of independent loads into an fp32
     // LDS image (aliasing the K/V tile buffers, which are first written after it is consumed):
@@ -554,7 +542,7 @@ __global__ __launch_bounds__(256, (NSET == 4 ? 1 : 3)) void attn_decode_mfma_ker
         }                                                                                                       \
     }
     KV_WRITE(kreg, vreg, ksc, vsc, 0)
-    KV_ISSUE(kreg, vreg, ksc, vsc, NSET)
+    KV_ISSUE(kreg, vreg, ksc, vsc, 2)
 
     f32x4 o[8];
 #pragma unroll
@@ -597,37 +585,23 @@ __global__ __launch_bounds__(256, (NSET == 4 ? 1 : 3)) void attn_decode_mfma_ker
             }
         }
     };
-    // LDS holds tile t; sets B (, C, D) carry tiles t + 1 .. t + NSET - 1 and set A tile t + NSET (NSET tiles in
-    // flight while a tile is scored); unrolled by NSET so every register array is indexed statically.
-    for (int t = 0; t < ntiles; t += NSET) {
+    // LDS holds tile t; set B carries tile t + 1 and set A tile t + 2 (two tiles in flight while a tile
+    // is scored); unrolled by two so every register array is indexed statically.  (Four sets in flight at
+    // one workgroup per CU measured SLOWER in round 5: B=1 at 13.5k +1.5-2.5 %, the TP=8 shard +10 %, the
+    // overshoot loads past a short split's last tile outweighing the deeper queue: r5_attn_deep_ab.jsonl.)
+    for (int t = 0; t < ntiles; t += 2) {
         compute(t);
         __syncthreads();
         if (t + 1 < ntiles) {
             KV_WRITE(kreg2, vreg2, ksc2, vsc2, t + 1)
-            KV_ISSUE(kreg2, vreg2, ksc2, vsc2, t + 1 + NSET)
+            KV_ISSUE(kreg2, vreg2, ksc2, vsc2, t + 3)
             __syncthreads();
             compute(t + 1);
             __syncthreads();
         }
-        if constexpr (NSET == 4) {
-            if (t + 2 < ntiles) {
-                KV_WRITE(kreg3, vreg3, ksc3, vsc3, t + 2)
-                KV_ISSUE(kreg3, vreg3, ksc3, vsc3, t + 6)
-                __syncthreads();
-                compute(t + 2);
-                __syncthreads();
-            }
-            if (t + 3 < ntiles) {
-                KV_WRITE(kreg4, vreg4, ksc4, vsc4, t + 3)
-                KV_ISSUE(kreg4, vreg4, ksc4, vsc4, t + 7)
-                __syncthreads();
-                compute(t + 3);
-                __syncthreads();
-            }
-        }
-        if (t + NSET < ntiles) {
-            KV_WRITE(kreg, vreg, ksc, vsc, t + NSET)
-            KV_ISSUE(kreg, vreg, ksc, vsc, t + 2 * NSET)
+        if (t + 2 < ntiles) {
+            KV_WRITE(kreg, vreg, ksc, vsc, t + 2)
+            KV_ISSUE(kreg, vreg, ksc, vsc, t + 4)
             __syncthreads();
         }
     }
@@ -674,10 +648,6 @@ __global__ __launch_bounds__(256, (NSET == 4 ? 1 : 3)) void attn_decode_mfma_ker
 // B=39 x 8 kv heads 7.02-7.05 vs 7.18-7.26 ms with the default policy; B <= 10 0.7-1 % slower with nt
 // (profiles/r1_decode_nt_ab.jsonl)
 constexpr int NT_MIN_GROUPS = 64;
-// the deep (NSET 4) ring: requested by the host (flag bit in the kv8 argument) for long splits, run only on
-// grids of at most one workgroup per CU (its launch bound is one workgroup per CU)
-constexpr int ATTN_DEEP = 0x100;
-constexpr int DEEP_MAX_WGS = 256;
 
 static bool decode_packed(int G) { return G == 1 || G == 2 || G == 4 || G == 8 || G == 16; }
 
@@ -693,10 +663,6 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
                        int B, int Hq, int Hkv, int D, int P, int S, float scale, const RopeArgs* rope, int* counters,
                        int kv8, hipStream_t s) {
     if (B <= 0) return 0;
-    // bit 8 of ``kv8`` (ATTN_DEEP): the caller asks for the four-register-set ring (long splits on a grid of at
-    // most one workgroup per CU, bf16 cache); honoured only where that holds
-    const bool want_deep = (kv8 & ATTN_DEEP) != 0;
-    kv8 &= ~ATTN_DEEP;
     if (D != 128 || P != 64 || Hkv <= 0 || Hq % Hkv || Hq / Hkv > 64 || S < 1 || S > MAX_SPLITS ||
         (kv8 != 0 && kv8 != 2 && kv8 != 3) || !out)
         return (int)hipErrorInvalidValue;
@@ -713,15 +679,9 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
     attn_decode_mfma_kernel<G_, R_, NT_, K8_><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride,  \
                                                                      positions, PO, PM, Hkv, S, sl, ra, counters, \
                                                                      (bf16*)out, out_stride, Hc, gq)
-    const bool deep = want_deep && kv8 == 0 && (long)S * Hkv * B <= DEEP_MAX_WGS;
-#define MFMA_DEEP(G_, R_, NT_)                                                                                \
-    attn_decode_mfma_kernel<G_, R_, NT_, 0, 4><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride, \
-                                                                      positions, PO, PM, Hkv, S, sl, ra, counters, \
-                                                                      (bf16*)out, out_stride, Hc, gq)
 #define MFMA_L(G_, R_)                                                                                        \
     do {                                                                                                      \
         const bool nt_ = B * Hkv >= NT_MIN_GROUPS;                                                            \
-        if (deep) { if (nt_) MFMA_DEEP(G_, R_, true); else MFMA_DEEP(G_, R_, false); break; }                 \
         if (kv8 == 3) { if (nt_) MFMA_K(G_, R_, true, 3); else MFMA_K(G_, R_, false, 3); }                    \
         else if (kv8 == 2) { if (nt_) MFMA_K(G_, R_, true, 2); else MFMA_K(G_, R_, false, 2); }               \
         else { if (nt_) MFMA_K(G_, R_, true, 0); else MFMA_K(G_, R_, false, 0); }                             \
@@ -739,7 +699,6 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
 #undef MFMA_G
 #undef MFMA_L
 #undef MFMA_K
-#undef MFMA_DEEP
     int e = (int)hipGetLastError();
     if (e || counters) return e;
     if (S > 16) {

@@ -478,16 +478,6 @@ def decode_groups(hq: int, hkv: int) -> int:
     return hkv if hq // hkv in (1, 2, 4, 8, 16) else hq
 
 
-ATTN_DEEP = 0x100  # attn_decode.hip: flag bit in the cache-kind argument -> the four-register-set (NSET 4) ring
-
-
-def _attn_deep_flag() -> int:
-    """The deep-ring request for decode attention launches (attn_decode.hip NSET 4, honoured only on grids of at
-    most one workgroup per CU with a bf16 cache): MRSUM_ATTN_DEEP=1, an in-situ measurement switch
-    (tools/exp_plans_insitu.py env:MRSUM_ATTN_DEEP=1); off by default."""
-    return ATTN_DEEP if os.environ.get("MRSUM_ATTN_DEEP", "0") == "1" else 0
-
-
 class DecodeWorkspace:
     """Split-K partial buffers + per-(seq, kv head) arrival counters for attn_decode
     (allocated once per batch bucket; counters start at 0 and every launch re-arms them).
@@ -537,8 +527,7 @@ def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.T
     _check(_fn("mrsum_attn_decode_rope")(_p(parts), SP, _p(cos_sin), _p(kcache), _p(vcache), _p(block_tables),
                                          block_tables.stride(0), _p(positions), _p(workspace.part_o),
                                          _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
-                                         workspace.splits, scale, _p(workspace.counters), kv8 | _attn_deep_flag(),
-                                         _stream()),
+                                         workspace.splits, scale, _p(workspace.counters), kv8, _stream()),
            "attn_decode_rope")
     return out
 
@@ -568,8 +557,7 @@ def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, blo
     _check(_fn("mrsum_attn_decode_mfma")(_p(q), q.stride(0), _p(kcache), _p(vcache), _p(block_tables),
                                          block_tables.stride(0), _p(positions), _p(workspace.part_o),
                                          _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
-                                         workspace.splits, scale, _p(workspace.counters), kv8 | _attn_deep_flag(),
-                                         _stream()),
+                                         workspace.splits, scale, _p(workspace.counters), kv8, _stream()),
            "attn_decode_mfma")
     return out
 

@@ -548,12 +548,9 @@ def test_fp8_swiglu_and_quant():
 @pytest.mark.parametrize("hq,hkv,S", [(32, 8, 4), (4, 1, 1), (16, 1, 3), (8, 2, 2), (4, 1, 16), (6, 2, 2), (24, 8, 4)])
 @pytest.mark.parametrize("fused_combine", [False, True])
 @pytest.mark.parametrize("kv8", ["bf16", "fp8", "fp8v"])
-@pytest.mark.parametrize("deep", ["0", "1"])
-def test_attn_decode_rope_fused(hq, hkv, S, fused_combine, kv8, deep, monkeypatch):
+def test_attn_decode_rope_fused(hq, hkv, S, fused_combine, kv8):
     """attn_decode_rope (q/k RoPE + new K/V written into the cache + attention, from the QKV GEMM's
-    fp32 split-K slabs) == reference rope_kv_parts followed by reference attention; ``deep`` "1": the
-    four-register-set ring where the launch takes it (bf16 cache, <= 256 workgroups)."""
-    monkeypatch.setenv("MRSUM_ATTN_DEEP", deep)
+    fp32 split-K slabs) == reference rope_kv_parts followed by reference attention."""
     d, page = 128, 64
     ctxs = [1, 64, 65, 700, 129, 1000]
     B = len(ctxs)
@@ -1088,42 +1085,3 @@ def test_linear_tall_lm_head(M):
     out = hip.linear(x, w)
     torch.cuda.synchronize()
     _close(out, x.float() @ w.float().t(), 2e-2)
-
-
-@pytest.mark.parametrize("ctxs,splits", [([1, 700, 6000, 4097], 2), ([4500, 300, 64, 5000], 3), ([12000], 8)])
-@pytest.mark.parametrize("fused", [False, True])
-def test_attn_decode_deep_ring(ctxs, splits, fused, monkeypatch):
-    """The four-register-set ring (attn_decode.hip NSET 4, MRSUM_ATTN_DEEP=1, grids of <= 256 workgroups):
-    tile counts per split that are not multiples of four, empty splits, one-page splits and 20+-page splits
-    against the fp32 reference, replayed (re-armed merge counters); and bit-identical to the two-set ring
-    (the same per-tile arithmetic in the same order)."""
-    hq, hkv, d, page = 32, 8, 128, 64
-    B = len(ctxs)
-    npgs = [-(-c // page) for c in ctxs]
-    g = torch.Generator().manual_seed(131)
-    n_pages = sum(npgs) + 1
-    kc = torch.randn(n_pages, hkv, page, d, generator=g).to(torch.bfloat16).to(DEV)
-    vc = torch.randn(n_pages, hkv, page, d, generator=g).to(torch.bfloat16).to(DEV)
-    perm = torch.randperm(n_pages - 1, generator=g) + 1
-    bt = torch.zeros(B, max(npgs), dtype=torch.int32)
-    used = 0
-    for b, n in enumerate(npgs):
-        bt[b, :n] = perm[used:used + n]
-        used += n
-    bt = bt.to(DEV)
-    pos = torch.tensor([c - 1 for c in ctxs], dtype=torch.int32, device=DEV)
-    q = _rand(B, hq * d, seed=132)
-    sc = 1.0 / math.sqrt(d)
-    assert splits * hkv * B <= 256  # the deep ring's grid bound (else the launch keeps two sets)
-    o_ref = reference.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc)
-    ws = hip.DecodeWorkspace(B, hq, d, splits, DEV, hkv, fused_combine=fused)
-    monkeypatch.setenv("MRSUM_ATTN_DEEP", "0")
-    o_two = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws).clone()
-    monkeypatch.setenv("MRSUM_ATTN_DEEP", "1")
-    ws.part_o.fill_(float("nan"))
-    for _ in range(3):
-        o_deep = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws)
-        _close(o_deep, o_ref, 2e-2)
-        assert torch.equal(o_deep, o_two)
-    if fused:
-        assert int(ws.counters.abs().sum()) == 0
