@@ -28,6 +28,38 @@
 // chip (70B fp8 TP=8 shard at 32k: 64 splits = 64 workgroups left its 16.8 MB of K/V at ~1.1 TB/s)
 constexpr int MAX_SPLITS = 256;
 
+// Diagnostic build only (tools/exp_attn_stamps.py compiles this file with -DMRSUM_ATTN_STAMPS into
+// _native/diag/): every wave accumulates s_memtime deltas per phase of the split kernel -- prologue, tile
+// compute, the barrier after it, the next tile's LDS write + load issue, the barrier after that, epilogue --
+// and lane 0 stores them to g_attn_stamps[(workgroup * 4 + wave) * 8 + phase] (6: total, 7: tiles).
+#ifdef MRSUM_ATTN_STAMPS
+__device__ unsigned long long* g_attn_stamps;
+MRSUM_API int mrsum_attn_set_stamps(void* p) {
+    return (int)hipMemcpyToSymbol(HIP_SYMBOL(g_attn_stamps), &p, sizeof(p));
+}
+#define ST_DECL                                                        \
+    unsigned long long st_last_ = __builtin_amdgcn_s_memtime(), st_t0_ = st_last_; \
+    unsigned long long st_acc_[6] = {0, 0, 0, 0, 0, 0};
+#define ST(i)                                                          \
+    {                                                                  \
+        const unsigned long long n_ = __builtin_amdgcn_s_memtime();   \
+        st_acc_[i] += n_ - st_last_;                                   \
+        st_last_ = n_;                                                 \
+    }
+#define ST_STORE(NT_)                                                                                   \
+    if (g_attn_stamps && (threadIdx.x & 63) == 0) {                                                      \
+        const size_t wg_ = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;      \
+        unsigned long long* o_ = g_attn_stamps + (wg_ * 4 + (threadIdx.x >> 6)) * 8;                   \
+        for (int i_ = 0; i_ < 6; ++i_) o_[i_] = st_acc_[i_];                                            \
+        o_[6] = __builtin_amdgcn_s_memtime() - st_t0_;                                                  \
+        o_[7] = (unsigned long long)(NT_);                                                              \
+    }
+#else
+#define ST_DECL
+#define ST(i)
+#define ST_STORE(NT_)
+#endif
+
 // partial-result store: agent-scope atomic (global_store sc1, write-through) when a last-arriving
 // workgroup of another XCD will read it in the same launch (combine_if_last<G, true>), else plain
 __device__ __forceinline__ void st_part(float* p, float v, bool wt) {
@@ -306,6 +338,7 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int S, float scale_log2, RopeArgs ra,
     int* __restrict__ counters, bf16* __restrict__ out, int out_stride, int Hc_rt, int gq) {
     constexpr int D = 128, PG = 64;
+    ST_DECL
     __shared__ __attribute__((aligned(16))) char lds[2 * PG * 256 + 2 * 4 * 16 * 4];
     __shared__ __attribute__((aligned(16))) bf16 lds_new[2 * D];  // ROPE: the new token's K | V row (bf16)
     // fused split merge (``counters``): weights [G][MAX_SPLITS] + denominators + last flag, aliasing lds
@@ -589,20 +622,29 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     // is scored); unrolled by two so every register array is indexed statically.  (Four sets in flight at
     // one workgroup per CU measured SLOWER in round 5: B=1 at 13.5k +1.5-2.5 %, the TP=8 shard +10 %, the
     // overshoot loads past a short split's last tile outweighing the deeper queue: r5_attn_deep_ab.jsonl.)
+    ST(0)
     for (int t = 0; t < ntiles; t += 2) {
         compute(t);
+        ST(1)
         __syncthreads();
+        ST(2)
         if (t + 1 < ntiles) {
             KV_WRITE(kreg2, vreg2, ksc2, vsc2, t + 1)
             KV_ISSUE(kreg2, vreg2, ksc2, vsc2, t + 3)
+            ST(3)
             __syncthreads();
+            ST(4)
             compute(t + 1);
+            ST(1)
             __syncthreads();
+            ST(2)
         }
         if (t + 2 < ntiles) {
             KV_WRITE(kreg, vreg, ksc, vsc, t + 2)
             KV_ISSUE(kreg, vreg, ksc, vsc, t + 4)
+            ST(3)
             __syncthreads();
+            ST(4)
         }
     }
 #undef KV_ISSUE
@@ -642,6 +684,8 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
         }
     }
     if (counters) combine_if_last<G, true>(part_o, part_ml, counters, out, out_stride, b, kvh, Hq, Hkv, S, c_last, c_sw, c_den);
+    ST(5)
+    ST_STORE(ntiles)
 }
 
 // KV page loads are nontemporal from 64 (sequence, kv head) groups up -- measured, step at 4k context:

@@ -202,12 +202,17 @@ class LLMEngine:
     def __init__(self, cfg: ModelConfig, device="cuda", dtype=torch.bfloat16, seed: int = 0,
                  max_num_seqs: int = 256, max_model_len: int = 16384, max_new_cap: int = 2048,
                  kv_pages: Optional[int] = None, kv_fraction: float = 0.6, page_size: int = 64,
-                 max_prefill_tokens: int = 16384, use_graphs: bool = True, sync_every: int = 16,
+                 max_prefill_tokens: int = 32768, use_graphs: bool = True, sync_every: int = 16,
                  eos_ids: Sequence[int] = (128001, 128009), tp_rank: int = 0, tp_size: int = 1, tp_group=None,
                  weight_dtype: str = "bf16", weights_path: Optional[str] = None, prefill_chunk: int = PREFILL_CHUNK,
                  kv_dtype: Optional[str] = None):
         """``kv_dtype``: "bf16" (default, $MRSUM_KV_DTYPE), "fp8v" (V rows fp8, K bf16) or "fp8" -- e4m3fn K/V rows with power-of-two
         row scales (engine/kv_cache.py): half the KV bytes per decode step; no context-parallel prefill.
+
+        ``max_prefill_tokens``: rows of one packed prefill pass (whole prompts up to it; longer prompts are sliced
+        by ``prefill_chunk``).  32768: the headline's 39 map prompts of ~4k in 5 passes instead of 10 and its 10
+        level-1 prompts of ~5.4k in 2 instead of 4 -- 10 h bench 18.10 / 18.10 -> 18.06 / 18.01 s, A/B/A/B on one
+        box (profiles/r6_prefill_budget_ab.jsonl).
 
         ``prefill_chunk``: cut prompts longer than this many tokens into slices prefilled one pass
         after the other through the paged cache (chunked prefill; 0 = one pass per prompt).  At 32k
