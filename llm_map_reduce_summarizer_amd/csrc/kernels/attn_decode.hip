@@ -31,8 +31,7 @@ constexpr int MAX_SPLITS = 256;
 // Diagnostic build only (tools/exp_attn_stamps.py compiles this file with -DMRSUM_ATTN_STAMPS into
 // _native/diag/): every wave accumulates s_memtime deltas per phase of the split kernel -- prologue, tile
 // compute, the barrier after it, the next tile's LDS write + load issue, the barrier after that, epilogue --
-// and lane 0 stores them to g_attn_stamps[(workgroup * 8 + wave) * 8 + phase] (6: total, 7: tiles; 8 wave slots
-// per workgroup, for the 512-thread SPEC variant).
+// and lane 0 stores them to g_attn_stamps[(workgroup * 4 + wave) * 8 + phase] (6: total, 7: tiles).
 #ifdef MRSUM_ATTN_STAMPS
 __device__ unsigned long long* g_attn_stamps;
 MRSUM_API int mrsum_attn_set_stamps(void* p) {
@@ -50,7 +49,7 @@ MRSUM_API int mrsum_attn_set_stamps(void* p) {
 #define ST_STORE(NT_)                                                                                   \
     if (g_attn_stamps && (threadIdx.x & 63) == 0) {                                                      \
         const size_t wg_ = ((size_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;      \
-        unsigned long long* o_ = g_attn_stamps + (wg_ * 8 + (threadIdx.x >> 6)) * 8;                   \
+        unsigned long long* o_ = g_attn_stamps + (wg_ * 4 + (threadIdx.x >> 6)) * 8;                   \
         for (int i_ = 0; i_ < 6; ++i_) o_[i_] = st_acc_[i_];                                            \
         o_[6] = __builtin_amdgcn_s_memtime() - st_t0_;                                                  \
         o_[7] = (unsigned long long)(NT_);                                                              \
@@ -110,10 +109,8 @@ __device__ __forceinline__ void combine_group(const float* part_o, const float* 
         }
     }
     // 2. split weights: one wave per head, lane l holds splits l, l + 64, l + 128, l + 192 (S <= MAX_SPLITS)
-    //    (waves 4-7 of a 512-thread workgroup -- the loader waves of the specialised split kernel -- only join
-    //    the barriers: every step below works on the first 256 threads)
     static_assert(MAX_SPLITS <= 4 * 64, "four splits per lane");
-    for (int g = wv; g < G && wv < 4; g += 4) {
+    for (int g = wv; g < G; g += 4) {
         float ms[4], ls[4], mloc = -INFINITY;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -167,9 +164,9 @@ __device__ __forceinline__ void combine_group(const float* part_o, const float* 
             }
         }
         if constexpr (NH > 1) {
-            if (tid < 256) red[tid] = acc;
+            red[tid] = acc;
             __syncthreads();
-            if (h == 0 && tid < 256) {
+            if (h == 0) {
 #pragma unroll
                 for (int j = 1; j < NH; ++j) {
                     const float4 v = red[j * NV + item];
@@ -180,7 +177,7 @@ __device__ __forceinline__ void combine_group(const float* part_o, const float* 
                 }
             }
         }
-        if (h == 0 && tid < 256) {
+        if (h == 0) {
             const float den = sden[g];
             const float inv = den > 0.f ? 1.f / den : 0.f;
             uint2 o;
@@ -297,7 +294,7 @@ struct RopeArgs {
 // kvr = kvh except for the per-query-head fallback of other GQA ratios) (D floats each), into ``sq``.
 // Work items = float4 columns x slab subsets (NH subsets when there are fewer than 256 columns), so
 // every thread has its loads in flight at once; the subsets are merged through LDS.
-template <int G, int NTH = 256>
+template <int G>
 __device__ __forceinline__ void rope_slab_sums(const RopeArgs& ra, const float* prow, int kvh, int kvr, int Hc,
                                                bool with_kv, float* sq) {
     constexpr int D = 128;
@@ -306,7 +303,7 @@ __device__ __forceinline__ void rope_slab_sums(const RopeArgs& ra, const float* 
     const int nv = nq + (with_kv ? 2 * D / 4 : 0);
     const int nh = nv >= 256 ? 1 : 256 / nv;
     float4* red = reinterpret_cast<float4*>(sq) + nv;  // [nh][nv] partials after the [nv] result
-    for (int it = tid; it < nv * nh; it += NTH) {  // (the 256-thread partition, whatever NTH: same sums)
+    for (int it = tid; it < nv * nh; it += 256) {
         const int item = it % nv, h = it / nv;
         int colf;
         if (item < nq) colf = kvh * G * D + 4 * item;
@@ -323,7 +320,7 @@ __device__ __forceinline__ void rope_slab_sums(const RopeArgs& ra, const float* 
     }
     __syncthreads();
     float4* out = reinterpret_cast<float4*>(sq);
-    for (int item = tid; item < nv; item += NTH) {
+    for (int item = tid; item < nv; item += 256) {
         float4 acc = red[item];
         for (int h = 1; h < nh; ++h) {
             const float4 v = red[h * nv + item];
@@ -349,25 +346,15 @@ __device__ __forceinline__ u32x4 ld_kv(const T* p) {
 // values into the tile, so this step and later steps see the same K/V.  KVM is a bitmask: bit 0 = the K
 // cache is fp8 slabs, bit 1 = the V cache is; KVM 2 ("fp8v": bf16 K, fp8 V) stages K with the bf16
 // mapping and V with the slab mapping, each into its own LDS tile.
-//
-// SPEC (specialised waves, grids of at most one workgroup per CU, bf16 cache): 512 threads, waves 0-3 score
-// tiles, waves 4-7 only stage them -- each loader lane waits for its own register set, writes it into the
-// OTHER of two LDS tile buffers and issues the loads two tiles ahead, while the scoring waves work on the
-// current buffer; one barrier per tile.  With one workgroup per CU the plain kernel's waves run the tile
-// chain serially (scoring ~1200 cycles, staging ~850, two barriers ~400 per 64-key tile at B = 10:
-// tools/exp_attn_stamps.py, profiles/r6_attn_stamps.jsonl); here staging and scoring of consecutive tiles
-// overlap on the same SIMDs.  Same arithmetic in the same order as the plain kernel.
-template <int G, bool ROPE, bool NT = false, int KVM = 0, bool SPEC = false>
-__global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mfma_kernel(
+template <int G, bool ROPE, bool NT = false, int KVM = 0>
+__global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     const bf16* __restrict__ q, int q_stride, bf16* __restrict__ kc, bf16* __restrict__ vc,
     const int* __restrict__ block_tables, int bt_stride, const int* __restrict__ positions,
     float* __restrict__ part_o, float* __restrict__ part_ml, int Hkv, int S, float scale_log2, RopeArgs ra,
     int* __restrict__ counters, bf16* __restrict__ out, int out_stride, int Hc_rt, int gq) {
     constexpr int D = 128, PG = 64;
-    constexpr int NTHR = SPEC ? 512 : 256, NBUF = SPEC ? 2 : 1;
-    static_assert(!SPEC || KVM == 0, "the specialised kernel stages bf16 pages only");
     ST_DECL
-    __shared__ __attribute__((aligned(16))) char lds[NBUF * 2 * PG * 256 + 2 * 4 * 16 * 4];
+    __shared__ __attribute__((aligned(16))) char lds[2 * PG * 256 + 2 * 4 * 16 * 4];
     __shared__ __attribute__((aligned(16))) bf16 lds_new[2 * D];  // ROPE: the new token's K | V row (bf16)
     // fused split merge (``counters``): weights [G][MAX_SPLITS] + denominators + last flag, aliasing lds
     float* c_sw = reinterpret_cast<float*>(lds);
@@ -375,9 +362,7 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mf
     int* c_last = reinterpret_cast<int*>(c_den + 16);
     char* ldsK = lds;
     char* ldsV = lds + PG * 256;
-    char* ldsK1 = lds + (NBUF - 1) * 2 * PG * 256;  // SPEC: the second tile buffer
-    char* ldsV1 = ldsK1 + PG * 256;
-    float* sm_ml = reinterpret_cast<float*>(lds + NBUF * 2 * PG * 256);  // [2][4 waves][16 heads]
+    float* sm_ml = reinterpret_cast<float*>(lds + 2 * PG * 256);  // [2][4 waves][16 heads]
 
     const int split = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
     const int Hq = Hkv * G;
@@ -385,9 +370,6 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mf
     const int kvr = G == 1 ? kvh / gq : kvh;
     const int Hc = G == 1 ? Hc_rt : Hkv;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, col = lane & 15, grp = lane >> 4;
-    // SPEC roles: threads 0-255 score (``computer``), 256-511 stage (``loader``, staging index ltid = tid - 256)
-    const bool computer = !SPEC || tid < 256, loader = !SPEC || tid >= 256;
-    const int ltid = tid & 255;
     const int ctx = positions[b] + 1;
     int chunk = (ctx + S - 1) / S;
     chunk = (chunk + PG - 1) & ~(PG - 1);
@@ -397,7 +379,7 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mf
     if (ks >= ke) {
         // an empty split (the context ends before it) still publishes a zero slab: the merge weights it by
         // 0, and 0 x a stale NaN / inf left in the (reused, uninitialised) workspace would be NaN
-        for (int i = tid; i < G * D; i += NTHR)
+        for (int i = tid; i < G * D; i += 256)
             st_part(part_o + (ml_base + (size_t)(i / D) * S) * D + i % D, 0.f, counters != nullptr);
         if (tid < G) {
             st_part(part_ml + (ml_base + (size_t)tid * S) * 2 + 0, -INFINITY, counters != nullptr);
@@ -411,7 +393,7 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mf
     const float* prow = ROPE ? ra.parts + (size_t)b * ra.width : nullptr;
     const float2* cs = ROPE ? ra.cos_sin + (size_t)(ctx - 1) * (D / 2) : nullptr;
     const int* bt = block_tables + (size_t)b * bt_stride + ks / PG;
-    const int st_row = ltid >> 4, st_chunk = ltid & 15;
+    const int st_row = tid >> 4, st_chunk = tid & 15;
     const size_t head_off = (size_t)kvr * PG * D + (size_t)st_row * D + st_chunk * 8;
     // KV8 staging: row r8 + 32 i, 16-B fp8 chunk c8 (dims 16 c8 .. +16) of the (page, head) slab
     const int r8 = tid >> 3, c8 = tid & 7;
@@ -453,10 +435,8 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mf
             _Pragma("unroll") for (int i = 0; i < 4; ++i) VR[i] = ld_kv<NT>(vc + base_ + (size_t)16 * i * D); \
         }                                                                                           \
     }
-    if (loader) {
-        KV_ISSUE(kreg, vreg, ksc, vsc, 0)
-        KV_ISSUE(kreg2, vreg2, ksc2, vsc2, 1)
-    }
+    KV_ISSUE(kreg, vreg, ksc, vsc, 0)
+    KV_ISSUE(kreg2, vreg2, ksc2, vsc2, 1)
     // ROPE: the q rows of this group (and, for the split holding the new token, its K and V rows)
     // summed over the SP slabs by ALL 256 threads in one round of independent loads into an fp32
     // LDS image (aliasing the K/V tile buffers, which are first written after it is consumed):
@@ -466,7 +446,7 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mf
     const bool has_pos = ROPE && ks <= ctx - 1 && ctx - 1 < ke;
     if constexpr (ROPE) {
         if (has_pos) {
-            rope_slab_sums<G, NTHR>(ra, prow, kvh, kvr, Hc, true, sq);
+            rope_slab_sums<G>(ra, prow, kvh, kvr, Hc, true, sq);
             // the new token's K (rotated) and V row of this kv head -> paged cache for the next steps;
             // THIS launch never reads it back from memory (no store drain on the critical path): the
             // staging of the page that holds it patches the row into LDS from the fp32 image
@@ -533,7 +513,7 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mf
     if constexpr (ROPE) {
         // dims 32k + 8grp + j (k = 0, 1) pair with dims 64 + the same (k = 2, 3): the rotation of a
         // lane's q values needs only the lane's own values
-        if (!has_pos) rope_slab_sums<G, NTHR>(ra, prow, kvh, kvr, Hc, false, sq);  // overlaps the first page's loads
+        if (!has_pos) rope_slab_sums<G>(ra, prow, kvh, kvr, Hc, false, sq);  // overlaps the first page's loads
         float a[4][8];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -568,7 +548,7 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mf
     if constexpr (ROPE) {
         __syncthreads();  // every lane has its q out of the fp32 image the tiles overwrite
     }
-#define KV_WRITE(KR, VR, KS, VS, TILE, LK, LV)                                                                    \
+#define KV_WRITE(KR, VR, KS, VS, TILE)                                                                          \
     if constexpr (K8) {                                                                                         \
         _Pragma("unroll") for (int i = 0; i < 2; ++i) {                                                         \
             const bool pt = ROPE && ptile == (TILE) && patcher_k && i == (pr >> 5);                             \
@@ -579,13 +559,13 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mf
                 klo = *reinterpret_cast<const u32x4*>(lds_new + 16 * c8);                                       \
                 khi = *reinterpret_cast<const u32x4*>(lds_new + 16 * c8 + 8);                                   \
             }                                                                                                   \
-            *reinterpret_cast<u32x4*>((LK) + dk_off(row_, 2 * c8)) = klo;                                      \
-            *reinterpret_cast<u32x4*>((LK) + dk_off(row_, 2 * c8 + 1)) = khi;                                  \
+            *reinterpret_cast<u32x4*>(ldsK + dk_off(row_, 2 * c8)) = klo;                                      \
+            *reinterpret_cast<u32x4*>(ldsK + dk_off(row_, 2 * c8 + 1)) = khi;                                  \
         }                                                                                                       \
     } else {                                                                                                    \
         _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                         \
             const bool pt = ROPE && ptile == (TILE) && patcher_k && i == (pr >> 4);                             \
-            *reinterpret_cast<u32x4*>((LK) + dk_off(st_row + 16 * i, st_chunk)) =                               \
+            *reinterpret_cast<u32x4*>(ldsK + dk_off(st_row + 16 * i, st_chunk)) =                               \
                 pt ? *reinterpret_cast<const u32x4*>(lds_new + st_chunk * 8) : KR[i];                           \
         }                                                                                                       \
     }                                                                                                           \
@@ -599,20 +579,18 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mf
                 vlo = *reinterpret_cast<const u32x4*>(lds_new + D + 16 * c8);                                   \
                 vhi = *reinterpret_cast<const u32x4*>(lds_new + D + 16 * c8 + 8);                               \
             }                                                                                                   \
-            *reinterpret_cast<u32x4*>((LV) + dv_off(row_, 2 * c8)) = vlo;                                      \
-            *reinterpret_cast<u32x4*>((LV) + dv_off(row_, 2 * c8 + 1)) = vhi;                                  \
+            *reinterpret_cast<u32x4*>(ldsV + dv_off(row_, 2 * c8)) = vlo;                                      \
+            *reinterpret_cast<u32x4*>(ldsV + dv_off(row_, 2 * c8 + 1)) = vhi;                                  \
         }                                                                                                       \
     } else {                                                                                                    \
         _Pragma("unroll") for (int i = 0; i < 4; ++i) {                                                         \
             const bool pt = ROPE && ptile == (TILE) && patcher_v && i == (pr >> 4);                             \
-            *reinterpret_cast<u32x4*>((LV) + dv_off(st_row + 16 * i, st_chunk)) =                               \
+            *reinterpret_cast<u32x4*>(ldsV + dv_off(st_row + 16 * i, st_chunk)) =                               \
                 pt ? *reinterpret_cast<const u32x4*>(lds_new + D + st_chunk * 8) : VR[i];                       \
         }                                                                                                       \
     }
-    if (loader) {
-        KV_WRITE(kreg, vreg, ksc, vsc, 0, ldsK, ldsV)
-        KV_ISSUE(kreg, vreg, ksc, vsc, 2)
-    }
+    KV_WRITE(kreg, vreg, ksc, vsc, 0)
+    KV_ISSUE(kreg, vreg, ksc, vsc, 2)
 
     f32x4 o[8];
 #pragma unroll
@@ -621,13 +599,13 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mf
     const int q4 = col >> 2, p4 = col & 3;
     __syncthreads();
 
-    auto compute = [&](int t, const char* LK, const char* LV) {
+    auto compute = [&](int t) {
         const int key0 = ks + t * PG + 16 * w;  // this wave's 16 keys
         if (key0 < ke) {
             f32x4 sacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const uint4 a = *reinterpret_cast<const uint4*>(LK + dk_off(16 * w + col, 4 * k + grp));
+                const uint4 a = *reinterpret_cast<const uint4*>(ldsK + dk_off(16 * w + col, 4 * k + grp));
                 sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), qf[k], sacc, 0, 0, 0);
             }
             const int kb = key0 + 4 * grp;
@@ -649,7 +627,7 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mf
             for (int dt = 0; dt < 8; ++dt) {
                 o[dt] *= alpha;
                 const s4v a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                    (lds_s4v*)(LV + dv_off(vrow, 2 * dt + (p4 >> 1)) + 8 * (p4 & 1)));
+                    (lds_s4v*)(ldsV + dv_off(vrow, 2 * dt + (p4 >> 1)) + 8 * (p4 & 1)));
                 o[dt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, pb, o[dt], 0, 0, 0);
             }
         }
@@ -659,57 +637,28 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mf
     // one workgroup per CU measured SLOWER in round 5: B=1 at 13.5k +1.5-2.5 %, the TP=8 shard +10 %, the
     // overshoot loads past a short split's last tile outweighing the deeper queue: r5_attn_deep_ab.jsonl.)
     ST(0)
-    if constexpr (SPEC) {
-        // tile t in buffer t & 1: the scoring waves work on it while the loader waves write tile t + 1 (register
-        // set B for odd tiles, A for even ones) into the other buffer and issue tile t + 3; one barrier per tile
-        for (int t = 0; t < ntiles; t += 2) {
-            if (computer) {
-                compute(t, ldsK, ldsV);
-                ST(1)
-            } else if (t + 1 < ntiles) {
-                KV_WRITE(kreg2, vreg2, ksc2, vsc2, t + 1, ldsK1, ldsV1)
-                KV_ISSUE(kreg2, vreg2, ksc2, vsc2, t + 3)
-                ST(3)
-            }
+    for (int t = 0; t < ntiles; t += 2) {
+        compute(t);
+        ST(1)
+        __syncthreads();
+        ST(2)
+        if (t + 1 < ntiles) {
+            KV_WRITE(kreg2, vreg2, ksc2, vsc2, t + 1)
+            KV_ISSUE(kreg2, vreg2, ksc2, vsc2, t + 3)
+            ST(3)
             __syncthreads();
-            ST(2)
-            if (t + 1 < ntiles) {
-                if (computer) {
-                    compute(t + 1, ldsK1, ldsV1);
-                    ST(1)
-                } else if (t + 2 < ntiles) {
-                    KV_WRITE(kreg, vreg, ksc, vsc, t + 2, ldsK, ldsV)
-                    KV_ISSUE(kreg, vreg, ksc, vsc, t + 4)
-                    ST(3)
-                }
-                __syncthreads();
-                ST(2)
-            }
-        }
-    } else {
-        for (int t = 0; t < ntiles; t += 2) {
-            compute(t, ldsK, ldsV);
+            ST(4)
+            compute(t + 1);
             ST(1)
             __syncthreads();
             ST(2)
-            if (t + 1 < ntiles) {
-                KV_WRITE(kreg2, vreg2, ksc2, vsc2, t + 1, ldsK, ldsV)
-                KV_ISSUE(kreg2, vreg2, ksc2, vsc2, t + 3)
-                ST(3)
-                __syncthreads();
-                ST(4)
-                compute(t + 1, ldsK, ldsV);
-                ST(1)
-                __syncthreads();
-                ST(2)
-            }
-            if (t + 2 < ntiles) {
-                KV_WRITE(kreg, vreg, ksc, vsc, t + 2, ldsK, ldsV)
-                KV_ISSUE(kreg, vreg, ksc, vsc, t + 4)
-                ST(3)
-                __syncthreads();
-                ST(4)
-            }
+        }
+        if (t + 2 < ntiles) {
+            KV_WRITE(kreg, vreg, ksc, vsc, t + 2)
+            KV_ISSUE(kreg, vreg, ksc, vsc, t + 4)
+            ST(3)
+            __syncthreads();
+            ST(4)
         }
     }
 #undef KV_ISSUE
@@ -718,18 +667,16 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mf
     // merge the 4 waves: lane (grp, col) holds O^T[d = 16dt + 4grp + j][head col]
     lsum = rows_sum4(lsum);
     float* sm_o = reinterpret_cast<float*>(lds);  // [4][128][16] f32 = 32 KiB, reuses the tile buffers
-    if (computer) {
 #pragma unroll
-        for (int dt = 0; dt < 8; ++dt)
+    for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) sm_o[(w * D + 16 * dt + 4 * grp + j) * 16 + col] = o[dt][j];
-        if (grp == 0) {
-            sm_ml[w * 16 + col] = m;
-            sm_ml[64 + w * 16 + col] = lsum;
-        }
+        for (int j = 0; j < 4; ++j) sm_o[(w * D + 16 * dt + 4 * grp + j) * 16 + col] = o[dt][j];
+    if (grp == 0) {
+        sm_ml[w * 16 + col] = m;
+        sm_ml[64 + w * 16 + col] = lsum;
     }
     __syncthreads();
-    for (int i = tid; i < G * D && tid < 256; i += 256) {
+    for (int i = tid; i < G * D; i += 256) {
         const int h = i / D, d = i % D;
         float M = -INFINITY;
 #pragma unroll
@@ -758,7 +705,6 @@ __global__ __launch_bounds__(SPEC ? 512 : 256, SPEC ? 1 : 3) void attn_decode_mf
 // B=39 x 8 kv heads 7.02-7.05 vs 7.18-7.26 ms with the default policy; B <= 10 0.7-1 % slower with nt
 // (profiles/r1_decode_nt_ab.jsonl)
 constexpr int NT_MIN_GROUPS = 64;
-constexpr int ATTN_SPEC = 0x100;  // launch flag (kv8 argument, bit 8): the specialised-wave kernel
 
 static bool decode_packed(int G) { return G == 1 || G == 2 || G == 4 || G == 8 || G == 16; }
 
@@ -774,10 +720,6 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
                        int B, int Hq, int Hkv, int D, int P, int S, float scale, const RopeArgs* rope, int* counters,
                        int kv8, hipStream_t s) {
     if (B <= 0) return 0;
-    // bit 8 of kv8 (ATTN_SPEC) asks for the specialised-wave kernel; taken for a bf16 cache on a grid of at
-    // most one workgroup per CU, ignored otherwise
-    const bool spec_req = (kv8 & ATTN_SPEC) != 0;
-    kv8 &= ~ATTN_SPEC;
     if (D != 128 || P != 64 || Hkv <= 0 || Hq % Hkv || Hq / Hkv > 64 || S < 1 || S > MAX_SPLITS ||
         (kv8 != 0 && kv8 != 2 && kv8 != 3) || !out)
         return (int)hipErrorInvalidValue;
@@ -786,22 +728,19 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
     Hkv = Hq / (decode_packed(Hq / Hc) ? Hq / Hc : 1);  // head groups of the grid (virtual kv heads)
     const int G = Hq / Hkv;
     const float sl = scale * 1.4426950408889634f;
-    const bool spec = spec_req && kv8 == 0 && (long)S * Hkv * B <= 256;
-    dim3 grid(S, Hkv, B), block(spec ? 512 : 256);
+    dim3 grid(S, Hkv, B), block(256);
     auto Qp = (const bf16*)q; auto K = (bf16*)kcache; auto V = (bf16*)vcache;
     auto PO = (float*)part_o; auto PM = (float*)part_ml;
     const RopeArgs ra = rope ? *rope : RopeArgs{nullptr, 0, 0, 0, 0, nullptr};
-#define MFMA_KS(G_, R_, NT_, K8_, SP_)                                                                           \
-    attn_decode_mfma_kernel<G_, R_, NT_, K8_, SP_><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables,       \
-                                                                          bt_stride, positions, PO, PM, Hkv, S, sl, \
-                                                                          ra, counters, (bf16*)out, out_stride, Hc, gq)
-#define MFMA_K(G_, R_, NT_, K8_) MFMA_KS(G_, R_, NT_, K8_, false)
+#define MFMA_K(G_, R_, NT_, K8_)                                                                                \
+    attn_decode_mfma_kernel<G_, R_, NT_, K8_><<<grid, block, 0, s>>>(Qp, q_stride, K, V, block_tables, bt_stride,  \
+                                                                     positions, PO, PM, Hkv, S, sl, ra, counters, \
+                                                                     (bf16*)out, out_stride, Hc, gq)
 #define MFMA_L(G_, R_)                                                                                        \
     do {                                                                                                      \
         const bool nt_ = B * Hkv >= NT_MIN_GROUPS;                                                            \
         if (kv8 == 3) { if (nt_) MFMA_K(G_, R_, true, 3); else MFMA_K(G_, R_, false, 3); }                    \
         else if (kv8 == 2) { if (nt_) MFMA_K(G_, R_, true, 2); else MFMA_K(G_, R_, false, 2); }               \
-        else if (spec) MFMA_KS(G_, R_, false, 0, true);                                                    \
         else { if (nt_) MFMA_K(G_, R_, true, 0); else MFMA_K(G_, R_, false, 0); }                             \
     } while (0)
 #define MFMA_G(R_)                            \
@@ -817,7 +756,6 @@ static int launch_mfma(const void* q, int q_stride, const void* kcache, const vo
 #undef MFMA_G
 #undef MFMA_L
 #undef MFMA_K
-#undef MFMA_KS
     int e = (int)hipGetLastError();
     if (e || counters) return e;
     if (S > 16) {

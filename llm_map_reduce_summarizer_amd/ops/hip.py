@@ -486,26 +486,16 @@ class DecodeWorkspace:
     by every workgroup costing what the merge launch did: profiles/r5_consumer_merge_ab.jsonl.  Removed.)"""
 
     def __init__(self, batch: int, hq: int, d: int, splits: int, device, hkv: Optional[int] = None,
-                 fused_combine: bool = False, spec: Optional[bool] = None):
+                 fused_combine: bool = False):
         # fused_combine (last-arriver merge inside the split kernel) measured SLOWER than the separate
         # merge kernel at every B >= 8 (the per-workgroup drain + agent release costs more than the
         # launch boundary it saves: B=39 238 vs 189 us), so the separate kernel is the default.
         self.splits = splits
-        # spec: ask for the specialised-wave kernel (attn_decode.hip SPEC: taken on a bf16 cache when the grid
-        # has at most one workgroup per CU); MRSUM_ATTN_SPEC=1 turns it on for A/B runs
-        self.spec = os.environ.get("MRSUM_ATTN_SPEC", "0") == "1" if spec is None else bool(spec)
         self.part_o = torch.empty(batch * hq * splits * d, dtype=torch.float32, device=device)
         self.part_ml = torch.empty(batch * hq * splits * 2, dtype=torch.float32, device=device)
         self.counters = (torch.zeros(batch * (hkv or hq), dtype=torch.int32, device=device)
                          if fused_combine else None)
 
-
-
-ATTN_SPEC = 0x100  # attn_decode.hip launch flag (bit 8 of the cache-kind argument)
-
-
-def _spec_flag(workspace: DecodeWorkspace) -> int:
-    return ATTN_SPEC if getattr(workspace, "spec", False) else 0
 
 
 def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor,
@@ -537,8 +527,7 @@ def attn_decode_rope(parts: torch.Tensor, cos_sin: torch.Tensor, kcache: torch.T
     _check(_fn("mrsum_attn_decode_rope")(_p(parts), SP, _p(cos_sin), _p(kcache), _p(vcache), _p(block_tables),
                                          block_tables.stride(0), _p(positions), _p(workspace.part_o),
                                          _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
-                                         workspace.splits, scale, _p(workspace.counters), kv8 | _spec_flag(workspace),
-                                         _stream()),
+                                         workspace.splits, scale, _p(workspace.counters), kv8, _stream()),
            "attn_decode_rope")
     return out
 
@@ -568,8 +557,7 @@ def attn_decode(q: torch.Tensor, kcache: torch.Tensor, vcache: torch.Tensor, blo
     _check(_fn("mrsum_attn_decode_mfma")(_p(q), q.stride(0), _p(kcache), _p(vcache), _p(block_tables),
                                          block_tables.stride(0), _p(positions), _p(workspace.part_o),
                                          _p(workspace.part_ml), _p(out), out.stride(0), B, hq, hkv, d, page,
-                                         workspace.splits, scale, _p(workspace.counters), kv8 | _spec_flag(workspace),
-                                         _stream()),
+                                         workspace.splits, scale, _p(workspace.counters), kv8, _stream()),
            "attn_decode_mfma")
     return out
 

@@ -548,12 +548,9 @@ def test_fp8_swiglu_and_quant():
 @pytest.mark.parametrize("hq,hkv,S", [(32, 8, 4), (4, 1, 1), (16, 1, 3), (8, 2, 2), (4, 1, 16), (6, 2, 2), (24, 8, 4)])
 @pytest.mark.parametrize("fused_combine", [False, True])
 @pytest.mark.parametrize("kv8", ["bf16", "fp8", "fp8v"])
-@pytest.mark.parametrize("spec", ["0", "1"])
-def test_attn_decode_rope_fused(hq, hkv, S, fused_combine, kv8, spec, monkeypatch):
+def test_attn_decode_rope_fused(hq, hkv, S, fused_combine, kv8):
     """attn_decode_rope (q/k RoPE + new K/V written into the cache + attention, from the QKV GEMM's
-    fp32 split-K slabs) == reference rope_kv_parts followed by reference attention; ``spec`` "1": the
-    specialised-wave kernel where the launch takes it (bf16 cache, <= 256 workgroups)."""
-    monkeypatch.setenv("MRSUM_ATTN_SPEC", spec)
+    fp32 split-K slabs) == reference rope_kv_parts followed by reference attention."""
     d, page = 128, 64
     ctxs = [1, 64, 65, 700, 129, 1000]
     B = len(ctxs)
@@ -1088,45 +1085,3 @@ def test_linear_tall_lm_head(M):
     out = hip.linear(x, w)
     torch.cuda.synchronize()
     _close(out, x.float() @ w.float().t(), 2e-2)
-
-
-@pytest.mark.parametrize("hq,hkv,ctxs,splits", [
-    (32, 8, [1, 700, 6000, 4097], 2), (32, 8, [4500, 300, 64, 5000], 3), (32, 8, [12000], 8),
-    (32, 8, [65, 128, 129, 191], 1), (4, 1, [4000], 63), (16, 1, [3000, 10], 5), (8, 8, [2500, 640], 4),
-    (16, 8, [900], 16)])
-@pytest.mark.parametrize("fused", [False, True])
-def test_attn_decode_spec(hq, hkv, ctxs, splits, fused):
-    """The specialised-wave kernel (attn_decode.hip SPEC: 512 threads, 4 scoring + 4 staging waves, two LDS
-    tile buffers; launch flag ATTN_SPEC, grids of <= 256 workgroups): odd and even tile counts per split,
-    one-tile and empty splits, G = 1 / 2 / 4 / 16, against the fp32 reference, replayed (re-armed merge
-    counters); and bit-identical to the 256-thread kernel (the same per-tile arithmetic in the same order)."""
-    d, page = 128, 64
-    B = len(ctxs)
-    npgs = [-(-c // page) for c in ctxs]
-    g = torch.Generator().manual_seed(131)
-    n_pages = sum(npgs) + 1
-    kc = torch.randn(n_pages, hkv, page, d, generator=g).to(torch.bfloat16).to(DEV)
-    vc = torch.randn(n_pages, hkv, page, d, generator=g).to(torch.bfloat16).to(DEV)
-    perm = torch.randperm(n_pages - 1, generator=g) + 1
-    bt = torch.zeros(B, max(npgs), dtype=torch.int32)
-    used = 0
-    for b, n in enumerate(npgs):
-        bt[b, :n] = perm[used:used + n]
-        used += n
-    bt = bt.to(DEV)
-    pos = torch.tensor([c - 1 for c in ctxs], dtype=torch.int32, device=DEV)
-    q = _rand(B, hq * d, seed=132)
-    sc = 1.0 / math.sqrt(d)
-    assert splits * hip.decode_groups(hq, hkv) * B <= 256  # the SPEC grid bound (else the launch keeps 256 threads)
-    o_ref = reference.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc)
-    ng = hip.decode_groups(hq, hkv)
-    ws = hip.DecodeWorkspace(B, hq, d, splits, DEV, ng, fused_combine=fused, spec=False)
-    o_plain = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws).clone()
-    ws.spec = True
-    ws.part_o.fill_(float("nan"))
-    for _ in range(3):
-        o_spec = hip.attn_decode(q, kc, vc, bt, pos, hq, hkv, d, page, sc, workspace=ws)
-        _close(o_spec, o_ref, 2e-2)
-        assert torch.equal(o_spec, o_plain)
-    if fused:
-        assert int(ws.counters.abs().sum()) == 0

@@ -50,16 +50,12 @@ def main():
     dev = "cuda:0"
     d, page = 128, 64
     # (name, B, hq, hkv, ctx, splits, fused): the headline's map (B=39), level-1 (B=10) and final (B=1) shapes
-    # with their plans, and a Llama-3-8B TP=8 shard at B=1
-    # a "_spec" case: the same shape on the specialised-wave kernel (launch flag 0x100; waves 0-3 score, 4-7 stage,
-    # reported separately: the loader waves' "write_issue" phase is their staging, "compute" stays 0)
+    # with their plans, and a Llama-3-8B TP=8 shard at B=1.  (A 512-thread specialised-wave variant -- 4 scoring
+    # + 4 staging waves, two LDS tile buffers -- was stamped here too and removed: profiles/r6_attn_stamps.jsonl.)
     cases = [("map_b39", 39, 32, 8, 4400, 4, False), ("l1_b10", 10, 32, 8, 4800, 3, True),
-             ("l1_b10_spec", 10, 32, 8, 4800, 3, True),
              ("l1_b10_sep6", 10, 32, 8, 4800, 6, False), ("final_b1", 1, 32, 8, 13000, 32, False),
-             ("final_b1_spec", 1, 32, 8, 13000, 32, False),
-             ("tp8_b1", 1, 4, 1, 4000, 63, False), ("tp8_b1_spec", 1, 4, 1, 4000, 63, False)]
+             ("tp8_b1", 1, 4, 1, 4000, 63, False)]
     for name, B, hq, hkv, ctx, S, fused in cases:
-        flag = 0x100 if name.endswith("_spec") else 0
         npg = -(-ctx // page)
         layers = 8
         caches = [(torch.randn(B * npg + 1, hkv, page, d, device=dev, dtype=torch.bfloat16),
@@ -72,14 +68,14 @@ def main():
         pm = torch.empty(B * hq * S * 2, device=dev)
         cnt = torch.zeros(B * hkv, dtype=torch.int32, device=dev) if fused else None
         nwg = S * hkv * B
-        stamps = torch.zeros(nwg * 8 * 8, dtype=torch.int64, device=dev)
+        stamps = torch.zeros(nwg * 4 * 8, dtype=torch.int64, device=dev)
 
         def call(i):
             kc, vc = caches[i % layers]
             rc = lib.mrsum_attn_decode_mfma(q.data_ptr(), q.stride(0), kc.data_ptr(), vc.data_ptr(), bt.data_ptr(),
                                             bt.stride(0), pos.data_ptr(), po.data_ptr(), pm.data_ptr(), out.data_ptr(),
                                             out.stride(0), B, hq, hkv, d, page, S, 1 / math.sqrt(d),
-                                            cnt.data_ptr() if cnt is not None else None, flag,
+                                            cnt.data_ptr() if cnt is not None else None, 0,
                                             torch.cuda.current_stream().cuda_stream)
             assert rc == 0, rc
 
@@ -98,19 +94,16 @@ def main():
         call(3)
         torch.cuda.synchronize()
         lib.mrsum_attn_set_stamps(None)
-        st = stamps.view(nwg, 8, 8).double().cpu()
-        roles = [("all", st[:, :4])] if not flag else [("scoring", st[:, :4]), ("loader", st[:, 4:])]
-        for role, sr in roles:
-            sr = sr.reshape(-1, 8)
-            sr = sr[sr[:, 7] > 0]  # waves of workgroups with tiles
-            mean = sr.mean(0)
-            tiles = float(mean[7])
-            rec = {"case": name, "waves": role, "B": B, "hq": hq, "hkv": hkv, "ctx": ctx, "splits": S, "fused": fused,
-                   "wall_us": round(us, 2), "tiles_per_wg": round(tiles, 2), "total_cycles": round(float(mean[6]))}
-            rec.update({p: round(float(mean[i])) for i, p in enumerate(PHASES)})
-            rec["per_tile"] = {p: round(float(mean[i]) / max(tiles, 1)) for i, p in enumerate(PHASES) if 1 <= i <= 4}
-            rec["max_total_cycles"] = round(float(sr[:, 6].max()))
-            print(json.dumps(rec), flush=True)
+        st = stamps.view(nwg * 4, 8).double().cpu()
+        st = st[st[:, 7] > 0]  # waves of workgroups with tiles
+        mean = st.mean(0)
+        tiles = float(mean[7])
+        rec = {"case": name, "B": B, "hq": hq, "hkv": hkv, "ctx": ctx, "splits": S, "fused": fused, "wall_us": round(us, 2),
+               "tiles_per_wg": round(tiles, 2), "total_cycles": round(float(mean[6]))}
+        rec.update({p: round(float(mean[i])) for i, p in enumerate(PHASES)})
+        rec["per_tile"] = {p: round(float(mean[i]) / max(tiles, 1)) for i, p in enumerate(PHASES) if 1 <= i <= 4}
+        rec["max_total_cycles"] = round(float(st[:, 6].max()))
+        print(json.dumps(rec), flush=True)
         del caches
 
 
