@@ -680,7 +680,7 @@ __global__ __launch_bounds__(64 * WPB, 1) void stream_fp8_kernel(const bf16* __r
     stream_epilogue<MT, EPI, WPB>(acc, lds, reinterpret_cast<float*>(xtra + 1024), n0, M, out, ldo, parts, counters, e);
 }
 
-// Same contract as mrsum_stream_gemm (epilogues BF16 / F32_PARTIAL / SWIGLU / RESID_SPLIT, deferred
+// Same contract as mrsum_stream_gemm (epilogues BF16 / F32_PARTIAL / SWIGLU / SWIGLU_SPLIT / RESID_SPLIT, deferred
 // RMSNorm operands) with W e4m3fn [N, K] row-major and wscale fp32 [N]; K % 256 == 0, (K / 256) % splits == 0.
 MRSUM_API int mrsum_stream_fp8(const void* x, int ldx, const void* W, const float* wscale, int N, int K, int M,
                                void* out, int ldo, int epi, int splits, int wpb, void* parts, int* counters,
@@ -688,10 +688,12 @@ MRSUM_API int mrsum_stream_fp8(const void* x, int ldx, const void* W, const floa
                                void* ar, hipStream_t s) {
     if (M <= 0) return 0;
     if (wpb < 4 || wpb > 8 || M > 64 || K % KB8 || N % (16 * wpb) || splits < 1 || (K / KB8) % splits ||
-        epi < EPI_BF16 || epi > EPI_RESID_SPLIT || epi == EPI_SWIGLU_SPLIT)
+        epi < EPI_BF16 || epi > EPI_RESID_SPLIT)
         return (int)hipErrorInvalidValue;
-    if (epi != EPI_F32_PARTIAL && epi != EPI_RESID_SPLIT && splits != 1) return (int)hipErrorInvalidValue;
-    if (epi == EPI_RESID_SPLIT && (!parts || !counters || !resid || !ssp || ldr % 4)) return (int)hipErrorInvalidValue;
+    const bool split_epi = epi == EPI_SWIGLU_SPLIT || epi == EPI_RESID_SPLIT;
+    if (epi != EPI_F32_PARTIAL && !split_epi && splits != 1) return (int)hipErrorInvalidValue;
+    if (split_epi && (!parts || !counters)) return (int)hipErrorInvalidValue;
+    if (epi == EPI_RESID_SPLIT && (!resid || !ssp || ldr % 4)) return (int)hipErrorInvalidValue;
     if (ssq && (ssq_tiles <= 0 || ssq_tiles % (4 * SS_PARTS))) return (int)hipErrorInvalidValue;
     if (!tp_push_ok(ar, epi, M, N)) return (int)hipErrorInvalidValue;
     NormArgs e;
@@ -727,6 +729,7 @@ MRSUM_API int mrsum_stream_fp8(const void* x, int ldx, const void* W, const floa
     if (epi == EPI_BF16) { BY_WPB8(MT_, EPI_BF16) }                       \
     else if (epi == EPI_F32_PARTIAL) { BY_WPB8(MT_, EPI_F32_PARTIAL) }    \
     else if (epi == EPI_SWIGLU) { BY_WPB8(MT_, EPI_SWIGLU) }              \
+    else if (epi == EPI_SWIGLU_SPLIT) { BY_WPB8(MT_, EPI_SWIGLU_SPLIT) }  \
     else { BY_WPB8(MT_, EPI_RESID_SPLIT) }
     switch (mt) {
         case 1: BY_EPI8(1); break;

@@ -1234,7 +1234,31 @@ def stream_config_fp8(N: int, K: int, swiglu: bool = False, splits: Optional[int
     every M (o 12.9 vs 22.7, qkv 13.4 vs 18.1, down 13.7 vs 15.3 at M=1)."""
     if K % 256 or (M <= 8 and N * K >= (64 << 20)):
         return None
-    return stream_config(N, K // 2, swiglu=swiglu, splits=splits)  # K/256 slots == (K/2)/128 blocks
+    cfg = stream_config(N, K // 2, swiglu=swiglu, splits=splits)  # K/256 slots == (K/2)/128 blocks
+    if cfg is None and swiglu and splits is None and N >= 4096:
+        cfg = fp8_swiglu_split_cfg(N, K)
+    return cfg
+
+
+def fp8_swiglu_split_cfg(N: int, K: int):
+    """(wpb, S > 1) of the split-K SwiGLU on the fp8 stream kernel for a gate_up too narrow to fill the chip
+    with one workgroup per column tile, or None.  The best-filling grid of 2 / 4 / 8 splits.  In situ,
+    Llama-3-70B fp8 TP=8 shard (N 7168, K 8192; profiles/r6_fp8_swiglu_split_insitu.jsonl), ms per step vs
+    the register-streaming kernel: B=1 at 32k 4.40 (wpb 7, S 4) / 4.37 (8, 4) vs 4.44, B=10 at 4k 4.75 /
+    4.76 vs 5.55; two splits lose (4.53-4.58 at B=1)."""
+    best, best_key = None, None
+    for wpb in (8, 7, 6, 5, 4):
+        if N % (16 * wpb):
+            continue
+        tiles = N // (16 * wpb)
+        for S in (4, 8, 2):
+            if (K // 256) % S or K // S < 1024:
+                continue
+            grid = tiles * S
+            key = (round(grid / (-(-grid // N_CU) * N_CU), 3), S == 4, wpb)
+            if best_key is None or key > best_key:
+                best, best_key = (wpb, S), key
+    return best if best_key is not None and best_key[0] >= 0.7 else None
 
 
 def _stream_fp8(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, norm=None, resid=None, ssp=None,
@@ -1249,12 +1273,12 @@ def _stream_fp8(x, w, out, epi, splits, ldo, wpb, parts=None, counters=None, nor
          "stream_fp8: weight must be e4m3fn [N, K] contiguous")
     _req(w.scale.dtype == torch.float32 and w.scale.numel() == N and w.scale.is_contiguous(), "stream_fp8: scale")
     _req(1 <= M <= SKINNY_MAX_M and K % 256 == 0 and 4 <= wpb <= 8 and N % (16 * wpb) == 0
-         and (K // 256) % splits == 0 and epi != EPI_SWIGLU_SPLIT, "stream_fp8: unsupported shape M=%d N=%d K=%d S=%d "
+         and (K // 256) % splits == 0, "stream_fp8: unsupported shape M=%d N=%d K=%d S=%d "
          "wpb=%d" % (M, N, K, splits, wpb))
-    if epi == EPI_RESID_SPLIT:
+    if epi in (EPI_RESID_SPLIT, EPI_SWIGLU_SPLIT):
         _req(parts is not None and parts.shape == (splits, M, N) and parts.dtype == torch.float32
-             and counters is not None and counters.numel() >= N // (16 * wpb) and ssp.shape[1] == N // (16 * wpb),
-             "stream_fp8: split-K scratch")
+             and counters is not None and counters.numel() >= N // (16 * wpb)
+             and (epi == EPI_SWIGLU_SPLIT or ssp.shape[1] == N // (16 * wpb)), "stream_fp8: split-K scratch")
     sq, tiles, eps = _norm_args(x, norm)
     rp, ldr, sp = _resid_args(x, N, epi, resid, ssp)
     _check(_fn("mrsum_stream_fp8")(_p(x), x.stride(0), _p(w.q), _p(w.scale), N, K, M, _p(out), ldo, epi, splits, wpb,
@@ -1329,6 +1353,12 @@ def fp8_linear_swiglu(x: torch.Tensor, w, norm=None) -> torch.Tensor:
     if M > SKINNY_MAX_M:
         return fp8_linear(x, w, swiglu=True)  # 64-row chunks up to STREAM_MAX_M_SWIGLU, else the fp8 GEMM
     out = torch.empty(M, F2 // 2, dtype=torch.bfloat16, device=x.device)
+    if cfg is not None and cfg[1] > 1:
+        # split-K over cfg[1] workgroups per column tile, silu(gate) * up by the last split to arrive (the
+        # bf16 stream_swiglu_split of a narrow gate_up, e.g. a Llama-3-70B TP=8 shard's 7168 rows)
+        parts = torch.empty(cfg[1], M, F2, dtype=torch.float32, device=x.device)
+        cnt = _tile_counters(x.device, F2 // (16 * cfg[0]))
+        return _stream_fp8(x, w, out, EPI_SWIGLU_SPLIT, cfg[1], F2 // 2, cfg[0], parts=parts, counters=cnt, norm=norm)
     if cfg is not None:
         return _stream_fp8(x, w, out, EPI_SWIGLU, 1, F2 // 2, cfg[0], norm=norm)
     return _skinny_fp8(x, w, out, EPI_SWIGLU, 1, 1, F2 // 2, norm=norm)

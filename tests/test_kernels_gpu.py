@@ -529,6 +529,34 @@ def test_stream_fp8(M, N, K, wpb, S):
     _close(hip._stream_fp8(x, wgu, act, hip.EPI_SWIGLU, 1, N // 2, wpb), g * torch.sigmoid(g) * u, 3e-2)
 
 
+@pytest.mark.parametrize("M", [1, 10, 16, 40])
+@pytest.mark.parametrize("N,K,wpb,S", [(7168, 8192, 7, 4), (7168, 8192, 4, 2), (896, 1024, 7, 2), (1024, 512, 8, 1)])
+def test_stream_fp8_swiglu_split(M, N, K, wpb, S, monkeypatch):
+    """fp8 stream GEMM with the split-K SwiGLU epilogue (a narrow gate_up, e.g. a Llama-3-70B TP=8 shard's
+    7168 rows: S workgroups per column tile, the last to arrive applies silu(gate) * up) vs fp32 of the
+    dequantised weights; twice in a row (the tickets re-arm), and through fp8_linear_swiglu with the split
+    configuration forced."""
+    from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight
+    x = _rand(M, K, seed=84)
+    wg, wu = _rand(N // 2, K, scale=0.05, seed=85), _rand(N // 2, K, scale=0.05, seed=86)
+    wgu = Fp8Weight.quantize(reference.interleave_gate_up(wg, wu).contiguous())
+    g, u = reference.split_gate_up(x.float() @ wgu.dequant().t())
+    ref = g * torch.sigmoid(g) * u
+    parts = torch.empty(S, M, N, dtype=torch.float32, device=DEV)
+    cnt = hip._tile_counters(x.device, N // (16 * wpb))
+    first = None
+    for _ in range(2):
+        act = torch.empty(M, N // 2, dtype=torch.bfloat16, device=DEV)
+        hip._stream_fp8(x, wgu, act, hip.EPI_SWIGLU_SPLIT, S, N // 2, wpb, parts=parts, counters=cnt)
+        _close(act, ref, 3e-2)
+        first = act.clone() if first is None else first
+        assert torch.equal(act, first)
+    assert int(cnt[:N // (16 * wpb)].abs().sum()) == 0
+    if S > 1 and M <= hip.SKINNY_MAX_M:
+        monkeypatch.setattr(hip, "stream_config_fp8", lambda N_, K_, swiglu=False, splits=None, M=1: (wpb, S))
+        _close(hip.fp8_linear_swiglu(x, wgu), ref, 3e-2)
+
+
 def test_fp8_swiglu_and_quant():
     from llm_map_reduce_summarizer_amd.ops.reference import Fp8Weight
     M, F, K = 9, 512, 1024
