@@ -1147,7 +1147,10 @@ def plan(role: str, M: int, N: int, K: int, splits: Optional[int] = None, stream
         # (tools/bench_tp_shard.py with write-through partials, us: TP=4 N=7168 M=10 15.7 vs 17.0, M=39
         # 21.2 vs 29.4 (M=1 14.9 vs 14.4: skinny); TP=8 N=3584 M=39 15.2 vs 15.8, M <= 10 12.2-12.8 vs
         # 10.3: skinny)
-        if N >= 7168 and N % 112 == 0 and M > 8:
+        if N >= 7168 and N % 112 == 0 and (M > 8 or N // 112 * 4 <= N_CU):
+            # (a TP=4 shard's 7168 rows at one row too, where the 4-split grid is one round: in situ 8B TP=4
+            # B=1 1.634 / 1.636 ms vs 1.669 / 1.662 on the register-streaming kernel; a TP=8 shard's 3584 rows
+            # stay there, every split grid measured slower: profiles/r6_bf16_swiglu_split_insitu.jsonl)
             return ("stream_split", 7, 4)
         if N % 64 == 0 and M > 16:
             # (> 32 rows measured as above; 17..32 rows fell through to the 256 x 256 prefill GEMM: 81 us per

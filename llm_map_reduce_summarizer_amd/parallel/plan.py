@@ -18,9 +18,10 @@ node, so the choice is a cost model whose hardware constants are *measured*:
 * ``hbm_bw``, ``step_floor_s``, ``tp_row_s``, ``tp_shard_s``, ``fp8_row_s``, ``fp8_floor_s``: one MINIMAX fit
   (tools/fit_hwmodel.py) over the round-6 decode steps of TP=1 and of one rank's TP=2/4/8 shard with the TP
   kernel sequence over a group of one rank (TP push in the row-parallel GEMM epilogues), Llama-3-8B bf16 at
-  B=1/10/39 x 4k and Llama-3-70B fp8 at TP=1 / TP=8 (profiles/r6_decode_steps.jsonl):
-  t = (W + B ctx kv) / TP / 6.02 TB/s + L/32 x (0.862 ms + 7.58 us x B log2(TP) + [TP > 1] 0.438 ms / TP
-  + [fp8] (55.7 us + 46.4 us x B)), every point within 4.3 % (tests/test_plan.py pins that);
+  B=1/10/39 x 4k and Llama-3-70B fp8 at TP=1 / TP=8 (profiles/r6_decode_steps_final.jsonl):
+  t = (W + B ctx kv) / TP / 6.02 TB/s + L/32 x (0.858 ms + 7.43 us x B log2(TP) + [TP > 1] 0.384 ms / TP
+  + [fp8] (86.8 us + 5.28 us x B)), every point within 3.9 % (tests/test_plan.py pins that; the fp8 per-row
+  term fell from 46.4 us with the split-K SwiGLU of the narrow fp8 gate_up);
 * ``prefill_flops``: the engine's prefill rate in the 10 h bench (~76k tok/s of Llama-3-8B);
 * ``ar_lat_s`` / ``ar_lat_row_s`` and ``ar_bw``: timed at start-up on the job's own GPUs (the fused
   all-reduce inside a replayed hipGraph at 1 and 64 rows against the same kernel over a group of one
@@ -49,11 +50,11 @@ from typing import Dict, List, Sequence
 @dataclass(frozen=True)
 class HWModel:
     hbm_bw: float = 6.02e12         # bytes/s streamed by the decode GEMM + attention kernels
-    step_floor_s: float = 0.862e-3  # fixed per-step cost of the decode graph (kernel latencies), per 32 layers
-    tp_shard_s: float = 0.438e-3    # a TP shard's extra fixed cost per 32 layers, divided by TP ...
-    tp_row_s: float = 7.58e-6       # ... plus this per decode row per log2(TP) (few-kv-head attention is latency-bound)
-    fp8_floor_s: float = 55.7e-6    # W8A16 decode kernels: extra fixed cost per 32 layers ...
-    fp8_row_s: float = 46.4e-6      # ... and per decode row (the e4m3 -> bf16 conversion grows with the rows)
+    step_floor_s: float = 0.858e-3  # fixed per-step cost of the decode graph (kernel latencies), per 32 layers
+    tp_shard_s: float = 0.384e-3    # a TP shard's extra fixed cost per 32 layers, divided by TP ...
+    tp_row_s: float = 7.43e-6       # ... plus this per decode row per log2(TP) (few-kv-head attention is latency-bound)
+    fp8_floor_s: float = 86.8e-6    # W8A16 decode kernels: extra fixed cost per 32 layers ...
+    fp8_row_s: float = 5.28e-6      # ... and per decode row (the e4m3 -> bf16 conversion grows with the rows)
     prefill_flops: float = 1.1e15   # effective prefill FLOP/s (MFMA GEMMs + flash attention)
     ar_lat_s: float = 20e-6         # one decode all-reduce (custom P2P kernel), measured at start-up ...
     ar_lat_row_s: float = 0.0       # ... plus this per decode row (the push sends every row to every peer)

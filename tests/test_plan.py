@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 D8B = plan.ModelDims.of(get_model_config("llama3-8b"))
 
 
-STEPS = os.path.join(ROOT, "profiles", "r6_decode_steps.jsonl")
+STEPS = os.path.join(ROOT, "profiles", "r6_decode_steps_final.jsonl")
 
 
 def _dims(r):
@@ -21,7 +21,7 @@ def _dims(r):
 
 def test_decode_model_matches_every_measured_step():
     """VERDICT r5 #2c: the default constants reproduce every measured MI355X decode step of the current kernels
-    (profiles/r6_decode_steps.jsonl: TP=1 and one rank's TP=2/4/8 shard, Llama-3-8B bf16 and Llama-3-70B fp8)
+    (profiles/r6_decode_steps_final.jsonl: TP=1 and one rank's TP=2/4/8 shard, Llama-3-8B bf16 and Llama-3-70B fp8)
     within 5 %."""
     rows = [json.loads(l) for l in open(STEPS) if l.startswith("{")]
     assert {r["tp_shard"] for r in rows} >= {1, 2, 4, 8} and {r["dtype"] for r in rows} == {"bf16", "fp8"}
