@@ -154,13 +154,24 @@ __device__ __forceinline__ void combine_group(const float* part_o, const float* 
                 acc.z += ws * pre[r][j].z;
                 acc.w += ws * pre[r][j].w;
             }
-            for (int sp = h + PRE * NH; sp < S; sp += NH) {
-                const float4 v = ld_o(g, sp, d4);
-                const float ws = w[sp];
-                acc.x += ws * v.x;
-                acc.y += ws * v.y;
-                acc.z += ws * v.z;
-                acc.w += ws * v.w;
+            // splits beyond the preloaded ones (S > PRE * NH: the one-row TP-shard plans of 128-256 splits)
+            // in batches of 8 independent loads (clamped, weighted 0 past S): a few round trips, not one per
+            // split; the same summation order as one at a time
+            for (int sp0 = h + PRE * NH; sp0 < S; sp0 += 8 * NH) {
+                float4 v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = ld_o(g, min(sp0 + j * NH, S - 1), d4);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int sp = sp0 + j * NH;
+                    if (sp < S) {
+                        const float ws = w[sp];
+                        acc.x += ws * v[j].x;
+                        acc.y += ws * v[j].y;
+                        acc.z += ws * v[j].z;
+                        acc.w += ws * v[j].w;
+                    }
+                }
             }
         }
         if constexpr (NH > 1) {
