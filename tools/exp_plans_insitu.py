@@ -10,7 +10,9 @@ Variants (comma separated, ``plan`` = unchanged):
   gate_up:stream_split:WPB:S   split-K gate_up with the SwiGLU in the last arriver
   deferM                       the TP=1 deferred RMSNorm up to M rows (ops.DEFER_NORM_MAX_M)
   waves:W                      register-streaming kernels with W (4 | 8) waves per workgroup at every grid
-  fp8stream:N:K:WPB:S          the fp8 weight of shape N x K on the LDS-DMA stream kernel with (wpb, S) (S 1 for SwiGLU)
+  fp8stream:N:K:WPB:S          the fp8 weight of shape N x K on the LDS-DMA stream kernel with (wpb, S) (SwiGLU: S > 1
+                               = the split-K SwiGLU epilogue)
+  fp8skinny:N:K                the fp8 weight of shape N x K on the register-streaming kernel
   w8max:N                      8-wave register-streaming workgroups for one row up to N workgroups
   fp8resid:N:K:WPB:S           the fp8 deferred-norm producer (stream_fp8, residual epilogue) of one shape
   buckets:B1+B2+...            decode graph buckets up to the largest given (the rest unchanged)
@@ -115,6 +117,11 @@ def main():
                     return (wpb, splits or S)
                 return base_scf8(N, K, swiglu=swiglu, splits=splits, M=M)
             hip.stream_config_fp8 = scf8
+            return
+        if v.startswith("fp8skinny:"):  # fp8skinny:N:K -- that fp8 shape on the register-streaming kernel
+            N0, K0 = (int(t) for t in v.split(":")[1:])
+            hip.stream_config_fp8 = (lambda N, K, swiglu=False, splits=None, M=1:
+                                     None if (N, K) == (N0, K0) else base_scf8(N, K, swiglu=swiglu, splits=splits, M=M))
             return
         if v.startswith("fp8resid:"):  # fp8resid:N:K:wpb:S -- the fp8 deferred-norm producer of one shape
             N0, K0, wpb, S = (int(t) for t in v.split(":")[1:])
