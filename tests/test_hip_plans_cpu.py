@@ -98,3 +98,21 @@ def test_fp8_tp_push_producer_rule(monkeypatch):
     assert ops._resid_plan(hip, a(10, 3584), w(8192, 3584), "down", tp=True)[0] == "stream"
     assert ops._resid_plan(hip, a(1, 8192), w(8192, 8192), "o", tp=False)[0] == "stream"
     assert ops._resid_plan(hip, a(1, 1024), w(8192, 1024), "o", tp=True, force="stream")[0] == "stream"
+
+
+def test_narrow_gate_up_split_rules():
+    # fp8: a gate_up too narrow for one stream tile per CU takes the split-K SwiGLU (70B TP=8 shard, every decode
+    # row count: profiles/r6_fp8_swiglu_split_insitu.jsonl); TP=1 / TP=4 at <= 8 rows stay on the register-
+    # streaming kernel (N x K >= 64 M), and wider gate_ups keep one tile per column
+    assert hip.stream_config_fp8(7168, 8192, swiglu=True, M=1) == (7, 4)
+    assert hip.stream_config_fp8(7168, 8192, swiglu=True, M=39) == (7, 4)
+    assert hip.stream_config_fp8(14336, 8192, swiglu=True, M=1) is None
+    assert hip.stream_config_fp8(57344, 8192, swiglu=True, M=1) is None
+    assert hip.stream_config_fp8(57344, 8192, swiglu=True, M=16) == (7, 1)
+    # bf16: the TP=4 shard's 7168-row gate_up splits at one row too (one-round grid), the TP=8 shard's 3584 rows
+    # stay on the register-streaming kernel up to 16 rows, the TP=2 shard's 14336 rows on one tile per column
+    # (profiles/r6_bf16_swiglu_split_insitu.jsonl)
+    assert hip.plan("gate_up", 1, 7168, 4096) == ("stream_split", 7, 4)
+    assert hip.plan("gate_up", 10, 7168, 4096) == ("stream_split", 7, 4)
+    assert hip.plan("gate_up", 1, 3584, 4096)[0] == "skinny"
+    assert hip.plan("gate_up", 1, 14336, 4096) == ("stream", 4, 1)
