@@ -646,7 +646,9 @@ __global__ __launch_bounds__(256, 3) void attn_decode_mfma_kernel(
     // LDS holds tile t; set B carries tile t + 1 and set A tile t + 2 (two tiles in flight while a tile
     // is scored); unrolled by two so every register array is indexed statically.  (Four sets in flight at
     // one workgroup per CU measured SLOWER in round 5: B=1 at 13.5k +1.5-2.5 %, the TP=8 shard +10 %, the
-    // overshoot loads past a short split's last tile outweighing the deeper queue: r5_attn_deep_ab.jsonl.)
+    // overshoot loads past a short split's last tile outweighing the deeper queue: r5_attn_deep_ab.jsonl; again
+    // in round 6, r6_attn_deep_ring_insitu.jsonl.  Nor did 4 staging waves beside the 4 scoring ones over two
+    // LDS tile buffers: the loaders wait on the page loads, r6_attn_stamps.jsonl.)
     ST(0)
     for (int t = 0; t < ntiles; t += 2) {
         compute(t);
