@@ -555,6 +555,16 @@ def test_stream_fp8_swiglu_split(M, N, K, wpb, S, monkeypatch):
     if S > 1 and M <= hip.SKINNY_MAX_M:
         monkeypatch.setattr(hip, "stream_config_fp8", lambda N_, K_, swiglu=False, splits=None, M=1: (wpb, S))
         _close(hip.fp8_linear_swiglu(x, wgu), ref, 3e-2)
+    # consuming a deferred RMSNorm (per-tile sums of squares of the un-normalised rows, the TP-push producer's
+    # output): the row scale multiplies every split's partial tile before the last arriver sums them
+    tiles = 64
+    h = x * 3
+    ssq = h.float().pow(2).view(M, tiles, K // tiles).sum(-1).contiguous()
+    hf = h.float()
+    gn, un = reference.split_gate_up((hf * torch.rsqrt(hf.pow(2).mean(-1, keepdim=True) + 1e-5)) @ wgu.dequant().t())
+    act = torch.empty(M, N // 2, dtype=torch.bfloat16, device=DEV)
+    hip._stream_fp8(h, wgu, act, hip.EPI_SWIGLU_SPLIT, S, N // 2, wpb, parts=parts, counters=cnt, norm=(ssq, 1e-5))
+    _close(act, gn * torch.sigmoid(gn) * un, 3e-2, 3e-2)
 
 
 def test_fp8_swiglu_and_quant():
